@@ -1,0 +1,117 @@
+"""ctypes binding of libgr_amd.so (the C ABI declared in include/gr_amd.h).
+
+The library is built in-tree by ``build.py`` (``__graft_entry__.build()``).  There is no CPU or
+PyTorch fallback: if the library is missing, or a tensor is not on a ROCm device, the call raises.
+"""
+import ctypes
+import os
+
+import torch
+
+_PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_PKG, "lib", "libgr_amd.so")
+
+GR_ACT_NONE = 0
+GR_ACT_RELU = 1
+GR_MAX_LEVELS = 8
+GR_MAX_LINEAR = 8
+
+_c_int_p = ctypes.POINTER(ctypes.c_int32)
+_vp = ctypes.c_void_p
+_i64 = ctypes.c_int64
+_i32 = ctypes.c_int32
+_sz = ctypes.c_size_t
+_f32 = ctypes.c_float
+
+
+class SasrecParams(ctypes.Structure):
+    """Mirror of ``gr_sasrec_params`` (include/gr_amd.h)."""
+    _fields_ = [("d", _i32), ("n_blocks", _i32), ("n_heads", _i32), ("mlp", _i32),
+                ("max_len", _i32), ("eps", _f32), ("item_rows", _i64),
+                ("item_emb", _vp), ("pos_emb", _vp),
+                ("attn_ln_w", _vp), ("attn_ln_b", _vp), ("in_proj_w", _vp), ("in_proj_b", _vp),
+                ("out_proj_w", _vp), ("out_proj_b", _vp), ("ffn_ln_w", _vp), ("ffn_ln_b", _vp),
+                ("ffn1_w", _vp), ("ffn1_b", _vp), ("ffn2_w", _vp), ("ffn2_b", _vp),
+                ("last_ln_w", _vp), ("last_ln_b", _vp)]
+
+
+# (name, restype, argtypes) for every entry point of include/gr_amd.h
+SIGNATURES = {
+    "gr_version": (ctypes.c_char_p, []),
+    "gr_last_error": (ctypes.c_char_p, []),
+    "gr_linear_f32": (ctypes.c_int, [_vp, _i64, _i32, _vp, _i32, _vp, _vp, _i64, _i32, _vp, _i64, _vp]),
+    "gr_rq_codebook_norms_f32": (ctypes.c_int, [_vp, _i32, _i32, _vp, _vp]),
+    "gr_rq_quantize_f32": (ctypes.c_int, [_vp, _i64, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "gr_rq_encode_workspace_bytes": (_sz, [_i64, _i32, _vp, _i32, _vp]),
+    "gr_rq_encode_f32": (ctypes.c_int, [_vp, _i64, _i32, _vp, _vp, _vp, _i32, _vp, _vp, _vp, _vp,
+                                        _vp, _vp, _vp, _sz, _vp]),
+    "gr_sasrec_workspace_bytes": (_sz, [ctypes.POINTER(SasrecParams), _i64, _i32]),
+    "gr_sasrec_forward_f32": (ctypes.c_int, [ctypes.POINTER(SasrecParams), _vp, _i64, _i32, _vp,
+                                             _i32, _vp, _sz, _vp, _vp]),
+    "gr_sasrec_predict_f32": (ctypes.c_int, [ctypes.POINTER(SasrecParams), _vp, _i64, _i32, _vp,
+                                             _vp, _sz, _vp, _vp]),
+    "gr_score_f32": (ctypes.c_int, [_vp, _i64, _i32, _vp, _i64, _vp, _i64, _vp]),
+    "gr_rank_f32": (ctypes.c_int, [_vp, _i64, _i64, _i64, _vp, _i32, _vp, _vp]),
+}
+
+_lib = None
+
+
+def lib():
+    """Load (once) and return the ctypes handle; raises if the library has not been built."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"gr_amd: {LIB_PATH} is missing - run __graft_entry__.build() "
+                               "(there is no CPU fallback)")
+        handle = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(handle, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = handle
+    return _lib
+
+
+def check(rc, what):
+    if rc != 0:
+        msg = lib().gr_last_error().decode(errors="replace")
+        raise RuntimeError(f"{what} failed (code {rc}): {msg}")
+
+
+def require_gpu(*tensors):
+    """The product path runs only on a ROCm device: refuse CPU tensors loudly."""
+    for t in tensors:
+        if not t.is_cuda:
+            raise RuntimeError("gr_amd kernels run on a ROCm GPU only (tensor on "
+                               f"{t.device}); there is no CPU fallback")
+
+
+def ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def stream_of(device):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def ptr_array(tensors):
+    """Host array of device pointers (``const float* const*``)."""
+    arr = (ctypes.c_void_p * len(tensors))(*[t.data_ptr() for t in tensors])
+    return arr
+
+
+def i32_array(values):
+    return (ctypes.c_int32 * len(values))(*values)
+
+
+def workspace(nbytes, device):
+    """Caller-owned scratch from the PyTorch caching allocator (the library never allocates)."""
+    return torch.empty(max(int(nbytes), 1), dtype=torch.uint8, device=device)
+
+
+def as_f32(t):
+    """Contiguous fp32 view (the kernels are fp32 end to end, like the reference)."""
+    if t.dtype != torch.float32:
+        raise TypeError(f"gr_amd kernels take float32 tensors, got {t.dtype}")
+    return t.contiguous()

@@ -1,0 +1,55 @@
+// Shared definitions for the gfx950 kernels of libgr_amd.so (see include/gr_amd.h).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string>
+
+#include "gr_amd.h"
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+namespace gr {
+
+// Thread-local message behind gr_last_error().
+void set_error(const std::string& msg);
+void clear_error();
+
+inline int fail(int code, const std::string& msg) {
+  set_error(msg);
+  return code;
+}
+
+// Check the launch that was just enqueued.
+inline int check_launch(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(GR_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
+  return GR_OK;
+}
+
+inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
+
+// Bijective XCD-aware remap of a 1-D workgroup id (cdna_hip_programming.md §5 T1): blocks that the
+// dispatcher deals to one XCD (orig % 8 equal) get consecutive logical ids, so neighbouring tiles
+// that share an operand panel share that XCD's L2.  Placement only affects speed, never results.
+__device__ __forceinline__ int xcd_remap(int orig, int nwg) {
+  const int xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
+  const int start = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  return start + (orig >> 3);
+}
+
+// f32-input MFMA 32x32x2 (exact k-ordered fp32 fma chain; cdna_hip_programming.md §3).
+// Lane l supplies A[i = l&31][k = l>>5] and B[k = l>>5][j = l&31];
+// D register v of lane l holds row (v&3) + 8*(v>>2) + 4*(l>>5), column l&31.
+__device__ __forceinline__ f32x16 mfma32(float a, float b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+
+}  // namespace gr
+
+// Internal launchers shared between translation units (all enqueue on `stream`, no sync).
+int gr_linear_launch(const float* x, int64_t m, int32_t k, const float* w, int32_t n,
+                     const float* bias, const float* residual, int64_t ldr, int32_t act, float* y,
+                     int64_t ldy, hipStream_t stream);

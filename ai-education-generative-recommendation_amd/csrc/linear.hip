@@ -1,0 +1,193 @@
+// fp32 dense layer on the gfx950 matrix cores: y = act(x . w^T + bias) (+ residual).
+//
+// Replaces the reference's F.linear/addmm calls (RQ-VAE/models/layers.py:23 encoder Linear,
+// SASRec/model.py:37-45 FFN, torch functional.py MHA in/out projections, SASRec/model.py:107
+// full-catalog scoring).  Both operands are K-contiguous ("NT"): x[m,k], w[n,k] (nn.Linear layout).
+//
+// Tile: BM x BN outputs per 256-thread workgroup (4 waves), K staged 32-deep through a double-
+// buffered LDS image with register staging (rows padded to 36 floats: conflict-free ds_read_b128).
+// Each wave owns (BM/WM) x (BN/WN) outputs as TMxTN accumulators of v_mfma_f32_32x32x2_f32.
+// Operand trick: a lane reads one float4 per operand per 8-deep k-slice ([row][4h..4h+3]) and feeds
+// element s to MFMA step s, so MFMA step s covers k = {8kc+s, 8kc+4+s}.  Every output element
+// therefore sees the same k-ordered fp32 fma chain, independent of its tile position — the property
+// the fused rank epilogue relies on (SURVEY §7 hard part 3).
+#include "gr_common.h"
+
+namespace gr {
+
+constexpr int LIN_BK = 32;
+constexpr int LIN_PITCH = LIN_BK + 4;
+
+template <int BM, int BN, int WM, int WN, int ACT, bool RES, bool NMAJOR>
+__global__ __launch_bounds__(256) void linear_f32_kernel(
+    const float* __restrict__ x, const float* __restrict__ w, const float* __restrict__ bias,
+    const float* residual, float* y, int64_t M, int N, int K, int64_t ldy, int64_t ldr,
+    int tiles_m, int tiles_n) {
+  static_assert(WM * WN == 4, "4 waves");
+  constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
+  constexpr int AV = BM * LIN_BK / 4 / 256, BV = BN * LIN_BK / 4 / 256;
+  static_assert(TM >= 1 && TN >= 1 && AV >= 1 && BV >= 1, "tile");
+  __shared__ __attribute__((aligned(16))) float lds[2][(BM + BN) * LIN_PITCH];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN, r = lane & 31, h = lane >> 5;
+  const int wgid = xcd_remap(blockIdx.x, gridDim.x);
+  int tmi, tni;
+  if (NMAJOR) { tmi = wgid % tiles_m; tni = wgid / tiles_m; }
+  else        { tni = wgid % tiles_n; tmi = wgid / tiles_n; }
+  const int64_t m0 = (int64_t)tmi * BM;
+  const int n0 = tni * BN;
+
+  f32x4 ra[AV], rb[BV];
+  auto gload = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < AV; ++i) {
+      const int f = tid + 256 * i, row = f >> 3, kk = k0 + (f & 7) * 4;
+      const int64_t gr_ = m0 + row;
+      ra[i] = (gr_ < M && kk < K) ? *reinterpret_cast<const f32x4*>(x + gr_ * K + kk)
+                                  : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int i = 0; i < BV; ++i) {
+      const int f = tid + 256 * i, row = f >> 3, kk = k0 + (f & 7) * 4;
+      const int gn = n0 + row;
+      rb[i] = (gn < N && kk < K) ? *reinterpret_cast<const f32x4*>(w + (int64_t)gn * K + kk)
+                                 : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+  auto swrite = [&](int buf) {
+    float* s = lds[buf];
+#pragma unroll
+    for (int i = 0; i < AV; ++i) {
+      const int f = tid + 256 * i;
+      *reinterpret_cast<f32x4*>(s + (f >> 3) * LIN_PITCH + (f & 7) * 4) = ra[i];
+    }
+#pragma unroll
+    for (int i = 0; i < BV; ++i) {
+      const int f = tid + 256 * i;
+      *reinterpret_cast<f32x4*>(s + (BM + (f >> 3)) * LIN_PITCH + (f & 7) * 4) = rb[i];
+    }
+  };
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int a = 0; a < TM; ++a)
+#pragma unroll
+    for (int b = 0; b < TN; ++b)
+#pragma unroll
+      for (int v = 0; v < 16; ++v) acc[a][b][v] = 0.f;
+
+  const int nk = (K + LIN_BK - 1) / LIN_BK;
+  gload(0);
+  swrite(0);
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) gload((kt + 1) * LIN_BK);
+    const float* As = lds[cur] + (wm * (BM / WM) + r) * LIN_PITCH + 4 * h;
+    const float* Bs = lds[cur] + (BM + wn * (BN / WN) + r) * LIN_PITCH + 4 * h;
+#pragma unroll
+    for (int kc = 0; kc < LIN_BK / 8; ++kc) {
+      f32x4 a[TM], b[TN];
+#pragma unroll
+      for (int t = 0; t < TM; ++t)
+        a[t] = *reinterpret_cast<const f32x4*>(As + t * 32 * LIN_PITCH + kc * 8);
+#pragma unroll
+      for (int t = 0; t < TN; ++t)
+        b[t] = *reinterpret_cast<const f32x4*>(Bs + t * 32 * LIN_PITCH + kc * 8);
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) acc[i][j] = mfma32(a[i][s], b[j][s], acc[i][j]);
+    }
+    if (kt + 1 < nk) swrite(cur ^ 1);
+    __syncthreads();
+  }
+
+  // Epilogue: bias, activation, residual; D register v -> row (v&3)+8(v>>2)+4h, column r.
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int col = n0 + wn * (BN / WN) + j * 32 + r;
+    const bool cok = col < N;
+    const float bv = (bias != nullptr && cok) ? bias[col] : 0.f;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+#pragma unroll
+      for (int v = 0; v < 16; ++v) {
+        const int64_t row = m0 + wm * (BM / WM) + i * 32 + (v & 3) + 8 * (v >> 2) + 4 * h;
+        if (cok && row < M) {
+          float o = acc[i][j][v];
+          if (bias != nullptr) o = o + bv;
+          if (ACT == GR_ACT_RELU) o = (o < 0.f) ? 0.f : o;  // NaN propagates like torch.relu
+          if (RES) o = residual[row * ldr + col] + o;
+          y[row * ldy + col] = o;
+        }
+      }
+    }
+  }
+}
+
+template <int BM, int BN, int WM, int WN>
+static int launch_tile(const float* x, int64_t m, int k, const float* w, int n, const float* bias,
+                       const float* residual, int64_t ldr, int act, float* y, int64_t ldy,
+                       hipStream_t stream) {
+  const int64_t tm = (m + BM - 1) / BM;
+  const int tn = (n + BN - 1) / BN;
+  if (tm * tn > 0x7fffffffLL) return fail(GR_ERR_UNSUPPORTED, "gr_linear_f32: grid too large");
+  const bool nmajor = (int64_t)n > m;  // iterate the smaller operand's tiles fastest
+  const dim3 grid((unsigned)(tm * tn)), block(256);
+  const bool res = residual != nullptr;
+#define GR_LIN_CASE(A, R, NM)                                                                    \
+  if (act == A && res == R && nmajor == NM) {                                                     \
+    hipLaunchKernelGGL((linear_f32_kernel<BM, BN, WM, WN, A, R, NM>), grid, block, 0, stream, x, \
+                       w, bias, residual, y, m, n, k, ldy, ldr, (int)tm, tn);                    \
+    return check_launch("gr_linear_f32");                                                        \
+  }
+  GR_LIN_CASE(GR_ACT_NONE, false, false)
+  GR_LIN_CASE(GR_ACT_NONE, false, true)
+  GR_LIN_CASE(GR_ACT_NONE, true, false)
+  GR_LIN_CASE(GR_ACT_NONE, true, true)
+  GR_LIN_CASE(GR_ACT_RELU, false, false)
+  GR_LIN_CASE(GR_ACT_RELU, false, true)
+  GR_LIN_CASE(GR_ACT_RELU, true, false)
+  GR_LIN_CASE(GR_ACT_RELU, true, true)
+#undef GR_LIN_CASE
+  return fail(GR_ERR_ARG, "gr_linear_f32: bad activation");
+}
+
+}  // namespace gr
+
+int gr_linear_launch(const float* x, int64_t m, int32_t k, const float* w, int32_t n,
+                     const float* bias, const float* residual, int64_t ldr, int32_t act, float* y,
+                     int64_t ldy, hipStream_t stream) {
+  using namespace gr;
+  if (m < 0 || k <= 0 || n <= 0) return fail(GR_ERR_ARG, "gr_linear_f32: bad shape");
+  if (m == 0) return GR_OK;
+  if (!x || !w || !y) return fail(GR_ERR_ARG, "gr_linear_f32: null pointer");
+  if (k % 4 != 0) return fail(GR_ERR_UNSUPPORTED, "gr_linear_f32: k must be a multiple of 4");
+  if (!aligned16(x) || !aligned16(w))
+    return fail(GR_ERR_ARG, "gr_linear_f32: x and w must be 16-byte aligned");
+  if (ldy < n || (residual && ldr < n)) return fail(GR_ERR_ARG, "gr_linear_f32: bad row stride");
+  if (act != GR_ACT_NONE && act != GR_ACT_RELU) return fail(GR_ERR_ARG, "gr_linear_f32: bad act");
+  if (n >= 128) return launch_tile<128, 128, 2, 2>(x, m, k, w, n, bias, residual, ldr, act, y, ldy, stream);
+  if (n > 32) return launch_tile<128, 64, 2, 2>(x, m, k, w, n, bias, residual, ldr, act, y, ldy, stream);
+  return launch_tile<128, 32, 4, 1>(x, m, k, w, n, bias, residual, ldr, act, y, ldy, stream);
+}
+
+extern "C" int gr_linear_f32(const float* x, int64_t m, int32_t k, const float* w, int32_t n,
+                             const float* bias, const float* residual, int64_t ldr, int32_t act,
+                             float* y, int64_t ldy, void* stream) {
+  gr::clear_error();
+  return gr_linear_launch(x, m, k, w, n, bias, residual, ldr, act, y, ldy,
+                          reinterpret_cast<hipStream_t>(stream));
+}
+
+extern "C" int gr_score_f32(const float* h, int64_t B, int32_t d, const float* table, int64_t rows,
+                            float* logits, int64_t ld, void* stream) {
+  gr::clear_error();
+  if (rows > 0x7fffffffLL) return gr::fail(GR_ERR_UNSUPPORTED, "gr_score_f32: rows >= 2^31");
+  return gr_linear_launch(h, B, d, table, (int32_t)rows, nullptr, nullptr, 0, GR_ACT_NONE, logits,
+                          ld, reinterpret_cast<hipStream_t>(stream));
+}

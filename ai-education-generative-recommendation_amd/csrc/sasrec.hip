@@ -1,0 +1,357 @@
+// SASRec eval forward / predict on gfx950 (replaces SASRec/model.py:49-108 and the
+// nn.MultiheadAttention math of torch functional.py:6576-6600; the evaluate.py:27-32 rank tail).
+//
+// Layer-wise pipeline over the batch (B*n token rows), all buffers in the caller's workspace:
+//   embed      X = M[s] + P[t]                                  (model.py:58-60, exact fp32 add)
+//   per block  H = LN_a(X); QKV = H.W_in^T + b_in                (model.py:80, functional.py:5823)
+//              O = causal softmax((q*sqrt(1/hd)).k^T) . v        (functional.py:6578-6594)
+//              X = X + (O.W_o^T + b_o)                           (functional.py:6600, model.py:84)
+//              H = LN_f(X); F = relu(H.W1^T + b1); X = X + (F.W2^T + b2)   (model.py:92-94)
+//   last LN    on every row (forward) or on the last position only (predict, model.py:104)
+//   scoring    logits = h . M^T                                   (model.py:107)
+// The dead W_Q/W_K/W_V projections (model.py:63-65) are elided: no output depends on them.
+#include <cmath>
+
+#include "gr_common.h"
+
+namespace gr {
+
+// ---------------------------------------------------------------------------------- embedding
+__global__ __launch_bounds__(256) void embed_kernel(const int64_t* __restrict__ seqs, int64_t rows,
+                                                    int n, int d, const float* __restrict__ item,
+                                                    int64_t item_rows,
+                                                    const float* __restrict__ pos,
+                                                    float* __restrict__ x, int32_t* err) {
+  const int d4 = d >> 2;
+  const int64_t f = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (f >= rows * d4) return;
+  const int64_t row = f / d4;
+  const int c = (int)(f % d4) * 4;
+  const int t = (int)(row % n);
+  int64_t id = seqs[row];
+  if (id < 0 || id >= item_rows) {  // torch raises IndexError here; flag it and read the pad row
+    if (err) *err = 1;
+    id = 0;
+  }
+  const f32x4 a = *reinterpret_cast<const f32x4*>(item + id * d + c);
+  const f32x4 p = *reinterpret_cast<const f32x4*>(pos + (int64_t)t * d + c);
+  *reinterpret_cast<f32x4*>(x + row * d + c) = a + p;
+}
+
+// ---------------------------------------------------------------------------------- layernorm
+// One wave per row: mean, biased variance, (x - mean) * rsqrt(var + eps) * w + b (F.layer_norm).
+// Input row r is read at in + (r * in_stride + in_offset) * d (in_stride = n, in_offset = n-1
+// selects the last position of every sequence).
+__global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict__ in, int64_t rows,
+                                                        int d, int64_t in_stride, int64_t in_offset,
+                                                        const float* __restrict__ w,
+                                                        const float* __restrict__ b, float eps,
+                                                        float* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const float* xr = in + (row * in_stride + in_offset) * d;
+  float s = 0.f;
+  for (int c = lane; c < d; c += 64) s += xr[c];
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+  const float mean = s / (float)d;
+  float v = 0.f;
+  for (int c = lane; c < d; c += 64) {
+    const float t = xr[c] - mean;
+    v = fmaf(t, t, v);
+  }
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  const float rstd = 1.0f / sqrtf(v / (float)d + eps);
+  float* yr = out + row * d;
+  for (int c = lane; c < d; c += 64) yr[c] = (xr[c] - mean) * rstd * w[c] + b[c];
+}
+
+// ---------------------------------------------------------------------------------- attention
+// Causal multi-head attention for one (sequence, head) and a tile of QT query rows.
+// qkv: [B, n, 3d] rows (q | k | v, head h at columns h*hd); out: [B, n, d].
+// Scores of the tile's rows against keys [0, q0+QT) live in LDS, softmax is exact (row max,
+// exp, sum, divide), then O = P . V.  Keys beyond a row's causal limit are -inf -> weight 0.
+constexpr int ATT_QT = 16;
+constexpr int ATT_KC = 64;
+
+__global__ __launch_bounds__(256) void causal_attn_kernel(const float* __restrict__ qkv,
+                                                          float* __restrict__ out, int n, int H,
+                                                          int hd, float scale) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int hp = hd + 1;
+  float* Qs = sm;                        // [QT][hd+1]
+  float* KVs = Qs + ATT_QT * hp;          // [KC][hd+1]
+  float* S = KVs + ATT_KC * hp;           // [QT][n]
+  const int tid = threadIdx.x;
+  const int b = blockIdx.x / H, hh = blockIdx.x % H;
+  const int q0 = blockIdx.y * ATT_QT;
+  const int d = H * hd;
+  const int64_t rs = 3LL * d;
+  const float* base = qkv + (int64_t)b * n * rs + hh * hd;
+  const int qn = min(ATT_QT, n - q0);
+  const int kmax = q0 + qn;
+
+  for (int i = tid; i < qn * hd; i += 256) {
+    const int qi = i / hd, c = i % hd;
+    Qs[qi * hp + c] = base[(int64_t)(q0 + qi) * rs + c] * scale;  // q * sqrt(1/hd) (functional.py:6578)
+  }
+  for (int k0 = 0; k0 < kmax; k0 += ATT_KC) {
+    const int kn = min(ATT_KC, kmax - k0);
+    __syncthreads();
+    for (int i = tid; i < kn * hd; i += 256) {
+      const int j = i / hd, c = i % hd;
+      KVs[j * hp + c] = base[(int64_t)(k0 + j) * rs + d + c];
+    }
+    __syncthreads();
+    for (int i = tid; i < ATT_QT * ATT_KC; i += 256) {
+      const int qi = i / ATT_KC, j = i % ATT_KC;
+      if (qi < qn && j < kn) {
+        const int kj = k0 + j;
+        float s = -__builtin_inff();
+        if (kj <= q0 + qi) {
+          s = 0.f;
+          const float* qr = Qs + qi * hp;
+          const float* kr = KVs + j * hp;
+          for (int c = 0; c < hd; ++c) s = fmaf(qr[c], kr[c], s);
+        }
+        S[qi * n + kj] = s;
+      }
+    }
+  }
+  __syncthreads();
+  // softmax: one wave per row
+  const int lane = tid & 63, wave = tid >> 6;
+  for (int qi = wave; qi < qn; qi += 4) {
+    float* sr = S + qi * n;
+    const int lim = q0 + qi + 1;  // causal keys [0, lim)
+    float m = -__builtin_inff();
+    for (int j = lane; j < lim; j += 64) m = fmaxf(m, sr[j]);
+    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+    float sum = 0.f;
+    for (int j = lane; j < lim; j += 64) {
+      const float e = expf(sr[j] - m);
+      sr[j] = e;
+      sum += e;
+    }
+    for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o);
+    for (int j = lane; j < lim; j += 64) sr[j] = sr[j] / sum;
+    for (int j = lim + lane; j < kmax; j += 64) sr[j] = 0.f;
+  }
+  // O = P . V
+  constexpr int MAXO = ATT_QT * 128 / 256;  // outputs per thread for hd <= 128
+  float acc[MAXO];
+#pragma unroll
+  for (int u = 0; u < MAXO; ++u) acc[u] = 0.f;
+  for (int k0 = 0; k0 < kmax; k0 += ATT_KC) {
+    const int kn = min(ATT_KC, kmax - k0);
+    __syncthreads();
+    for (int i = tid; i < kn * hd; i += 256) {
+      const int j = i / hd, c = i % hd;
+      KVs[j * hp + c] = base[(int64_t)(k0 + j) * rs + 2 * d + c];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < MAXO; ++u) {
+      const int i = tid + 256 * u;
+      if (i < qn * hd) {
+        const int qi = i / hd, c = i % hd;
+        const float* pr = S + qi * n + k0;
+        float a = acc[u];
+        for (int j = 0; j < kn; ++j) a = fmaf(pr[j], KVs[j * hp + c], a);
+        acc[u] = a;
+      }
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < MAXO; ++u) {
+    const int i = tid + 256 * u;
+    if (i < qn * hd) {
+      const int qi = i / hd, c = i % hd;
+      out[((int64_t)b * n + q0 + qi) * d + hh * hd + c] = acc[u];
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------- rank
+// rank[b] = 1 + #{j : l'[b,j] > l'[b,t]} with l'[b,0] = -1e9 when mask_col0 (evaluate.py:27-32).
+__global__ __launch_bounds__(256) void rank_kernel(const float* __restrict__ logits, int64_t cols,
+                                                   int64_t ld, const int64_t* __restrict__ targets,
+                                                   int mask0, int64_t* __restrict__ ranks) {
+  __shared__ int64_t part[4];
+  const int64_t b = blockIdx.x;
+  const float* row = logits + b * ld;
+  const int64_t t = targets[b];
+  if (t < 0 || t >= cols) {  // torch.gather raises here; report rank -1
+    if (threadIdx.x == 0) ranks[b] = -1;
+    return;
+  }
+  const float pad = -1e9f;
+  float ts = (t == 0 && mask0) ? pad : row[t];
+  int64_t cnt = 0;
+  for (int64_t j = threadIdx.x; j < cols; j += 256) {
+    const float v = (j == 0 && mask0) ? pad : row[j];
+    cnt += v > ts ? 1 : 0;
+  }
+  for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o);
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = cnt;
+  __syncthreads();
+  if (threadIdx.x == 0) ranks[b] = part[0] + part[1] + part[2] + part[3] + 1;
+}
+
+// ---------------------------------------------------------------------------------- driver
+struct SasWs {
+  float *x, *h, *qkv, *o, *f;
+};
+
+static size_t ws_layout(const gr_sasrec_params* p, int64_t B, int32_t n, char* base, SasWs* w) {
+  const size_t rows = (size_t)B * n;
+  const size_t sx = align_up(rows * p->d * 4, 256);
+  const size_t sq = align_up(rows * 3 * p->d * 4, 256);
+  const size_t sf = align_up(rows * (size_t)p->mlp * 4, 256);
+  if (w) {
+    w->x = reinterpret_cast<float*>(base);
+    w->h = reinterpret_cast<float*>(base + sx);
+    w->o = reinterpret_cast<float*>(base + 2 * sx);
+    w->qkv = reinterpret_cast<float*>(base + 3 * sx);
+    w->f = reinterpret_cast<float*>(base + 3 * sx + sq);
+  }
+  return 3 * sx + sq + sf + 256;
+}
+
+static int check_params(const gr_sasrec_params* p, int64_t B, int32_t n) {
+  if (!p) return fail(GR_ERR_ARG, "sasrec: null params");
+  if (p->d < 4 || p->d % 4 || p->n_heads < 1 || p->d % p->n_heads)
+    return fail(GR_ERR_UNSUPPORTED, "sasrec: d must be a multiple of 4 and of num_heads");
+  if (p->d / p->n_heads > 128) return fail(GR_ERR_UNSUPPORTED, "sasrec: head dim > 128");
+  if (p->mlp < 4 || p->mlp % 4) return fail(GR_ERR_UNSUPPORTED, "sasrec: mlp_layer must be a multiple of 4");
+  if (p->n_blocks < 0) return fail(GR_ERR_ARG, "sasrec: num_blocks < 0");
+  if (n < 1 || n > p->max_len) return fail(GR_ERR_ARG, "sasrec: sequence length outside [1, max_len]");
+  if (n > 1024) return fail(GR_ERR_UNSUPPORTED, "sasrec: sequence length > 1024");
+  if (B < 0) return fail(GR_ERR_ARG, "sasrec: B < 0");
+  if (!p->item_emb || !p->pos_emb || !p->last_ln_w || !p->last_ln_b || p->item_rows < 1)
+    return fail(GR_ERR_ARG, "sasrec: null embedding / last layernorm");
+  if (p->item_rows > 0x7fffffffLL) return fail(GR_ERR_UNSUPPORTED, "sasrec: item_rows >= 2^31");
+  if (!aligned16(p->item_emb) || !aligned16(p->pos_emb))
+    return fail(GR_ERR_ARG, "sasrec: embeddings must be 16-byte aligned");
+  return GR_OK;
+}
+
+static int run_layernorm(const float* in, int64_t rows, int d, int64_t stride, int64_t off,
+                         const float* w, const float* b, float eps, float* out, hipStream_t st) {
+  hipLaunchKernelGGL(layernorm_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, st, in, rows,
+                     d, stride, off, w, b, eps, out);
+  return check_launch("sasrec layernorm");
+}
+
+static int run_forward(const gr_sasrec_params* p, const int64_t* seqs, int64_t B, int32_t n,
+                       const SasWs& w, int32_t* err, hipStream_t st) {
+  const int d = p->d, H = p->n_heads, hd = d / H;
+  const int64_t rows = B * n;
+  {
+    const int64_t tot = rows * (d / 4);
+    hipLaunchKernelGGL(embed_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, seqs,
+                       rows, n, d, p->item_emb, p->item_rows, p->pos_emb, w.x, err);
+    int rc = check_launch("sasrec embed");
+    if (rc) return rc;
+  }
+  const float scale = (float)std::sqrt(1.0 / (double)hd);
+  const size_t att_lds = (size_t)(ATT_QT + ATT_KC) * (hd + 1) * 4 + (size_t)ATT_QT * n * 4;
+  if (att_lds > 64 * 1024) {
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&causal_attn_kernel),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)att_lds) != hipSuccess)
+      return fail(GR_ERR_HIP, "sasrec attention: cannot raise the LDS limit");
+  }
+  for (int i = 0; i < p->n_blocks; ++i) {
+    int rc = run_layernorm(w.x, rows, d, 1, 0, p->attn_ln_w[i], p->attn_ln_b[i], p->eps, w.h, st);
+    if (rc) return rc;
+    rc = gr_linear_launch(w.h, rows, d, p->in_proj_w[i], 3 * d, p->in_proj_b[i], nullptr, 0,
+                          GR_ACT_NONE, w.qkv, 3 * d, st);
+    if (rc) return rc;
+    hipLaunchKernelGGL(causal_attn_kernel, dim3((unsigned)(B * H), (unsigned)((n + ATT_QT - 1) / ATT_QT)),
+                       dim3(256), att_lds, st, w.qkv, w.o, n, H, hd, scale);
+    rc = check_launch("sasrec attention");
+    if (rc) return rc;
+    rc = gr_linear_launch(w.o, rows, d, p->out_proj_w[i], d, p->out_proj_b[i], w.x, d, GR_ACT_NONE,
+                          w.x, d, st);
+    if (rc) return rc;
+    rc = run_layernorm(w.x, rows, d, 1, 0, p->ffn_ln_w[i], p->ffn_ln_b[i], p->eps, w.h, st);
+    if (rc) return rc;
+    rc = gr_linear_launch(w.h, rows, d, p->ffn1_w[i], p->mlp, p->ffn1_b[i], nullptr, 0, GR_ACT_RELU,
+                          w.f, p->mlp, st);
+    if (rc) return rc;
+    rc = gr_linear_launch(w.f, rows, p->mlp, p->ffn2_w[i], d, p->ffn2_b[i], w.x, d, GR_ACT_NONE,
+                          w.x, d, st);
+    if (rc) return rc;
+  }
+  return GR_OK;
+}
+
+}  // namespace gr
+
+extern "C" size_t gr_sasrec_workspace_bytes(const gr_sasrec_params* p, int64_t B, int32_t n) {
+  if (!p || B < 0 || n < 1) return 0;
+  return gr::ws_layout(p, B, n, nullptr, nullptr);
+}
+
+static int sas_prepare(const gr_sasrec_params* p, int64_t B, int32_t n, void* ws, size_t wsb,
+                       gr::SasWs* w) {
+  using namespace gr;
+  int rc = check_params(p, B, n);
+  if (rc) return rc;
+  const size_t need = ws_layout(p, B, n, nullptr, nullptr);
+  if (!ws || wsb < need)
+    return fail(GR_ERR_WORKSPACE, "sasrec: workspace too small (need " + std::to_string(need) + " bytes)");
+  char* base = reinterpret_cast<char*>(align_up(reinterpret_cast<uintptr_t>(ws), 256));
+  ws_layout(p, B, n, base, w);
+  return GR_OK;
+}
+
+extern "C" int gr_sasrec_forward_f32(const gr_sasrec_params* p, const int64_t* seqs, int64_t B,
+                                     int32_t n, float* out, int32_t last_only, void* workspace,
+                                     size_t workspace_bytes, int32_t* err_flag, void* stream) {
+  using namespace gr;
+  clear_error();
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  SasWs w;
+  int rc = sas_prepare(p, B, n, workspace, workspace_bytes, &w);
+  if (rc) return rc;
+  if (B == 0) return GR_OK;
+  if (!seqs || !out) return fail(GR_ERR_ARG, "gr_sasrec_forward_f32: null seqs / out");
+  rc = run_forward(p, seqs, B, n, w, err_flag, st);
+  if (rc) return rc;
+  if (last_only) return run_layernorm(w.x, B, p->d, n, n - 1, p->last_ln_w, p->last_ln_b, p->eps, out, st);
+  return run_layernorm(w.x, B * n, p->d, 1, 0, p->last_ln_w, p->last_ln_b, p->eps, out, st);
+}
+
+extern "C" int gr_sasrec_predict_f32(const gr_sasrec_params* p, const int64_t* seqs, int64_t B,
+                                     int32_t n, float* logits, void* workspace,
+                                     size_t workspace_bytes, int32_t* err_flag, void* stream) {
+  using namespace gr;
+  clear_error();
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  SasWs w;
+  int rc = sas_prepare(p, B, n, workspace, workspace_bytes, &w);
+  if (rc) return rc;
+  if (B == 0) return GR_OK;
+  if (!seqs || !logits) return fail(GR_ERR_ARG, "gr_sasrec_predict_f32: null seqs / logits");
+  rc = run_forward(p, seqs, B, n, w, err_flag, st);
+  if (rc) return rc;
+  rc = run_layernorm(w.x, B, p->d, n, n - 1, p->last_ln_w, p->last_ln_b, p->eps, w.h, st);
+  if (rc) return rc;
+  return gr_linear_launch(w.h, B, p->d, p->item_emb, (int32_t)p->item_rows, nullptr, nullptr, 0,
+                          GR_ACT_NONE, logits, p->item_rows, st);
+}
+
+extern "C" int gr_rank_f32(const float* logits, int64_t B, int64_t cols, int64_t ld,
+                           const int64_t* targets, int32_t mask_col0, int64_t* ranks_out,
+                           void* stream) {
+  using namespace gr;
+  clear_error();
+  if (B < 0 || cols < 1 || ld < cols) return fail(GR_ERR_ARG, "gr_rank_f32: bad shape");
+  if (B == 0) return GR_OK;
+  if (!logits || !targets || !ranks_out) return fail(GR_ERR_ARG, "gr_rank_f32: null pointer");
+  if (B > 0x7fffffffLL) return fail(GR_ERR_UNSUPPORTED, "gr_rank_f32: B >= 2^31");
+  hipLaunchKernelGGL(rank_kernel, dim3((unsigned)B), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
+                     logits, cols, ld, targets, mask_col0, ranks_out);
+  return check_launch("gr_rank_f32");
+}

@@ -1,0 +1,234 @@
+"""Tensor-level wrappers of the C ABI (include/gr_amd.h).
+
+Each function takes/returns torch tensors on a ROCm device, enqueues on the current stream and
+never synchronises.  Argument checking mirrors the ATen errors the reference would raise.
+"""
+import ctypes
+import os
+
+import torch
+
+from . import _lib as L
+
+# GR_AMD_CHECK=1 synchronises after SASRec calls and raises on out-of-range item ids (the
+# reference raises IndexError there; the kernels only flag it to stay asynchronous).
+CHECK = os.environ.get("GR_AMD_CHECK", "0") == "1"
+
+
+def linear(x, weight, bias=None, act="none", residual=None, out=None):
+    """``act(x @ weight.T + bias) (+ residual)`` — F.linear (+ ReLU) on the matrix cores."""
+    L.require_gpu(x, weight)
+    x2 = L.as_f32(x).reshape(-1, x.shape[-1])
+    w = L.as_f32(weight)
+    m, k = x2.shape
+    n = w.shape[0]
+    if w.shape[1] != k:
+        raise RuntimeError(f"linear: shape mismatch x[..., {k}] vs weight{tuple(w.shape)}")
+    b = L.as_f32(bias) if bias is not None else None
+    r = L.as_f32(residual).reshape(m, n) if residual is not None else None
+    y = out if out is not None else torch.empty((m, n), dtype=torch.float32, device=x.device)
+    a = {"none": L.GR_ACT_NONE, "relu": L.GR_ACT_RELU}[act]
+    with torch.cuda.device(x.device):
+        L.check(L.lib().gr_linear_f32(L.ptr(x2), m, k, L.ptr(w), n, L.ptr(b), L.ptr(r),
+                                      n if r is not None else 0, a, L.ptr(y), n,
+                                      L.stream_of(x.device)), "gr_linear_f32")
+    return y.reshape(*x.shape[:-1], n)
+
+
+def score(h, table, out=None):
+    """Full-catalog logits ``h @ table.T`` (SASRec/model.py:107)."""
+    L.require_gpu(h, table)
+    h = L.as_f32(h)
+    t = L.as_f32(table)
+    B, d = h.shape
+    rows = t.shape[0]
+    y = out if out is not None else torch.empty((B, rows), dtype=torch.float32, device=h.device)
+    with torch.cuda.device(h.device):
+        L.check(L.lib().gr_score_f32(L.ptr(h), B, d, L.ptr(t), rows, L.ptr(y), y.stride(0),
+                                     L.stream_of(h.device)), "gr_score_f32")
+    return y
+
+
+def rank(logits, targets, mask_col0=True):
+    """Strict rank of each target (SASRec/evaluate.py:27-32) without mutating ``logits``."""
+    L.require_gpu(logits, targets)
+    if logits.stride(1) != 1:
+        logits = logits.contiguous()
+    t = targets.reshape(-1).to(torch.int64).contiguous()
+    B, cols = logits.shape
+    out = torch.empty(B, dtype=torch.int64, device=logits.device)
+    with torch.cuda.device(logits.device):
+        L.check(L.lib().gr_rank_f32(L.ptr(logits), B, cols, logits.stride(0), L.ptr(t),
+                                    1 if mask_col0 else 0, L.ptr(out),
+                                    L.stream_of(logits.device)), "gr_rank_f32")
+    return out
+
+
+def rq_quantize(z, codebooks, with_gap=False):
+    """Residual quantization of latents (RQ-VAE/models/rq.py:39-56, use_sk=False).
+
+    With ``with_gap`` also returns the best distance and the best/second-best gap per level."""
+    L.require_gpu(z, *codebooks)
+    z = L.as_f32(z)
+    n, e = z.shape
+    cbs = [L.as_f32(c) for c in codebooks]
+    Ks = [c.shape[0] for c in cbs]
+    for c in cbs:
+        if c.shape[1] != e:
+            raise RuntimeError("rq_quantize: codebook width != latent width")
+    dev = z.device
+    norms = [torch.empty(k, dtype=torch.float32, device=dev) for k in Ks]
+    idx = torch.empty((n, len(cbs)), dtype=torch.int64, device=dev)
+    gap = torch.empty((n, len(cbs)), dtype=torch.float32, device=dev) if with_gap else None
+    best = torch.empty((n, len(cbs)), dtype=torch.float32, device=dev) if with_gap else None
+    lib = L.lib()
+    st = L.stream_of(dev)
+    with torch.cuda.device(dev):
+        for c, cn in zip(cbs, norms):
+            L.check(lib.gr_rq_codebook_norms_f32(L.ptr(c), c.shape[0], e, L.ptr(cn), st),
+                    "gr_rq_codebook_norms_f32")
+        L.check(lib.gr_rq_quantize_f32(L.ptr(z), n, e, len(cbs), L.i32_array(Ks), L.ptr_array(cbs),
+                                       L.ptr_array(norms), L.ptr(idx), L.ptr(best), L.ptr(gap), st),
+                "gr_rq_quantize_f32")
+    return (idx, best, gap) if with_gap else idx
+
+
+def rq_encode(x, weights, biases, codebooks, with_gap=False, with_z=False):
+    """RQVAE.get_indices(xs, use_sk=False): encoder MLP + residual quantization (rqvae.py:67-71).
+
+    Returns ``idx`` [n, L] int64, plus ``best`` and ``gap`` [n, L] (best distance and second-best
+    minus best) and the encoder output ``z`` when requested.
+    """
+    L.require_gpu(x, *weights, *codebooks)
+    x2 = L.as_f32(x)
+    n = x2.shape[0]
+    ws = [L.as_f32(w) for w in weights]
+    bs = [L.as_f32(b) for b in biases]
+    cbs = [L.as_f32(c) for c in codebooks]
+    dims = [x2.shape[1]] + [w.shape[0] for w in ws]
+    for i, w in enumerate(ws):
+        if w.shape[1] != dims[i]:
+            raise RuntimeError(f"rq_encode: Linear {i} expects {w.shape[1]} inputs, got {dims[i]}")
+    Ks = [c.shape[0] for c in cbs]
+    dev = x.device
+    lib = L.lib()
+    dims_c, ks_c = L.i32_array(dims), L.i32_array(Ks)
+    nbytes = lib.gr_rq_encode_workspace_bytes(n, len(ws), dims_c, len(cbs), ks_c)
+    if nbytes == 0:
+        raise RuntimeError("rq_encode: bad encoder description")
+    wsp = L.workspace(nbytes, dev)
+    idx = torch.empty((n, len(cbs)), dtype=torch.int64, device=dev)
+    gap = torch.empty((n, len(cbs)), dtype=torch.float32, device=dev) if with_gap else None
+    best = torch.empty((n, len(cbs)), dtype=torch.float32, device=dev) if with_gap else None
+    z = torch.empty((n, dims[-1]), dtype=torch.float32, device=dev) if with_z else None
+    with torch.cuda.device(dev):
+        L.check(lib.gr_rq_encode_f32(L.ptr(x2), n, len(ws), dims_c, L.ptr_array(ws), L.ptr_array(bs),
+                                     len(cbs), ks_c, L.ptr_array(cbs), L.ptr(idx), L.ptr(best), L.ptr(gap),
+                                     L.ptr(z), L.ptr(wsp), nbytes, L.stream_of(dev)),
+                "gr_rq_encode_f32")
+    out = [idx]
+    if with_gap:
+        out += [best, gap]
+    if with_z:
+        out.append(z)
+    return out[0] if len(out) == 1 else tuple(out)
+
+
+class SasrecBinding:
+    """Device-pointer view of a SASRec module's parameters (``gr_sasrec_params``).
+
+    Rebuilt on every call (cheap), so in-place weight updates and ``load_state_dict`` are seen.
+    """
+
+    def __init__(self, model):
+        self.keep = []
+        f = self._f
+        nb = model.num_blocks
+        p = L.SasrecParams()
+        p.d, p.n_blocks, p.n_heads, p.mlp = model.d, nb, model.num_heads, model.mlp_layer
+        p.max_len = model.pos_emb.weight.shape[0]
+        p.eps = float(model.layernorm_eps)
+        p.item_rows = model.item_emb.weight.shape[0]
+        p.item_emb = f(model.item_emb.weight)
+        p.pos_emb = f(model.pos_emb.weight)
+        arr = self._arr
+        p.attn_ln_w = arr([m.weight for m in model.attention_layernorms])
+        p.attn_ln_b = arr([m.bias for m in model.attention_layernorms])
+        p.in_proj_w = arr([m.in_proj_weight for m in model.attention_layers])
+        p.in_proj_b = arr([m.in_proj_bias for m in model.attention_layers])
+        p.out_proj_w = arr([m.out_proj.weight for m in model.attention_layers])
+        p.out_proj_b = arr([m.out_proj.bias for m in model.attention_layers])
+        p.ffn_ln_w = arr([m.weight for m in model.forward_layernorms])
+        p.ffn_ln_b = arr([m.bias for m in model.forward_layernorms])
+        p.ffn1_w = arr([m[0].weight for m in model.forward_layers])
+        p.ffn1_b = arr([m[0].bias for m in model.forward_layers])
+        p.ffn2_w = arr([m[3].weight for m in model.forward_layers])
+        p.ffn2_b = arr([m[3].bias for m in model.forward_layers])
+        p.last_ln_w = f(model.last_layernorm.weight)
+        p.last_ln_b = f(model.last_layernorm.bias)
+        self.p = p
+        self.device = model.item_emb.weight.device
+
+    def _f(self, t):
+        L.require_gpu(t)
+        t = L.as_f32(t.detach())
+        self.keep.append(t)
+        return t.data_ptr()
+
+    def _arr(self, ts):
+        a = (ctypes.c_void_p * max(1, len(ts)))(*[self._f(t) for t in ts])
+        self.keep.append(a)
+        return ctypes.cast(a, ctypes.c_void_p)
+
+    def workspace_bytes(self, B, n):
+        return L.lib().gr_sasrec_workspace_bytes(ctypes.byref(self.p), B, n)
+
+
+def _sas_ids(log_seqs, binding):
+    L.require_gpu(log_seqs)
+    if log_seqs.dim() != 2:
+        raise RuntimeError("SASRec expects log_seqs of shape [B, n]")
+    if log_seqs.device != binding.device:
+        raise RuntimeError(f"log_seqs on {log_seqs.device}, model on {binding.device}")
+    return log_seqs.to(torch.int64).contiguous()
+
+
+def _check_err(err):
+    if CHECK:
+        torch.cuda.synchronize(err.device)
+        if int(err.item()) != 0:
+            raise IndexError("index out of range in self (item id outside the embedding table)")
+
+
+def sasrec_forward(binding, log_seqs, last_only=False):
+    ids = _sas_ids(log_seqs, binding)
+    B, n = ids.shape
+    dev = ids.device
+    d = binding.p.d
+    out = torch.empty((B, d) if last_only else (B, n, d), dtype=torch.float32, device=dev)
+    nbytes = binding.workspace_bytes(B, n)
+    wsp = L.workspace(nbytes, dev)
+    err = torch.zeros(1, dtype=torch.int32, device=dev)
+    with torch.cuda.device(dev):
+        L.check(L.lib().gr_sasrec_forward_f32(ctypes.byref(binding.p), L.ptr(ids), B, n, L.ptr(out),
+                                              1 if last_only else 0, L.ptr(wsp), nbytes, L.ptr(err),
+                                              L.stream_of(dev)), "gr_sasrec_forward_f32")
+    _check_err(err)
+    return out
+
+
+def sasrec_predict(binding, log_seqs, out=None):
+    ids = _sas_ids(log_seqs, binding)
+    B, n = ids.shape
+    dev = ids.device
+    rows = binding.p.item_rows
+    logits = out if out is not None else torch.empty((B, rows), dtype=torch.float32, device=dev)
+    nbytes = binding.workspace_bytes(B, n)
+    wsp = L.workspace(nbytes, dev)
+    err = torch.zeros(1, dtype=torch.int32, device=dev)
+    with torch.cuda.device(dev):
+        L.check(L.lib().gr_sasrec_predict_f32(ctypes.byref(binding.p), L.ptr(ids), B, n,
+                                              L.ptr(logits), L.ptr(wsp), nbytes, L.ptr(err),
+                                              L.stream_of(dev)), "gr_sasrec_predict_f32")
+    _check_err(err)
+    return logits

@@ -1,0 +1,207 @@
+"""Drop-in RQ-VAE module whose encode path runs on the gfx950 kernels.
+
+Same constructor, submodule tree and ``state_dict`` keys as the reference
+(RQ-VAE/models/rqvae.py:10-53, rq.py:13-30, vq.py:9-27, layers.py:9-40), so reference checkpoints
+load unchanged and ``RQ-VAE/infer.py`` / ``generate_code.py`` can swap the import:
+
+    from models.rqvae import RQVAE            ->   from gr_amd.rqvae import RQVAE
+
+``get_indices(xs, use_sk=False)`` (rqvae.py:67-71) is one C-ABI call, ``gr_rq_encode_f32``.
+"""
+import torch
+from torch import nn
+from torch.nn.init import xavier_normal_
+
+from . import ops
+
+# Near-tie certificate (SURVEY §7 hard part 1).  The encoder output of any fp32 implementation
+# differs from the reference's CPU/MKL bits by |dz| <= Z_TAU |z| (per row; Z_TAU = 3x the largest
+# ratio measured on the golden fixtures).  That moves every level's residual by ~dz, so
+# d = |r - c|^2 moves by <= 2 sqrt(d) |dz|; the fp32 evaluation (|r|^2 + |c|^2) - 2 r.c rounds at
+# ~eps (|r| + |c|)^2 <= eps (|z| + sqrt(d))^2.  A level whose best/second-best gap is below the sum
+# of both bounds (for the two distances) can legitimately resolve either way; every other row
+# must match the reference bit for bit.
+Z_TAU = 2e-6
+D_EPS = 2.4e-7     # 4 x 2^-24
+
+
+def near_tie_bound(best, gap, znorm2):
+    """Upper bound of the fp32 disagreement on (second-best - best) at each level; tensors or
+    numpy arrays: best/gap [n, L], znorm2 = ||z||^2 [n]."""
+    zn = znorm2[:, None] ** 0.5
+    d2 = (best + gap).clip(0) ** 0.5 if hasattr(best, "clip") else (best + gap).clamp_min(0) ** 0.5
+    return 4 * d2 * Z_TAU * zn + 2 * D_EPS * (zn + d2) ** 2
+
+
+def near_tie_rows(best, gap, znorm2):
+    """Rows with at least one level whose argmin is within the fp32 certificate."""
+    return (gap <= near_tie_bound(best, gap, znorm2)).any(1)
+
+
+class MLPLayers(nn.Module):
+    """Module tree of RQ-VAE/models/layers.py:9-40 (Dropout, Linear, [BN], ReLU per layer; no
+    activation after the last Linear), xavier_normal_ weights and zero biases."""
+
+    def __init__(self, layers, dropout=0.0, activation="relu", bn=False):
+        super().__init__()
+        self.layers = layers
+        self.dropout = dropout
+        self.activation = activation
+        self.use_bn = bn
+        mods = []
+        last = len(layers) - 2
+        for idx, (i, o) in enumerate(zip(layers[:-1], layers[1:])):
+            mods.append(nn.Dropout(p=dropout))
+            mods.append(nn.Linear(i, o))
+            if bn and idx != last:
+                mods.append(nn.BatchNorm1d(num_features=o))
+            if activation is not None and str(activation).lower() != "none" and idx != last:
+                if str(activation).lower() != "relu":
+                    raise NotImplementedError("gr_amd encoder kernels implement ReLU only "
+                                              "(the activation RQ-VAE/main.py uses)")
+                mods.append(nn.ReLU())
+        self.mlp_layers = nn.Sequential(*mods)
+        self.apply(self._init_weights)
+
+    @staticmethod
+    def _init_weights(module):
+        if isinstance(module, nn.Linear):
+            xavier_normal_(module.weight.data)
+            if module.bias is not None:
+                module.bias.data.fill_(0.0)
+
+    def linears(self):
+        return [m for m in self.mlp_layers if isinstance(m, nn.Linear)]
+
+    def forward(self, x):
+        if self.use_bn:
+            raise NotImplementedError("gr_amd: BatchNorm encoders are not supported (bn=False in "
+                                      "RQ-VAE/main.py)")
+        lin = self.linears()
+        for i, m in enumerate(lin):
+            x = ops.linear(x, m.weight, m.bias, act="relu" if i < len(lin) - 1 else "none")
+        return x
+
+
+class VectorQuantizer(nn.Module):
+    """Parameter holder of RQ-VAE/models/vq.py:9-27 (``embedding`` [n_e, e_dim]).  Initialised
+    uniform(-1/n_e, 1/n_e), or zeros when ``kmeans_init`` (vq.py:21-27)."""
+
+    def __init__(self, n_e, e_dim, beta=0.25, kmeans_init=False, kmeans_iters=10,
+                 sk_epsilon=0.003, sk_iters=100):
+        super().__init__()
+        self.n_e = n_e
+        self.e_dim = e_dim
+        self.beta = beta
+        self.kmeans_init = kmeans_init
+        self.kmeans_iters = kmeans_iters
+        self.sk_epsilon = sk_epsilon
+        self.sk_iters = sk_iters
+        self.embedding = nn.Embedding(n_e, e_dim)
+        if not kmeans_init:
+            self.initted = True
+            self.embedding.weight.data.uniform_(-1.0 / n_e, 1.0 / n_e)
+        else:
+            self.initted = False
+            self.embedding.weight.data.zero_()
+
+    def get_codebook(self):
+        return self.embedding.weight
+
+    def get_codebook_entry(self, indices, shape=None):
+        z_q = self.embedding(indices)
+        return z_q.view(shape) if shape is not None else z_q
+
+
+class ResidualVectorQuantizer(nn.Module):
+    """Module tree of RQ-VAE/models/rq.py:13-30."""
+
+    def __init__(self, n_e_list, e_dim, sk_epsilons, beta=0.25, kmeans_init=False,
+                 kmeans_iters=100, sk_iters=100):
+        super().__init__()
+        self.n_e_list = n_e_list
+        self.e_dim = e_dim
+        self.num_quantizers = len(n_e_list)
+        self.beta = beta
+        self.kmeans_init = kmeans_init
+        self.kmeans_iters = kmeans_iters
+        self.sk_epsilons = sk_epsilons
+        self.sk_iters = sk_iters
+        self.vq_layers = nn.ModuleList([
+            VectorQuantizer(n_e, e_dim, beta=beta, kmeans_init=kmeans_init,
+                            kmeans_iters=kmeans_iters, sk_epsilon=eps, sk_iters=sk_iters)
+            for n_e, eps in zip(n_e_list, sk_epsilons)])
+
+    def get_codebook(self):
+        return torch.stack([q.get_codebook() for q in self.vq_layers])
+
+    def codebooks(self):
+        return [q.embedding.weight.detach() for q in self.vq_layers]
+
+
+class RQVAE(nn.Module):
+    """Drop-in for RQ-VAE/models/rqvae.py:RQVAE (same arguments, same ``state_dict``)."""
+
+    def __init__(self, in_dim=768, num_emb_list=None, e_dim=64, layers=None, dropout_prob=0.0,
+                 bn=False, loss_type="mse", quant_loss_weight=1.0, beta=0.25, kmeans_init=False,
+                 kmeans_iters=100, sk_epsilons=None, sk_iters=100):
+        super().__init__()
+        self.in_dim = in_dim
+        self.num_emb_list = num_emb_list
+        self.e_dim = e_dim
+        self.layers = layers
+        self.dropout_prob = dropout_prob
+        self.bn = bn
+        self.loss_type = loss_type
+        self.quant_loss_weight = quant_loss_weight
+        self.beta = beta
+        self.kmeans_init = kmeans_init
+        self.kmeans_iters = kmeans_iters
+        self.sk_epsilons = sk_epsilons
+        self.sk_iters = sk_iters
+        self.encode_layer_dims = [in_dim] + list(layers) + [e_dim]
+        self.encoder = MLPLayers(layers=self.encode_layer_dims, dropout=dropout_prob, bn=bn)
+        self.rq = ResidualVectorQuantizer(num_emb_list, e_dim, beta=beta, kmeans_init=kmeans_init,
+                                          kmeans_iters=kmeans_iters, sk_epsilons=sk_epsilons,
+                                          sk_iters=sk_iters)
+        self.decode_layer_dims = self.encode_layer_dims[::-1]
+        self.decoder = MLPLayers(layers=self.decode_layer_dims, dropout=dropout_prob, bn=bn)
+
+    def forward(self, x, use_sk=True):
+        """Training forward (rqvae.py:60-65) is outside the ported hot path."""
+        raise NotImplementedError("gr_amd RQVAE implements the encode path (get_indices); the "
+                                  "training forward with the decoder is out of scope")
+
+    def _check_encode(self, xs, use_sk):
+        if self.bn:
+            raise NotImplementedError("gr_amd: bn=True encoders are not supported")
+        if self.training and self.dropout_prob > 0:
+            raise RuntimeError("gr_amd RQVAE.get_indices runs the eval-mode encoder: call .eval() "
+                               "(dropout is active in train mode)")
+        if use_sk and any(q.sk_epsilon > 0 for q in self.rq.vq_layers):
+            raise NotImplementedError("gr_amd: use_sk=True with sk_epsilon > 0 (Sinkhorn collision "
+                                      "re-encode, vq.py:76-83) is not implemented yet")
+        if xs.dim() != 2 or xs.shape[1] != self.in_dim:
+            raise RuntimeError(f"get_indices expects [B, {self.in_dim}] inputs, got {tuple(xs.shape)}")
+
+    @torch.no_grad()
+    def get_indices(self, xs, use_sk=False):
+        """rqvae.py:67-71: ``[B, in_dim]`` fp32 -> ``[B, L]`` int64 semantic IDs (one C-ABI call)."""
+        self._check_encode(xs, use_sk)
+        lin = self.encoder.linears()
+        return ops.rq_encode(xs, [m.weight.detach() for m in lin], [m.bias.detach() for m in lin],
+                             self.rq.codebooks())
+
+    @torch.no_grad()
+    def get_indices_certified(self, xs):
+        """``get_indices`` plus a per-row near-tie flag: ``(idx [B, L], flags [B] bool)``.
+
+        A flagged row has a level whose best/second-best fp32 distance gap is within the rounding
+        certificate (``near_tie_bound``): it may legitimately differ from a CPU run of the reference.
+        Every unflagged row is the reference's answer."""
+        self._check_encode(xs, False)
+        lin = self.encoder.linears()
+        idx, best, gap, z = ops.rq_encode(xs, [m.weight.detach() for m in lin],
+                                          [m.bias.detach() for m in lin], self.rq.codebooks(),
+                                          with_gap=True, with_z=True)
+        return idx, near_tie_rows(best, gap, (z * z).sum(1))

@@ -1,0 +1,69 @@
+"""Drop-in SASRec module whose eval forward / full-catalog scoring run on the gfx950 kernels.
+
+Same constructor ``SASRec(item_num, params)``, submodule tree and ``state_dict`` keys as the
+reference (SASRec/model.py:6-47), so ``SASRec/evaluate.py`` runs unchanged after swapping
+
+    from model import SASRec                  ->   from gr_amd.sasrec import SASRec
+
+``predict(log_seqs)`` (model.py:98-108) is one C-ABI call (``gr_sasrec_predict_f32``) and returns a
+fresh writable ``[B, item_num+1]`` tensor (evaluate.py:27 writes column 0 in place).
+"""
+import torch
+import torch.nn as nn
+
+from . import ops
+
+
+class SASRec(nn.Module):
+    def __init__(self, item_num, params):
+        super().__init__()
+        self.item_num = item_num
+        self.dev = params["device"]
+        self.d = params["d"]
+        self.mlp_layer = params["mlp_layer"]
+        self.dropout = params["dropout"]
+        self.layernorm_eps = params["layernorm_eps"]
+        self.num_blocks = params["num_blocks"]
+        self.num_heads = params["num_heads"]
+        self.item_emb = nn.Embedding(item_num + 1, self.d, padding_idx=0)
+        self.pos_emb = nn.Embedding(params["max_len"], self.d)
+        # model.py:23-25: these projections are computed by the reference but never used; they are
+        # kept only so that checkpoints load with identical keys.
+        self.W_Q = nn.Linear(self.d, self.d)
+        self.W_K = nn.Linear(self.d, self.d)
+        self.W_V = nn.Linear(self.d, self.d)
+        self.attention_layernorms = nn.ModuleList(
+            [nn.LayerNorm(self.d, eps=self.layernorm_eps) for _ in range(self.num_blocks)])
+        self.attention_layers = nn.ModuleList(
+            [nn.MultiheadAttention(self.d, self.num_heads, self.dropout, batch_first=True)
+             for _ in range(self.num_blocks)])
+        self.forward_layernorms = nn.ModuleList(
+            [nn.LayerNorm(self.d, eps=self.layernorm_eps) for _ in range(self.num_blocks)])
+        self.forward_layers = nn.ModuleList([
+            nn.Sequential(nn.Linear(self.d, self.mlp_layer), nn.ReLU(), nn.Dropout(self.dropout),
+                          nn.Linear(self.mlp_layer, self.d), nn.Dropout(self.dropout))
+            for _ in range(self.num_blocks)])
+        self.last_layernorm = nn.LayerNorm(self.d, eps=self.layernorm_eps)
+
+    def _binding(self, log_seqs):
+        if self.training and self.dropout > 0:
+            raise RuntimeError("gr_amd SASRec kernels implement eval mode (dropout off): call .eval()")
+        n = log_seqs.shape[-1]
+        if n > self.pos_emb.weight.shape[0]:
+            raise IndexError(f"sequence length {n} exceeds max_len {self.pos_emb.weight.shape[0]}")
+        return ops.SasrecBinding(self)
+
+    @torch.no_grad()
+    def forward(self, log_seqs):
+        """model.py:49-96: ``[B, n]`` item ids -> ``[B, n, d]`` final hidden states (eval mode)."""
+        return ops.sasrec_forward(self._binding(log_seqs), log_seqs)
+
+    @torch.no_grad()
+    def last_hidden(self, log_seqs):
+        """``forward(log_seqs)[:, -1, :]`` (model.py:104) without materialising other positions."""
+        return ops.sasrec_forward(self._binding(log_seqs), log_seqs, last_only=True)
+
+    @torch.no_grad()
+    def predict(self, log_seqs):
+        """model.py:98-108: logits ``[B, item_num+1]`` = last hidden state x item table^T."""
+        return ops.sasrec_predict(self._binding(log_seqs), log_seqs)

@@ -1,0 +1,153 @@
+/*
+ * gr_amd.h — C ABI of the MI355X (gfx950) hot-path library libgr_amd.so.
+ *
+ * The reference (CatchMan1/AI-education-generative-recommendation) has no native layer: its hot
+ * paths are sequences of ATen ops inside two nn.Modules.  This ABI is what those modules' methods
+ * bottom out in here; each entry point names the reference code it replaces (paths relative to the
+ * reference root).  The Python drop-in modules (RQVAE, SASRec) bind these through ctypes.
+ *
+ * Conventions
+ *  - Every pointer argument named x/w/z/... is a DEVICE pointer to contiguous row-major data in the
+ *    layout PyTorch uses (nn.Linear weight = [out, in], nn.Embedding weight = [rows, dim]).
+ *    Arguments documented as "host array" are host arrays OF device pointers / sizes.
+ *  - All work is enqueued on `stream` (a hipStream_t; NULL = the default stream).  No call
+ *    synchronises, allocates or frees device memory: scratch comes from the caller's workspace
+ *    (size from the matching *_workspace_bytes query).  Calls are reentrant and stateless.
+ *  - Return 0 (GR_OK) on success, a negative GR_ERR_* code otherwise; gr_last_error() returns a
+ *    thread-local message for the last failure on the calling thread.  No exceptions cross the ABI.
+ *  - Floating point is fp32 throughout (f32-input MFMA, f32 accumulate); indices are int64.
+ */
+#ifndef GR_AMD_H
+#define GR_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GR_OK 0
+#define GR_ERR_ARG (-1)          /* bad shape / null pointer / misalignment                   */
+#define GR_ERR_UNSUPPORTED (-2)  /* shape outside what the kernels are built for               */
+#define GR_ERR_HIP (-3)          /* a HIP runtime error at launch                              */
+#define GR_ERR_WORKSPACE (-4)    /* workspace too small                                        */
+
+#define GR_MAX_LEVELS 8          /* RQ levels supported by one gr_rq_* call                    */
+#define GR_MAX_LINEAR 8          /* encoder Linear layers supported by gr_rq_encode_f32        */
+
+#define GR_ACT_NONE 0
+#define GR_ACT_RELU 1
+
+/* Library identification ("gr_amd <version> gfx950"). */
+const char* gr_version(void);
+/* Message of the last failed call on this thread ("" if none). */
+const char* gr_last_error(void);
+
+/* ------------------------------------------------------------------------------------------ */
+/* Dense layer  y[m, n] = act(x[m, k] . w[n, k]^T + bias[n]) (+ residual[m, n])
+ * Replaces nn.Linear -> F.linear -> addmm (+ nn.ReLU): RQ-VAE/models/layers.py:23-30 (encoder),
+ * SASRec/model.py:37-45 (FFN), torch functional.py:5785-5830 / :6600 (MHA in/out projections) and
+ * SASRec/model.py:107 (scoring: w = item table, bias = NULL).
+ * bias, residual may be NULL.  `residual` may alias `y` (in-place residual add).
+ * Requires k % 4 == 0 and 16-byte aligned x, w.  ldy / ldr are row strides (elements) of y / residual. */
+int gr_linear_f32(const float* x, int64_t m, int32_t k, const float* w, int32_t n,
+                  const float* bias, const float* residual, int64_t ldr, int32_t act,
+                  float* y, int64_t ldy, void* stream);
+
+/* ------------------------------------------------------------------------------------------ */
+/* RQ-VAE encode.
+ * Squared norms of codebook rows, cn[c] = sum_k C[c,k]^2 (the `torch.sum(self.embedding.weight**2,
+ * dim=1)` term of RQ-VAE/models/vq.py:72), computed once per codebook. */
+int gr_rq_codebook_norms_f32(const float* codebook, int32_t K, int32_t e, float* cn_out, void* stream);
+
+/* Residual quantization of latents z[n, e] over L levels (RQ-VAE/models/rq.py:39-56 with
+ * VectorQuantizer.forward(use_sk=False), vq.py:63-99):
+ *   d = (||r||^2 + ||C_l||^2) - 2 r.C_l^T ;  idx = first argmin ;  r <- r - (r + (C_l[idx] - r))
+ * K, codebooks, code_norms: host arrays of length L (code_norms from gr_rq_codebook_norms_f32).
+ * idx_out[n, L] int64 row-major (the stacked `indices` of rq.py:54).
+ * best_out[n, L], gap_out[n, L] (optional, may be NULL): the best fp32 distance and the gap to the
+ * second best per level — the near-tie certificate (a row whose gap is within fp32 rounding of
+ * the distances may legitimately differ from a CPU run of the reference).
+ * Supports e in {16, 32, 64}, 1 <= L <= GR_MAX_LEVELS, any K >= 1. */
+int gr_rq_quantize_f32(const float* z, int64_t n, int32_t e, int32_t L, const int32_t* K,
+                       const float* const* codebooks, const float* const* code_norms,
+                       int64_t* idx_out, float* best_out, float* gap_out, void* stream);
+
+/* Workspace for gr_rq_encode_f32 (bytes).  dims: host array of n_linear+1 layer widths
+ * (in_dim, hidden..., e_dim) = RQVAE.encode_layer_dims (RQ-VAE/models/rqvae.py:45). */
+size_t gr_rq_encode_workspace_bytes(int64_t n, int32_t n_linear, const int32_t* dims,
+                                    int32_t L, const int32_t* K);
+
+/* RQVAE.get_indices(xs, use_sk=False) (RQ-VAE/models/rqvae.py:67-71): encoder MLP
+ * (layers.py:42-43; ReLU after every Linear but the last) followed by gr_rq_quantize_f32.
+ * weights/biases: host arrays (n_linear) of device pointers; codebooks, K: host arrays (L).
+ * best_out, gap_out: as gr_rq_quantize_f32 (optional).
+ * z_out (optional, may be NULL): the encoder output [n, e]. */
+int gr_rq_encode_f32(const float* x, int64_t n, int32_t n_linear, const int32_t* dims,
+                     const float* const* weights, const float* const* biases, int32_t L,
+                     const int32_t* K, const float* const* codebooks, int64_t* idx_out,
+                     float* best_out, float* gap_out, float* z_out, void* workspace,
+                     size_t workspace_bytes, void* stream);
+
+/* ------------------------------------------------------------------------------------------ */
+/* SASRec.  Parameters of one model, as device pointers to the tensors of SASRec.state_dict()
+ * (SASRec/model.py:17-47).  Per-block fields are host arrays of length n_blocks.  The dead
+ * W_Q/W_K/W_V projections (model.py:23-25, 63-65) do not affect any output and are not passed. */
+typedef struct gr_sasrec_params {
+  int32_t d;            /* hidden size                          params['d']            */
+  int32_t n_blocks;     /* params['num_blocks']                                        */
+  int32_t n_heads;      /* params['num_heads'] (d % n_heads == 0)                      */
+  int32_t mlp;          /* params['mlp_layer']                                         */
+  int32_t max_len;      /* rows of pos_emb                      params['max_len']      */
+  float eps;            /* params['layernorm_eps']                                     */
+  int64_t item_rows;    /* item_num + 1 (row 0 = padding)                              */
+  const float* item_emb;          /* [item_rows, d]   item_emb.weight                  */
+  const float* pos_emb;           /* [max_len, d]     pos_emb.weight                   */
+  const float* const* attn_ln_w;  /* attention_layernorms.{i}.weight  [d]              */
+  const float* const* attn_ln_b;  /* attention_layernorms.{i}.bias    [d]              */
+  const float* const* in_proj_w;  /* attention_layers.{i}.in_proj_weight  [3d, d]      */
+  const float* const* in_proj_b;  /* attention_layers.{i}.in_proj_bias    [3d]         */
+  const float* const* out_proj_w; /* attention_layers.{i}.out_proj.weight [d, d]       */
+  const float* const* out_proj_b; /* attention_layers.{i}.out_proj.bias   [d]          */
+  const float* const* ffn_ln_w;   /* forward_layernorms.{i}.weight  [d]                */
+  const float* const* ffn_ln_b;   /* forward_layernorms.{i}.bias    [d]                */
+  const float* const* ffn1_w;     /* forward_layers.{i}.0.weight [mlp, d]              */
+  const float* const* ffn1_b;     /* forward_layers.{i}.0.bias   [mlp]                 */
+  const float* const* ffn2_w;     /* forward_layers.{i}.3.weight [d, mlp]              */
+  const float* const* ffn2_b;     /* forward_layers.{i}.3.bias   [d]                   */
+  const float* last_ln_w;         /* last_layernorm.weight [d]                         */
+  const float* last_ln_b;         /* last_layernorm.bias   [d]                         */
+} gr_sasrec_params;
+
+/* Workspace (bytes) for gr_sasrec_forward_f32 / gr_sasrec_predict_f32 at batch B, length n. */
+size_t gr_sasrec_workspace_bytes(const gr_sasrec_params* p, int64_t B, int32_t n);
+
+/* SASRec.forward(log_seqs) (SASRec/model.py:49-96) in eval mode: seqs[B, n] int64 ids ->
+ * out[B, n, d] (last_only = 0) or only the last position out[B, d] (last_only = 1, the
+ * `final_feats[:, -1, :]` of model.py:104).  err_flag (optional device int32, may be NULL) is set
+ * to 1 when an id is outside [0, item_rows) (such ids read the zero padding row instead). */
+int gr_sasrec_forward_f32(const gr_sasrec_params* p, const int64_t* seqs, int64_t B, int32_t n,
+                          float* out, int32_t last_only, void* workspace, size_t workspace_bytes,
+                          int32_t* err_flag, void* stream);
+
+/* SASRec.predict(log_seqs) (SASRec/model.py:98-108): logits[B, item_rows] = h_last . item_emb^T. */
+int gr_sasrec_predict_f32(const gr_sasrec_params* p, const int64_t* seqs, int64_t B, int32_t n,
+                          float* logits, void* workspace, size_t workspace_bytes,
+                          int32_t* err_flag, void* stream);
+
+/* Full-catalog (or catalog-shard) scoring logits[B, rows] = h[B, d] . table[rows, d]^T
+ * (SASRec/model.py:107).  ld = row stride of logits. */
+int gr_score_f32(const float* h, int64_t B, int32_t d, const float* table, int64_t rows,
+                 float* logits, int64_t ld, void* stream);
+
+/* Strict rank of each user's target (SASRec/evaluate.py:27-32) without mutating logits:
+ * with column 0 taken as -1e9 (when mask_col0), rank[b] = #{j : l[b,j] > l[b,t_b]} + 1.
+ * ld = row stride of logits, cols = number of columns. */
+int gr_rank_f32(const float* logits, int64_t B, int64_t cols, int64_t ld, const int64_t* targets,
+                int32_t mask_col0, int64_t* ranks_out, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GR_AMD_H */

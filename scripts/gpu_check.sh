@@ -1,0 +1,46 @@
+#!/bin/bash
+# One GPU-box session: GPU tests, smoke, bench, rocprofv3 kernel stats.  Every GPU step has its own
+# time limit; a fault / abort / timeout (exit codes other than 0 and 1) ends the script at once.
+# Usage: scripts/gpu_check.sh [tag] [steps...]   steps: tests smoke bench prof pmc (default: all but pmc)
+set -u
+ROOT=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
+TAG=${1:-run}; shift || true
+STEPS=${*:-tests smoke bench prof}
+OUT=$ROOT/gpurun_out/$TAG
+mkdir -p "$OUT"
+cd "$ROOT"
+export HSA_ENABLE_IPC_MODE_LEGACY=0
+
+step() {  # name, timeout, command...
+  local name=$1 t=$2; shift 2
+  echo "== $name ($(date +%T))"
+  timeout -k 10 "$t" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "== $name rc=$rc"
+  tail -n 30 "$OUT/$name.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "!! $name ended with $rc: stopping"; exit $rc; fi
+  return 0
+}
+
+for s in $STEPS; do
+  case $s in
+    tests) step pytest_gpu 1200 python -m pytest tests -m gpu -q -rs ;;
+    smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) step bench 900 python bench.py ;;
+    prof)
+      export TMPDIR=/tmp
+      cd /tmp
+      step rocprof 900 rocprofv3 --kernel-trace --stats --output-format csv \
+          -d "$OUT/rocprof" -o run -- python3 "$ROOT/bench.py" --steps 10 --warmup 3 --no-cpu-baseline
+      cd "$ROOT" ;;
+    pmc)  # HBM traffic: FETCH_SIZE and WRITE_SIZE in separate passes (MI355X_MICROARCH.md §HBM)
+      export TMPDIR=/tmp
+      for c in FETCH_SIZE WRITE_SIZE; do
+        cd /tmp
+        step pmc_$c 900 rocprofv3 --pmc $c --output-format csv \
+            -d "$OUT/pmc_$c" -o run -- python3 "$ROOT/bench.py" --steps 5 --warmup 2 --no-cpu-baseline
+        cd "$ROOT"
+      done ;;
+  esac
+done
+echo "== done"

@@ -1,0 +1,171 @@
+"""RQ-VAE encode on the GPU vs the reference's golden vectors and the CPU oracle.
+
+Parity bar (north_star): semantic IDs bit-exact.  fp32 distances computed with a different (but
+equally valid) accumulation order than the reference's CPU MKL run can only flip a row whose
+best/second-best distance gap is within fp32 rounding; such rows are reported and must be
+certified near-ties (gr_amd.rqvae.near_tie_rows on the reference's own distances), every other
+row must be identical.
+"""
+import numpy as np
+import pytest
+import torch
+
+import golden_lib as gl
+from oracle import rq_oracle
+
+pytestmark = pytest.mark.gpu
+RQ = ["rq_csv_3x8", "rq_syn_3x256", "rq_syn_4x1024", "rq_syn_randinit_3x256"]
+
+
+def build_model(meta, sd, dev):
+    from gr_amd import RQVAE
+    m = RQVAE(in_dim=meta["in_dim"], num_emb_list=[meta["K"]] * meta["L"], e_dim=meta["e_dim"],
+              layers=meta["layers"], dropout_prob=0.1, sk_epsilons=[0.01] * meta["L"])
+    missing, unexpected = m.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()}, strict=False)
+    assert not unexpected and all(k.startswith("decoder.") for k in missing)
+    return m.to(dev).eval()
+
+
+def near_tie_rows(out):
+    """The product's own certificate (gr_amd.rqvae.near_tie_rows) on the reference's fp32 distances."""
+    from gr_amd.rqvae import near_tie_rows as cert
+    return cert(out["dbest"], out["gap"], out["znorm"])
+
+
+@pytest.mark.parametrize("name", RQ)
+def test_get_indices_matches_reference(name, dev):
+    x, sd, out, meta = gl.rq_inputs(name)
+    m = build_model(meta, sd, dev)
+    xg = torch.from_numpy(x).to(dev)
+    idx = m.get_indices(xg).cpu().numpy()
+    ref = out["idx_full"]
+    assert idx.shape == ref.shape and idx.dtype == np.int64
+    diff = (idx != ref).any(1)
+    tie = near_tie_rows(out)
+    print(f"\n{name}: {diff.sum()}/{len(diff)} rows differ, {tie.sum()} certified near-ties")
+    assert not (diff & ~tie).any(), f"non-near-tie rows differ: {np.nonzero(diff & ~tie)[0][:10]}"
+    if meta["data_codebooks"]:
+        assert diff.sum() <= max(2, len(diff) // 1000)
+    # the product's own certificate (from the GPU's distances) flags every row that differs
+    idx2, flags = m.get_indices_certified(xg)
+    assert np.array_equal(idx2.cpu().numpy(), idx)
+    flags = flags.cpu().numpy()
+    print(f"{name}: product flags {flags.sum()} rows")
+    assert not (diff & ~flags).any()
+    # the batch-64 call pattern of RQ-VAE/infer.py:84-95 gives the same IDs as one batch
+    idx64 = torch.cat([m.get_indices(xg[i:i + 64]) for i in range(0, len(xg), 64)]).cpu().numpy()
+    assert np.array_equal(idx64, idx)
+
+
+def test_quantize_on_reference_latents(dev):
+    """Given the reference's own encoder output bits, only the distance reduction order differs."""
+    from gr_amd import ops
+    x, sd, out, meta = gl.rq_inputs("rq_syn_3x256")
+    cbs = [torch.from_numpy(sd[f"rq.vq_layers.{l}.embedding.weight"]).to(dev) for l in range(meta["L"])]
+    idx, best, gap = ops.rq_quantize(torch.from_numpy(out["z"]).to(dev), cbs, with_gap=True)
+    diff = (idx.cpu().numpy() != out["idx_full"]).any(1)
+    tie = near_tie_rows(out)
+    assert not (diff & ~tie).any()
+    assert diff.sum() <= 2
+    g = gap.cpu().numpy()
+    assert (g >= 0).all()
+    # the kernel's best distance and gap are the reference's fp32 values up to rounding
+    np.testing.assert_allclose(best.cpu().numpy(), out["dbest"], rtol=0, atol=1e-5 * out["znorm"].max())
+    np.testing.assert_allclose(g[~diff], out["gap"][~diff], rtol=0, atol=1e-5 * out["znorm"].max())
+
+
+def test_encoder_latents_close_to_reference(dev):
+    from gr_amd import ops
+    x, sd, out, meta = gl.rq_inputs("rq_syn_3x256")
+    m = build_model(meta, sd, dev)
+    lin = m.encoder.linears()
+    idx, z = ops.rq_encode(torch.from_numpy(x).to(dev), [l.weight for l in lin], [l.bias for l in lin],
+                           m.rq.codebooks(), with_z=True)
+    zr = out["z"]
+    err = np.abs(z.cpu().numpy() - zr).max() / np.abs(zr).max()
+    assert err < 1e-5, err
+    from gr_amd.rqvae import Z_TAU
+    row = np.linalg.norm(z.cpu().numpy().astype(np.float64) - zr, axis=1) / np.linalg.norm(zr, axis=1)
+    print(f"\nper-row |dz|/|z|: median {np.median(row):.3g}  p99.9 {np.quantile(row, 0.999):.3g}  "
+          f"max {row.max():.3g}  (Z_TAU {Z_TAU:g})")
+    assert row.max() <= Z_TAU
+    # the encoder alone through the drop-in module
+    z2 = m.encoder(torch.from_numpy(x).to(dev)).cpu().numpy()
+    assert np.array_equal(z2, z.cpu().numpy())
+
+
+def _random_case(n, e, Ks, layers, seed, dev):
+    g = torch.Generator().manual_seed(seed)
+    c = np.load(gl.os.path.join(gl.HERE, "csv_bert.npz"))
+    x, _ = gl.synth_items(n, c["mu"], c["sigma"], seed)
+    from gr_amd import RQVAE
+    torch.manual_seed(seed)
+    m = RQVAE(in_dim=768, num_emb_list=Ks, e_dim=e, layers=layers, sk_epsilons=[0.0] * len(Ks)).eval()
+    xt = torch.from_numpy(x)
+    with torch.no_grad():
+        for lin in m.encoder.linears():
+            lin.bias.copy_(0.01 * torch.randn(lin.bias.shape, generator=g))
+        lin = m.encoder.linears()
+        r = rq_oracle.mlp_encode(xt, [l.weight for l in lin], [l.bias for l in lin])
+        for q in m.rq.vq_layers:   # data-derived codebooks (possibly K > n: sample with replacement)
+            pick = torch.randint(0, n, (q.n_e,), generator=g)
+            q.embedding.weight.copy_(r[pick] + 0.01 * r.std() * torch.randn(q.embedding.weight.shape, generator=g))
+            xq, ind, _ = rq_oracle.vq_level(r, q.embedding.weight)
+            r = r - xq
+    ws = [l.weight.detach() for l in m.encoder.linears()]
+    bs = [l.bias.detach() for l in m.encoder.linears()]
+    cbs = m.rq.codebooks()
+    z = rq_oracle.mlp_encode(xt, ws, bs)
+    ref, residuals, gaps = rq_oracle.rq_quantize(z, cbs, return_detail=True)
+    dbest = torch.stack([rq_oracle.vq_level(r, c)[2].min(1).values for r, c in zip(residuals, cbs)], -1)
+    tie = near_tie_rows({"dbest": dbest.numpy(), "gap": gaps.numpy(), "znorm": (z ** 2).sum(1).numpy()})
+    return m.to(dev), xt.to(dev), ref.numpy(), tie
+
+
+@pytest.mark.parametrize("n,e,Ks,layers", [
+    (1, 32, [8, 8, 8], [256, 128]),          # single item
+    (129, 32, [256, 256, 256], [256, 128]),  # ragged last workgroup
+    (500, 16, [300, 7], [64]),               # K not a multiple of 32, K > LDS chunk, e = 16
+    (700, 64, [1024, 1, 33, 5], [512, 256, 128]),  # K = 1 (single code), e = 64, reference-default dims
+    (333, 32, [16] * 8, [128]),              # L = 8 levels (GR_MAX_LEVELS)
+])
+def test_edge_shapes_vs_oracle(n, e, Ks, layers, dev):
+    m, x, ref, tie = _random_case(n, e, Ks, layers, seed=n + e, dev=dev)
+    idx = m.get_indices(x).cpu().numpy()
+    diff = (idx != ref).any(1)
+    assert not (diff & ~tie).any()
+    assert (idx >= 0).all() and (idx < np.array(Ks)[None, :]).all()
+
+
+def test_empty_batch(dev):
+    x, sd, out, meta = gl.rq_inputs("rq_csv_3x8")
+    m = build_model(meta, sd, dev)
+    idx = m.get_indices(torch.zeros((0, 768), device=dev))
+    assert idx.shape == (0, 3) and idx.dtype == torch.int64
+
+
+def test_full_size_c2_properties(dev):
+    """Config 2 size (100k items, 3x256): determinism, range, agreement with the oracle on a sample,
+    and self-consistency of the two entry points (encode == quantize(encoder(x)))."""
+    from gr_amd import ops
+    m, _, _, _ = _random_case(64, 32, [256] * 3, [256, 128], seed=5, dev=dev)
+    c = np.load(gl.os.path.join(gl.HERE, "csv_bert.npz"))
+    x, _ = gl.synth_items(100_000, c["mu"], c["sigma"], 99)
+    xg = torch.from_numpy(x).to(dev)
+    a = m.get_indices(xg)
+    b = m.get_indices(xg)
+    assert torch.equal(a, b)
+    assert int(a.min()) >= 0 and int(a.max()) < 256
+    lin = m.encoder.linears()
+    z = m.encoder(xg)
+    assert torch.equal(ops.rq_quantize(z, m.rq.codebooks()), a)
+    sample = torch.arange(0, 100_000, 49)
+    ws = [l.weight.detach().cpu() for l in lin]
+    bs = [l.bias.detach().cpu() for l in lin]
+    cbs = [q.cpu() for q in m.rq.codebooks()]
+    zs = rq_oracle.mlp_encode(torch.from_numpy(x[sample.numpy()]), ws, bs)
+    ref, res, gaps = rq_oracle.rq_quantize(zs, cbs, return_detail=True)
+    dbest = torch.stack([rq_oracle.vq_level(r, c)[2].min(1).values for r, c in zip(res, cbs)], -1)
+    diff = (a[sample.to(dev)].cpu().numpy() != ref.numpy()).any(1)
+    tie = near_tie_rows({"dbest": dbest.numpy(), "gap": gaps.numpy(), "znorm": (zs ** 2).sum(1).numpy()})
+    assert not (diff & ~tie).any()
