@@ -39,6 +39,8 @@ class SasrecParams(ctypes.Structure):
 SIGNATURES = {
     "gr_version": (ctypes.c_char_p, []),
     "gr_last_error": (ctypes.c_char_p, []),
+    "gr_set_option": (ctypes.c_int, [ctypes.c_char_p, _i64]),
+    "gr_get_option": (_i64, [ctypes.c_char_p]),
     "gr_linear_f32": (ctypes.c_int, [_vp, _i64, _i32, _vp, _i32, _vp, _vp, _i64, _i32, _vp, _i64, _vp]),
     "gr_rq_codebook_norms_f32": (ctypes.c_int, [_vp, _i32, _i32, _vp, _vp]),
     "gr_rq_quantize_f32": (ctypes.c_int, [_vp, _i64, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
@@ -115,3 +117,12 @@ def as_f32(t):
     if t.dtype != torch.float32:
         raise TypeError(f"gr_amd kernels take float32 tensors, got {t.dtype}")
     return t.contiguous()
+
+
+def set_option(name, value):
+    """gr_set_option (include/gr_amd.h): process-wide path / tuning switches."""
+    check(lib().gr_set_option(name.encode(), int(value)), "gr_set_option")
+
+
+def get_option(name):
+    return int(lib().gr_get_option(name.encode()))

@@ -236,6 +236,13 @@ extern "C" int gr_rq_encode_f32(const float* x, int64_t n, int32_t n_linear, con
   if (!workspace || workspace_bytes < need)
     return fail(GR_ERR_WORKSPACE, "gr_rq_encode_f32: workspace too small (need " + std::to_string(need) + " bytes)");
   char* ws = reinterpret_cast<char*>(align_up(reinterpret_cast<uintptr_t>(workspace), 256));
+  if (n > 0 && (!x || !idx_out)) return fail(GR_ERR_ARG, "gr_rq_encode_f32: null x / idx_out");
+  if (option("rq_fused") == 1) {
+    rc = gr_rq_encode_fused_launch(x, n, n_linear, dims, weights, biases, L, K, codebooks,
+                                   reinterpret_cast<float*>(ws), idx_out, best_out, gap_out, z_out, st);
+    if (rc != GR_ERR_UNSUPPORTED) return rc;
+    clear_error();
+  }
   RQLevels lv{};
   for (int l = 0; l < L; ++l) {
     lv.cb[l] = codebooks[l];

@@ -43,6 +43,14 @@ extern "C" {
 const char* gr_version(void);
 /* Message of the last failed call on this thread ("" if none). */
 const char* gr_last_error(void);
+/* Process-wide path / tuning options (no reference counterpart; used for A/B measurement):
+ *   "rq_fused"      1 (default): gr_rq_encode_f32 runs the fused persistent kernel when the encoder
+ *                   shape is in -> 256 -> 128 -> 32; 0: the layer-wise path (gr_linear + quantize)
+ *   "rq_wg_per_cu"  1 (default) or 2 resident workgroups per CU for the fused kernel
+ * gr_set_option returns GR_ERR_ARG for an unknown name/value; gr_get_option returns -1 for an
+ * unknown name. */
+int gr_set_option(const char* name, int64_t value);
+int64_t gr_get_option(const char* name);
 
 /* ------------------------------------------------------------------------------------------ */
 /* Dense layer  y[m, n] = act(x[m, k] . w[n, k]^T + bias[n]) (+ residual[m, n])

@@ -17,6 +17,19 @@ pytestmark = pytest.mark.gpu
 RQ = ["rq_csv_3x8", "rq_syn_3x256", "rq_syn_4x1024", "rq_syn_randinit_3x256"]
 
 
+@pytest.fixture(params=[(1, 1), (1, 2), (0, 1)], ids=["fused", "fused-2wg", "layerwise"])
+def rq_path(request):
+    """Run a test through the fused persistent kernel (1 or 2 workgroups per CU) and through the
+    layer-wise path (gr_linear + gr_rq_quantize): both must meet the same bar."""
+    from gr_amd import _lib
+    fused, occ = request.param
+    _lib.set_option("rq_fused", fused)
+    _lib.set_option("rq_wg_per_cu", occ)
+    yield request.param
+    _lib.set_option("rq_fused", 1)
+    _lib.set_option("rq_wg_per_cu", 1)
+
+
 def build_model(meta, sd, dev):
     from gr_amd import RQVAE
     m = RQVAE(in_dim=meta["in_dim"], num_emb_list=[meta["K"]] * meta["L"], e_dim=meta["e_dim"],
@@ -33,7 +46,7 @@ def near_tie_rows(out):
 
 
 @pytest.mark.parametrize("name", RQ)
-def test_get_indices_matches_reference(name, dev):
+def test_get_indices_matches_reference(name, dev, rq_path):
     x, sd, out, meta = gl.rq_inputs(name)
     m = build_model(meta, sd, dev)
     xg = torch.from_numpy(x).to(dev)
@@ -74,7 +87,7 @@ def test_quantize_on_reference_latents(dev):
     np.testing.assert_allclose(g[~diff], out["gap"][~diff], rtol=0, atol=1e-5 * out["znorm"].max())
 
 
-def test_encoder_latents_close_to_reference(dev):
+def test_encoder_latents_close_to_reference(dev, rq_path):
     from gr_amd import ops
     x, sd, out, meta = gl.rq_inputs("rq_syn_3x256")
     m = build_model(meta, sd, dev)
@@ -89,9 +102,12 @@ def test_encoder_latents_close_to_reference(dev):
     print(f"\nper-row |dz|/|z|: median {np.median(row):.3g}  p99.9 {np.quantile(row, 0.999):.3g}  "
           f"max {row.max():.3g}  (Z_TAU {Z_TAU:g})")
     assert row.max() <= Z_TAU
-    # the encoder alone through the drop-in module
+    # the encoder alone through the drop-in module (layer-wise kernels)
     z2 = m.encoder(torch.from_numpy(x).to(dev)).cpu().numpy()
-    assert np.array_equal(z2, z.cpu().numpy())
+    if rq_path[0] == 0:
+        assert np.array_equal(z2, z.cpu().numpy())
+    else:
+        assert np.abs(z2 - zr).max() / np.abs(zr).max() < 1e-5
 
 
 def _random_case(n, e, Ks, layers, seed, dev):
@@ -125,11 +141,13 @@ def _random_case(n, e, Ks, layers, seed, dev):
 @pytest.mark.parametrize("n,e,Ks,layers", [
     (1, 32, [8, 8, 8], [256, 128]),          # single item
     (129, 32, [256, 256, 256], [256, 128]),  # ragged last workgroup
+    (1000, 32, [1024, 1, 33, 5], [256, 128]),  # fused kernel: K=1, K not a multiple of 32
+    (257, 32, [16] * 8, [256, 128]),         # fused kernel: L = 8
     (500, 16, [300, 7], [64]),               # K not a multiple of 32, K > LDS chunk, e = 16
     (700, 64, [1024, 1, 33, 5], [512, 256, 128]),  # K = 1 (single code), e = 64, reference-default dims
     (333, 32, [16] * 8, [128]),              # L = 8 levels (GR_MAX_LEVELS)
 ])
-def test_edge_shapes_vs_oracle(n, e, Ks, layers, dev):
+def test_edge_shapes_vs_oracle(n, e, Ks, layers, dev, rq_path):
     m, x, ref, tie = _random_case(n, e, Ks, layers, seed=n + e, dev=dev)
     idx = m.get_indices(x).cpu().numpy()
     diff = (idx != ref).any(1)
@@ -144,7 +162,7 @@ def test_empty_batch(dev):
     assert idx.shape == (0, 3) and idx.dtype == torch.int64
 
 
-def test_full_size_c2_properties(dev):
+def test_full_size_c2_properties(dev, rq_path):
     """Config 2 size (100k items, 3x256): determinism, range, agreement with the oracle on a sample,
     and self-consistency of the two entry points (encode == quantize(encoder(x)))."""
     from gr_amd import ops
@@ -157,8 +175,11 @@ def test_full_size_c2_properties(dev):
     assert torch.equal(a, b)
     assert int(a.min()) >= 0 and int(a.max()) < 256
     lin = m.encoder.linears()
-    z = m.encoder(xg)
-    assert torch.equal(ops.rq_quantize(z, m.rq.codebooks()), a)
+    idx_z, z = ops.rq_encode(xg, [l.weight for l in lin], [l.bias for l in lin], m.rq.codebooks(),
+                             with_z=True)
+    assert torch.equal(idx_z, a)
+    q = ops.rq_quantize(z, m.rq.codebooks())   # the standalone quantizer on the same latents
+    assert (q != a).any(1).sum().item() <= 10  # ||r||^2 order differs between the two kernels
     sample = torch.arange(0, 100_000, 49)
     ws = [l.weight.detach().cpu() for l in lin]
     bs = [l.bias.detach().cpu() for l in lin]
