@@ -10,14 +10,11 @@ static thread_local std::string g_last_error;
 void set_error(const std::string& msg) { g_last_error = msg; }
 void clear_error() { g_last_error.clear(); }
 
-// Options: rq_fused (1: fused persistent encode kernel when the shape allows, 0: layer-wise path),
-// rq_wg_per_cu (1 or 2 resident workgroups per CU for the fused kernel).
+// Options: rq_fused (1: fused persistent encode kernel when the shape allows, 0: layer-wise path).
 static std::atomic<int64_t> g_rq_fused{1};
-static std::atomic<int64_t> g_rq_wg_per_cu{1};
 
 int64_t option(const char* name) {
   if (!strcmp(name, "rq_fused")) return g_rq_fused.load();
-  if (!strcmp(name, "rq_wg_per_cu")) return g_rq_wg_per_cu.load();
   return -1;
 }
 }  // namespace gr
@@ -26,7 +23,6 @@ extern "C" int gr_set_option(const char* name, int64_t value) {
   gr::clear_error();
   if (!name) return gr::fail(GR_ERR_ARG, "gr_set_option: null name");
   if (!strcmp(name, "rq_fused") && (value == 0 || value == 1)) { gr::g_rq_fused = value; return GR_OK; }
-  if (!strcmp(name, "rq_wg_per_cu") && (value == 1 || value == 2)) { gr::g_rq_wg_per_cu = value; return GR_OK; }
   return gr::fail(GR_ERR_ARG, std::string("gr_set_option: unknown option or value: ") + name);
 }
 

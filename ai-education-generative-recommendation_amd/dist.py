@@ -1,0 +1,109 @@
+"""Multi-GPU layer: one process per GPU, ``torch.distributed`` (RCCL over xGMI) — SURVEY §8(e).
+
+The reference is single-device ("device": "cuda:0", RQ-VAE/main.py:34, SASRec/main.py:8).  Both
+hot paths are data-parallel:
+
+* RQ encode: items shard across ranks (``shard_range``); no collective on the data path.
+* SASRec C3: users shard across ranks; no collective.
+* SASRec C5 (1M-item catalog): the *catalog* shards.  ``sharded_rank_topk`` scores every user
+  against the local rows, then exchanges only per-user scalars and k candidates:
+    1. the owner of each target contributes the target's logit (zeros elsewhere) to an
+       all-reduce(sum) — the logit comes out of the same scoring kernel, so its bits equal the
+       full-catalog value and the strict '>' never counts the target itself (SURVEY §7 part 3);
+    2. local strict-'>' counts -> all-reduce(sum) -> global rank (SASRec/evaluate.py:27-32);
+    3. local top-k (value, global id) -> all-gather -> deterministic merge (value desc, id asc).
+  Messages are B*(8 + 8 + 12k) bytes per rank: latency-bound over xGMI, never bandwidth-bound.
+
+The scorer / counter / top-k callables default to the HIP kernels (``ops``); they are parameters
+only so that the collective logic can be exercised with the gloo backend on CPU in tests.
+"""
+import torch
+import torch.distributed as dist
+
+
+def shard_range(n, rank, world):
+    """Contiguous, balanced [lo, hi) slice of n units for ``rank`` of ``world``."""
+    return n * rank // world, n * (rank + 1) // world
+
+
+def all_gather_rows(t, group=None):
+    """Concatenate a [n_r, ...] tensor over ranks (n_r may differ by rank)."""
+    world = dist.get_world_size(group)
+    n = torch.tensor([t.shape[0]], dtype=torch.int64, device=t.device)
+    sizes = [torch.zeros_like(n) for _ in range(world)]
+    dist.all_gather(sizes, n, group=group)
+    sizes = [int(s.item()) for s in sizes]
+    m = max(sizes)
+    pad = torch.zeros((m - t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+    buf = torch.cat([t, pad])
+    out = [torch.empty_like(buf) for _ in range(world)]
+    dist.all_gather(out, buf, group=group)
+    return torch.cat([o[:s] for o, s in zip(out, sizes)])
+
+
+def merge_topk(vals, ids, k):
+    """Top-k of candidate lists [B, C] (values, global ids): value descending, ties to the lower id;
+    ids < 0 are padding."""
+    v = torch.where(ids < 0, torch.full_like(vals, float("-inf")), vals)
+    big = torch.iinfo(torch.int64).max
+    i = torch.where(ids < 0, torch.full_like(ids, big), ids)
+    o1 = torch.argsort(i, dim=1, descending=False, stable=True)                    # secondary key: id ascending
+    v1, i1 = v.gather(1, o1), i.gather(1, o1)
+    o2 = torch.argsort(v1, dim=1, descending=True, stable=True)  # primary key: value descending
+    vk, ik = v1.gather(1, o2)[:, :k], i1.gather(1, o2)[:, :k]
+    return vk, torch.where(ik == big, torch.full_like(ik, -1), ik)
+
+
+def _default_ops():
+    from . import ops
+    return ops.score, ops.count_gt, ops.topk
+
+
+@torch.no_grad()
+def sharded_rank_topk(h, table_shard, row_offset, targets, k=10, group=None, mask_row0=True,
+                      scorer=None, counter=None, topk_fn=None):
+    """Catalog-sharded scoring: every rank holds ``table_shard`` = rows [row_offset, ...) of the
+    item table and the same ``h`` [B, d] / global ``targets`` [B].  Returns (rank [B] int64,
+    top values [B, k], top ids [B, k]) identical on every rank."""
+    s_fn, c_fn, t_fn = _default_ops()
+    scorer, counter, topk_fn = scorer or s_fn, counter or c_fn, topk_fn or t_fn
+    logits = scorer(h, table_shard)
+    rows = logits.shape[1]
+    if mask_row0 and row_offset == 0 and rows > 0:
+        logits[:, 0] = -1e9                                  # evaluate.py:27
+    t = targets.reshape(-1).to(torch.int64)
+    own = (t >= row_offset) & (t < row_offset + rows)
+    local = torch.where(own, t - row_offset, torch.zeros_like(t))
+    ts = torch.where(own, logits.gather(1, local.unsqueeze(1)).squeeze(1), torch.zeros_like(t, dtype=logits.dtype))
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    if world > 1:
+        dist.all_reduce(ts, op=dist.ReduceOp.SUM, group=group)
+    cnt = counter(logits, ts)
+    if world > 1:
+        dist.all_reduce(cnt, op=dist.ReduceOp.SUM, group=group)
+    kk = min(k, rows) if rows > 0 else 0
+    if kk > 0:
+        v, i = topk_fn(logits, kk, row_offset)
+    else:
+        v = torch.empty((logits.shape[0], 0), dtype=logits.dtype, device=logits.device)
+        i = torch.empty((logits.shape[0], 0), dtype=torch.int64, device=logits.device)
+    if kk < k:
+        pad = k - kk
+        v = torch.cat([v, torch.full((v.shape[0], pad), float("-inf"), dtype=v.dtype, device=v.device)], 1)
+        i = torch.cat([i, torch.full((i.shape[0], pad), -1, dtype=i.dtype, device=i.device)], 1)
+    if world > 1:
+        vs = [torch.empty_like(v) for _ in range(world)]
+        is_ = [torch.empty_like(i) for _ in range(world)]
+        dist.all_gather(vs, v.contiguous(), group=group)
+        dist.all_gather(is_, i.contiguous(), group=group)
+        v, i = merge_topk(torch.cat(vs, 1), torch.cat(is_, 1), k)
+    return cnt + 1, v, i
+
+
+def hr_ndcg(ranks, top_k=10):
+    """HR@k / NDCG@k of SASRec/evaluate.py:36-47 (per-user float64 terms, then the mean)."""
+    import numpy as np
+    r = np.asarray(ranks.cpu() if torch.is_tensor(ranks) else ranks, dtype=np.int64)
+    hit = r <= top_k
+    ndcg = np.where(hit, 1.0 / np.log2(r.astype(np.float64) + 1.0), 0.0)
+    return float(np.mean(hit.astype(np.float64))), float(np.mean(ndcg))

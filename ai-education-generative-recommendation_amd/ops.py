@@ -64,6 +64,35 @@ def rank(logits, targets, mask_col0=True):
     return out
 
 
+def count_gt(logits, thresholds):
+    """``#{j : logits[b, j] > thresholds[b]}`` per row (strict, SASRec/evaluate.py:32)."""
+    L.require_gpu(logits, thresholds)
+    if logits.stride(1) != 1:
+        logits = logits.contiguous()
+    th = L.as_f32(thresholds.reshape(-1))
+    B, cols = logits.shape
+    out = torch.empty(B, dtype=torch.int64, device=logits.device)
+    with torch.cuda.device(logits.device):
+        L.check(L.lib().gr_count_gt_f32(L.ptr(logits), B, cols, logits.stride(0), L.ptr(th),
+                                        L.ptr(out), L.stream_of(logits.device)), "gr_count_gt_f32")
+    return out
+
+
+def topk(logits, k, id_offset=0):
+    """Per-row top-k: (values [B,k] descending, ids [B,k] = column + id_offset); ties -> lower id."""
+    L.require_gpu(logits)
+    if logits.stride(1) != 1:
+        logits = logits.contiguous()
+    B, cols = logits.shape
+    vals = torch.empty((B, k), dtype=torch.float32, device=logits.device)
+    ids = torch.empty((B, k), dtype=torch.int64, device=logits.device)
+    with torch.cuda.device(logits.device):
+        L.check(L.lib().gr_topk_f32(L.ptr(logits), B, cols, logits.stride(0), k, id_offset,
+                                    L.ptr(vals), L.ptr(ids), L.stream_of(logits.device)),
+                "gr_topk_f32")
+    return vals, ids
+
+
 def rq_quantize(z, codebooks, with_gap=False):
     """Residual quantization of latents (RQ-VAE/models/rq.py:39-56, use_sk=False).
 

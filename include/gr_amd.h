@@ -46,7 +46,6 @@ const char* gr_last_error(void);
 /* Process-wide path / tuning options (no reference counterpart; used for A/B measurement):
  *   "rq_fused"      1 (default): gr_rq_encode_f32 runs the fused persistent kernel when the encoder
  *                   shape is in -> 256 -> 128 -> 32; 0: the layer-wise path (gr_linear + quantize)
- *   "rq_wg_per_cu"  1 (default) or 2 resident workgroups per CU for the fused kernel
  * gr_set_option returns GR_ERR_ARG for an unknown name/value; gr_get_option returns -1 for an
  * unknown name. */
 int gr_set_option(const char* name, int64_t value);
@@ -154,6 +153,16 @@ int gr_score_f32(const float* h, int64_t B, int32_t d, const float* table, int64
  * ld = row stride of logits, cols = number of columns. */
 int gr_rank_f32(const float* logits, int64_t B, int64_t cols, int64_t ld, const int64_t* targets,
                 int32_t mask_col0, int64_t* ranks_out, void* stream);
+
+/* Catalog-shard helpers.  count: cnt[b] = #{j < cols : l[b,j] > thresholds[b]}
+ * (the strict '>' of SASRec/evaluate.py:32; summed over shards it gives rank - 1). */
+int gr_count_gt_f32(const float* logits, int64_t B, int64_t cols, int64_t ld,
+                    const float* thresholds, int64_t* counts_out, void* stream);
+
+/* Per-row top-k (k <= 64) of logits[B, cols]: values descending, ties to the lower column;
+ * ids_out = column + id_offset (the shard's first catalog row); -1 pads rows with < k entries. */
+int gr_topk_f32(const float* logits, int64_t B, int64_t cols, int64_t ld, int32_t k,
+                int64_t id_offset, float* vals_out, int64_t* ids_out, void* stream);
 
 #ifdef __cplusplus
 }

@@ -27,6 +27,7 @@ for s in $STEPS; do
     tests) step pytest_gpu 1200 python -m pytest tests -m gpu -q -rs ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 900 python bench.py ;;
+    ab) step ab_rq 600 python scripts/ab_rq.py && step ab_rq_4x1024 600 python scripts/ab_rq.py --L 4 --K 1024 ;;
     prof)
       export TMPDIR=/tmp
       cd /tmp
@@ -41,6 +42,17 @@ for s in $STEPS; do
             -d "$OUT/pmc_$c" -o run -- python3 "$ROOT/bench.py" --steps 5 --warmup 2 --no-cpu-baseline
         cd "$ROOT"
       done ;;
+    pmcrq)  # SQ counters of the RQ encode kernels (one variant per pass)
+      export TMPDIR=/tmp
+      cd /tmp
+      rocprofv3 -L > "$OUT/counters_list.txt" 2>&1 || true
+      for f in 1 0; do
+        step pmcrq_f$f 600 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES \
+            --output-format csv -d "$OUT/pmcrq_f$f" -o run -- python3 "$ROOT/scripts/prof_rq.py" --fused $f
+        step pmcrq2_f$f 600 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE TA_BUSY_avr \
+            --output-format csv -d "$OUT/pmcrq2_f$f" -o run -- python3 "$ROOT/scripts/prof_rq.py" --fused $f
+      done
+      cd "$ROOT" ;;
   esac
 done
 echo "== done"

@@ -1,0 +1,111 @@
+"""Multi-rank logic of the catalog-sharded SASRec scoring and the item/user sharding,
+exercised with the gloo backend on CPU (world sizes 2 and 3).  The HIP scorer/counter/top-k are
+replaced by CPU torch stand-ins with the same semantics; the GPU kernels themselves are covered
+by the -m gpu tests."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def cpu_score(h, table):
+    return h @ table.t()
+
+
+def cpu_count(logits, thr):
+    return (logits > thr.unsqueeze(1)).sum(1)
+
+
+def cpu_topk(logits, k, off):
+    cols = torch.arange(logits.shape[1]).expand_as(logits)
+    o1 = None
+    o2 = torch.argsort(logits, dim=1, descending=True, stable=True)
+    return logits.gather(1, o2)[:, :k], o2[:, :k] + off
+
+
+def _worker(rank, world, port, data, out):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import gr_amd.dist as D
+    h, table, targets, k = data
+    lo, hi = D.shard_range(table.shape[0], rank, world)
+    rk, v, i = D.sharded_rank_topk(h, table[lo:hi], lo, targets, k, scorer=cpu_score,
+                                   counter=cpu_count, topk_fn=cpu_topk)
+    # user-sharded transformer output gathered back (variable shard sizes)
+    ulo, uhi = D.shard_range(h.shape[0], rank, world)
+    hg = D.all_gather_rows(h[ulo:uhi])
+    out[rank] = (rk, v, i, hg)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _run(world, data):
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_worker, args=(world, _free_port(), data, out), nprocs=world, join=True)
+    return [out[r] for r in range(world)]
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_catalog_sharded_rank_topk_equals_full_catalog(world):
+    g = torch.Generator().manual_seed(world)
+    B, d, rows, k = 37, 16, 1001, 10
+    table = torch.randn(rows, d, generator=g)
+    table[0] = 0
+    # duplicated rows force exact ties across shards (tie -> lower global id)
+    table[700] = table[10]
+    h = torch.randn(B, d, generator=g)
+    targets = torch.randint(0, rows, (B,), generator=g)
+    targets[0] = 0          # padding target (evaluate.py: score -1e9)
+    targets[1] = 700
+    res = _run(world, (h, table, targets, k))
+    # single-device reference of evaluate.py:27-32 and a full-catalog top-k
+    lg = cpu_score(h, table)
+    lg[:, 0] = -1e9
+    ts = lg.gather(1, targets.unsqueeze(1))
+    ref_rank = (lg > ts).sum(1) + 1
+    ref_v, ref_i = cpu_topk(lg, k, 0)
+    for rk, v, i, hg in res:
+        assert torch.equal(rk, ref_rank)
+        assert torch.equal(i, ref_i) and torch.equal(v, ref_v)
+        assert torch.equal(hg, h)
+
+
+def test_merge_topk_tie_and_padding_rules():
+    from gr_amd.dist import merge_topk
+    vals = torch.tensor([[1.0, 3.0, 3.0, 2.0, 0.0]])
+    ids = torch.tensor([[5, 9, 4, 1, -1]])
+    v, i = merge_topk(vals, ids, 4)
+    assert i.tolist() == [[4, 9, 1, 5]] and v.tolist() == [[3.0, 3.0, 2.0, 1.0]]
+    v, i = merge_topk(vals, ids, 5)
+    assert i[0, 4].item() == -1
+
+
+def test_shard_range_partitions():
+    from gr_amd.dist import shard_range
+    for n in (0, 1, 7, 100_000, 10_000_000):
+        for w in (1, 2, 3, 8):
+            parts = [shard_range(n, r, w) for r in range(w)]
+            assert parts[0][0] == 0 and parts[-1][1] == n
+            assert all(parts[r][1] == parts[r + 1][0] for r in range(w - 1))
+            assert max(b - a for a, b in parts) - min(b - a for a, b in parts) <= 1
+
+
+def test_hr_ndcg_matches_reference_tail():
+    from gr_amd.dist import hr_ndcg
+    from oracle import metrics_oracle
+    ranks = np.array([1, 2, 10, 11, 500, 3, 1])
+    assert hr_ndcg(torch.from_numpy(ranks)) == metrics_oracle.hr_ndcg(ranks, 10)

@@ -146,3 +146,57 @@ def test_score_matches_linear_and_rank_consistency(dev):
     t = torch.randint(1, 5001, (33,), generator=g).to(dev)
     ranks = ops.rank(lg, t)
     assert (ranks >= 1).all()
+
+
+def test_count_gt_and_topk_kernels(dev):
+    """gr_count_gt_f32 / gr_topk_f32 vs torch on the same device logits (ties included)."""
+    from gr_amd import ops
+    g = torch.Generator().manual_seed(5)
+    lg = torch.randn(65, 3001, generator=g)
+    lg[:, 1234] = lg[:, 17]          # exact ties: the lower column must win
+    lg[3, :] = 1.0                   # a constant row
+    lgd = lg.to(dev)
+    thr = lg[torch.arange(65), torch.randint(0, 3001, (65,), generator=g)]
+    assert torch.equal(ops.count_gt(lgd, thr.to(dev)).cpu(), (lg > thr[:, None]).sum(1))
+    for k in (1, 10, 16, 40):
+        v, i = ops.topk(lgd, k, id_offset=1000)
+        o = torch.argsort(lg, dim=1, descending=True, stable=True)[:, :k]
+        assert torch.equal(i.cpu(), o + 1000)
+        assert torch.equal(v.cpu(), lg.gather(1, o))
+    v, i = ops.topk(lgd[:, :5], 10)
+    assert (i.cpu()[:, 5:] == -1).all()
+
+
+def test_sharded_scoring_on_one_gpu_equals_full_catalog(dev):
+    """Catalog-sharded rank/top-k simulated as 8 sequential shards on one GPU with the
+    HIP kernels: the strict-'>' counts summed over shards and the merged top-k equal the
+    full-catalog result bit for bit."""
+    from gr_amd import dist as D, ops
+    g = torch.Generator().manual_seed(9)
+    B, d, rows, k = 64, 128, 8001, 10
+    table = torch.randn(rows, d, generator=g).to(dev)
+    h = torch.randn(B, d, generator=g).to(dev)
+    t = torch.randint(1, rows, (B,), generator=g).to(dev)
+    full = ops.score(h, table)
+    ref_rank = ops.rank(full, t)
+    full[:, 0] = -1e9
+    ref_v, ref_i = ops.topk(full, k)
+    cnt = torch.zeros(B, dtype=torch.int64, device=dev)
+    ts = torch.zeros(B, device=dev)
+    vs, is_ = [], []
+    shards = [D.shard_range(rows, r, 8) for r in range(8)]
+    parts = [ops.score(h, table[lo:hi]) for lo, hi in shards]
+    for (lo, hi), lg in zip(shards, parts):
+        if lo == 0:
+            lg[:, 0] = -1e9
+        own = (t >= lo) & (t < hi)
+        ts += torch.where(own, lg.gather(1, (t - lo).clamp(0, hi - lo - 1).unsqueeze(1)).squeeze(1),
+                          torch.zeros_like(ts))
+    for (lo, hi), lg in zip(shards, parts):
+        cnt += ops.count_gt(lg, ts)
+        v, i = ops.topk(lg, k, lo)
+        vs.append(v)
+        is_.append(i)
+    v, i = D.merge_topk(torch.cat(vs, 1), torch.cat(is_, 1), k)
+    assert torch.equal(cnt + 1, ref_rank)
+    assert torch.equal(i, ref_i) and torch.equal(v, ref_v)
