@@ -53,11 +53,11 @@ __device__ __forceinline__ f32x16 mfma32(float a, float b, f32x16 c) {
 }  // namespace gr
 
 // Internal launchers shared between translation units (all enqueue on `stream`, no sync).
-int gr_rq_encode_fused_launch(const float* x, int64_t n, int32_t n_linear, const int32_t* dims,
-                              const float* const* weights, const float* const* biases, int32_t L,
-                              const int32_t* K, const float* const* codebooks, float* norms_ws,
-                              int64_t* idx_out, float* best_out, float* gap_out, float* z_out,
-                              hipStream_t st);
+int gr_rq_encoder_fused_launch(const float* x, int64_t n, int32_t n_linear, const int32_t* dims,
+                               const float* const* weights, const float* const* biases,
+                               float* z_out, hipStream_t st);
+int gr_score_launch(const float* h, int64_t B, int32_t d, const float* table, int64_t rows,
+                    float* logits, int64_t ld, hipStream_t st);
 int gr_linear_launch(const float* x, int64_t m, int32_t k, const float* w, int32_t n,
                      const float* bias, const float* residual, int64_t ldr, int32_t act, float* y,
                      int64_t ldy, hipStream_t stream);

@@ -187,7 +187,13 @@ extern "C" int gr_linear_f32(const float* x, int64_t m, int32_t k, const float* 
 extern "C" int gr_score_f32(const float* h, int64_t B, int32_t d, const float* table, int64_t rows,
                             float* logits, int64_t ld, void* stream) {
   gr::clear_error();
+  if (B < 0 || d <= 0 || rows < 0 || ld < rows) return gr::fail(GR_ERR_ARG, "gr_score_f32: bad shape");
+  if (B > 0 && rows > 0 && (!h || !table || !logits)) return gr::fail(GR_ERR_ARG, "gr_score_f32: null pointer");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int rc = gr_score_launch(h, B, d, table, rows, logits, ld, st);
+  if (rc != GR_ERR_UNSUPPORTED) return rc;
+  gr::clear_error();
   if (rows > 0x7fffffffLL) return gr::fail(GR_ERR_UNSUPPORTED, "gr_score_f32: rows >= 2^31");
   return gr_linear_launch(h, B, d, table, (int32_t)rows, nullptr, nullptr, 0, GR_ACT_NONE, logits,
-                          ld, reinterpret_cast<hipStream_t>(stream));
+                          ld, st);
 }

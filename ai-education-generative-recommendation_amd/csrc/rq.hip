@@ -1,28 +1,32 @@
 // RQ-VAE residual quantization on gfx950 (replaces RQ-VAE/models/rq.py:39-56 +
-// vq.py:63-99 with use_sk=False, and the encoder chain of RQVAE.get_indices, rqvae.py:67-71).
-//
-// One wave quantizes 32 items through all L levels with the residual kept in registers.  The
-// distance tile is an MFMA product with the CODES on the A side, so the accumulator of a lane
-// holds 16 codes of ONE item (its column): the argmin is a per-lane running minimum plus one
-// exchange between the two lane halves — no cross-lane reduction per code tile.  Codebooks are
-// staged through LDS in chunks of 256 codes (pitch e+4 floats: conflict-free ds_read_b128), code
-// norms precomputed once per codebook.
+// vq.py:63-99 with use_sk=False) and the encode entry point RQVAE.get_indices (rqvae.py:67-71).
 //
 //   d = (||r||^2 + ||c||^2) - 2 (r . c)         (vq.py:71-73, evaluated in this association order)
 //   idx = first index of the minimum            (torch.argmin, vq.py:75)
 //   r  <- r - (r + (C[idx] - r))                (vq.py:95 straight-through value, rq.py:47)
+//
+// Quantize kernel: 8-wave workgroups, each owning a contiguous balanced range of 32-item tiles
+// (spread over its waves; several workgroups per CU when the codebook chunk is small, so the
+// per-CU work is balanced).  Levels are processed in order: the level's codebook is staged into
+// LDS (rows XOR-swizzled by 16-byte slot, norms computed in-kernel with the same fma chain as
+// gr_rq_codebook_norms_f32), then every wave sweeps all code tiles for its item tiles with no
+// further barrier: MFMA distance tile with the CODES on the A side (lane = item, 16 codes per
+// lane), a per-lane running argmin (codes visited in increasing order, strict '<'), one exchange
+// between the lane halves, and the residual update from the LDS row of the winner.  Residuals stay
+// in registers across levels.  Codebooks larger than one LDS chunk are streamed in chunks.
 #include "gr_common.h"
 
 namespace gr {
 
 struct RQLevels {
   const float* cb[GR_MAX_LEVELS];
-  const float* cn[GR_MAX_LEVELS];
   int K[GR_MAX_LEVELS];
 };
 
-constexpr int RQ_CHUNK = 256;      // codes per LDS chunk
-constexpr int RQ_ITEMS_PER_WG = 128;
+constexpr int RQ_WAVES = 8;           // waves per workgroup
+// max item tiles per wave (residuals held in registers): fewer at e = 64 to stay spill-free
+template <int E>
+struct RQMaxT { static constexpr int value = E >= 64 ? 2 : 4; };
 
 __global__ __launch_bounds__(256) void rq_code_norms_kernel(const float* __restrict__ cb, int K,
                                                             int e, float* __restrict__ cn) {
@@ -34,115 +38,170 @@ __global__ __launch_bounds__(256) void rq_code_norms_kernel(const float* __restr
   cn[c] = s;
 }
 
+// Float offset of 16-byte slot q of row c of an LDS codebook image with E/4 slots per row.
 template <int E>
-__global__ __launch_bounds__(256) void rq_quantize_kernel(const float* __restrict__ z, int64_t n,
-                                                          int L, RQLevels lv,
-                                                          int64_t* __restrict__ idx_out,
-                                                          float* __restrict__ best_out,
-                                                          float* __restrict__ gap_out) {
+__device__ __forceinline__ int cb_off(int c, int q) {
+  constexpr int S = E / 4;
+  constexpr int M = S >= 8 ? 7 : S - 1;
+  return c * E + 4 * (q ^ (c & M));
+}
+
+template <int E, bool SECOND>
+__global__ __launch_bounds__(RQ_WAVES * 64) void rq_quantize_kernel(
+    const float* __restrict__ z, int64_t n, int L, RQLevels lv, int kch, int64_t* __restrict__ idx_out,
+    float* __restrict__ best_out, float* __restrict__ gap_out, int tiles) {
   static_assert(E % 8 == 0 && E <= 64, "e");
-  constexpr int P = E + 4;
-  constexpr int KC = E / 8;
-  __shared__ __attribute__((aligned(16))) float cbs[RQ_CHUNK * P];
-  __shared__ __attribute__((aligned(16))) float cns[RQ_CHUNK];
+  constexpr int HQ = E / 8;            // float4 per lane half
+  constexpr int RQ_MAXT = RQMaxT<E>::value;
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  float* cbs = sm;                     // [kch][E] swizzled
+  float* cns = sm + kch * E;           // [kch]
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r = lane & 31, h = lane >> 5;
+  const int t_begin = (int)((int64_t)blockIdx.x * tiles / gridDim.x);
+  const int t_end = (int)((int64_t)(blockIdx.x + 1) * tiles / gridDim.x);
+  const int my = (t_end - t_begin - w + RQ_WAVES - 1) / RQ_WAVES;  // tiles of this wave (<= MAXT)
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, h = lane >> 5;
-  const int64_t item = (int64_t)blockIdx.x * RQ_ITEMS_PER_WG + wave * 32 + r;
-  const bool valid = item < n;
-
-  // This lane's half of the residual: element s of res[kc] is k = 8kc + 4h + s.
-  f32x4 res[KC];
+  // residual of this lane's item for each of the wave's tiles: lane half h holds k in [hE/2, ...)
+  f32x4 res[RQ_MAXT][HQ];
 #pragma unroll
-  for (int kc = 0; kc < KC; ++kc)
-    res[kc] = valid ? *reinterpret_cast<const f32x4*>(z + item * E + kc * 8 + 4 * h)
-                    : f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int i = 0; i < RQ_MAXT; ++i) {
+    const int64_t item = (int64_t)(t_begin + w + i * RQ_WAVES) * 32 + r;
+    const bool ok = i < my && item < n;
+    const int64_t ic = ok ? item : 0;
+#pragma unroll
+    for (int j = 0; j < HQ; ++j) {
+      const f32x4 v = *reinterpret_cast<const f32x4*>(z + ic * E + (E / 2) * h + 4 * j);
+      res[i][j] = ok ? v : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  }
 
   for (int l = 0; l < L; ++l) {
-    // ||r||^2: each half sums its 16 (E/2) elements, the halves are then added (commutative, so
-    // both halves hold the same bits).
-    float part = 0.f;
-#pragma unroll
-    for (int kc = 0; kc < KC; ++kc)
-#pragma unroll
-      for (int s = 0; s < 4; ++s) part = fmaf(res[kc][s], res[kc][s], part);
-    const float rn = part + __shfl_xor(part, 32);
-
     const int K = lv.K[l];
     const float* cb = lv.cb[l];
-    const float* cn = lv.cn[l];
-    float best = __builtin_inff(), second = __builtin_inff();
-    int bi = 0x7fffffff;
-
-    for (int c0 = 0; c0 < K; c0 += RQ_CHUNK) {
-      const int cnt = min(RQ_CHUNK, K - c0);
-      __syncthreads();  // previous chunk fully consumed
-      for (int f = tid; f < RQ_CHUNK * (E / 4); f += 256) {
-        const int code = f / (E / 4), k4 = (f % (E / 4)) * 4;
-        f32x4 v = {0.f, 0.f, 0.f, 0.f};
-        if (code < cnt) v = *reinterpret_cast<const f32x4*>(cb + (int64_t)(c0 + code) * E + k4);
-        *reinterpret_cast<f32x4*>(cbs + code * P + k4) = v;
+    float rn[RQ_MAXT], best[RQ_MAXT], second[RQ_MAXT];
+    int bi[RQ_MAXT];
+#pragma unroll
+    for (int i = 0; i < RQ_MAXT; ++i) {
+      float part = 0.f;
+#pragma unroll
+      for (int j = 0; j < HQ; ++j)
+#pragma unroll
+        for (int s = 0; s < 4; ++s) part = fmaf(res[i][j][s], res[i][j][s], part);
+      rn[i] = part + __shfl_xor(part, 32);
+      best[i] = __builtin_inff();
+      second[i] = __builtin_inff();
+      bi[i] = 0x7fffffff;
+    }
+    const int c_last = ((K - 1) / kch) * kch;   // first code of the chunk left in LDS
+    for (int c0 = 0; c0 < K; c0 += kch) {
+      const int cnt = min(kch, K - c0);
+      __syncthreads();   // previous chunk / level fully consumed
+      for (int f = tid; f < cnt * (E / 4); f += RQ_WAVES * 64) {
+        const int c = f / (E / 4), q = f % (E / 4);
+        *reinterpret_cast<f32x4*>(cbs + cb_off<E>(c, q)) =
+            *reinterpret_cast<const f32x4*>(cb + (int64_t)(c0 + c) * E + 4 * q);
       }
-      for (int c = tid; c < RQ_CHUNK; c += 256) cns[c] = c < cnt ? cn[c0 + c] : __builtin_inff();
       __syncthreads();
-
-      const int ntiles = (cnt + 31) >> 5;
-      for (int t = 0; t < ntiles; ++t) {
-        f32x16 acc;
+      // code norms from the LDS image, same k-ordered fma chain as rq_code_norms_kernel
+      for (int c = tid; c < ((cnt + 31) & ~31); c += RQ_WAVES * 64) {
+        float s = __builtin_inff();    // codes past K can never win
+        if (c < cnt) {
+          s = 0.f;
 #pragma unroll
-        for (int v = 0; v < 16; ++v) acc[v] = 0.f;
-        const float* arow = cbs + (t * 32 + r) * P + 4 * h;
+          for (int q = 0; q < E / 4; ++q) {
+            const f32x4 v = *reinterpret_cast<const f32x4*>(cbs + cb_off<E>(c, q));
 #pragma unroll
-        for (int kc = 0; kc < KC; ++kc) {
-          const f32x4 a = *reinterpret_cast<const f32x4*>(arow + kc * 8);
-#pragma unroll
-          for (int s = 0; s < 4; ++s) acc = mfma32(a[s], res[kc][s], acc);
+            for (int i = 0; i < 4; ++i) s = fmaf(v[i], v[i], s);
+          }
         }
-        f32x4 c4[4];
+        cns[c] = s;
+      }
+      __syncthreads();
+      const int ct_n = (cnt + 31) >> 5;
+#pragma unroll 1
+      for (int ct = 0; ct < ct_n; ++ct) {
+        const int code = min(ct * 32 + r, cnt - 1);   // rows past cnt: any valid row (norm = inf)
+        f32x4 a[HQ];
 #pragma unroll
-        for (int g = 0; g < 4; ++g)
-          c4[g] = *reinterpret_cast<const f32x4*>(cns + t * 32 + 8 * g + 4 * h);
+        for (int j = 0; j < HQ; ++j)
+          a[j] = *reinterpret_cast<const f32x4*>(cbs + cb_off<E>(code, HQ * h + j));
+        float cnv[16];
 #pragma unroll
-        for (int v = 0; v < 16; ++v) {
-          const int code = c0 + t * 32 + (v & 3) + 8 * (v >> 2) + 4 * h;
-          const float dd = (rn + c4[v >> 2][v & 3]) - 2.f * acc[v];
-          if (dd < best || (dd == best && code < bi)) {
-            second = best;
-            best = dd;
-            bi = code;
-          } else if (dd < second) {
-            second = dd;
+        for (int g4 = 0; g4 < 4; ++g4) {
+          const f32x4 q = *reinterpret_cast<const f32x4*>(cns + ct * 32 + 8 * g4 + 4 * h);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) cnv[4 * g4 + i] = q[i];
+        }
+#pragma unroll
+        for (int i = 0; i < RQ_MAXT; ++i) {
+          if (i < my) {   // wave-uniform
+            f32x16 acc;
+#pragma unroll
+            for (int v = 0; v < 16; ++v) acc[v] = 0.f;
+#pragma unroll
+            for (int j = 0; j < HQ; ++j)
+#pragma unroll
+              for (int s = 0; s < 4; ++s) acc = mfma32(a[j][s], res[i][j][s], acc);
+#pragma unroll
+            for (int v = 0; v < 16; ++v) {
+              const int cd = c0 + ct * 32 + (v & 3) + 8 * (v >> 2) + 4 * h;
+              const float dd = (rn[i] + cnv[v]) - 2.f * acc[v];
+              if (SECOND) second[i] = fminf(second[i], fmaxf(best[i], dd));
+              bi[i] = dd < best[i] ? cd : bi[i];
+              best[i] = fminf(best[i], dd);
+            }
           }
         }
       }
     }
-    // Merge the two lane halves (codes 4h.. of every 8): lowest distance, then lowest index.
-    const float ob = __shfl_xor(best, 32), os = __shfl_xor(second, 32);
-    const int oi = __shfl_xor(bi, 32);
-    if (ob < best || (ob == best && oi < bi)) {
-      second = fminf(os, best);
-      best = ob;
-      bi = oi;
-    } else {
-      second = fminf(second, ob);
-    }
-    if (bi >= K) bi = 0;  // only when no finite distance exists (NaN/inf input): torch.argmin -> 0
-    if (valid && h == 0) {
-      idx_out[item * L + l] = (int64_t)bi;
-      if (best_out) best_out[item * L + l] = best;
-      if (gap_out) gap_out[item * L + l] = second - best;
-    }
-    // Straight-through residual update with the exact reference expression.
-    const float* crow = cb + (int64_t)bi * E + 4 * h;
+    // merge the two lane halves (lowest distance, then lowest index), write, update the residual
 #pragma unroll
-    for (int kc = 0; kc < KC; ++kc) {
-      const f32x4 c = *reinterpret_cast<const f32x4*>(crow + kc * 8);
+    for (int i = 0; i < RQ_MAXT; ++i) {
+      if (i < my) {
+        const float ob = __shfl_xor(best[i], 32), os = __shfl_xor(second[i], 32);
+        const int oi = __shfl_xor(bi[i], 32);
+        if (ob < best[i] || (ob == best[i] && oi < bi[i])) {
+          second[i] = fminf(os, best[i]);
+          best[i] = ob;
+          bi[i] = oi;
+        } else {
+          second[i] = fminf(second[i], ob);
+        }
+        int b = bi[i];
+        if (b >= K) b = 0;  // no finite distance (NaN/inf input): torch.argmin -> 0
+        const int64_t item = (int64_t)(t_begin + w + i * RQ_WAVES) * 32 + r;
+        if (h == 0 && item < n) {
+          idx_out[item * L + l] = (int64_t)b;
+          if (best_out) best_out[item * L + l] = best[i];
+          if (gap_out) gap_out[item * L + l] = second[i] - best[i];
+        }
+        const bool in_lds = b >= c_last;   // the winner's row is still in the LDS image
+        f32x4 c[HQ];
 #pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        const float xr = res[kc][s] + (c[s] - res[kc][s]);
-        res[kc][s] = res[kc][s] - xr;
+        for (int j = 0; j < HQ; ++j)
+          c[j] = in_lds ? *reinterpret_cast<const f32x4*>(cbs + cb_off<E>(b - c_last, HQ * h + j))
+                        : *reinterpret_cast<const f32x4*>(cb + (int64_t)b * E + (E / 2) * h + 4 * j);
+#pragma unroll
+        for (int j = 0; j < HQ; ++j)
+#pragma unroll
+          for (int s = 0; s < 4; ++s) {
+            const float xq = res[i][j][s] + (c[j][s] - res[i][j][s]);   // vq.py:95
+            res[i][j][s] = res[i][j][s] - xq;                           // rq.py:47
+          }
       }
     }
   }
+}
+
+static int cu_count() {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
+      cus = 256;
+  }
+  return cus;
 }
 
 static int launch_norms(const float* cb, int K, int e, float* cn, hipStream_t st) {
@@ -150,18 +209,43 @@ static int launch_norms(const float* cb, int K, int e, float* cn, hipStream_t st
   return check_launch("gr_rq_codebook_norms_f32");
 }
 
+template <int E>
+static int launch_quantize_e(const float* z, int64_t n, int L, const RQLevels& lv, int64_t* idx,
+                             float* best, float* gap, hipStream_t st) {
+  int kmax = 0;
+  for (int l = 0; l < L; ++l) kmax = lv.K[l] > kmax ? lv.K[l] : kmax;
+  const int kch_max = 1024 * 32 / E;                         // 128 KiB of codebook per chunk
+  const int kch = ((kmax < kch_max ? kmax : kch_max) + 31) & ~31;
+  const size_t lds = (size_t)kch * E * 4 + (size_t)kch * 4;
+  // persistent: one 8-wave workgroup per CU (2 waves per SIMD at this register budget), each with
+  // a contiguous balanced range of tiles; more workgroups only when a range would exceed the
+  // register-resident residuals (RQ_WAVES x MT tiles)
+  const int64_t tiles = (n + 31) / 32;
+  int64_t grid = (int64_t)cu_count();
+  constexpr int MT = RQMaxT<E>::value;
+  const int64_t min_grid = (tiles + RQ_WAVES * MT - 1) / (RQ_WAVES * MT);
+  if (grid < min_grid) grid = min_grid;
+  if (grid > tiles) grid = tiles;
+  if (grid > 0x7fffffffLL || tiles > 0x7fffffffLL) return fail(GR_ERR_UNSUPPORTED, "rq quantize: n too large");
+  auto k = (best || gap) ? rq_quantize_kernel<E, true> : rq_quantize_kernel<E, false>;
+  if (lds > 64 * 1024 &&
+      hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)lds) != hipSuccess)
+    return fail(GR_ERR_HIP, "rq quantize: cannot raise the LDS limit");
+  hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(RQ_WAVES * 64), lds, st, z, n, L, lv, kch, idx,
+                     best, gap, (int)tiles);
+  return check_launch("gr_rq_quantize_f32");
+}
+
 static int launch_quantize(const float* z, int64_t n, int e, int L, const RQLevels& lv,
                            int64_t* idx, float* best, float* gap, hipStream_t st) {
-  const int64_t nb = (n + RQ_ITEMS_PER_WG - 1) / RQ_ITEMS_PER_WG;
-  if (nb > 0x7fffffffLL) return fail(GR_ERR_UNSUPPORTED, "gr_rq_quantize_f32: n too large");
-  const dim3 grid((unsigned)nb), block(256);
+  if (n == 0) return GR_OK;
   switch (e) {
-    case 16: hipLaunchKernelGGL(rq_quantize_kernel<16>, grid, block, 0, st, z, n, L, lv, idx, best, gap); break;
-    case 32: hipLaunchKernelGGL(rq_quantize_kernel<32>, grid, block, 0, st, z, n, L, lv, idx, best, gap); break;
-    case 64: hipLaunchKernelGGL(rq_quantize_kernel<64>, grid, block, 0, st, z, n, L, lv, idx, best, gap); break;
+    case 16: return launch_quantize_e<16>(z, n, L, lv, idx, best, gap, st);
+    case 32: return launch_quantize_e<32>(z, n, L, lv, idx, best, gap, st);
+    case 64: return launch_quantize_e<64>(z, n, L, lv, idx, best, gap, st);
     default: return fail(GR_ERR_UNSUPPORTED, "gr_rq_quantize_f32: e_dim must be 16, 32 or 64");
   }
-  return check_launch("gr_rq_quantize_f32");
 }
 
 static int check_levels(int32_t e, int32_t L, const int32_t* K, const float* const* cbs) {
@@ -190,32 +274,29 @@ extern "C" int gr_rq_quantize_f32(const float* z, int64_t n, int32_t e, int32_t 
                                   void* stream) {
   using namespace gr;
   clear_error();
+  (void)code_norms;  // norms are recomputed in-kernel with the identical fma chain
   int rc = check_levels(e, L, K, codebooks);
   if (rc) return rc;
   if (n < 0) return fail(GR_ERR_ARG, "gr_rq_quantize_f32: n < 0");
   if (n == 0) return GR_OK;
-  if (!z || !idx_out || !code_norms || !aligned16(z)) return fail(GR_ERR_ARG, "gr_rq_quantize_f32: bad pointer");
+  if (!z || !idx_out || !aligned16(z)) return fail(GR_ERR_ARG, "gr_rq_quantize_f32: bad pointer");
   RQLevels lv{};
   for (int l = 0; l < L; ++l) {
     lv.cb[l] = codebooks[l];
-    lv.cn[l] = code_norms[l];
     lv.K[l] = K[l];
-    if (!lv.cn[l]) return fail(GR_ERR_ARG, "gr_rq_quantize_f32: null code norms");
   }
-  return launch_quantize(z, n, e, L, lv, idx_out, best_out, gap_out,
-                         reinterpret_cast<hipStream_t>(stream));
+  return launch_quantize(z, n, e, L, lv, idx_out, best_out, gap_out, reinterpret_cast<hipStream_t>(stream));
 }
 
-// Workspace layout: [code norms, sum_l K_l floats][two ping-pong activation buffers].
+// Workspace layout: two ping-pong activation buffers of the widest layer (the fused path uses the
+// first one for the encoder output z).
 extern "C" size_t gr_rq_encode_workspace_bytes(int64_t n, int32_t n_linear, const int32_t* dims,
                                                int32_t L, const int32_t* K) {
   if (n < 0 || n_linear < 1 || !dims || L < 1 || !K) return 0;
-  size_t norms = 0;
-  for (int l = 0; l < L; ++l) norms += gr::align_up((size_t)K[l] * 4, 256);
   int widest = 0;
   for (int i = 1; i <= n_linear; ++i) widest = dims[i] > widest ? dims[i] : widest;
   const size_t act = gr::align_up((size_t)n * widest * 4, 256);
-  return norms + 2 * act + 256;
+  return 2 * act + 256;
 }
 
 extern "C" int gr_rq_encode_f32(const float* x, int64_t n, int32_t n_linear, const int32_t* dims,
@@ -235,37 +316,37 @@ extern "C" int gr_rq_encode_f32(const float* x, int64_t n, int32_t n_linear, con
   const size_t need = gr_rq_encode_workspace_bytes(n, n_linear, dims, L, K);
   if (!workspace || workspace_bytes < need)
     return fail(GR_ERR_WORKSPACE, "gr_rq_encode_f32: workspace too small (need " + std::to_string(need) + " bytes)");
-  char* ws = reinterpret_cast<char*>(align_up(reinterpret_cast<uintptr_t>(workspace), 256));
-  if (n > 0 && (!x || !idx_out)) return fail(GR_ERR_ARG, "gr_rq_encode_f32: null x / idx_out");
-  if (option("rq_fused") == 1) {
-    rc = gr_rq_encode_fused_launch(x, n, n_linear, dims, weights, biases, L, K, codebooks,
-                                   reinterpret_cast<float*>(ws), idx_out, best_out, gap_out, z_out, st);
-    if (rc != GR_ERR_UNSUPPORTED) return rc;
-    clear_error();
-  }
-  RQLevels lv{};
-  for (int l = 0; l < L; ++l) {
-    lv.cb[l] = codebooks[l];
-    lv.K[l] = K[l];
-    lv.cn[l] = reinterpret_cast<float*>(ws);
-    rc = launch_norms(codebooks[l], K[l], e, reinterpret_cast<float*>(ws), st);
-    if (rc) return rc;
-    ws += align_up((size_t)K[l] * 4, 256);
-  }
   if (n == 0) return GR_OK;
   if (!x || !idx_out) return fail(GR_ERR_ARG, "gr_rq_encode_f32: null x / idx_out");
+  char* ws = reinterpret_cast<char*>(align_up(reinterpret_cast<uintptr_t>(workspace), 256));
   int widest = 0;
   for (int i = 1; i <= n_linear; ++i) widest = dims[i] > widest ? dims[i] : widest;
   float* buf[2] = {reinterpret_cast<float*>(ws),
                    reinterpret_cast<float*>(ws + align_up((size_t)n * widest * 4, 256))};
-  const float* cur = x;
-  for (int i = 0; i < n_linear; ++i) {
-    const bool last = i == n_linear - 1;
-    float* out = (last && z_out) ? z_out : buf[i & 1];
-    rc = gr_linear_launch(cur, n, dims[i], weights[i], dims[i + 1], biases ? biases[i] : nullptr,
-                          nullptr, 0, last ? GR_ACT_NONE : GR_ACT_RELU, out, dims[i + 1], st);
-    if (rc) return rc;
-    cur = out;
+  RQLevels lv{};
+  for (int l = 0; l < L; ++l) {
+    lv.cb[l] = codebooks[l];
+    lv.K[l] = K[l];
   }
-  return launch_quantize(cur, n, e, L, lv, idx_out, best_out, gap_out, st);
+  const float* z = nullptr;
+  if (option("rq_fused") == 1) {
+    float* zb = z_out ? z_out : buf[0];
+    rc = gr_rq_encoder_fused_launch(x, n, n_linear, dims, weights, biases, zb, st);
+    if (rc == GR_OK) z = zb;
+    else if (rc != GR_ERR_UNSUPPORTED) return rc;
+    else clear_error();
+  }
+  if (!z) {  // layer-wise path
+    const float* cur = x;
+    for (int i = 0; i < n_linear; ++i) {
+      const bool last = i == n_linear - 1;
+      float* out = (last && z_out) ? z_out : buf[i & 1];
+      rc = gr_linear_launch(cur, n, dims[i], weights[i], dims[i + 1], biases ? biases[i] : nullptr,
+                            nullptr, 0, last ? GR_ACT_NONE : GR_ACT_RELU, out, dims[i + 1], st);
+      if (rc) return rc;
+      cur = out;
+    }
+    z = cur;
+  }
+  return launch_quantize(z, n, e, L, lv, idx_out, best_out, gap_out, st);
 }

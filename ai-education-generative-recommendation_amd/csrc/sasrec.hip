@@ -338,6 +338,9 @@ extern "C" int gr_sasrec_predict_f32(const gr_sasrec_params* p, const int64_t* s
   if (rc) return rc;
   rc = run_layernorm(w.x, B, p->d, n, n - 1, p->last_ln_w, p->last_ln_b, p->eps, w.h, st);
   if (rc) return rc;
+  rc = gr_score_launch(w.h, B, p->d, p->item_emb, p->item_rows, logits, p->item_rows, st);
+  if (rc != GR_ERR_UNSUPPORTED) return rc;
+  clear_error();
   return gr_linear_launch(w.h, B, p->d, p->item_emb, (int32_t)p->item_rows, nullptr, nullptr, 0,
                           GR_ACT_NONE, logits, p->item_rows, st);
 }

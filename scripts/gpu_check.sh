@@ -27,6 +27,16 @@ for s in $STEPS; do
     tests) step pytest_gpu 1200 python -m pytest tests -m gpu -q -rs ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 900 python bench.py ;;
+    stamps) step stamps_rq 300 python scripts/stamps_rq.py 3 256 && step stamps_rq4 300 python scripts/stamps_rq.py 4 1024 ;;
+    ablate) GR_STAMPS_VARIANT=_now1 step stamps_now1 300 python scripts/stamps_rq.py 3 256 && \
+            GR_STAMPS_VARIANT=_nox step stamps_nox 300 python scripts/stamps_rq.py 3 256 && \
+            GR_STAMPS_VARIANT=_noxw step stamps_noxw 300 python scripts/stamps_rq.py 3 256 ;;
+    trace_rq)
+      export TMPDIR=/tmp
+      cd /tmp
+      step trace_rq 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace_rq" -o run -- python3 "$ROOT/scripts/prof_rq.py" --fused 1 && \
+      step trace_rq4 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace_rq4" -o run -- python3 "$ROOT/scripts/prof_rq.py" --fused 1 --L 4 --K 1024
+      cd "$ROOT" ;;
     ab) step ab_rq 600 python scripts/ab_rq.py && step ab_rq_4x1024 600 python scripts/ab_rq.py --L 4 --K 1024 ;;
     prof)
       export TMPDIR=/tmp

@@ -200,3 +200,18 @@ def test_sharded_scoring_on_one_gpu_equals_full_catalog(dev):
     v, i = D.merge_topk(torch.cat(vs, 1), torch.cat(is_, 1), k)
     assert torch.equal(cnt + 1, ref_rank)
     assert torch.equal(i, ref_i) and torch.equal(v, ref_v)
+
+
+@pytest.mark.parametrize("B,d,rows", [(1, 64, 33), (300, 64, 100001), (64, 128, 5000), (257, 32, 1000),
+                                      (5, 16, 77)])
+def test_score_kernel_vs_fp64(B, d, rows, dev):
+    """gr_score_f32 (dedicated streaming kernel for d in {32, 64, 128}, linear fallback otherwise)
+    against an fp64 reference, ragged B / rows included."""
+    from gr_amd import ops
+    g = torch.Generator().manual_seed(B + d + rows)
+    h = torch.randn(B, d, generator=g)
+    t = torch.randn(rows, d, generator=g)
+    y = ops.score(h.to(dev), t.to(dev)).cpu().double()
+    ref = h.double() @ t.double().t()
+    bound = (h.double().abs() @ t.double().abs().t()) * 4e-7 * d ** 0.5 + 1e-6
+    assert ((y - ref).abs() <= bound).all()
