@@ -89,5 +89,6 @@ if __name__ == "__main__":
         print(build_stamps(extra=["-DGR_ABL_NOW1"], suffix="_now1"))
         print(build_stamps(extra=["-DGR_ABL_NOX"], suffix="_nox"))
         print(build_stamps(extra=["-DGR_ABL_NOX", "-DGR_ABL_NOW1"], suffix="_noxw"))
+        print(build_stamps(extra=["-DGR_ABL_W1COAL"], suffix="_w1coal"))
     else:
         print(build(verbose=True))

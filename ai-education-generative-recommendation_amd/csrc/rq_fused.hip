@@ -17,13 +17,15 @@
 //
 // MFMA k-mapping: within a 32-deep k group, lane half h holds k = 16h + 4j + s (j, s = 0..3), so
 // every operand fragment is four 16-byte loads of one row (W rows from L2, x/h rows from LDS).
+#include <type_traits>
+
 #include "gr_common.h"
 
 // Diagnostic build only (-DGR_STAMPS, lib/libgr_amd_stamps.so): per-phase cycle totals of the
 // fused kernel, wave 0 of every workgroup, summed over workgroups and passes.  The product library
 // is built without it: no stamp executes in the real kernel.
 #ifdef GR_STAMPS
-__device__ unsigned long long g_rq_stamps[8];
+__device__ unsigned long long g_rq_stamps[10];
 #define GR_STAMP(var) \
   __builtin_amdgcn_sched_barrier(0); \
   asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(var)::"memory"); \
@@ -104,7 +106,10 @@ __device__ __forceinline__ void rq_fused_pass(FusedCtx<H1, H2>& cx, int tb) {
   const int w = cx.w, r = cx.r, h = cx.h;
   const int NC = cx.NC;
   const int next_tb = tb + NP;
-  const bool more = next_tb < cx.t_end;
+  // The later phases' operands (biases, W2/W3 fragments, their addresses) are loop-invariant
+  // across passes; hiding the base pointers behind an empty asm keeps the compiler from hoisting
+  // them out of the pass loop, where they would stay live (and take registers) through L1.
+  asm volatile("" : "+s"(cx.W2), "+s"(cx.W3), "+s"(cx.b1), "+s"(cx.b2), "+s"(cx.b3));
 #ifdef GR_STAMPS
   unsigned long long s0, s1, s2, s3, s4, s5;
 #endif
@@ -118,46 +123,62 @@ __device__ __forceinline__ void rq_fused_pass(FusedCtx<H1, H2>& cx, int tb) {
     for (int it = 0; it < NP; ++it)
 #pragma unroll
       for (int v = 0; v < 16; ++v) acc1[t][it][v] = 0.f;
-  // W1 is software-pipelined one 32-deep group ahead: the loads are issued at the top of the
-  // group body and pinned by a scheduling barrier in a non-unrolled loop, so the compiler cannot
-  // sink them next to their MFMAs.  The prefetch wraps to group 0 at the end of the pass (W1 is
-  // the same for every pass): only the first pass pays the latency.
-  const int NG = NC * (FXC / 32);
-#pragma unroll 1
-  for (int gi = 0; gi < NG; ++gi) {
-    const int g = gi & 1;              // group within the chunk (FXC == 64)
-    const int c = gi >> 1;
-    const int gn = (gi + 1 == NG) ? 0 : gi + 1;
+  // W1 is software-pipelined one 32-deep group ahead (the prefetch wraps to group 0 at the end of
+  // the pass: W1 is the same for every pass, only the first pass pays the latency).  The x chunk
+  // after the current one is loaded during group 0 and written to the other LDS buffer at the end
+  // of group 1 — unconditionally (clamped rows, zero-filled): after the last chunk of the last pass
+  // the staged image is simply never read.  Each group body is one basic block whose global loads,
+  // LDS reads and LDS writes are interleaved one-by-one with its MFMAs (sched_group_barrier): with
+  // one wave per SIMD a burst of memory instructions would stall MFMA issue behind the load queue.
+  // vmcnt retires in order, so the W1 loads are fenced ahead of the x loads: the next group's W1
+  // wait then never includes an HBM x load issued in the same group.
+  constexpr int M1 = 16 * NP * TW1;      // MFMAs per 32-deep group
+  const float* xsrc[C::XV];              // x rows of this pass / of the next pass (clamped)
+  const float* xnxt[C::XV];
+  bool xok_cur[C::XV], xok_nxt[C::XV];   // rows past n / past this workgroup's range -> zeros
+#pragma unroll
+  for (int i = 0; i < C::XV; ++i) {
+    const int f = cx.tid + 256 * i, it = f >> 4, k4 = (f & 15) * 4;
+    const int64_t a = (int64_t)tb * FT + it, b = (int64_t)next_tb * FT + it;
+    xsrc[i] = cx.x + (a < cx.n ? a : cx.n - 1) * cx.D0 + k4;
+    xnxt[i] = cx.x + (b < cx.n ? b : cx.n - 1) * cx.D0 + k4;
+    xok_cur[i] = a < cx.n;
+    xok_nxt[i] = b < cx.n && (next_tb + it / FT) < cx.t_end;
+  }
+  auto group = [&](auto gsel, int c) {
+    constexpr int g = decltype(gsel)::value;
+    const int gi = 2 * c + g;
+    const int gn = (gi + 1 == 2 * NC) ? 0 : gi + 1;
     f32x4 awn[TW1][4];
-#ifndef GR_ABL_NOW1
 #pragma unroll
     for (int t = 0; t < TW1; ++t)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) awn[t][j] = *reinterpret_cast<const f32x4*>(cx.w1row[t] + gn * 32 + 4 * j);
-#else  // ablation (diagnostic builds only): no W1 stream, fragments stay those of group 0
-    (void)gn;
-#pragma unroll
-    for (int t = 0; t < TW1; ++t)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) awn[t][j] = cx.awc[t][j];
+      for (int j = 0; j < 4; ++j) {
+#if defined(GR_ABL_W1COAL)  // ablation: the same W1 lines, 8 full lines per load (wrong data)
+        awn[t][j] = *reinterpret_cast<const f32x4*>(
+            cx.w1row[t] - (int64_t)r * cx.D0 - 16 * h +
+            (int64_t)(j * 8 + ((r + 32 * h) >> 3)) * cx.D0 + gn * 32 + ((r + 32 * h) & 7) * 4);
+#elif !defined(GR_ABL_NOW1)
+        awn[t][j] = *reinterpret_cast<const f32x4*>(cx.w1row[t] + gn * 32 + 4 * j);
+#else  // ablation (diagnostic builds only): no W1 stream
+        awn[t][j] = cx.awc[t][j];
 #endif
-    bool stage = (c + 1 < NC) || more;
-#ifdef GR_ABL_NOX  // ablation (diagnostic builds only): no x stream
-    stage = false;
-#endif
-    if (g == 0 && stage) {
-      const bool same = c + 1 < NC;
-      cx.gload_x(same ? tb : next_tb, same ? c + 1 : 0);
-    }
+      }
     const float* xb = cx.xs + cx.buf * PI * FXP + r * FXP + 16 * h + g * 32;
-    // all of the group's LDS fragments are issued before the scheduling barrier, so the MFMAs
-    // wait once per group (counted lgkmcnt) instead of once per ds_read
     f32x4 bx[NP][4];
 #pragma unroll
     for (int it = 0; it < NP; ++it)
 #pragma unroll
       for (int j = 0; j < 4; ++j) bx[it][j] = *reinterpret_cast<const f32x4*>(xb + it * FT * FXP + 4 * j);
-    __builtin_amdgcn_sched_barrier(0);
+#ifndef GR_ABL_NOX
+    if constexpr (g == 0) {
+      asm volatile("" ::: "memory");   // x loads stay behind the W1 loads and LDS reads
+      const bool same = c + 1 < NC;
+#pragma unroll
+      for (int i = 0; i < C::XV; ++i)
+        cx.xr[i] = *reinterpret_cast<const f32x4*>(same ? xsrc[i] + (c + 1) * FXC : xnxt[i]);
+    }
+#endif
 #pragma unroll
     for (int it = 0; it < NP; ++it)
 #pragma unroll
@@ -166,15 +187,65 @@ __device__ __forceinline__ void rq_fused_pass(FusedCtx<H1, H2>& cx, int tb) {
         for (int s = 0; s < 4; ++s)
 #pragma unroll
           for (int t = 0; t < TW1; ++t) acc1[t][it] = mfma32(cx.awc[t][j][s], bx[it][j][s], acc1[t][it]);
+    if constexpr (g == 1) {
+#ifndef GR_ABL_NOX
+      const bool same = c + 1 < NC;
+#pragma unroll
+      for (int i = 0; i < C::XV; ++i) {
+        const int f = cx.tid + 256 * i;
+        const bool ok = same ? xok_cur[i] : xok_nxt[i];
+        *reinterpret_cast<f32x4*>(cx.xs + (cx.buf ^ 1) * PI * FXP + (f >> 4) * FXP + (f & 15) * 4) =
+            ok ? cx.xr[i] : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+#endif
+    }
+    // schedule: item tile 0's LDS fragments, the W1 loads and item tile 1's LDS fragments one per
+    // MFMA, then (group 0) the x loads, (group 1) the x image write near the end
+#ifdef GR_ABL_NOX
+    constexpr int NX = 0, NDW = 0;
+#else
+    constexpr int NX = (g == 0) ? C::XV : 0, NDW = (g == 1) ? C::XV : 0;
+#endif
+#ifdef GR_ABL_NOW1
+    constexpr int NW = 0;
+#else
+    constexpr int NW = 4 * TW1;
+#endif
+    static_assert(NW + 4 * (NP - 1) + NX + 2 * NDW <= M1, "schedule");
+    __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+#pragma unroll
+    for (int i = 0; i < NW; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < 4 * (NP - 1); ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < NX; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+    }
+    __builtin_amdgcn_sched_group_barrier(0x008, M1 - NW - 4 * (NP - 1) - NX - 2 * NDW, 0);
+#pragma unroll
+    for (int i = 0; i < NDW; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
+    }
+    __builtin_amdgcn_sched_group_barrier(0x008, NDW, 0);
 #pragma unroll
     for (int t = 0; t < TW1; ++t)
 #pragma unroll
       for (int j = 0; j < 4; ++j) cx.awc[t][j] = awn[t][j];
-    if (g == 1) {
-      if (stage) cx.swrite_x(cx.buf ^ 1);
-      __syncthreads();
-      cx.buf ^= 1;
-    }
+  };
+#pragma unroll 1
+  for (int c = 0; c < NC; ++c) {
+    group(std::integral_constant<int, 0>{}, c);
+    group(std::integral_constant<int, 1>{}, c);
+    __syncthreads();
+    cx.buf ^= 1;
   }
   GR_STAMP(s1);
   // bias + ReLU, h1 -> LDS as [item][feature]
@@ -229,7 +300,6 @@ __device__ __forceinline__ void rq_fused_pass(FusedCtx<H1, H2>& cx, int tb) {
       for (int it = 0; it < NP; ++it)
 #pragma unroll
         for (int j = 0; j < 4; ++j) bx[it][j] = *reinterpret_cast<const f32x4*>(hb + it * FT * P1 + g * 32 + 4 * j);
-      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int it = 0; it < NP; ++it)
 #pragma unroll
@@ -238,6 +308,19 @@ __device__ __forceinline__ void rq_fused_pass(FusedCtx<H1, H2>& cx, int tb) {
           for (int s = 0; s < 4; ++s)
 #pragma unroll
             for (int t = 0; t < TW2; ++t) acc2[t][it] = mfma32(aw2[t][j][s], bx[it][j][s], acc2[t][it]);
+      // same interleave as L1: item tile 0's h1 fragments first, then one load per MFMA
+      __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+#pragma unroll
+      for (int i = 0; i < 4 * TW2; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+      }
+#pragma unroll
+      for (int i = 0; i < 4 * (NP - 1); ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, 16 * NP * TW2 - 4 * TW2 - 4 * (NP - 1), 0);
 #pragma unroll
       for (int t = 0; t < TW2; ++t)
 #pragma unroll
@@ -339,6 +422,11 @@ __global__ __launch_bounds__(256, 1) void rq_encoder_kernel(
   const int t_begin = (int)((int64_t)blockIdx.x * tiles / gridDim.x);
   const int t_end = (int)((int64_t)(blockIdx.x + 1) * tiles / gridDim.x);
   if (t_begin >= t_end) return;
+#ifdef GR_STAMPS
+  // whole-workgroup span in shader cycles and in the 100 MHz real-time clock (-> effective clock)
+  unsigned long long k0, r0;
+  asm volatile("s_memtime %0\n\ts_memrealtime %1\n\ts_waitcnt lgkmcnt(0)" : "=s"(k0), "=s"(r0)::"memory");
+#endif
   FusedCtx<H1, H2> cx;
   cx.x = x; cx.n = n; cx.D0 = D0; cx.NC = D0 / FXC; cx.t_end = t_end;
   cx.W2 = W2; cx.b1 = b1; cx.b2 = b2; cx.W3 = W3; cx.b3 = b3; cx.z_out = z_out;
@@ -352,7 +440,9 @@ __global__ __launch_bounds__(256, 1) void rq_encoder_kernel(
   for (int t = 0; t < C::TW1; ++t) {
     cx.w1row[t] = W1 + (int64_t)((cx.w * C::TW1 + t) * 32 + cx.r) * D0 + 16 * cx.h;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) cx.awc[t][j] = *reinterpret_cast<const f32x4*>(cx.w1row[t] + 4 * j);
+    for (int j = 0; j < 4; ++j) {
+      cx.awc[t][j] = *reinterpret_cast<const f32x4*>(cx.w1row[t] + 4 * j);
+    }
   }
   cx.buf = 0;
   cx.gload_x(t_begin, 0);
@@ -361,6 +451,16 @@ __global__ __launch_bounds__(256, 1) void rq_encoder_kernel(
   int tb = t_begin;
   for (; tb + FP <= t_end; tb += FP) rq_fused_pass<FP, H1, H2>(cx, tb);
   if (tb < t_end) rq_fused_pass<1, H1, H2>(cx, tb);   // FP == 2: at most one tile left
+#ifdef GR_STAMPS
+  unsigned long long k1, r1;
+  asm volatile("s_memtime %0\n\ts_memrealtime %1\n\ts_waitcnt lgkmcnt(0)" : "=s"(k1), "=s"(r1)::"memory");
+  if (threadIdx.x == 0) {
+    atomicAdd(&g_rq_stamps[6], k1 - k0);
+    atomicAdd(&g_rq_stamps[7], r1 - r0);
+    atomicMax(&g_rq_stamps[8], k1 - k0);
+    atomicMax(&g_rq_stamps[9], r1 - r0);
+  }
+#endif
 }
 
 }  // namespace gr
@@ -395,10 +495,10 @@ int gr_rq_encoder_fused_launch(const float* x, int64_t n, int32_t n_linear, cons
 
 #ifdef GR_STAMPS
 // Diagnostic: read and reset the per-phase totals (L1, h1 store, L2, L3, RQ, tiles).
-extern "C" int gr_debug_rq_stamps(unsigned long long* out8) {
-  if (hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_rq_stamps), 8 * sizeof(unsigned long long)) != hipSuccess)
+extern "C" int gr_debug_rq_stamps(unsigned long long* out10) {
+  if (hipMemcpyFromSymbol(out10, HIP_SYMBOL(g_rq_stamps), 10 * sizeof(unsigned long long)) != hipSuccess)
     return GR_ERR_HIP;
-  unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long z[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   return hipMemcpyToSymbol(HIP_SYMBOL(g_rq_stamps), z, sizeof(z)) == hipSuccess ? GR_OK : GR_ERR_HIP;
 }
 #endif

@@ -30,7 +30,8 @@ for s in $STEPS; do
     stamps) step stamps_rq 300 python scripts/stamps_rq.py 3 256 && step stamps_rq4 300 python scripts/stamps_rq.py 4 1024 ;;
     ablate) GR_STAMPS_VARIANT=_now1 step stamps_now1 300 python scripts/stamps_rq.py 3 256 && \
             GR_STAMPS_VARIANT=_nox step stamps_nox 300 python scripts/stamps_rq.py 3 256 && \
-            GR_STAMPS_VARIANT=_noxw step stamps_noxw 300 python scripts/stamps_rq.py 3 256 ;;
+            GR_STAMPS_VARIANT=_noxw step stamps_noxw 300 python scripts/stamps_rq.py 3 256 && \
+            GR_STAMPS_VARIANT=_w1coal step stamps_w1coal 300 python scripts/stamps_rq.py 3 256 ;;
     trace_rq)
       export TMPDIR=/tmp
       cd /tmp

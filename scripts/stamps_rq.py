@@ -22,11 +22,12 @@ m = synth.rqvae_model(L, K, dev)
 x = synth.items(100_000, 7, dev)
 lib = _lib.lib()
 lib.gr_debug_rq_stamps.argtypes = [ctypes.c_void_p]
-buf = (ctypes.c_ulonglong * 8)()
+buf = (ctypes.c_ulonglong * 10)()
 m.get_indices(x)
 torch.cuda.synchronize()
 lib.gr_debug_rq_stamps(buf)
-for _ in range(5):
+REPS = 5
+for _ in range(REPS):
     m.get_indices(x)
 torch.cuda.synchronize()
 lib.gr_debug_rq_stamps(buf)
@@ -37,3 +38,6 @@ mf = {"L1": 768, "h1 store": 0, "L2": 128, "L3": 16, "z store": 0}
 for i, nm in enumerate(names):
     per_tile = buf[i] / max(buf[5], 1)
     print(f"  {nm:9s} {100 * buf[i] / tot:5.1f} %   {per_tile:9.0f} cyc/tile   MFMA floor {mf[nm] * 64:7.0f}")
+if buf[7]:
+    print(f"  effective clock {100e6 * buf[6] / buf[7] / 1e9:.3f} GHz (sum over workgroups); "
+          f"longest workgroup {buf[8]} cyc = {buf[9] / 100:.1f} us (max over {REPS} launches)")
