@@ -12,9 +12,12 @@ void clear_error() { g_last_error.clear(); }
 
 // Options: rq_fused (1: fused persistent encode kernel when the shape allows, 0: layer-wise path).
 static std::atomic<int64_t> g_rq_fused{1};
+// sas_fused (1: register-resident fused SASRec forward when n <= 64 and d <= 64, 0: layer-wise).
+static std::atomic<int64_t> g_sas_fused{1};
 
 int64_t option(const char* name) {
   if (!strcmp(name, "rq_fused")) return g_rq_fused.load();
+  if (!strcmp(name, "sas_fused")) return g_sas_fused.load();
   return -1;
 }
 }  // namespace gr
@@ -23,6 +26,7 @@ extern "C" int gr_set_option(const char* name, int64_t value) {
   gr::clear_error();
   if (!name) return gr::fail(GR_ERR_ARG, "gr_set_option: null name");
   if (!strcmp(name, "rq_fused") && (value == 0 || value == 1)) { gr::g_rq_fused = value; return GR_OK; }
+  if (!strcmp(name, "sas_fused") && (value == 0 || value == 1)) { gr::g_sas_fused = value; return GR_OK; }
   return gr::fail(GR_ERR_ARG, std::string("gr_set_option: unknown option or value: ") + name);
 }
 

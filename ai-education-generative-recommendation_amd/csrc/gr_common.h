@@ -56,6 +56,8 @@ __device__ __forceinline__ f32x16 mfma32(float a, float b, f32x16 c) {
 int gr_rq_encoder_fused_launch(const float* x, int64_t n, int32_t n_linear, const int32_t* dims,
                                const float* const* weights, const float* const* biases,
                                float* z_out, hipStream_t st);
+int gr_sasrec_fused_launch(const gr_sasrec_params* p, const int64_t* seqs, int64_t B, int32_t n,
+                           float* out, int32_t last_only, int32_t* err, hipStream_t st);
 int gr_score_launch(const float* h, int64_t B, int32_t d, const float* table, int64_t rows,
                     float* logits, int64_t ld, hipStream_t st);
 int gr_linear_launch(const float* x, int64_t m, int32_t k, const float* w, int32_t n,

@@ -203,7 +203,21 @@ struct SasWs {
   float *x, *h, *qkv, *o, *f;
 };
 
+// The fused kernel (sasrec_fused.hip) covers n <= 64, d <= 64; it needs only the [B, d] last
+// hidden states.  Must agree with the shape test of gr_sasrec_fused_launch.
+static bool fused_ok(const gr_sasrec_params* p, int32_t n) {
+  return option("sas_fused") == 1 && n <= 64 && p->d <= 64 && p->d % 8 == 0 &&
+         (p->d / p->n_heads) % 8 == 0 && p->mlp <= 128 && p->n_blocks <= 8;
+}
+
 static size_t ws_layout(const gr_sasrec_params* p, int64_t B, int32_t n, char* base, SasWs* w) {
+  if (fused_ok(p, n)) {
+    if (w) {
+      *w = SasWs{};
+      w->h = reinterpret_cast<float*>(base);
+    }
+    return align_up((size_t)B * p->d * 4, 256) + 256;
+  }
   const size_t rows = (size_t)B * n;
   const size_t sx = align_up(rows * p->d * 4, 256);
   const size_t sq = align_up(rows * 3 * p->d * 4, 256);
@@ -317,6 +331,11 @@ extern "C" int gr_sasrec_forward_f32(const gr_sasrec_params* p, const int64_t* s
   if (rc) return rc;
   if (B == 0) return GR_OK;
   if (!seqs || !out) return fail(GR_ERR_ARG, "gr_sasrec_forward_f32: null seqs / out");
+  if (fused_ok(p, n)) {
+    rc = gr_sasrec_fused_launch(p, seqs, B, n, out, last_only, err_flag, st);
+    if (rc != GR_ERR_UNSUPPORTED) return rc;
+    return fail(GR_ERR_UNSUPPORTED, "sasrec: fused path refused a shape fused_ok accepted");
+  }
   rc = run_forward(p, seqs, B, n, w, err_flag, st);
   if (rc) return rc;
   if (last_only) return run_layernorm(w.x, B, p->d, n, n - 1, p->last_ln_w, p->last_ln_b, p->eps, out, st);
@@ -334,9 +353,15 @@ extern "C" int gr_sasrec_predict_f32(const gr_sasrec_params* p, const int64_t* s
   if (rc) return rc;
   if (B == 0) return GR_OK;
   if (!seqs || !logits) return fail(GR_ERR_ARG, "gr_sasrec_predict_f32: null seqs / logits");
-  rc = run_forward(p, seqs, B, n, w, err_flag, st);
-  if (rc) return rc;
-  rc = run_layernorm(w.x, B, p->d, n, n - 1, p->last_ln_w, p->last_ln_b, p->eps, w.h, st);
+  if (fused_ok(p, n)) {
+    rc = gr_sasrec_fused_launch(p, seqs, B, n, w.h, 1, err_flag, st);
+    if (rc == GR_ERR_UNSUPPORTED)
+      return fail(GR_ERR_UNSUPPORTED, "sasrec: fused path refused a shape fused_ok accepted");
+  } else {
+    rc = run_forward(p, seqs, B, n, w, err_flag, st);
+    if (rc) return rc;
+    rc = run_layernorm(w.x, B, p->d, n, n - 1, p->last_ln_w, p->last_ln_b, p->eps, w.h, st);
+  }
   if (rc) return rc;
   rc = gr_score_launch(w.h, B, p->d, p->item_emb, p->item_rows, logits, p->item_rows, st);
   if (rc != GR_ERR_UNSUPPORTED) return rc;

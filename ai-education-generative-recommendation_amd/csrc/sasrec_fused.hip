@@ -1,0 +1,431 @@
+// Fused SASRec eval forward for short sequences (n <= 64, d <= 64): one wavefront per sequence,
+// every activation of the whole network kept in registers as MFMA accumulators.
+// Replaces SASRec/model.py:49-104 (embedding gather, num_blocks x [LN, causal MHA, residual, LN,
+// FFN, residual], last LN) with the nn.MultiheadAttention math of torch functional.py:6576-6600.
+//
+// Orientation.  Activations are held TRANSPOSED: a 32x32 v_mfma_f32_32x32x2_f32 accumulator
+// holds [32 features] x [32 tokens]; lane (r, h) = (lane & 31, lane >> 5) owns token r of the tile
+// and features (v & 3) + 8 (v >> 2) + 4h in register v.  MFMA step s of a 32-deep reduction takes
+// feature (s & 3) + 8 (s >> 2) + 4h from lane half h — exactly register s of such an accumulator.
+// Hence the output of one layer is directly the B operand of the next (Y^T = W . X^T), with no
+// LDS round trip:
+//   X^T, H^T, Q^T, K^T, O^T, F^T  [feature x token]   (B operands; K^T also serves as the A operand
+//                                                     of S^T = K . Q^T: lane = key token)
+//   V                              [token x feature]   (computed as H . Wv^T, so that it is the A
+//                                                     operand of O^T = V^T . P^T: lane = feature)
+//   S^T / P^T                      [key x query]       (lane = query: softmax over registers + one
+//                                                     exchange between the lane halves)
+// Weights are read as A-operand fragments (row = lane & 31, 4 float4 per 32-deep group) straight
+// from L1/L2; every wave of a workgroup streams the same weights, so they stay cache-resident.
+//
+// Padding.  Tokens n..32*TT-1 and features d..32*DT-1 (mlp..32*MT-1) are computed but inert:
+// padded features are exactly zero throughout (zero weight rows/biases, LN weight 0), padded
+// tokens come after every real query and the causal mask removes them.  Per-step head masks let
+// any head width that is a multiple of 8 share the same code (H == 1 takes no mask).
+#include <cmath>
+
+#include "gr_common.h"
+
+namespace gr {
+
+namespace sf {
+
+__device__ __forceinline__ f32x4 ld4(const float* p, bool ok) {
+  return ok ? *reinterpret_cast<const f32x4*>(p) : f32x4{0.f, 0.f, 0.f, 0.f};
+}
+
+// A-operand fragment: row `row` of W[rows, ld] at the 32-deep input group `it`:
+// f[q] = W[row][32 it + 8q + 4h .. +3]  (zeros outside [0, nrow) x [0, ncol)).  EXACT: every
+// dimension is a multiple of 32, no masks are generated.
+template <bool EXACT>
+__device__ __forceinline__ void frag(f32x4 (&f)[4], const float* W, int ld, int row, int nrow,
+                                     int it, int ncol, int h) {
+  if (EXACT) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      f[q] = *reinterpret_cast<const f32x4*>(W + (int64_t)row * ld + 32 * it + 8 * q + 4 * h);
+    return;
+  }
+  const bool rok = row < nrow;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int c = 32 * it + 8 * q + 4 * h;
+    f[q] = ld4(W + (int64_t)(rok ? row : 0) * ld + c, rok && c < ncol);
+  }
+}
+
+// Per-lane vector of a [feature]-indexed parameter in accumulator order:
+// p[v] = P[32 ft + (v & 3) + 8 (v >> 2) + 4h]  (zero past n).
+template <bool EXACT>
+__device__ __forceinline__ f32x16 featvec(const float* P, int ft, int n, int h) {
+  f32x16 o;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int c = 32 * ft + 8 * q + 4 * h;
+    const f32x4 t = EXACT ? *reinterpret_cast<const f32x4*>(P + c) : ld4(P + c, c < n);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) o[4 * q + i] = t[i];
+  }
+  return o;
+}
+
+__device__ __forceinline__ float swap_halves(float v) { return __shfl_xor(v, 32); }
+
+// Y^T[OT][TT] = W . X^T + bias (rows >= nout / inputs >= nin are zero).
+template <bool EXACT, int OT, int IT, int TT>
+__device__ __forceinline__ void proj(f32x16 (&y)[OT][TT], const float* W, const float* bias,
+                                     int nout, int nin, const f32x16 (&x)[IT][TT], int r, int h) {
+#pragma unroll
+  for (int ot = 0; ot < OT; ++ot) {
+    // the bias initialises the accumulator: the result never passes through a VALU op, so it can
+    // stay in AGPRs and feed the next MFMA from there
+    const f32x16 b = featvec<EXACT>(bias, ot, nout, h);
+#pragma unroll
+    for (int tt = 0; tt < TT; ++tt) y[ot][tt] = b;
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+      f32x4 a[4];
+      frag<EXACT>(a, W, nin, 32 * ot + r, nout, it, nin, h);
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+#pragma unroll
+          for (int tt = 0; tt < TT; ++tt) y[ot][tt] = mfma32(a[q][e], x[it][tt][4 * q + e], y[ot][tt]);
+    }
+  }
+}
+
+// LayerNorm over the features of every token (F.layer_norm: biased variance, eps inside the sqrt).
+template <bool EXACT, int DT, int TT>
+__device__ __forceinline__ void layernorm(f32x16 (&y)[DT][TT], const f32x16 (&x)[DT][TT],
+                                          const float* w, const float* b, int d, float eps, int h) {
+  f32x16 wv[DT], bv[DT];
+#pragma unroll
+  for (int ft = 0; ft < DT; ++ft) {
+    wv[ft] = featvec<EXACT>(w, ft, d, h);
+    bv[ft] = featvec<EXACT>(b, ft, d, h);
+  }
+  const float inv_d = 1.0f / (float)d;
+#pragma unroll
+  for (int tt = 0; tt < TT; ++tt) {
+    float s = 0.f;
+#pragma unroll
+    for (int ft = 0; ft < DT; ++ft)
+#pragma unroll
+      for (int v = 0; v < 16; ++v) s += x[ft][tt][v];   // padded features are exactly 0
+    s += swap_halves(s);
+    const float mean = s * inv_d;
+    float var = 0.f;
+#pragma unroll
+    for (int ft = 0; ft < DT; ++ft)
+#pragma unroll
+      for (int v = 0; v < 16; ++v) {
+        const int f = 32 * ft + (v & 3) + 8 * (v >> 2) + 4 * h;
+        const float t = x[ft][tt][v] - mean;
+        var = (EXACT || f < d) ? fmaf(t, t, var) : var;
+      }
+    var += swap_halves(var);
+    const float rstd = 1.0f / sqrtf(var * inv_d + eps);
+#pragma unroll
+    for (int ft = 0; ft < DT; ++ft)
+#pragma unroll
+      for (int v = 0; v < 16; ++v) y[ft][tt][v] = (x[ft][tt][v] - mean) * rstd * wv[ft][v] + bv[ft][v];
+  }
+}
+
+}  // namespace sf
+
+struct SasBlockPtrs {
+  const float *ln_a_w, *ln_a_b, *w_in, *b_in, *w_o, *b_o, *ln_f_w, *ln_f_b, *w1, *b1, *w2, *b2;
+};
+constexpr int SF_MAX_BLOCKS = 8;
+struct SasFusedArgs {
+  SasBlockPtrs blk[SF_MAX_BLOCKS];
+  const float *item, *pos, *ln_w, *ln_b;
+  int64_t item_rows;
+  int nb, d, heads, mlp, n;
+  float eps, scale;
+};
+
+// out: last_only ? [B, d] (LN_last of position n-1) : [B, n, d].
+template <int TT, int DT, int MT, bool EXACT, bool SINGLE>
+__global__ __launch_bounds__(256) void sasrec_fused_kernel(const SasFusedArgs a,
+                                                           const int64_t* __restrict__ seqs,
+                                                           int64_t B, float* __restrict__ out,
+                                                           int last_only, int32_t* err) {
+  using namespace sf;
+  const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
+  const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= B) return;   // whole wave; the kernel has no barrier
+  const int d = a.d, n = a.n, mlp = a.mlp;
+  const int hd = d / a.heads;
+  __shared__ __attribute__((aligned(16))) float sm[4 * DT * TT * 16 * 64];
+  float* xs = sm + (threadIdx.x >> 6) * (DT * TT * 16 * 64);
+
+  // ---- embedding gather: X^T = (M[s] + P[pos])^T  (model.py:58-60)
+  f32x16 X[DT][TT];
+#pragma unroll
+  for (int tt = 0; tt < TT; ++tt) {
+    const int p = 32 * tt + r;
+    int64_t id = 0;
+    if (p < n) {
+      id = seqs[b * n + p];
+      if (id < 0 || id >= a.item_rows) {   // torch raises IndexError; flag and read the pad row
+        if (err) *err = 1;
+        id = 0;
+      }
+    }
+#pragma unroll
+    for (int ft = 0; ft < DT; ++ft)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int c = 32 * ft + 8 * q + 4 * h;
+        const bool ok = p < n && (EXACT || c < d);
+        const f32x4 e = ld4(a.item + id * d + c, ok);
+        const f32x4 ps = ld4(a.pos + (int64_t)(p < n ? p : 0) * d + c, ok);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) X[ft][tt][4 * q + i] = e[i] + ps[i];
+      }
+  }
+
+  // Per-block parameters are read straight from the kernarg segment with the runtime block index
+  // (a by-value array indexed dynamically would be copied into SGPRs / spilled).
+#if defined(__HIP_DEVICE_COMPILE__)
+  typedef const __attribute__((address_space(4))) SasFusedArgs* KargPtr;
+  const KargPtr ka = (KargPtr)__builtin_amdgcn_kernarg_segment_ptr();
+#else
+  const SasFusedArgs* ka = &a;   // host pass of the single-source compile: never executed
+#endif
+#pragma unroll 1
+  for (int blk = 0; blk < a.nb; ++blk) {
+    const SasBlockPtrs P = ka->blk[blk];
+    // ---- attention sub-block: X += out_proj(MHA(LN_a(X)))  (model.py:80-84)
+    {
+      f32x16 Hn[DT][TT];
+      layernorm<EXACT, DT, TT>(Hn, X, P.ln_a_w, P.ln_a_b, d, a.eps, h);
+      // X is parked in this wave's LDS slice during attention (registers are the limit); the
+      // empty asm keeps the compiler from forwarding the stored values instead of reloading
+#pragma unroll
+      for (int ft = 0; ft < DT; ++ft)
+#pragma unroll
+        for (int tt = 0; tt < TT; ++tt)
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            *reinterpret_cast<f32x4*>(xs + ((ft * TT + tt) * 4 + q) * 256 + lane * 4) =
+                f32x4{X[ft][tt][4 * q], X[ft][tt][4 * q + 1], X[ft][tt][4 * q + 2], X[ft][tt][4 * q + 3]};
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      f32x16 K[DT][TT], V[TT][DT];
+      proj<EXACT, DT, DT, TT>(K, P.w_in + (int64_t)d * d, P.b_in + d, d, d, Hn, r, h);
+      __builtin_amdgcn_sched_barrier(0);
+      // V = H . Wv^T + bv: [token x feature], H^T's registers as the A operand
+#pragma unroll
+      for (int ft = 0; ft < DT; ++ft) {
+        const int f = 32 * ft + r;
+        const float bv = (EXACT || f < d) ? P.b_in[2 * d + f] : 0.f;
+#pragma unroll
+        for (int tt = 0; tt < TT; ++tt)
+#pragma unroll
+          for (int v = 0; v < 16; ++v) V[tt][ft][v] = bv;
+#pragma unroll
+        for (int it = 0; it < DT; ++it) {
+          f32x4 w[4];
+          frag<EXACT>(w, P.w_in + 2 * (int64_t)d * d, d, 32 * ft + r, d, it, d, h);
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+#pragma unroll
+              for (int tt = 0; tt < TT; ++tt) V[tt][ft] = mfma32(Hn[it][tt][4 * q + e], w[q][e], V[tt][ft]);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      const bool narrow = !SINGLE && hd < 32;   // heads narrower than a feature tile: step masks
+      // one query tile at a time: Q^T tile, per-head S^T -> P^T -> O^T, out_proj, residual
+#pragma unroll
+      for (int qt = 0; qt < TT; ++qt) {
+        f32x16 Q[DT][1];
+        {
+          f32x16 Hq[DT][1];
+#pragma unroll
+          for (int it = 0; it < DT; ++it) Hq[it][0] = Hn[it][qt];
+          proj<EXACT, DT, DT, 1>(Q, P.w_in, P.b_in, d, d, Hq, r, h);
+        }
+#pragma unroll
+        for (int ft = 0; ft < DT; ++ft) Q[ft][0] *= a.scale;   // q * sqrt(1/hd) (functional.py:6578)
+        __builtin_amdgcn_sched_barrier(0);
+        f32x16 O[DT][1];
+#pragma unroll
+        for (int ft = 0; ft < DT; ++ft)
+#pragma unroll
+          for (int v = 0; v < 16; ++v) O[ft][0][v] = 0.f;
+#pragma unroll 1
+        for (int hh = 0; hh < (SINGLE ? 1 : a.heads); ++hh) {
+          const int f_lo = SINGLE ? 0 : hh * hd, f_hi = SINGLE ? 32 * DT : f_lo + hd;
+          f32x16 S[TT];
+#pragma unroll
+          for (int kt = 0; kt <= qt; ++kt) {
+#pragma unroll
+            for (int v = 0; v < 16; ++v) S[kt][v] = 0.f;
+#pragma unroll
+            for (int it = 0; it < DT; ++it) {
+              if (32 * it >= f_hi || 32 * it + 32 <= f_lo) continue;   // tile outside the head
+#pragma unroll
+              for (int s = 0; s < 16; ++s) {
+                const int f = 32 * it + (s & 3) + 8 * (s >> 2);   // + 4h: same 8-group, same head
+                const float qv = (!narrow || (f >= f_lo && f < f_hi)) ? Q[it][0][s] : 0.f;
+                S[kt] = mfma32(K[it][kt][s], qv, S[kt]);
+              }
+            }
+          }
+          // causal mask (key > query -> -inf), softmax over keys (registers + the other half)
+          const int qi = 32 * qt + r;
+          float m = -INFINITY;
+#pragma unroll
+          for (int kt = 0; kt <= qt; ++kt)
+#pragma unroll
+            for (int v = 0; v < 16; ++v) {
+              const int kj = 32 * kt + (v & 3) + 8 * (v >> 2) + 4 * h;
+              if (kt == qt && kj > qi) S[kt][v] = -INFINITY;
+              m = fmaxf(m, S[kt][v]);
+            }
+          m = fmaxf(m, swap_halves(m));
+          float sum = 0.f;
+#pragma unroll
+          for (int kt = 0; kt <= qt; ++kt)
+#pragma unroll
+            for (int v = 0; v < 16; ++v) {
+              const float e = __expf(S[kt][v] - m);
+              S[kt][v] = e;
+              sum += e;
+            }
+          sum += swap_halves(sum);
+          const float inv = 1.0f / sum;
+#pragma unroll
+          for (int kt = 0; kt <= qt; ++kt) S[kt] *= inv;
+          // O^T[f][i] += sum_j V[j][f] P^T[j][i]  (rows of this head only)
+#pragma unroll
+          for (int ft = 0; ft < DT; ++ft) {
+            if (32 * ft >= f_hi || 32 * ft + 32 <= f_lo) continue;
+            const int f = 32 * ft + r;
+            const bool mine = !narrow || (f >= f_lo && f < f_hi);
+#pragma unroll
+            for (int kt = 0; kt <= qt; ++kt)
+#pragma unroll
+              for (int s = 0; s < 16; ++s)
+                O[ft][0] = mfma32(mine ? V[kt][ft][s] : 0.f, S[kt][s], O[ft][0]);
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        f32x16 Y[DT][1];
+        proj<EXACT, DT, DT, 1>(Y, P.w_o, P.b_o, d, d, O, r, h);   // out_proj (functional.py:6600)
+#pragma unroll
+        for (int ft = 0; ft < DT; ++ft) {   // residual (model.py:84)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const f32x4 t = *reinterpret_cast<const f32x4*>(xs + ((ft * TT + qt) * 4 + q) * 256 + lane * 4);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) X[ft][qt][4 * q + i] = t[i];
+          }
+          X[ft][qt] += Y[ft][0];
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    // ---- feed-forward sub-block: X += W2 relu(W1 LN_f(X) + b1) + b2  (model.py:92-94)
+    {
+      f32x16 Hn[DT][TT];
+      layernorm<EXACT, DT, TT>(Hn, X, P.ln_f_w, P.ln_f_b, d, a.eps, h);
+      __builtin_amdgcn_sched_barrier(0);
+      f32x16 F[MT][TT];
+      proj<EXACT, MT, DT, TT>(F, P.w1, P.b1, mlp, d, Hn, r, h);
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int tt = 0; tt < TT; ++tt)
+#pragma unroll
+          for (int v = 0; v < 16; ++v) F[mt][tt][v] = F[mt][tt][v] < 0.f ? 0.f : F[mt][tt][v];
+      __builtin_amdgcn_sched_barrier(0);
+      f32x16 Y[DT][TT];
+      proj<EXACT, DT, MT, TT>(Y, P.w2, P.b2, d, mlp, F, r, h);
+#pragma unroll
+      for (int ft = 0; ft < DT; ++ft)
+#pragma unroll
+        for (int tt = 0; tt < TT; ++tt) X[ft][tt] += Y[ft][tt];
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+
+  // ---- last LayerNorm (model.py:96) and store
+  f32x16 Y[DT][TT];
+  sf::layernorm<EXACT, DT, TT>(Y, X, a.ln_w, a.ln_b, d, a.eps, h);
+#pragma unroll
+  for (int tt = 0; tt < TT; ++tt) {
+    const int p = 32 * tt + r;
+    const bool keep = last_only ? (p == n - 1) : (p < n);
+    if (!keep) continue;
+    float* o = out + (last_only ? b * d : (b * n + p) * d);
+#pragma unroll
+    for (int ft = 0; ft < DT; ++ft)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int c = 32 * ft + 8 * q + 4 * h;
+        if (EXACT || c < d)
+          *reinterpret_cast<f32x4*>(o + c) =
+              f32x4{Y[ft][tt][4 * q], Y[ft][tt][4 * q + 1], Y[ft][tt][4 * q + 2], Y[ft][tt][4 * q + 3]};
+      }
+  }
+}
+
+}  // namespace gr
+
+// Fused path for n <= 64, d <= 64 (d % 8 == 0, head width % 8 == 0), mlp <= 128, blocks <= 8.
+// Returns GR_ERR_UNSUPPORTED (error message untouched) for any other shape: the caller then runs
+// the layer-wise pipeline.
+int gr_sasrec_fused_launch(const gr_sasrec_params* p, const int64_t* seqs, int64_t B, int32_t n,
+                           float* out, int32_t last_only, int32_t* err, hipStream_t st) {
+  using namespace gr;
+  const int d = p->d, H = p->n_heads;
+  if (n > 64 || d > 64 || d % 8 || (d / H) % 8 || p->mlp > 128 || p->mlp % 4 ||
+      p->n_blocks > SF_MAX_BLOCKS)
+    return GR_ERR_UNSUPPORTED;
+  SasFusedArgs a;
+  for (int i = 0; i < p->n_blocks; ++i) {
+    SasBlockPtrs& b = a.blk[i];
+    b.ln_a_w = p->attn_ln_w[i]; b.ln_a_b = p->attn_ln_b[i];
+    b.w_in = p->in_proj_w[i];   b.b_in = p->in_proj_b[i];
+    b.w_o = p->out_proj_w[i];   b.b_o = p->out_proj_b[i];
+    b.ln_f_w = p->ffn_ln_w[i];  b.ln_f_b = p->ffn_ln_b[i];
+    b.w1 = p->ffn1_w[i];        b.b1 = p->ffn1_b[i];
+    b.w2 = p->ffn2_w[i];        b.b2 = p->ffn2_b[i];
+    const float* ptrs[12] = {b.ln_a_w, b.ln_a_b, b.w_in, b.b_in, b.w_o, b.b_o,
+                             b.ln_f_w, b.ln_f_b, b.w1, b.b1, b.w2, b.b2};
+    for (const float* q : ptrs)
+      if (!q || !aligned16(q)) return GR_ERR_UNSUPPORTED;
+  }
+  if (!aligned16(p->last_ln_w) || !aligned16(p->last_ln_b) || !aligned16(out)) return GR_ERR_UNSUPPORTED;
+  a.item = p->item_emb; a.pos = p->pos_emb; a.ln_w = p->last_ln_w; a.ln_b = p->last_ln_b;
+  a.item_rows = p->item_rows; a.nb = p->n_blocks; a.d = d; a.heads = H; a.mlp = p->mlp; a.n = n;
+  a.eps = p->eps;
+  a.scale = (float)std::sqrt(1.0 / (double)(d / H));
+  const int TT = n > 32 ? 2 : 1, DT = d > 32 ? 2 : 1, MT = (p->mlp + 31) / 32;
+  const dim3 g((unsigned)((B + 3) / 4)), blk(256);
+  const bool exact = d == 32 * DT && p->mlp == 32 * MT;
+#define GR_SF_LAUNCH(tt, dt, mt)                                                                   \
+  if (TT == tt && DT == dt && MT == mt) {                                                          \
+    if (exact && H == 1)                                                                           \
+      hipLaunchKernelGGL((sasrec_fused_kernel<tt, dt, mt, true, true>), g, blk, 0, st, a, seqs, B, out, last_only, err); \
+    else if (H == 1)                                                                               \
+      hipLaunchKernelGGL((sasrec_fused_kernel<tt, dt, mt, false, true>), g, blk, 0, st, a, seqs, B, out, last_only, err); \
+    else                                                                                           \
+      hipLaunchKernelGGL((sasrec_fused_kernel<tt, dt, mt, false, false>), g, blk, 0, st, a, seqs, B, out, last_only, err); \
+    return check_launch("sasrec fused");                                                           \
+  }
+  GR_SF_LAUNCH(1, 1, 1) GR_SF_LAUNCH(1, 1, 2) GR_SF_LAUNCH(1, 1, 3) GR_SF_LAUNCH(1, 1, 4)
+  GR_SF_LAUNCH(1, 2, 1) GR_SF_LAUNCH(1, 2, 2) GR_SF_LAUNCH(1, 2, 3) GR_SF_LAUNCH(1, 2, 4)
+  GR_SF_LAUNCH(2, 1, 1) GR_SF_LAUNCH(2, 1, 2) GR_SF_LAUNCH(2, 1, 3) GR_SF_LAUNCH(2, 1, 4)
+  GR_SF_LAUNCH(2, 2, 1) GR_SF_LAUNCH(2, 2, 2) GR_SF_LAUNCH(2, 2, 3) GR_SF_LAUNCH(2, 2, 4)
+#undef GR_SF_LAUNCH
+  return GR_ERR_UNSUPPORTED;
+}

@@ -68,9 +68,9 @@ def sasrec_model(item_num, params, device, seed=0):
 
 
 def sequences(B, n, item_num, seed, device):
-    """Lengths U[3, n+1] (truncated to n), ids U[1, item_num], left-padded with 0."""
+    """Lengths U[2, n] (U[1, 1] at n = 1), ids U[1, item_num], left-padded with 0."""
     g = torch.Generator(device=device).manual_seed(seed)
     ids = torch.randint(1, item_num + 1, (B, n), generator=g, device=device)
-    lens = torch.randint(2, n + 1, (B, 1), generator=g, device=device)
+    lens = torch.randint(min(2, n), n + 1, (B, 1), generator=g, device=device)
     pos = torch.arange(n, device=device)[None, :]
     return torch.where(pos >= n - lens, ids, torch.zeros_like(ids))

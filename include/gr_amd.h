@@ -46,6 +46,10 @@ const char* gr_last_error(void);
 /* Process-wide path / tuning options (no reference counterpart; used for A/B measurement):
  *   "rq_fused"      1 (default): gr_rq_encode_f32 runs the fused persistent kernel when the encoder
  *                   shape is in -> 256 -> 128 -> 32; 0: the layer-wise path (gr_linear + quantize)
+ *   "sas_fused"     1 (default): gr_sasrec_forward_f32 / gr_sasrec_predict_f32 run the fused
+ *                   register-resident forward kernel when n <= 64, d <= 64 (d and the head width
+ *                   multiples of 8), mlp <= 128, num_blocks <= 8; 0: the layer-wise pipeline
+ *                   (the workspace query follows the option in force when it is called)
  * gr_set_option returns GR_ERR_ARG for an unknown name/value; gr_get_option returns -1 for an
  * unknown name. */
 int gr_set_option(const char* name, int64_t value);

@@ -53,6 +53,15 @@ for s in $STEPS; do
             -d "$OUT/pmc_$c" -o run -- python3 "$ROOT/bench.py" --steps 5 --warmup 2 --no-cpu-baseline
         cd "$ROOT"
       done ;;
+    pmc2)  # HBM bytes per kernel (FETCH_SIZE / WRITE_SIZE in separate passes) + SQ counters, RQ and SASRec
+      export TMPDIR=/tmp
+      cd /tmp
+      for c in FETCH_SIZE WRITE_SIZE "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES" "GRBM_GUI_ACTIVE SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VMEM"; do
+        tag=$(echo $c | cut -d' ' -f1)
+        step pmc_rq_$tag 120 rocprofv3 --pmc $c --output-format csv -d "$OUT/pmc_rq_$tag" -o run -- python3 "$ROOT/scripts/prof_rq.py" --iters 5 && \
+        step pmc_sas_$tag 120 rocprofv3 --pmc $c --output-format csv -d "$OUT/pmc_sas_$tag" -o run -- python3 "$ROOT/scripts/prof_sas.py" --iters 5
+      done
+      cd "$ROOT" ;;
     pmcrq)  # SQ counters of the RQ encode kernels (one variant per pass)
       export TMPDIR=/tmp
       cd /tmp

@@ -17,6 +17,17 @@ TOL = 1e-5
 SAS = ["sas_csv_c1", "sas_syn_c3", "sas_syn_c5", "sas_syn_h2", "sas_syn_d32_h4"]
 
 
+@pytest.fixture(params=[1, 0], ids=["fused", "layerwise"])
+def sas_path(request):
+    """Run a test through the register-resident fused forward (n <= 64, d <= 64) and through the
+    layer-wise pipeline: both must meet the same bar (shapes outside the fused kernel's range run
+    layer-wise either way)."""
+    from gr_amd import _lib
+    _lib.set_option("sas_fused", request.param)
+    yield request.param
+    _lib.set_option("sas_fused", 1)
+
+
 def build(name, dev):
     from gr_amd import SASRec
     sd, out, meta = gl.load(name)
@@ -27,7 +38,7 @@ def build(name, dev):
 
 
 @pytest.mark.parametrize("name", SAS)
-def test_predict_logits_match_reference(name, dev):
+def test_predict_logits_match_reference(name, dev, sas_path):
     m, out, meta = build(name, dev)
     logits = m.predict(torch.from_numpy(out["seqs"]).to(dev))
     ref = torch.from_numpy(out["logits"])
@@ -40,7 +51,7 @@ def test_predict_logits_match_reference(name, dev):
 
 
 @pytest.mark.parametrize("name", SAS)
-def test_ranks_and_hr_ndcg_match_reference(name, dev):
+def test_ranks_and_hr_ndcg_match_reference(name, dev, sas_path):
     from gr_amd import ops
     m, out, meta = build(name, dev)
     seqs = torch.from_numpy(out["seqs"]).to(dev)
@@ -59,7 +70,7 @@ def test_ranks_and_hr_ndcg_match_reference(name, dev):
 
 
 @pytest.mark.parametrize("name", SAS)
-def test_forward_matches_reference(name, dev):
+def test_forward_matches_reference(name, dev, sas_path):
     m, out, meta = build(name, dev)
     k = out["forward"].shape[0]
     seqs = torch.from_numpy(out["seqs"][:k]).to(dev)
@@ -79,7 +90,7 @@ def test_predict_returns_fresh_writable_tensor(dev):
     assert not torch.equal(a[:, 0], b[:, 0]) and torch.equal(a[:, 1:], b[:, 1:])
 
 
-def test_deterministic_and_batch_invariant(dev):
+def test_deterministic_and_batch_invariant(dev, sas_path):
     m, out, meta = build("sas_syn_c3", dev)
     seqs = torch.from_numpy(out["seqs"]).to(dev)
     a = m.predict(seqs)
@@ -215,3 +226,29 @@ def test_score_kernel_vs_fp64(B, d, rows, dev):
     ref = h.double() @ t.double().t()
     bound = (h.double().abs() @ t.double().abs().t()) * 4e-7 * d ** 0.5 + 1e-6
     assert ((y - ref).abs() <= bound).all()
+
+
+@pytest.mark.parametrize("d,heads,mlp,n,blocks,B", [
+    (64, 1, 64, 50, 2, 37), (64, 1, 64, 64, 2, 5), (64, 1, 64, 1, 2, 9), (32, 1, 32, 32, 1, 6),
+    (32, 1, 32, 33, 3, 7), (16, 1, 64, 20, 2, 3), (48, 2, 96, 40, 2, 11), (64, 8, 128, 17, 4, 4),
+    (40, 5, 20, 64, 1, 13), (64, 2, 64, 50, 8, 2),
+])
+def test_fused_forward_vs_oracle(d, heads, mlp, n, blocks, B, dev):
+    """The fused kernel across its whole shape range (token / feature / mlp tiles, exact and padded
+    widths, narrow heads, n = 1, tile boundaries) against the CPU oracle, forward and predict."""
+    from gr_amd import _lib, synth
+    from oracle import sasrec_oracle
+    _lib.set_option("sas_fused", 1)
+    items = 500
+    p = synth.sasrec_params(d, n, blocks, heads, mlp, dev)
+    m = synth.sasrec_model(items, p, dev, seed=d + n + blocks)
+    seqs = synth.sequences(B, n, items, 3 + n, dev)
+    sd = {k: v.detach().cpu() for k, v in m.state_dict().items()}
+    ref_f = sasrec_oracle.forward(seqs.cpu(), sd, blocks, heads, 1e-8)
+    got_f = m.forward(seqs).cpu()
+    assert (got_f - ref_f).abs().max().item() < 5e-5
+    ref = sasrec_oracle.predict(seqs.cpu(), sd, blocks, heads, 1e-8)
+    got = m.predict(seqs).cpu()
+    err = ((got - ref).abs() / ref.abs().amax(1, keepdim=True)).max().item()
+    assert err <= TOL, err
+    assert torch.equal(m.last_hidden(seqs).cpu(), got_f[:, -1, :])
