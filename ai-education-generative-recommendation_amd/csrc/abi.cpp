@@ -14,10 +14,14 @@ void clear_error() { g_last_error.clear(); }
 static std::atomic<int64_t> g_rq_fused{1};
 // sas_fused (1: register-resident fused SASRec forward when n <= 64 and d <= 64, 0: layer-wise).
 static std::atomic<int64_t> g_sas_fused{1};
+// score_ablate (diagnostic, results INVALID when != 0): 1 = scoring kernel skips its logits
+// stores, 2 = skips its matrix work.  Used by scripts/ab_score.py to split the kernel's time.
+static std::atomic<int64_t> g_score_ablate{0};
 
 int64_t option(const char* name) {
   if (!strcmp(name, "rq_fused")) return g_rq_fused.load();
   if (!strcmp(name, "sas_fused")) return g_sas_fused.load();
+  if (!strcmp(name, "score_ablate")) return g_score_ablate.load();
   return -1;
 }
 }  // namespace gr
@@ -27,6 +31,7 @@ extern "C" int gr_set_option(const char* name, int64_t value) {
   if (!name) return gr::fail(GR_ERR_ARG, "gr_set_option: null name");
   if (!strcmp(name, "rq_fused") && (value == 0 || value == 1)) { gr::g_rq_fused = value; return GR_OK; }
   if (!strcmp(name, "sas_fused") && (value == 0 || value == 1)) { gr::g_sas_fused = value; return GR_OK; }
+  if (!strcmp(name, "score_ablate") && value >= 0 && value <= 2) { gr::g_score_ablate = value; return GR_OK; }
   return gr::fail(GR_ERR_ARG, std::string("gr_set_option: unknown option or value: ") + name);
 }
 

@@ -50,6 +50,8 @@ const char* gr_last_error(void);
  *                   register-resident forward kernel when n <= 64, d <= 64 (d and the head width
  *                   multiples of 8), mlp <= 128, num_blocks <= 8; 0: the layer-wise pipeline
  *                   (the workspace query follows the option in force when it is called)
+ *   "score_ablate"  0 (default).  DIAGNOSTIC ONLY, outputs invalid otherwise: 1 = the scoring
+ *                   kernel skips the logits stores, 2 = it skips the matrix work
  * gr_set_option returns GR_ERR_ARG for an unknown name/value; gr_get_option returns -1 for an
  * unknown name. */
 int gr_set_option(const char* name, int64_t value);
