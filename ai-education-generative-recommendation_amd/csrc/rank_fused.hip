@@ -1,0 +1,257 @@
+// Fused full-catalog rank (SASRec/evaluate.py:26-32 without the [B, N+1] logits):
+//
+//   pairs:     t[u]   = h[u] . table[ids[u]]                   (the target's logit, model.py:107)
+//   count_gt:  cnt[u] = #{j : l'[u, j] > thr[u]}, l' = h . table^T with column 0 taken as -1e9 when
+//              mask_col0 (evaluate.py:27), strict '>' (evaluate.py:32)
+//   rank[u]  = count_gt(thr = pairs) + 1
+//
+// Both kernels evaluate every logit with EXACTLY the instruction sequence of the scoring kernel
+// (score.hip): the same v_mfma_f32_32x32x2_f32 operand layout and k order (step s of 32-deep group g
+// takes features 32g + 8(s>>2) + (s&3) + 4h), so t[u] is bitwise the logit the full scoring would
+// have produced and the target never counts itself (SURVEY §7 hard part 3).
+//
+// count_gt is the scoring kernel with the logits stream replaced by a compare-and-count epilogue:
+// MFMA-bound (12.8 Mflop per user at C3) and reads only the table.  Workgroup = 4 waves x 64 users,
+// one contiguous catalog slice walked in 64-item chunks (table chunk staged in LDS, prefetched into
+// registers one chunk ahead); per-lane counters, reduced over the 32 item lanes at the end, one
+// atomic add per (user, slice).
+#include "gr_common.h"
+
+namespace gr {
+
+constexpr int RK_CHUNK = 64;
+constexpr float RK_MASK = -1e9f;   // evaluate.py:27
+
+template <int D>
+__global__ __launch_bounds__(64) void score_pairs_kernel(const float* __restrict__ h, int64_t B,
+                                                         const float* __restrict__ table,
+                                                         int64_t rows, const int64_t* __restrict__ ids,
+                                                         int mask_col0, float* __restrict__ out,
+                                                         int32_t* err) {
+  constexpr int KG = D / 32;
+  const int lane = threadIdx.x, r = lane & 31, hh = lane >> 5;
+  const int64_t u0 = (int64_t)blockIdx.x * 32;
+  const int64_t u = u0 + r;
+  const int64_t uc = u < B ? u : B - 1;
+  int64_t t = ids[uc];
+  if (t < 0 || t >= rows) {
+    if (u < B && err) *err = 1;
+    t = 0;
+  }
+  f32x16 acc;
+#pragma unroll
+  for (int v = 0; v < 16; ++v) acc[v] = 0.f;
+  // A: user r of the tile; B: the target row of user r (column r of the tile)
+#pragma unroll
+  for (int g = 0; g < KG; ++g)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const f32x4 a = *reinterpret_cast<const f32x4*>(h + uc * D + 32 * g + 8 * q + 4 * hh);
+      const f32x4 b = *reinterpret_cast<const f32x4*>(table + t * D + 32 * g + 8 * q + 4 * hh);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) acc = mfma32(a[s], b[s], acc);
+    }
+  // diagonal: row (v&3) + 8(v>>2) + 4hh == column r
+  float d = 0.f;
+#pragma unroll
+  for (int v = 0; v < 16; ++v)
+    if ((v & 3) + 8 * (v >> 2) + 4 * hh == r) d = acc[v];
+  if (u < B && ((r >> 2) & 1) == hh) out[u] = (mask_col0 && t == 0) ? RK_MASK : d;
+}
+
+template <int D>
+__global__ __launch_bounds__(256, (D <= 32 ? 2 : 1)) void score_count_kernel(const float* __restrict__ h, int64_t B,
+                                                            const float* __restrict__ table,
+                                                            int64_t rows,
+                                                            const float* __restrict__ thr,
+                                                            int mask_col0,
+                                                            unsigned long long* __restrict__ cnt_out,
+                                                            int ublocks, int slices) {
+  constexpr int KG = D / 32;
+  constexpr int P = D + 4;
+  constexpr int LV = RK_CHUNK * D / 4 / 256;
+  __shared__ __attribute__((aligned(16))) float tab[2][RK_CHUNK * P];
+  const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, hh = lane >> 5;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wgid = xcd_remap(blockIdx.x, gridDim.x);
+  const int ub = wgid % ublocks, sl = wgid / ublocks;
+  const int64_t chunks = (rows + RK_CHUNK - 1) / RK_CHUNK;
+  const int64_t c_begin = chunks * sl / slices, c_end = chunks * (sl + 1) / slices;
+  if (c_begin >= c_end) return;
+  const int64_t u0 = ((int64_t)ub * 4 + w) * 64;
+
+  f32x4 hf[2][KG][4];
+  float th[2][16];
+#pragma unroll
+  for (int ut = 0; ut < 2; ++ut) {
+    const int64_t u = u0 + ut * 32 + r;
+    const int64_t uc = u < B ? u : B - 1;
+#pragma unroll
+    for (int g = 0; g < KG; ++g)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const f32x4 v = *reinterpret_cast<const f32x4*>(h + uc * D + 32 * g + 8 * q + 4 * hh);
+        hf[ut][g][q] = u < B ? v : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+    for (int v = 0; v < 16; ++v) {
+      const int64_t uu = u0 + ut * 32 + (v & 3) + 8 * (v >> 2) + 4 * hh;
+      th[ut][v] = thr[uu < B ? uu : B - 1];
+    }
+  }
+  f32x4 st[LV];
+  auto gload = [&](int64_t c) {
+#pragma unroll
+    for (int i = 0; i < LV; ++i) {
+      const int f = tid + 256 * i, row = f / (D / 4), col = (f % (D / 4)) * 4;
+      int64_t item = c * RK_CHUNK + row;
+      item = item < rows ? item : rows - 1;
+      st[i] = *reinterpret_cast<const f32x4*>(table + item * D + col);
+    }
+  };
+  auto swrite = [&](int b) {
+#pragma unroll
+    for (int i = 0; i < LV; ++i) {
+      const int f = tid + 256 * i, row = f / (D / 4), col = (f % (D / 4)) * 4;
+      *reinterpret_cast<f32x4*>(&tab[b][row * P + col]) = st[i];
+    }
+  };
+  gload(c_begin);
+  swrite(0);
+  __syncthreads();
+  int cnt[2][16];
+#pragma unroll
+  for (int ut = 0; ut < 2; ++ut)
+#pragma unroll
+    for (int v = 0; v < 16; ++v) cnt[ut][v] = 0;
+  int buf = 0;
+#pragma unroll 1
+  for (int64_t c = c_begin; c < c_end; ++c) {
+    if (c + 1 < c_end) gload(c + 1);
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int ut = 0; ut < 2; ++ut)
+#pragma unroll
+      for (int it = 0; it < 2; ++it)
+#pragma unroll
+        for (int v = 0; v < 16; ++v) acc[ut][it][v] = 0.f;
+    const float* tb = &tab[buf][r * P + 4 * hh];
+#pragma unroll
+    for (int g = 0; g < KG; ++g)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        f32x4 bt[2];
+#pragma unroll
+        for (int it = 0; it < 2; ++it) bt[it] = *reinterpret_cast<const f32x4*>(tb + it * 32 * P + 32 * g + 8 * q);
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+          for (int it = 0; it < 2; ++it)
+#pragma unroll
+            for (int ut = 0; ut < 2; ++ut) acc[ut][it] = mfma32(hf[ut][g][q][s], bt[it][s], acc[ut][it]);
+      }
+    const int64_t c0 = c * RK_CHUNK;
+    if (c0 + RK_CHUNK <= rows && !(mask_col0 && c0 == 0)) {   // steady state: no column masks
+#pragma unroll
+      for (int ut = 0; ut < 2; ++ut)
+#pragma unroll
+        for (int it = 0; it < 2; ++it)
+#pragma unroll
+          for (int v = 0; v < 16; ++v) cnt[ut][v] += acc[ut][it][v] > th[ut][v] ? 1 : 0;
+    } else {
+#pragma unroll
+      for (int it = 0; it < 2; ++it) {
+        const int64_t col = c0 + it * 32 + r;
+        const bool ok = col < rows;
+        const bool m0 = mask_col0 && col == 0;
+#pragma unroll
+        for (int ut = 0; ut < 2; ++ut)
+#pragma unroll
+          for (int v = 0; v < 16; ++v) {
+            const float l = m0 ? RK_MASK : acc[ut][it][v];
+            cnt[ut][v] += (ok && l > th[ut][v]) ? 1 : 0;
+          }
+      }
+    }
+    if (c + 1 < c_end) swrite(buf ^ 1);
+    __syncthreads();
+    buf ^= 1;
+  }
+  // reduce over the 32 item lanes of each half, one atomic per (user, slice)
+#pragma unroll
+  for (int ut = 0; ut < 2; ++ut)
+#pragma unroll
+    for (int v = 0; v < 16; ++v) {
+      int x = cnt[ut][v];
+#pragma unroll
+      for (int o = 1; o < 32; o <<= 1) x += __shfl_xor(x, o);
+      const int64_t u = u0 + ut * 32 + (v & 3) + 8 * (v >> 2) + 4 * hh;
+      if (r == 0 && u < B && x) atomicAdd(&cnt_out[u], (unsigned long long)x);
+    }
+}
+
+static int cu_count() {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
+      cus = 256;
+  }
+  return cus;
+}
+
+}  // namespace gr
+
+extern "C" int gr_score_pairs_f32(const float* h, int64_t B, int32_t d, const float* table,
+                                  int64_t rows, const int64_t* ids, int32_t mask_col0, float* out,
+                                  int32_t* err_flag, void* stream) {
+  using namespace gr;
+  clear_error();
+  if (B < 0 || rows < 1) return fail(GR_ERR_ARG, "gr_score_pairs_f32: bad shape");
+  if (B == 0) return GR_OK;
+  if (!h || !table || !ids || !out) return fail(GR_ERR_ARG, "gr_score_pairs_f32: null pointer");
+  if (d != 32 && d != 64 && d != 128)
+    return fail(GR_ERR_UNSUPPORTED, "gr_score_pairs_f32: d must be 32, 64 or 128");
+  if (!aligned16(h) || !aligned16(table)) return fail(GR_ERR_ARG, "gr_score_pairs_f32: h / table not 16-byte aligned");
+  const unsigned grid = (unsigned)((B + 31) / 32);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  switch (d) {
+    case 32: hipLaunchKernelGGL(score_pairs_kernel<32>, dim3(grid), dim3(64), 0, st, h, B, table, rows, ids, mask_col0, out, err_flag); break;
+    case 64: hipLaunchKernelGGL(score_pairs_kernel<64>, dim3(grid), dim3(64), 0, st, h, B, table, rows, ids, mask_col0, out, err_flag); break;
+    default: hipLaunchKernelGGL(score_pairs_kernel<128>, dim3(grid), dim3(64), 0, st, h, B, table, rows, ids, mask_col0, out, err_flag); break;
+  }
+  return check_launch("gr_score_pairs_f32");
+}
+
+extern "C" int gr_score_count_gt_f32(const float* h, int64_t B, int32_t d, const float* table,
+                                     int64_t rows, const float* thresholds, int32_t mask_col0,
+                                     int64_t* counts_out, void* stream) {
+  using namespace gr;
+  clear_error();
+  if (B < 0 || rows < 0) return fail(GR_ERR_ARG, "gr_score_count_gt_f32: bad shape");
+  if (B == 0) return GR_OK;
+  if (!h || !table || !thresholds || !counts_out) return fail(GR_ERR_ARG, "gr_score_count_gt_f32: null pointer");
+  if (d != 32 && d != 64 && d != 128)
+    return fail(GR_ERR_UNSUPPORTED, "gr_score_count_gt_f32: d must be 32, 64 or 128");
+  if (!aligned16(h) || !aligned16(table)) return fail(GR_ERR_ARG, "gr_score_count_gt_f32: h / table not 16-byte aligned");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (hipMemsetAsync(counts_out, 0, (size_t)B * sizeof(int64_t), st) != hipSuccess)
+    return fail(GR_ERR_HIP, "gr_score_count_gt_f32: memset failed");
+  if (rows == 0) return GR_OK;
+  const int64_t ublocks = (B + 255) / 256;
+  const int64_t chunks = (rows + RK_CHUNK - 1) / RK_CHUNK;
+  const int64_t per_cu = d <= 32 ? 2 : 1;   // resident workgroups per CU (registers)
+  int64_t slices = (per_cu * cu_count() + ublocks - 1) / ublocks;
+  if (slices > chunks) slices = chunks;
+  if (slices < 1) slices = 1;
+  if (ublocks * slices > 0x7fffffffLL) return fail(GR_ERR_UNSUPPORTED, "gr_score_count_gt_f32: grid too large");
+  const dim3 g((unsigned)(ublocks * slices)), b(256);
+  auto* cnt = reinterpret_cast<unsigned long long*>(counts_out);
+  switch (d) {
+    case 32: hipLaunchKernelGGL(score_count_kernel<32>, g, b, 0, st, h, B, table, rows, thresholds, mask_col0, cnt, (int)ublocks, (int)slices); break;
+    case 64: hipLaunchKernelGGL(score_count_kernel<64>, g, b, 0, st, h, B, table, rows, thresholds, mask_col0, cnt, (int)ublocks, (int)slices); break;
+    default: hipLaunchKernelGGL(score_count_kernel<128>, g, b, 0, st, h, B, table, rows, thresholds, mask_col0, cnt, (int)ublocks, (int)slices); break;
+  }
+  return check_launch("gr_score_count_gt_f32");
+}

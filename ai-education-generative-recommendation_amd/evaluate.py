@@ -1,0 +1,108 @@
+"""SASRec evaluation harness on the gfx950 kernels — SASRec/evaluate.py:10-89 and the multi-k
+evaluation of SASRec/train.py:33-56.
+
+The reference computes ``logits = model.predict(x)`` ([B, N+1] fp32), masks column 0 with -1e9,
+gathers the target's logit and counts strictly greater logits (evaluate.py:26-32).  Here the rank
+comes from ``ops.score_rank``: the last hidden state from the fused SASRec forward, then the target
+logit and the strict-'>' count straight from the scoring kernel's MFMA tiles — the [B, N+1] logits
+are never written (``materialize=True`` runs the reference's predict + rank sequence instead; both
+give the same ranks, tests/test_evaluate_gpu.py).  HR@k / NDCG@k are then formed on the host in
+float64 exactly as the reference does (per-user Python list, ``np.mean``, evaluate.py:35-47).
+"""
+import csv
+import os
+
+import numpy as np
+import torch
+
+from . import ops
+from .data import SASRecDataset
+
+
+def rank_batch(model, input_ids, targets, materialize=False):
+    """Strict 1-based rank of each target over the full catalog with column 0 masked
+    (SASRec/evaluate.py:26-32) for one batch on the model's device."""
+    if materialize:
+        logits = model.predict(input_ids)
+        logits[:, 0] = -1e9
+        t = logits.gather(1, targets.unsqueeze(1))
+        return (logits > t).sum(dim=1) + 1
+    if model.d not in (32, 64, 128):   # the fused kernels' widths; others: predict + rank kernel
+        return ops.rank(model.predict(input_ids), targets, mask_col0=True)
+    h = model.last_hidden(input_ids)
+    return ops.score_rank(h, model.item_emb.weight.detach(), targets, mask_col0=True)
+
+
+def hr_ndcg(ranks, top_k):
+    """evaluate.py:35-47: per-user hit / 1/log2(r+1), averaged with np.mean (float64)."""
+    ht, ndcg = [], []
+    for r in np.asarray(ranks):
+        if r <= top_k:
+            ht.append(1)
+            ndcg.append(1 / np.log2(r + 1))
+        else:
+            ht.append(0)
+            ndcg.append(0)
+    return float(np.mean(ht)), float(np.mean(ndcg))
+
+
+def multi_k(ranks, topk_list):
+    """SASRec/train.py:33-56: {k: HR@k}, {k: NDCG@k} for every k of ``topk_list``."""
+    hits = {k: [] for k in topk_list}
+    ndcgs = {k: [] for k in topk_list}
+    for r in np.asarray(ranks):
+        for k in topk_list:
+            hits[k].append(1 if r <= k else 0)
+            ndcgs[k].append(1 / np.log2(r + 1) if r <= k else 0)
+    return ({k: float(np.mean(v)) if v else 0.0 for k, v in hits.items()},
+            {k: float(np.mean(v)) if v else 0.0 for k, v in ndcgs.items()})
+
+
+@torch.no_grad()
+def evaluate(params, dataset=None, model=None, materialize=False, save_csv=True):
+    """SASRec/evaluate.py:evaluate(params).  ``dataset`` / ``model`` may be passed in directly (the
+    reference builds them from ``params['data_path']`` / ``params['ckpt']``); checkpoints are read
+    with ``torch.load(weights_only=True)``.  Returns {"Hit@k": ..., "NDCG@k": ...} (plus every k of
+    ``params['topk_list']`` when present) and the rank vector."""
+    from .sasrec import SASRec
+    device = torch.device(params["device"])
+    if dataset is None:
+        dataset = SASRecDataset(params["data_path"], max_len=params["max_len"], mode="test", params=params)
+    if model is None:
+        model = SASRec(dataset.item_num, params).to(device)
+        model.load_state_dict(torch.load(params["ckpt"], map_location=device, weights_only=True))
+    model.eval()
+    ranks = []
+    for input_ids, target in dataset.batches(params.get("eval_batch_size", 128)):
+        ranks.append(rank_batch(model, input_ids.to(device), target.to(device), materialize))
+    ranks = torch.cat(ranks).cpu().numpy() if ranks else np.zeros(0, np.int64)
+    top_k = params.get("top_k", 10)
+    hit, ndcg = hr_ndcg(ranks, top_k)
+    results = {f"Hit@{top_k}": hit, f"NDCG@{top_k}": ndcg}
+    if params.get("topk_list"):
+        hk, nk = multi_k(ranks, params["topk_list"])
+        for k in params["topk_list"]:
+            results.setdefault(f"Hit@{k}", hk[k])
+            results.setdefault(f"NDCG@{k}", nk[k])
+    if save_csv and params.get("params_path"):
+        save_results_to_csv(params, results)
+    return results, ranks
+
+
+def save_results_to_csv(params, results):
+    """evaluate.py:57-89: append task_id, the hyper-parameters and the metrics (6 decimals)."""
+    csv_path = params["params_path"]
+    os.makedirs(os.path.dirname(csv_path) if os.path.dirname(csv_path) else ".", exist_ok=True)
+    data = {"task_id": params.get("task_id")}
+    for name in ["d", "num_blocks", "num_heads", "dropout", "lr", "batch_size", "epochs",
+                 "mlp_layer", "max_len", "top_k"]:
+        if name in params:
+            data[name] = params[name]
+    for key, value in results.items():
+        data[key] = f"{value:.6f}"
+    exists = os.path.exists(csv_path)
+    with open(csv_path, "a", newline="", encoding="utf-8") as f:
+        w = csv.writer(f)
+        if not exists:
+            w.writerow(data.keys())
+        w.writerow(data.values())

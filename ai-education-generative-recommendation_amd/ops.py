@@ -93,6 +93,43 @@ def topk(logits, k, id_offset=0):
     return vals, ids
 
 
+def score_pairs(h, table, ids, mask_col0=True):
+    """Target logits ``h[b] . table[ids[b]]`` with the scoring kernel's exact fp32 chain (-1e9 for
+    id 0 when ``mask_col0``, SASRec/evaluate.py:27)."""
+    L.require_gpu(h, table, ids)
+    h, t = L.as_f32(h), L.as_f32(table)
+    ids = ids.reshape(-1).to(torch.int64).contiguous()
+    B, d = h.shape
+    out = torch.empty(B, dtype=torch.float32, device=h.device)
+    err = torch.zeros(1, dtype=torch.int32, device=h.device)
+    with torch.cuda.device(h.device):
+        L.check(L.lib().gr_score_pairs_f32(L.ptr(h), B, d, L.ptr(t), t.shape[0], L.ptr(ids),
+                                           1 if mask_col0 else 0, L.ptr(out), L.ptr(err),
+                                           L.stream_of(h.device)), "gr_score_pairs_f32")
+    _check_err(err)
+    return out
+
+
+def score_count_gt(h, table, thresholds, mask_col0=True):
+    """``#{j : (h . table^T)[b, j] > thresholds[b]}`` without materialising the logits."""
+    L.require_gpu(h, table, thresholds)
+    h, t = L.as_f32(h), L.as_f32(table)
+    th = L.as_f32(thresholds.reshape(-1))
+    B, d = h.shape
+    out = torch.empty(B, dtype=torch.int64, device=h.device)
+    with torch.cuda.device(h.device):
+        L.check(L.lib().gr_score_count_gt_f32(L.ptr(h), B, d, L.ptr(t), t.shape[0], L.ptr(th),
+                                              1 if mask_col0 else 0, L.ptr(out),
+                                              L.stream_of(h.device)), "gr_score_count_gt_f32")
+    return out
+
+
+def score_rank(h, table, targets, mask_col0=True):
+    """Strict rank of each target over the full catalog (SASRec/evaluate.py:27-32) without
+    writing the [B, rows] logits: count_gt(h, table, pairs(h, table, targets)) + 1."""
+    return score_count_gt(h, table, score_pairs(h, table, targets, mask_col0), mask_col0) + 1
+
+
 def rq_quantize(z, codebooks, with_gap=False):
     """Residual quantization of latents (RQ-VAE/models/rq.py:39-56, use_sk=False).
 

@@ -170,6 +170,25 @@ int gr_count_gt_f32(const float* logits, int64_t B, int64_t cols, int64_t ld,
 int gr_topk_f32(const float* logits, int64_t B, int64_t cols, int64_t ld, int32_t k,
                 int64_t id_offset, float* vals_out, int64_t* ids_out, void* stream);
 
+/* ------------------------------------------------------------------------------------------ */
+/* Fused rank without materialising logits (SASRec/evaluate.py:26-32).  Every
+ * logit is evaluated with exactly the instruction sequence of gr_score_f32 (d in {32, 64, 128}), so
+ * the values below are bitwise the entries gr_score_f32 / gr_sasrec_predict_f32 would write.
+ *
+ * Target logits: out[b] = h[b] . table[ids[b]] (-1e9 when mask_col0 and ids[b] == 0, the
+ * evaluate.py:27 mask).  err_flag (optional device int32) is set when an id is outside [0, rows). */
+int gr_score_pairs_f32(const float* h, int64_t B, int32_t d, const float* table, int64_t rows,
+                       const int64_t* ids, int32_t mask_col0, float* out, int32_t* err_flag,
+                       void* stream);
+
+/* counts_out[b] = #{j < rows : l[b, j] > thresholds[b]}, l = h . table^T with column 0 taken as
+ * -1e9 when mask_col0 (strict '>', evaluate.py:32).  With thresholds = gr_score_pairs_f32 of the
+ * targets, counts + 1 is the reference's rank.  On a catalog shard (rows = the shard's rows,
+ * mask_col0 only on the shard holding row 0) the counts of all shards sum to the global count. */
+int gr_score_count_gt_f32(const float* h, int64_t B, int32_t d, const float* table, int64_t rows,
+                          const float* thresholds, int32_t mask_col0, int64_t* counts_out,
+                          void* stream);
+
 #ifdef __cplusplus
 }
 #endif

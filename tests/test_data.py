@@ -1,0 +1,88 @@
+"""Host-side input formats and the evaluation tail's metric semantics."""
+import csv
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import golden_lib as gl
+from gr_amd.data import EmbDataset, SASRecDataset, read_interactions
+from gr_amd.evaluate import hr_ndcg, multi_k, save_results_to_csv
+
+
+def c1_records():
+    z = np.load(os.path.join(gl.HERE, "interactions_c1.npz"), allow_pickle=False)
+    return [(s, [int(c)]) for s, c in zip(z["student_id"], z["class_id"])]
+
+
+def test_sasrec_test_dataset_matches_config1_fixture():
+    """stu-major interactions -> per-user test sequences: the inputs / targets / item_num the C1
+    golden fixture was generated with (SASRec/data_vision.py:16-38, 74-87)."""
+    _, out, meta = gl.load("sas_csv_c1")
+    ds = SASRecDataset(c1_records(), max_len=20, mode="test", params={"min_seq_len": 3})
+    inp, tgt = ds.tensors()
+    assert ds.item_num == meta["item_num"]
+    assert np.array_equal(inp.numpy(), out["seqs"]) and np.array_equal(tgt.numpy(), out["targets"])
+    x, t = ds[3]
+    assert torch.equal(x, inp[3]) and int(t) == int(tgt[3])
+    b = list(ds.batches(5))
+    assert len(b) == 4 and torch.equal(torch.cat([p[0] for p in b]), inp)
+
+
+def test_sasrec_dataset_semantics():
+    recs = [("u2", [5, 6]), ("u1", [1, 2, 3]), ("u2", [7]), ("u3", [9, 1]), ("u4", [2, 3, 4, 5, 6])]
+    ds = SASRecDataset(recs, max_len=3, mode="test", params={"min_seq_len": 3})
+    assert ds.user_ids == ["u2", "u1", "u4"]                 # first-seen order, u3 too short
+    assert ds.item_num == 9                                  # max over ALL users (data_vision.py:36-38)
+    inp, tgt = ds.tensors()
+    assert inp.tolist() == [[0, 5, 6], [0, 1, 2], [3, 4, 5]] and tgt.tolist() == [7, 3, 6]
+    tr = SASRecDataset(recs, max_len=4, mode="train", params={"min_seq_len": 3})
+    x, y = tr[2]                                             # u4: train seq [2,3,4,5]
+    assert x.tolist() == [0, 2, 3, 4] and y.tolist() == [0, 3, 4, 5]
+
+
+def test_interaction_and_embedding_csv_readers(tmp_path):
+    p = tmp_path / "inter.csv"
+    vec = [0.5] * 4
+    with open(p, "w", newline="", encoding="utf-8") as f:
+        w = csv.writer(f)
+        w.writerow(["id", "student_id", "class_id", "bert_vector"])
+        w.writerow([1, "a", 3, json.dumps(vec)])
+        w.writerow([2, "", 4, json.dumps(vec)])
+        w.writerow([3, "b", 5, json.dumps([1.0] * 4)])
+    assert read_interactions(str(p)) == [("a", [3]), ("b", [5])]
+    e = EmbDataset(str(p))
+    assert e.embeddings.shape == (2, 4) and e.dim == 4 and e.embeddings.dtype == np.float32
+    np.save(tmp_path / "e.npy", np.arange(12, dtype=np.float32).reshape(3, 4))
+    e2 = EmbDataset(str(tmp_path / "e.npy"))
+    assert len(e2) == 3 and torch.equal(e2[1], torch.tensor([4.0, 5, 6, 7]))
+    assert [b.shape[0] for b in e2.batches(2)] == [2, 1]
+
+
+def test_h5_needs_h5py_message(tmp_path):
+    try:
+        import h5py  # noqa: F401
+        pytest.skip("h5py present")
+    except ImportError:
+        pass
+    with pytest.raises(ImportError, match="h5py"):
+        read_interactions(str(tmp_path / "x.h5"))
+
+
+def test_metrics_match_reference_tail(tmp_path):
+    """HR/NDCG exactly as evaluate.py:35-47 / train.py:33-56 (float64 np.mean of per-user lists)."""
+    ranks = np.array([1, 3, 10, 11, 2, 50, 7], np.int64)
+    hit, ndcg = hr_ndcg(ranks, 10)
+    ref_h = np.mean([1 if r <= 10 else 0 for r in ranks])
+    ref_n = np.mean([1 / np.log2(r + 1) if r <= 10 else 0 for r in ranks])
+    assert hit == ref_h and ndcg == ref_n
+    hk, nk = multi_k(ranks, [2, 5, 10, 20])
+    assert hk[10] == hit and nk[10] == ndcg and hk[2] == np.mean([1, 0, 0, 0, 1, 0, 0])
+    params = {"params_path": str(tmp_path / "r.csv"), "task_id": "t", "d": 16, "top_k": 10}
+    save_results_to_csv(params, {"Hit@10": hit, "NDCG@10": ndcg})
+    save_results_to_csv(params, {"Hit@10": hit, "NDCG@10": ndcg})
+    rows = list(csv.reader(open(params["params_path"])))
+    assert rows[0] == ["task_id", "d", "top_k", "Hit@10", "NDCG@10"] and len(rows) == 3
+    assert rows[1][3] == f"{hit:.6f}"

@@ -1,0 +1,77 @@
+"""Fused rank (no logits) and the evaluation harness on the GPU.
+
+Bar: target logits bitwise equal to the scoring kernel's entries; counts / ranks exactly equal to
+the reference tail (evaluate.py:27-32) run on the GPU's own logits; ranks / HR@10 / NDCG@10 equal
+to the golden fixtures."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import golden_lib as gl
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("B,d,rows", [(300, 64, 10001), (64, 128, 5000), (257, 32, 1000), (1, 64, 70),
+                                      (70, 64, 64)])
+def test_pairs_and_count_equal_materialised_logits(B, d, rows, dev):
+    from gr_amd import ops
+    g = torch.Generator().manual_seed(B * d + rows)
+    h = torch.randn(B, d, generator=g).to(dev)
+    t = torch.randn(rows, d, generator=g).to(dev)
+    tg = torch.randint(0, rows, (B,), generator=g).to(dev)
+    tg[0] = 0
+    logits = ops.score(h, t)
+    pairs = ops.score_pairs(h, t, tg, mask_col0=False)
+    assert torch.equal(pairs, logits.gather(1, tg[:, None])[:, 0])   # bitwise the same chain
+    lg = logits.clone()
+    lg[:, 0] = -1e9
+    ref = (lg > lg.gather(1, tg[:, None])).sum(1) + 1
+    assert torch.equal(ops.score_rank(h, t, tg), ref)
+    thr = torch.randn(B, generator=g).to(dev)
+    assert torch.equal(ops.score_count_gt(h, t, thr, mask_col0=False), (logits > thr[:, None]).sum(1))
+
+
+@pytest.mark.parametrize("name", ["sas_csv_c1", "sas_syn_c3", "sas_syn_c5"])
+def test_fused_rank_matches_fixture(name, dev):
+    from gr_amd import SASRec, ops
+    from gr_amd.evaluate import hr_ndcg
+    sd, out, meta = gl.load(name)
+    p = dict(meta["params"], device=str(dev))
+    m = SASRec(meta["item_num"], p)
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
+    m = m.to(dev).eval()
+    seqs = torch.from_numpy(out["seqs"]).to(dev)
+    tg = torch.from_numpy(out["targets"]).to(dev)
+    h = m.last_hidden(seqs)
+    if meta["params"]["d"] not in (32, 64, 128):
+        pytest.skip("fused rank covers d in {32, 64, 128}")
+    ranks = ops.score_rank(h, m.item_emb.weight, tg).cpu().numpy()
+    ref = ops.rank(m.predict(seqs), tg).cpu().numpy()
+    assert np.array_equal(ranks, ref)
+    cert = out["margin"] > 1e-5
+    assert np.array_equal(ranks[cert], out["ranks"][cert])
+    assert hr_ndcg(ranks, 10) == (meta["hr10"], pytest.approx(meta["ndcg10"], abs=0, rel=0))
+
+
+def test_evaluate_harness_config1(dev, tmp_path):
+    """SASRec/evaluate.py end to end on the config-1 data: dataset from the stu-major interactions,
+    checkpoint from the fixture's state dict (weights_only load), fused and materialised ranks."""
+    from gr_amd.data import SASRecDataset
+    from gr_amd.evaluate import evaluate
+    sd, out, meta = gl.load("sas_csv_c1")
+    z = np.load(os.path.join(gl.HERE, "interactions_c1.npz"), allow_pickle=False)
+    recs = [(s, [int(c)]) for s, c in zip(z["student_id"], z["class_id"])]
+    params = dict(meta["params"], device=str(dev), eval_batch_size=5, top_k=10, topk_list=[2, 5, 10, 20],
+                  min_seq_len=3, ckpt=str(tmp_path / "c1.pt"), params_path=str(tmp_path / "res.csv"),
+                  task_id="c1")
+    torch.save({k: torch.from_numpy(v) for k, v in sd.items()}, params["ckpt"])
+    ds = SASRecDataset(recs, max_len=params["max_len"], mode="test", params=params)
+    res, ranks = evaluate(params, dataset=ds)
+    assert np.array_equal(ranks, out["ranks"])
+    assert res["Hit@10"] == meta["hr10"]
+    res2, ranks2 = evaluate(params, dataset=ds, materialize=True, save_csv=False)
+    assert np.array_equal(ranks2, ranks) and res2 == res
+    assert os.path.exists(params["params_path"])
