@@ -4,6 +4,7 @@ Each function takes/returns torch tensors on a ROCm device, enqueues on the curr
 never synchronises.  Argument checking mirrors the ATen errors the reference would raise.
 """
 import ctypes
+import itertools
 import os
 
 import torch
@@ -198,6 +199,35 @@ def rq_encode(x, weights, biases, codebooks, with_gap=False, with_z=False):
     if with_z:
         out.append(z)
     return out[0] if len(out) == 1 else tuple(out)
+
+
+def rq_encode_sk(x, weights, biases, codebooks, sk_eps, sk_iters, group_sizes=None):
+    """RQVAE.get_indices(xs, use_sk=True) (RQ-VAE/models/rqvae.py:67-71 with vq.py:76-84) for
+    independent row groups in ONE launch: ``group_sizes`` partitions the rows of ``x`` into
+    consecutive groups, each one reference call (default: the whole batch is one group)."""
+    L.require_gpu(x, *weights, *codebooks)
+    n = x.shape[0]
+    _, z = rq_encode(x, weights, biases, codebooks, with_z=True)
+    cbs = [L.as_f32(c) for c in codebooks]
+    e = z.shape[1]
+    Ks = [c.shape[0] for c in cbs]
+    sizes = [n] if group_sizes is None else [int(s) for s in group_sizes]
+    if sum(sizes) != n or any(s < 1 for s in sizes):
+        raise RuntimeError("rq_encode_sk: group sizes must be positive and sum to the batch")
+    ptr = torch.tensor([0] + list(itertools.accumulate(sizes)), dtype=torch.int64)
+    dev = x.device
+    ptr = ptr.to(dev)
+    lib = L.lib()
+    ks_c = L.i32_array(Ks)
+    eps_c = (ctypes.c_double * len(cbs))(*[float(v) for v in sk_eps])
+    nbytes = lib.gr_rq_encode_sk_workspace_bytes(n, e, len(cbs), ks_c)
+    wsp = L.workspace(nbytes, dev)
+    idx = torch.empty((n, len(cbs)), dtype=torch.int64, device=dev)
+    with torch.cuda.device(dev):
+        L.check(lib.gr_rq_encode_sk_f32(L.ptr(z), n, e, len(cbs), ks_c, L.ptr_array(cbs), eps_c,
+                                        int(sk_iters), L.ptr(ptr), len(sizes), L.ptr(idx), L.ptr(wsp),
+                                        nbytes, L.stream_of(dev)), "gr_rq_encode_sk_f32")
+    return idx
 
 
 class SasrecBinding:

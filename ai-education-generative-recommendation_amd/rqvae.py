@@ -178,19 +178,33 @@ class RQVAE(nn.Module):
         if self.training and self.dropout_prob > 0:
             raise RuntimeError("gr_amd RQVAE.get_indices runs the eval-mode encoder: call .eval() "
                                "(dropout is active in train mode)")
-        if use_sk and any(q.sk_epsilon > 0 for q in self.rq.vq_layers):
-            raise NotImplementedError("gr_amd: use_sk=True with sk_epsilon > 0 (Sinkhorn collision "
-                                      "re-encode, vq.py:76-83) is not implemented yet")
         if xs.dim() != 2 or xs.shape[1] != self.in_dim:
             raise RuntimeError(f"get_indices expects [B, {self.in_dim}] inputs, got {tuple(xs.shape)}")
 
     @torch.no_grad()
     def get_indices(self, xs, use_sk=False):
-        """rqvae.py:67-71: ``[B, in_dim]`` fp32 -> ``[B, L]`` int64 semantic IDs (one C-ABI call)."""
+        """rqvae.py:67-71: ``[B, in_dim]`` fp32 -> ``[B, L]`` int64 semantic IDs (one C-ABI call).
+
+        ``use_sk=True`` with a level whose ``sk_epsilon > 0`` assigns that level by Sinkhorn over the
+        whole batch (vq.py:76-84), as the reference does; the batch is one group."""
         self._check_encode(xs, use_sk)
         lin = self.encoder.linears()
-        return ops.rq_encode(xs, [m.weight.detach() for m in lin], [m.bias.detach() for m in lin],
-                             self.rq.codebooks())
+        ws, bs = [m.weight.detach() for m in lin], [m.bias.detach() for m in lin]
+        if use_sk and any(q.sk_epsilon > 0 for q in self.rq.vq_layers):
+            return ops.rq_encode_sk(xs, ws, bs, self.rq.codebooks(), self.sk_eps(), self.rq.sk_iters)
+        return ops.rq_encode(xs, ws, bs, self.rq.codebooks())
+
+    def sk_eps(self):
+        return [float(q.sk_epsilon) for q in self.rq.vq_layers]
+
+    @torch.no_grad()
+    def get_indices_groups(self, xs, group_sizes):
+        """``torch.cat([get_indices(g, use_sk=True) for g in groups])`` for consecutive row groups
+        of ``xs`` in one launch — the per-group loop of RQ-VAE/infer.py:116-127."""
+        self._check_encode(xs, True)
+        lin = self.encoder.linears()
+        return ops.rq_encode_sk(xs, [m.weight.detach() for m in lin], [m.bias.detach() for m in lin],
+                                self.rq.codebooks(), self.sk_eps(), self.rq.sk_iters, group_sizes)
 
     @torch.no_grad()
     def get_indices_certified(self, xs):

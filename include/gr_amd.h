@@ -103,6 +103,19 @@ int gr_rq_encode_f32(const float* x, int64_t n, int32_t n_linear, const int32_t*
                      float* best_out, float* gap_out, float* z_out, void* workspace,
                      size_t workspace_bytes, void* stream);
 
+/* RQVAE.get_indices(xs, use_sk=True) over independent row groups (the collision re-encode of
+ * RQ-VAE/infer.py:108-130; vq.py:52-61, 76-84; layers.py:85-108).  z[n, e]: encoder outputs (as
+ * gr_rq_encode_f32's z_out), rows grouped contiguously: group g = rows [group_ptr[g],
+ * group_ptr[g+1]) (device int64 array of n_groups + 1, group_ptr[0] = 0, group_ptr[n_groups] = n).
+ * Each group is one reference call: a level with sk_eps[l] > 0 (host array, float64) assigns by
+ * sk_iters Sinkhorn iterations over the group's [rows, K] distances (batch-coupled), a level with
+ * sk_eps[l] <= 0 by the plain argmin.  idx_out[n, L] int64.  K[l] <= 1024. */
+size_t gr_rq_encode_sk_workspace_bytes(int64_t n, int32_t e, int32_t L, const int32_t* K);
+int gr_rq_encode_sk_f32(const float* z, int64_t n, int32_t e, int32_t L, const int32_t* K,
+                        const float* const* codebooks, const double* sk_eps, int32_t sk_iters,
+                        const int64_t* group_ptr, int64_t n_groups, int64_t* idx_out,
+                        void* workspace, size_t workspace_bytes, void* stream);
+
 /* ------------------------------------------------------------------------------------------ */
 /* SASRec.  Parameters of one model, as device pointers to the tensors of SASRec.state_dict()
  * (SASRec/model.py:17-47).  Per-block fields are host arrays of length n_blocks.  The dead

@@ -1,0 +1,68 @@
+"""RQVAE.get_indices(use_sk=True) (Sinkhorn collision re-encode) and the infer.py code emission on
+the GPU vs the reference's golden fixtures (tests/golden/make_golden_sk.py).
+
+Bar: semantic IDs equal to the reference's.  The Sinkhorn runs in float64 like the reference; its
+inputs are the fp32 distances, so a row can only move where the reference itself sits on a near-tie
+(reported; the count is asserted small)."""
+import numpy as np
+import pytest
+import torch
+
+import golden_lib as gl
+from test_rq_sk_oracle import _case
+
+pytestmark = pytest.mark.gpu
+CASES = ["rq_sk_csv_3x8", "rq_sk_syn_3x16"]
+
+
+def model_of(name, dev, eps):
+    from gr_amd import RQVAE
+    sd, out, meta = gl.load(name)
+    m = RQVAE(in_dim=768, num_emb_list=[meta["K"]] * meta["L"], e_dim=32, layers=[256, 128],
+              dropout_prob=0.1, sk_epsilons=list(eps), sk_iters=meta["sk_iters"])
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()}, strict=False)
+    return m.to(dev).eval()
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_grouped_sinkhorn_reencode_matches_reference(name, dev):
+    """Every collision round's groups, all in one launch, against the reference's per-group calls."""
+    x, _, _, _, out, meta = _case(name)
+    L = meta["L"]
+    m = model_of(name, dev, [0.0] * (L - 1) + [0.01])       # infer.py:109-110
+    rows, ptr = out["round_rows"], out["round_ptr"]
+    sizes = np.diff(ptr)
+    got = m.get_indices_groups(x[torch.from_numpy(rows)].to(dev), sizes.tolist()).cpu().numpy()
+    bad = (got != out["round_out"]).any(1)
+    print(f"\n{name}: {bad.sum()} / {len(bad)} re-encoded rows differ")
+    assert bad.sum() <= max(1, len(bad) // 500)
+    # a single group through the drop-in get_indices(use_sk=True) = the same rows of the launch
+    r0 = torch.from_numpy(rows[ptr[0]:ptr[1]])
+    assert np.array_equal(m.get_indices(x[r0].to(dev), use_sk=True).cpu().numpy(), got[:ptr[1]])
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_sinkhorn_every_level_matches_reference(name, dev):
+    x, _, _, _, out, meta = _case(name)
+    m = model_of(name, dev, [0.01] * meta["L"])
+    rows, ptr = out["all_rows"], out["all_ptr"]
+    got = m.get_indices_groups(x[torch.from_numpy(rows)].to(dev), np.diff(ptr).tolist()).cpu().numpy()
+    bad = (got != out["all_out"]).any(1)
+    print(f"\n{name}: {bad.sum()} / {len(bad)} rows differ")
+    assert bad.sum() <= max(1, len(bad) // 500)
+
+
+def test_infer_code_emission_matches_reference(dev, tmp_path):
+    """RQ-VAE/infer.py end to end on the config-1 items: codes, 30 collision rounds, dedup digit,
+    .npy + mapping json."""
+    import json
+    from gr_amd.infer import generate_codes, save_codes
+    x, _, _, _, out, meta = _case("rq_sk_csv_3x8")
+    m = model_of("rq_sk_csv_3x8", dev, [0.01] * meta["L"])
+    codes, final, stats = generate_codes(m, x, dev)
+    assert np.array_equal(codes, out["codes"]) and np.array_equal(final, out["final"])
+    assert stats["rounds"] == meta["rounds"]
+    f = str(tmp_path / "codes.npy")
+    mp = save_codes(final, f)
+    assert np.array_equal(np.load(f), final)
+    assert json.load(open(mp))["3"] == final[3].tolist()
