@@ -350,3 +350,48 @@ extern "C" int gr_rq_encode_f32(const float* x, int64_t n, int32_t n_linear, con
   }
   return launch_quantize(z, n, e, L, lv, idx_out, best_out, gap_out, st);
 }
+
+// MLPLayers.forward (RQ-VAE/models/layers.py:42-43, eval): z[n, dims[n_linear]] = the encoder
+// output alone — the fused persistent kernel when the shape is in -> 256 -> 128 -> 32, the
+// layer-wise path otherwise.  Workspace: gr_rq_mlp_workspace_bytes.
+extern "C" size_t gr_rq_mlp_workspace_bytes(int64_t n, int32_t n_linear, const int32_t* dims) {
+  if (n < 0 || n_linear < 1 || !dims) return 0;
+  int widest = 0;
+  for (int i = 1; i <= n_linear; ++i) widest = dims[i] > widest ? dims[i] : widest;
+  return 2 * gr::align_up((size_t)n * widest * 4, 256) + 256;
+}
+
+extern "C" int gr_rq_mlp_f32(const float* x, int64_t n, int32_t n_linear, const int32_t* dims,
+                             const float* const* weights, const float* const* biases, float* z_out,
+                             void* workspace, size_t workspace_bytes, void* stream) {
+  using namespace gr;
+  clear_error();
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (n_linear < 1 || n_linear > GR_MAX_LINEAR || !dims || !weights || n < 0)
+    return fail(GR_ERR_ARG, "gr_rq_mlp_f32: bad encoder description");
+  const size_t need = gr_rq_mlp_workspace_bytes(n, n_linear, dims);
+  if (!workspace || workspace_bytes < need)
+    return fail(GR_ERR_WORKSPACE, "gr_rq_mlp_f32: workspace too small (need " + std::to_string(need) + " bytes)");
+  if (n == 0) return GR_OK;
+  if (!x || !z_out) return fail(GR_ERR_ARG, "gr_rq_mlp_f32: null x / z_out");
+  if (option("rq_fused") == 1) {
+    const int rc = gr_rq_encoder_fused_launch(x, n, n_linear, dims, weights, biases, z_out, st);
+    if (rc != GR_ERR_UNSUPPORTED) return rc;
+    clear_error();
+  }
+  char* ws = reinterpret_cast<char*>(align_up(reinterpret_cast<uintptr_t>(workspace), 256));
+  int widest = 0;
+  for (int i = 1; i <= n_linear; ++i) widest = dims[i] > widest ? dims[i] : widest;
+  float* buf[2] = {reinterpret_cast<float*>(ws),
+                   reinterpret_cast<float*>(ws + align_up((size_t)n * widest * 4, 256))};
+  const float* cur = x;
+  for (int i = 0; i < n_linear; ++i) {
+    const bool last = i == n_linear - 1;
+    float* out = last ? z_out : buf[i & 1];
+    const int rc = gr_linear_launch(cur, n, dims[i], weights[i], dims[i + 1], biases ? biases[i] : nullptr,
+                                    nullptr, 0, last ? GR_ACT_NONE : GR_ACT_RELU, out, dims[i + 1], st);
+    if (rc) return rc;
+    cur = out;
+  }
+  return GR_OK;
+}

@@ -201,13 +201,36 @@ def rq_encode(x, weights, biases, codebooks, with_gap=False, with_z=False):
     return out[0] if len(out) == 1 else tuple(out)
 
 
+def rq_mlp(x, weights, biases):
+    """MLPLayers.forward (RQ-VAE/models/layers.py:42-43, eval): the encoder output ``z`` alone."""
+    L.require_gpu(x, *weights)
+    x2 = L.as_f32(x)
+    n = x2.shape[0]
+    ws = [L.as_f32(w) for w in weights]
+    bs = [L.as_f32(b) for b in biases]
+    dims = [x2.shape[1]] + [w.shape[0] for w in ws]
+    for i, w in enumerate(ws):
+        if w.shape[1] != dims[i]:
+            raise RuntimeError(f"rq_mlp: Linear {i} expects {w.shape[1]} inputs, got {dims[i]}")
+    dev = x.device
+    lib = L.lib()
+    dims_c = L.i32_array(dims)
+    nbytes = lib.gr_rq_mlp_workspace_bytes(n, len(ws), dims_c)
+    wsp = L.workspace(nbytes, dev)
+    z = torch.empty((n, dims[-1]), dtype=torch.float32, device=dev)
+    with torch.cuda.device(dev):
+        L.check(lib.gr_rq_mlp_f32(L.ptr(x2), n, len(ws), dims_c, L.ptr_array(ws), L.ptr_array(bs),
+                                  L.ptr(z), L.ptr(wsp), nbytes, L.stream_of(dev)), "gr_rq_mlp_f32")
+    return z
+
+
 def rq_encode_sk(x, weights, biases, codebooks, sk_eps, sk_iters, group_sizes=None):
     """RQVAE.get_indices(xs, use_sk=True) (RQ-VAE/models/rqvae.py:67-71 with vq.py:76-84) for
     independent row groups in ONE launch: ``group_sizes`` partitions the rows of ``x`` into
     consecutive groups, each one reference call (default: the whole batch is one group)."""
     L.require_gpu(x, *weights, *codebooks)
     n = x.shape[0]
-    _, z = rq_encode(x, weights, biases, codebooks, with_z=True)
+    z = rq_mlp(x, weights, biases)
     cbs = [L.as_f32(c) for c in codebooks]
     e = z.shape[1]
     Ks = [c.shape[0] for c in cbs]

@@ -77,10 +77,10 @@ class MLPLayers(nn.Module):
         if self.use_bn:
             raise NotImplementedError("gr_amd: BatchNorm encoders are not supported (bn=False in "
                                       "RQ-VAE/main.py)")
+        if self.training and self.dropout > 0:
+            raise RuntimeError("gr_amd MLPLayers runs the eval-mode encoder: call .eval()")
         lin = self.linears()
-        for i, m in enumerate(lin):
-            x = ops.linear(x, m.weight, m.bias, act="relu" if i < len(lin) - 1 else "none")
-        return x
+        return ops.rq_mlp(x, [m.weight.detach() for m in lin], [m.bias.detach() for m in lin])
 
 
 class VectorQuantizer(nn.Module):

@@ -1,16 +1,23 @@
 #!/usr/bin/env python3
 """Benchmark of the two hot paths (BASELINE.json metric:
-"RQ-VAE items encoded/s + SASRec seqs scored/s @1/8 GPU").
+"RQ-VAE items encoded/s + SASRec seqs scored/s @1/8 GPU; HR@10/NDCG@10 parity").
 
     python bench.py [--gpus N --steps K --warmup W]
-    torchrun --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
 
-Primary line (``value``): RQ-VAE encode, config C2 = 3x256 codebooks, in 768 -> [256,128] -> e 32,
+Primary line (``value``): RQ-VAE encode at config C2 = 3x256 codebooks, in 768 -> [256,128] -> e 32,
 100k synthetic items per rank per step (``RQVAE.get_indices`` on device-resident inputs).  Items
-shard across ranks with no collective ("scaling": "weak").  The SASRec scoring config C3 (2 blocks,
-d 64, n 50, 100k-item catalog, B users per rank per step, ``SASRec.predict``) is reported in the
-same JSON line under "sasrec".  Rank 0 also times the CPU oracle (oracle/) on a bounded sample of
-the same workload ("cpu_baseline").
+shard across ranks with no collective ("scaling": "weak").  The same JSON line carries:
+  * "sasrec"    — C3: SASRec.predict, 2 blocks, d 64, n 50, 100k-item catalog, logits written
+                  (users shard across ranks, no collective), plus the fused rank path (no logits);
+  * "rq_c4"     — C4: 4x1024 codebooks, a fixed 10M-item catalog split over the ranks (strong);
+  * "sasrec_c5" — C5: d 128, n 200, 1M-item catalog sharded over the ranks: users' hidden states
+                  all-gathered, every rank scores its catalog shard, strict-'>' counts all-reduced
+                  and per-shard top-10 all-gathered over RCCL (strong scaling).
+Each "roofline" is for the DOMINANT kernel of its path, timed alone with HIP events on the launch
+stream; "traffic" (HBM bytes per launch) comes from the committed rocprofv3 PMC summary
+(profiles/traffic.json, FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM).  Rank 0 at N=1 also
+times the CPU oracle (oracle/) on a bounded sample of the same workloads ("cpu_baseline").
 """
 import argparse
 import json
@@ -25,20 +32,25 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 import gr_amd  # noqa: E402
-from gr_amd import synth  # noqa: E402
+from gr_amd import ops, synth  # noqa: E402
 
 METRIC = "RQ-VAE items encoded/s + SASRec seqs scored/s @1/8 GPU; HR@10/NDCG@10 parity"
 FP32_PEAK_TFLOPS = 157.3      # MI355X fp32 matrix (= vector) peak, MI355X_MICROARCH.md
 HBM_PEAK_GBS = 8000.0
 
-# Algorithmic work per unit (SURVEY §8d / DESIGN.md)
-RQ_IN, RQ_LAYERS, RQ_E, RQ_L, RQ_K = 768, (256, 128), 32, 3, 256
-RQ_FLOP_PER_ITEM = 2 * (768 * 256 + 256 * 128 + 128 * 32) + 2 * RQ_L * RQ_K * RQ_E   # 516,096
-RQ_BYTES_PER_ITEM = 768 * 4 + RQ_L * 8                                                # 3,096
-SAS_D, SAS_N, SAS_ITEMS, SAS_MLP, SAS_BLOCKS = 64, 50, 100_000, 64, 2
+# Algorithmic work per unit (SURVEY §8d / DESIGN.md §4)
+ENC_FLOP_PER_ITEM = 2 * (768 * 256 + 256 * 128 + 128 * 32)          # 466,944: encoder MLP
 
 
-def sas_flop_per_user(d=SAS_D, n=SAS_N, items=SAS_ITEMS, mlp=SAS_MLP, blocks=SAS_BLOCKS):
+def rq_flop_per_item(L, K, e=32):
+    return ENC_FLOP_PER_ITEM + 2 * L * K * e                          # C2: 516,096
+
+
+def rq_bytes_per_item(L):
+    return 768 * 4 + L * 8                                            # C2: 3,096
+
+
+def sas_flop_per_user(d, n, items, mlp=64, blocks=2):
     """Reference formulation (dead W_Q/K/V excluded): per block in-proj 2*n*d*3d, scores and P.V
     2*2*n*n*d, out-proj 2*n*d*d, FFN 2*2*n*d*mlp; scoring 2*d*(items+1)."""
     per_block = 2 * n * d * 3 * d + 4 * n * n * d + 2 * n * d * d + 4 * n * d * mlp
@@ -52,10 +64,20 @@ def parse():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--rq-items", type=int, default=100_000)
     ap.add_argument("--sas-batch", type=int, default=2048)
+    ap.add_argument("--c4-items", type=int, default=10_000_000)
+    ap.add_argument("--c5-batch", type=int, default=512)
+    ap.add_argument("--c5-items", type=int, default=1_000_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="budget per CPU baseline leg")
-    ap.add_argument("--skip-sasrec", action="store_true")
+    ap.add_argument("--skip", default="", help="comma list of legs to skip: sasrec,c4,c5")
     return ap.parse_args()
+
+
+def sync_all(world):
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
 
 
 def timed(fn, steps, warmup, world):
@@ -63,20 +85,14 @@ def timed(fn, steps, warmup, world):
     wall seconds, mean device ms per step from HIP events on the launch stream)."""
     for _ in range(warmup):
         fn()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
+    sync_all(world)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
     t0 = time.perf_counter()
     for s, e in ev:
         s.record()
         fn()
         e.record()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
+    sync_all(world)
     wall = time.perf_counter() - t0
     dev_ms = sum(s.elapsed_time(e) for s, e in ev) / steps
     if world > 1:
@@ -84,6 +100,37 @@ def timed(fn, steps, warmup, world):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         wall = float(t.item())
     return wall, dev_ms
+
+
+def kernel_ms(fn, reps=10, warmup=2):
+    """Mean device time of one launch of ``fn`` (HIP events on torch's current stream, which is the
+    stream every gr_amd op enqueues on)."""
+    for _ in range(warmup):
+        fn()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps
+
+
+def traffic_of(kernel):
+    """HBM bytes per launch of ``kernel`` from the committed PMC summary, or None."""
+    p = os.path.join(ROOT, "profiles", "traffic.json")
+    if not os.path.exists(p):
+        return None, None
+    t = json.load(open(p)).get(kernel)
+    return (t["bytes_per_launch"], t["source"]) if t else (None, None)
+
+
+def roofline(kernel, flop, ms, bound="mfma"):
+    ach = flop / (ms * 1e-3) / 1e12
+    tr, src = traffic_of(kernel)
+    return {"bound": bound, "achieved": ach, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "frac": ach / FP32_PEAK_TFLOPS, "traffic": tr, "traffic_source": src, "kernel": kernel,
+            "flop_per_launch": flop, "kernel_ms": ms}
 
 
 def cpu_threads():
@@ -112,83 +159,153 @@ def cpu_rq_baseline(model, budget_s):
                       f"{dt:.1f} s, fp32 torch CPU)"}
 
 
-def cpu_sas_baseline(model, budget_s):
+def cpu_sas_baseline(model, budget_s, n, items):
     from oracle import sasrec_oracle
     torch.set_num_threads(cpu_threads())
     sd = {k: v.detach().cpu() for k, v in model.state_dict().items()}
-    seqs = synth.sequences(128, SAS_N, SAS_ITEMS, 777, "cuda").cpu()
-    sasrec_oracle.predict(seqs[:8], sd, SAS_BLOCKS, 1, 1e-8)
-    n, t0 = 0, time.perf_counter()
-    while time.perf_counter() - t0 < budget_s or n == 0:
-        sasrec_oracle.predict(seqs, sd, SAS_BLOCKS, 1, 1e-8)
-        n += seqs.shape[0]
+    seqs = synth.sequences(128, n, items, 777, "cuda").cpu()
+    sasrec_oracle.predict(seqs[:8], sd, model.num_blocks, model.num_heads, 1e-8)
+    cnt, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < budget_s or cnt == 0:
+        sasrec_oracle.predict(seqs, sd, model.num_blocks, model.num_heads, 1e-8)
+        cnt += seqs.shape[0]
     dt = time.perf_counter() - t0
-    return {"value": n / dt, "unit": "seqs/s", "cores": torch.get_num_threads(), "kind": "port",
-            "sample": f"oracle/sasrec_oracle.predict, {n} users in batches of 128 (C3 shapes, "
-                      f"{dt:.1f} s)"}
+    return {"value": cnt / dt, "unit": "seqs/s", "cores": torch.get_num_threads(), "kind": "port",
+            "sample": f"oracle/sasrec_oracle.predict, {cnt} users in batches of 128 "
+                      f"(d {model.d}, n {n}, {items} items, {dt:.1f} s)"}
+
+
+def bench_rq_c2(a, world, rank, dev):
+    L, K = 3, 256
+    model = synth.rqvae_model(L, K, dev)
+    x = synth.items(a.rq_items, 1000 + rank, dev)
+    wall, dev_ms = timed(lambda: model.get_indices(x), a.steps, a.warmup, world)
+    lin = model.encoder.linears()
+    ws, bs = [l.weight.detach() for l in lin], [l.bias.detach() for l in lin]
+    enc_ms = kernel_ms(lambda: ops.rq_mlp(x, ws, bs))
+    line = {
+        "metric": METRIC, "value": a.rq_items * world * a.steps / wall, "unit": "items/s",
+        "n_gpus": world, "steps": a.steps, "warmup": a.warmup, "ms_per_step": wall / a.steps * 1e3,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+        "data": "synthetic",
+        "config": {"workload": "rq_c2: RQ-VAE get_indices, 3x256 codebooks, in 768 -> [256,128] -> "
+                               "e 32, data-derived codebooks, BERT-statistics item embeddings",
+                   "items_per_rank_per_step": a.rq_items, "global_batch": a.rq_items * world,
+                   "parallelism": f"item-sharded x{world}, no collective"},
+        "roofline": roofline("rq_encoder_kernel<256,128>", ENC_FLOP_PER_ITEM * a.rq_items, enc_ms),
+        "call": {"kernels": "rq_encoder_kernel + rq_quantize_kernel", "device_ms": dev_ms,
+                 "flop_per_item": rq_flop_per_item(L, K),
+                 "frac_of_fp32_peak": rq_flop_per_item(L, K) * a.rq_items / (dev_ms * 1e-3) / 1e12 / FP32_PEAK_TFLOPS,
+                 "hbm_algorithmic_GBs": rq_bytes_per_item(L) * a.rq_items / (dev_ms * 1e-3) / 1e9,
+                 "quantize_ms": dev_ms - enc_ms},
+    }
+    return line, model
+
+
+def bench_rq_c4(a, world, rank, dev):
+    """C4: a fixed catalog of c4_items split over the ranks (strong scaling), 4x1024 codebooks."""
+    L, K = 4, 1024
+    model = synth.rqvae_model(L, K, dev, seed=4)
+    lo = a.c4_items * rank // world
+    hi = a.c4_items * (rank + 1) // world
+    x = synth.items(hi - lo, 4000 + rank, dev)
+    steps, warm = max(2, min(a.steps, 5)), 1
+    wall, dev_ms = timed(lambda: model.get_indices(x), steps, warm, world)
+    return {"metric": "items_encoded/s", "value": a.c4_items * steps / wall, "unit": "items/s",
+            "scaling": "strong", "ms_per_step": wall / steps * 1e3, "steps": steps,
+            "config": {"workload": "rq_c4: RQ-VAE get_indices, 4x1024 codebooks, in 768 -> [256,128] -> e 32",
+                       "catalog_items": a.c4_items, "items_per_rank": hi - lo,
+                       "parallelism": f"item-sharded x{world}, no collective"},
+            "call": {"device_ms": dev_ms, "flop_per_item": rq_flop_per_item(L, K),
+                     "frac_of_fp32_peak": rq_flop_per_item(L, K) * (hi - lo) / (dev_ms * 1e-3) / 1e12 / FP32_PEAK_TFLOPS}}
+
+
+def bench_sas_c3(a, world, rank, dev):
+    d, n, items = 64, 50, 100_000
+    p = synth.sasrec_params(d, n, 2, 1, 64, dev)
+    model = synth.sasrec_model(items, p, dev)
+    seqs = synth.sequences(a.sas_batch, n, items, 2000 + rank, dev)
+    out = torch.empty((a.sas_batch, items + 1), dtype=torch.float32, device=dev)
+    binding = ops.SasrecBinding(model)
+    wall, dev_ms = timed(lambda: ops.sasrec_predict(binding, seqs, out=out), a.steps, a.warmup, world)
+    h = model.last_hidden(seqs)
+    table = model.item_emb.weight.detach()
+    score_ms = kernel_ms(lambda: ops.score(h, table, out=out))
+    fwd_ms = kernel_ms(lambda: model.last_hidden(seqs))
+    targets = torch.randint(1, items + 1, (a.sas_batch,), generator=torch.Generator(device=dev).manual_seed(5), device=dev)
+    rank_ms = kernel_ms(lambda: ops.score_rank(h, table, targets))
+    fl = sas_flop_per_user(d, n, items)
+    res = {"metric": "seqs_scored/s", "value": a.sas_batch * world * a.steps / wall, "unit": "seqs/s",
+           "ms_per_step": wall / a.steps * 1e3, "scaling": "weak",
+           "config": {"workload": "sas_c3: SASRec predict, 2 blocks, d 64, n 50, H 1, mlp 64, "
+                                  "100k-item full-catalog logits written", "users_per_rank_per_step": a.sas_batch,
+                      "parallelism": f"user-sharded x{world}, no collective"},
+           "roofline": roofline("score_kernel<64>", 2 * d * (items + 1) * a.sas_batch, score_ms),
+           "call": {"device_ms": dev_ms, "flop_per_user": fl,
+                    "frac_of_fp32_peak": fl * a.sas_batch / (dev_ms * 1e-3) / 1e12 / FP32_PEAK_TFLOPS,
+                    "forward_ms": fwd_ms, "score_ms": score_ms,
+                    "logits_write_GBs": a.sas_batch * (items + 1) * 4 / (score_ms * 1e-3) / 1e9},
+           "rank_fused": {"note": "forward + target logit + strict count, logits never written",
+                          "value": a.sas_batch / ((fwd_ms + rank_ms) * 1e-3), "unit": "seqs/s",
+                          "rank_ms": rank_ms,
+                          "frac_of_fp32_peak": 2 * d * (items + 1) * a.sas_batch / (rank_ms * 1e-3) / 1e12 / FP32_PEAK_TFLOPS}}
+    return res, model, (n, items)
+
+
+def bench_sas_c5(a, world, rank, dev):
+    """C5: the catalog sharded over the ranks; every rank runs the transformer for its share of the
+    users, hidden states are all-gathered, each rank scores ALL users against its catalog shard,
+    then counts are all-reduced and top-10 lists all-gathered (gr_amd.dist)."""
+    from gr_amd import dist as D
+    d, n, items, B = 128, 200, a.c5_items, a.c5_batch
+    p = synth.sasrec_params(d, n, 2, 1, 64, dev)
+    model = synth.sasrec_model(items, p, dev, seed=5)
+    seqs = synth.sequences(B, n, items, 5000, dev)            # same users on every rank
+    targets = torch.randint(1, items + 1, (B,), generator=torch.Generator(device=dev).manual_seed(6), device=dev)
+    ulo, uhi = D.shard_range(B, rank, world)
+    lo, hi = D.shard_range(items + 1, rank, world)
+    shard = model.item_emb.weight.detach()[lo:hi]
+
+    def step():
+        hl = model.last_hidden(seqs[ulo:uhi])
+        h = D.all_gather_rows(hl) if world > 1 else hl
+        return D.sharded_rank_topk(h, shard, lo, targets, k=10)
+
+    steps, warm = max(2, min(a.steps, 10)), 2
+    wall, dev_ms = timed(step, steps, warm, world)
+    return {"metric": "seqs_scored/s", "value": B * steps / wall, "unit": "seqs/s", "scaling": "strong",
+            "ms_per_step": wall / steps * 1e3, "steps": steps,
+            "config": {"workload": "sas_c5: SASRec d 128, n 200, 2 blocks, 1M-item catalog, rank + top-10",
+                       "users_per_step": B, "catalog_rows": items + 1, "rows_per_rank": hi - lo,
+                       "parallelism": f"catalog-sharded x{world}: RCCL all-gather h + top-k, all-reduce counts"
+                       if world > 1 else "single shard"},
+            "call": {"device_ms_rank0": dev_ms, "flop_per_user": sas_flop_per_user(d, n, items)}}
 
 
 def main():
     a = parse()
+    skip = set(s for s in a.skip.split(",") if s)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if a.gpus != world:
-        if world == 1 and a.gpus > 1:
-            sys.exit("bench.py: --gpus N>1 must be launched with torch.distributed.run (one rank per GPU)")
+    if a.gpus != world and world == 1 and a.gpus > 1:
+        sys.exit("bench.py: --gpus N>1 must be launched with torch.distributed.run (one rank per GPU)")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
 
-    # ---------------- RQ-VAE encode, config C2 (items shard over ranks: per-rank batch fixed)
-    rq_model = synth.rqvae_model(RQ_L, RQ_K, dev)
-    x = synth.items(a.rq_items, 1000 + rank, dev)
-    rq_wall, rq_dev_ms = timed(lambda: rq_model.get_indices(x), a.steps, a.warmup, world)
-    items_total = a.rq_items * world * a.steps
-    rq_value = items_total / rq_wall
-    achieved_tf = RQ_FLOP_PER_ITEM * a.rq_items / (rq_dev_ms * 1e-3) / 1e12
-    line = {
-        "metric": METRIC, "value": rq_value, "unit": "items/s", "n_gpus": world, "steps": a.steps,
-        "warmup": a.warmup, "ms_per_step": rq_wall / a.steps * 1e3, "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
-        "config": {"workload": "rq_c2: RQ-VAE get_indices, 3x256 codebooks, in 768 -> [256,128] -> "
-                               "e 32, data-derived codebooks",
-                   "items_per_rank_per_step": a.rq_items, "global_batch": a.rq_items * world,
-                   "parallelism": f"item-sharded x{world}, no collective"},
-        "roofline": {"bound": "mfma", "achieved": achieved_tf, "peak": FP32_PEAK_TFLOPS,
-                     "unit": "TFLOP/s", "frac": achieved_tf / FP32_PEAK_TFLOPS, "traffic": None,
-                     "kernel": "gr_rq_encode_f32 (encoder linears + quantize, per call)",
-                     "flop_per_unit": RQ_FLOP_PER_ITEM, "units_per_launch": a.rq_items,
-                     "device_ms_per_launch": rq_dev_ms,
-                     "hbm_algorithmic_GBs": RQ_BYTES_PER_ITEM * a.rq_items / (rq_dev_ms * 1e-3) / 1e9},
-    }
-    # ---------------- SASRec predict, config C3 (users shard over ranks)
-    if not a.skip_sasrec:
-        p = synth.sasrec_params(SAS_D, SAS_N, SAS_BLOCKS, 1, SAS_MLP, dev)
-        sas_model = synth.sasrec_model(SAS_ITEMS, p, dev)
-        seqs = synth.sequences(a.sas_batch, SAS_N, SAS_ITEMS, 2000 + rank, dev)
-        out = torch.empty((a.sas_batch, SAS_ITEMS + 1), dtype=torch.float32, device=dev)
-        binding = gr_amd.ops.SasrecBinding(sas_model)
-        sas_wall, sas_dev_ms = timed(lambda: gr_amd.ops.sasrec_predict(binding, seqs, out=out),
-                                     a.steps, a.warmup, world)
-        users = a.sas_batch * world * a.steps
-        fl = sas_flop_per_user()
-        tf = fl * a.sas_batch / (sas_dev_ms * 1e-3) / 1e12
-        line["sasrec"] = {
-            "metric": "seqs_scored/s", "value": users / sas_wall, "unit": "seqs/s",
-            "ms_per_step": sas_wall / a.steps * 1e3,
-            "config": {"workload": "sas_c3: SASRec predict, 2 blocks, d 64, n 50, H 1, mlp 64, "
-                                   "100k-item full-catalog logits", "users_per_rank_per_step": a.sas_batch},
-            "roofline": {"bound": "mfma", "achieved": tf, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
-                         "frac": tf / FP32_PEAK_TFLOPS, "flop_per_unit": fl,
-                         "kernel": "gr_sasrec_predict_f32 (per call)", "device_ms_per_launch": sas_dev_ms,
-                         "logits_write_GBs": a.sas_batch * (SAS_ITEMS + 1) * 4 / (sas_dev_ms * 1e-3) / 1e9},
-        }
+    line, rq_model = bench_rq_c2(a, world, rank, dev)
+    if "sasrec" not in skip:
+        line["sasrec"], sas_model, (sn, sitems) = bench_sas_c3(a, world, rank, dev)
+    if "c4" not in skip:
+        line["rq_c4"] = bench_rq_c4(a, world, rank, dev)
+    if "c5" not in skip:
+        line["sasrec_c5"] = bench_sas_c5(a, world, rank, dev)
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         line["cpu_baseline"] = cpu_rq_baseline(rq_model, a.cpu_seconds)
-        if not a.skip_sasrec:
-            line["sasrec"]["cpu_baseline"] = cpu_sas_baseline(sas_model, a.cpu_seconds)
+        if "sasrec" not in skip:
+            line["sasrec"]["cpu_baseline"] = cpu_sas_baseline(sas_model, a.cpu_seconds, sn, sitems)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -103,6 +103,13 @@ int gr_rq_encode_f32(const float* x, int64_t n, int32_t n_linear, const int32_t*
                      float* best_out, float* gap_out, float* z_out, void* workspace,
                      size_t workspace_bytes, void* stream);
 
+/* MLPLayers.forward in eval mode (RQ-VAE/models/layers.py:42-43): z_out[n, dims[n_linear]] = the
+ * encoder output alone (ReLU after every Linear but the last).  Same kernels as gr_rq_encode_f32. */
+size_t gr_rq_mlp_workspace_bytes(int64_t n, int32_t n_linear, const int32_t* dims);
+int gr_rq_mlp_f32(const float* x, int64_t n, int32_t n_linear, const int32_t* dims,
+                  const float* const* weights, const float* const* biases, float* z_out,
+                  void* workspace, size_t workspace_bytes, void* stream);
+
 /* RQVAE.get_indices(xs, use_sk=True) over independent row groups (the collision re-encode of
  * RQ-VAE/infer.py:108-130; vq.py:52-61, 76-84; layers.py:85-108).  z[n, e]: encoder outputs (as
  * gr_rq_encode_f32's z_out), rows grouped contiguously: group g = rows [group_ptr[g],
