@@ -78,15 +78,18 @@ def sharded_rank_topk(h, table_shard, row_offset, targets, k=10, group=None, mas
     world = dist.get_world_size(group) if dist.is_initialized() else 1
     if world > 1:
         dist.all_reduce(ts, op=dist.ReduceOp.SUM, group=group)
-    cnt = counter(logits, ts)
+    kk = min(k, rows) if rows > 0 else 0
+    if kk > 0 and topk_fn is t_fn and counter is c_fn:
+        v, i, cnt = topk_fn(logits, kk, row_offset, thresholds=ts)   # one pass: top-k + counts
+    else:
+        cnt = counter(logits, ts)
+        if kk > 0:
+            v, i = topk_fn(logits, kk, row_offset)
+        else:
+            v = torch.empty((logits.shape[0], 0), dtype=logits.dtype, device=logits.device)
+            i = torch.empty((logits.shape[0], 0), dtype=torch.int64, device=logits.device)
     if world > 1:
         dist.all_reduce(cnt, op=dist.ReduceOp.SUM, group=group)
-    kk = min(k, rows) if rows > 0 else 0
-    if kk > 0:
-        v, i = topk_fn(logits, kk, row_offset)
-    else:
-        v = torch.empty((logits.shape[0], 0), dtype=logits.dtype, device=logits.device)
-        i = torch.empty((logits.shape[0], 0), dtype=torch.int64, device=logits.device)
     if kk < k:
         pad = k - kk
         v = torch.cat([v, torch.full((v.shape[0], pad), float("-inf"), dtype=v.dtype, device=v.device)], 1)

@@ -79,19 +79,25 @@ def count_gt(logits, thresholds):
     return out
 
 
-def topk(logits, k, id_offset=0):
-    """Per-row top-k: (values [B,k] descending, ids [B,k] = column + id_offset); ties -> lower id."""
+def topk(logits, k, id_offset=0, thresholds=None):
+    """Per-row top-k: (values [B,k] descending, ids [B,k] = column + id_offset); ties -> lower id.
+    With ``thresholds`` the same pass also returns the strict counts ``#{j : l[b,j] > thr[b]}``."""
     L.require_gpu(logits)
     if logits.stride(1) != 1:
         logits = logits.contiguous()
     B, cols = logits.shape
-    vals = torch.empty((B, k), dtype=torch.float32, device=logits.device)
-    ids = torch.empty((B, k), dtype=torch.int64, device=logits.device)
-    with torch.cuda.device(logits.device):
+    dev = logits.device
+    vals = torch.empty((B, k), dtype=torch.float32, device=dev)
+    ids = torch.empty((B, k), dtype=torch.int64, device=dev)
+    th = L.as_f32(thresholds.reshape(-1)) if thresholds is not None else None
+    cnt = torch.empty(B, dtype=torch.int64, device=dev) if th is not None else None
+    nbytes = L.lib().gr_topk_workspace_bytes(B, cols, k)
+    wsp = L.workspace(nbytes, dev)
+    with torch.cuda.device(dev):
         L.check(L.lib().gr_topk_f32(L.ptr(logits), B, cols, logits.stride(0), k, id_offset,
-                                    L.ptr(vals), L.ptr(ids), L.stream_of(logits.device)),
-                "gr_topk_f32")
-    return vals, ids
+                                    L.ptr(vals), L.ptr(ids), L.ptr(th), L.ptr(cnt), L.ptr(wsp), nbytes,
+                                    L.stream_of(dev)), "gr_topk_f32")
+    return (vals, ids) if th is None else (vals, ids, cnt)
 
 
 def score_pairs(h, table, ids, mask_col0=True):

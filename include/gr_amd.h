@@ -181,14 +181,19 @@ int gr_rank_f32(const float* logits, int64_t B, int64_t cols, int64_t ld, const 
                 int32_t mask_col0, int64_t* ranks_out, void* stream);
 
 /* Catalog-shard helpers.  count: cnt[b] = #{j < cols : l[b,j] > thresholds[b]}
- * (the strict '>' of SASRec/evaluate.py:32; summed over shards it gives rank - 1). */
+ * (the strict '>' of SASRec/evaluate.py:32; summed over shards it gives rank - 1).  B <= 65535. */
 int gr_count_gt_f32(const float* logits, int64_t B, int64_t cols, int64_t ld,
                     const float* thresholds, int64_t* counts_out, void* stream);
 
 /* Per-row top-k (k <= 64) of logits[B, cols]: values descending, ties to the lower column;
- * ids_out = column + id_offset (the shard's first catalog row); -1 pads rows with < k entries. */
+ * ids_out = column + id_offset (the shard's first catalog row); -1 pads rows with < k entries.
+ * When thresholds / counts_out are given (both or neither), the same single pass over the logits
+ * also produces gr_count_gt_f32's counts.  Rows are cut into segments (one workgroup each, local
+ * top-k to the workspace) and merged per row.  B <= 65535. */
+size_t gr_topk_workspace_bytes(int64_t B, int64_t cols, int32_t k);
 int gr_topk_f32(const float* logits, int64_t B, int64_t cols, int64_t ld, int32_t k,
-                int64_t id_offset, float* vals_out, int64_t* ids_out, void* stream);
+                int64_t id_offset, float* vals_out, int64_t* ids_out, const float* thresholds,
+                int64_t* counts_out, void* workspace, size_t workspace_bytes, void* stream);
 
 /* ------------------------------------------------------------------------------------------ */
 /* Fused rank without materialising logits (SASRec/evaluate.py:26-32).  Every

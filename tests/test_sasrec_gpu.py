@@ -252,3 +252,21 @@ def test_fused_forward_vs_oracle(d, heads, mlp, n, blocks, B, dev):
     err = ((got - ref).abs() / ref.abs().amax(1, keepdim=True)).max().item()
     assert err <= TOL, err
     assert torch.equal(m.last_hidden(seqs).cpu(), got_f[:, -1, :])
+
+
+@pytest.mark.parametrize("B,cols,ld", [(7, 100001, 100001), (33, 250000, 250003), (300, 5, 5), (2, 1, 1)])
+def test_segmented_topk_count_vs_torch(B, cols, ld, dev):
+    """Segmented top-k / count kernels on long, misaligned (odd stride) rows, single fused pass."""
+    from gr_amd import ops
+    g = torch.Generator().manual_seed(B + cols)
+    base = torch.randn(B, ld, generator=g)
+    base[:, cols // 3] = base[:, cols // 2]          # ties across segments: lower column wins
+    lg = base[:, :cols]
+    lgd = base.to(dev)[:, :cols]
+    thr = lg[torch.arange(B), torch.randint(0, cols, (B,), generator=g)]
+    k = min(10, cols)
+    v, i, c = ops.topk(lgd, k, id_offset=7, thresholds=thr.to(dev))
+    o = torch.argsort(lg, dim=1, descending=True, stable=True)[:, :k]
+    assert torch.equal(i.cpu(), o + 7) and torch.equal(v.cpu(), lg.gather(1, o))
+    assert torch.equal(c.cpu(), (lg > thr[:, None]).sum(1))
+    assert torch.equal(ops.count_gt(lgd, thr.to(dev)).cpu(), (lg > thr[:, None]).sum(1))
