@@ -281,9 +281,13 @@ static int run_forward(const gr_sasrec_params* p, const int64_t* seqs, int64_t B
     rc = gr_linear_launch(w.h, rows, d, p->in_proj_w[i], 3 * d, p->in_proj_b[i], nullptr, 0,
                           GR_ACT_NONE, w.qkv, 3 * d, st);
     if (rc) return rc;
-    hipLaunchKernelGGL(causal_attn_kernel, dim3((unsigned)(B * H), (unsigned)((n + ATT_QT - 1) / ATT_QT)),
-                       dim3(256), att_lds, st, w.qkv, w.o, n, H, hd, scale);
-    rc = check_launch("sasrec attention");
+    rc = gr_attn_mfma_launch(w.qkv, w.o, B, n, H, hd, scale, st);   // matrix cores (attn.hip)
+    if (rc == GR_ERR_UNSUPPORTED) {                                   // other head widths
+      clear_error();
+      hipLaunchKernelGGL(causal_attn_kernel, dim3((unsigned)(B * H), (unsigned)((n + ATT_QT - 1) / ATT_QT)),
+                         dim3(256), att_lds, st, w.qkv, w.o, n, H, hd, scale);
+      rc = check_launch("sasrec attention");
+    }
     if (rc) return rc;
     rc = gr_linear_launch(w.o, rows, d, p->out_proj_w[i], d, p->out_proj_b[i], w.x, d, GR_ACT_NONE,
                           w.x, d, st);
