@@ -17,11 +17,19 @@ static std::atomic<int64_t> g_sas_fused{1};
 // score_ablate (diagnostic, results INVALID when != 0): 1 = scoring kernel skips its logits
 // stores, 2 = skips its matrix work.  Used by scripts/ab_score.py to split the kernel's time.
 static std::atomic<int64_t> g_score_ablate{0};
+// topk_ablate (diagnostic, results INVALID when != 0): the fused score + top-k kernel skips 1 = all
+// top-k work (counts only), 2 = the appends and folds (keeps the per-chunk max test).
+static std::atomic<int64_t> g_topk_ablate{0};
+// topk_sample (1: gr_score_topk_f32 takes its threshold from a strided sample pass when the
+// catalog is long enough, 0: always one pass).  Same results either way; used for A/B timing.
+static std::atomic<int64_t> g_topk_sample{1};
 
 int64_t option(const char* name) {
   if (!strcmp(name, "rq_fused")) return g_rq_fused.load();
   if (!strcmp(name, "sas_fused")) return g_sas_fused.load();
   if (!strcmp(name, "score_ablate")) return g_score_ablate.load();
+  if (!strcmp(name, "topk_ablate")) return g_topk_ablate.load();
+  if (!strcmp(name, "topk_sample")) return g_topk_sample.load();
   return -1;
 }
 }  // namespace gr
@@ -32,6 +40,8 @@ extern "C" int gr_set_option(const char* name, int64_t value) {
   if (!strcmp(name, "rq_fused") && (value == 0 || value == 1)) { gr::g_rq_fused = value; return GR_OK; }
   if (!strcmp(name, "sas_fused") && (value == 0 || value == 1)) { gr::g_sas_fused = value; return GR_OK; }
   if (!strcmp(name, "score_ablate") && value >= 0 && value <= 2) { gr::g_score_ablate = value; return GR_OK; }
+  if (!strcmp(name, "topk_ablate") && value >= 0 && value <= 2) { gr::g_topk_ablate = value; return GR_OK; }
+  if (!strcmp(name, "topk_sample") && (value == 0 || value == 1)) { gr::g_topk_sample = value; return GR_OK; }
   return gr::fail(GR_ERR_ARG, std::string("gr_set_option: unknown option or value: ") + name);
 }
 

@@ -20,12 +20,12 @@ namespace gr {
 template <int HD>
 __global__ __launch_bounds__(256) void attn_mfma_kernel(const float* __restrict__ qkv,
                                                         float* __restrict__ out, int n, int H,
-                                                        float scale) {
+                                                        float scale, int qt_from) {
   constexpr int FT = HD / 32;            // feature tiles of the head
   const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
   const int w = threadIdx.x >> 6;
   const int bh = blockIdx.x, b = bh / H, hh = bh % H;
-  const int qt = blockIdx.y * 4 + w;     // this wave's query tile
+  const int qt = qt_from + blockIdx.y * 4 + w;   // this wave's query tile
   if (qt * 32 >= n) return;              // whole wave; no barrier in the kernel
   const int d = H * HD;
   const int64_t rs = 3LL * d;
@@ -113,17 +113,21 @@ __global__ __launch_bounds__(256) void attn_mfma_kernel(const float* __restrict_
 }  // namespace gr
 
 // Returns GR_ERR_UNSUPPORTED (message untouched) for head widths the kernel is not built for.
+// last_tile_only: only the query tile holding position n-1 (the rows a last-position-only forward
+// needs; every row is computed exactly as in the full launch).
 int gr_attn_mfma_launch(const float* qkv, float* out, int64_t B, int n, int H, int hd, float scale,
-                        hipStream_t st) {
+                        int last_tile_only, hipStream_t st) {
   using namespace gr;
   if (hd != 32 && hd != 64 && hd != 128) return GR_ERR_UNSUPPORTED;
   if (!aligned16(qkv) || !aligned16(out)) return GR_ERR_UNSUPPORTED;
   if (B * H > 0x7fffffffLL) return GR_ERR_UNSUPPORTED;
-  const dim3 g((unsigned)(B * H), (unsigned)((n + 127) / 128)), blk(256);
+  const int qt_from = last_tile_only ? (n - 1) / 32 : 0;
+  const dim3 g((unsigned)(B * H), last_tile_only ? 1u : (unsigned)((n + 127) / 128)),
+      blk(last_tile_only ? 64 : 256);
   switch (hd) {
-    case 32: hipLaunchKernelGGL(attn_mfma_kernel<32>, g, blk, 0, st, qkv, out, n, H, scale); break;
-    case 64: hipLaunchKernelGGL(attn_mfma_kernel<64>, g, blk, 0, st, qkv, out, n, H, scale); break;
-    default: hipLaunchKernelGGL(attn_mfma_kernel<128>, g, blk, 0, st, qkv, out, n, H, scale); break;
+    case 32: hipLaunchKernelGGL(attn_mfma_kernel<32>, g, blk, 0, st, qkv, out, n, H, scale, qt_from); break;
+    case 64: hipLaunchKernelGGL(attn_mfma_kernel<64>, g, blk, 0, st, qkv, out, n, H, scale, qt_from); break;
+    default: hipLaunchKernelGGL(attn_mfma_kernel<128>, g, blk, 0, st, qkv, out, n, H, scale, qt_from); break;
   }
   return check_launch("sasrec attention (mfma)");
 }

@@ -59,7 +59,7 @@ int gr_rq_encoder_fused_launch(const float* x, int64_t n, int32_t n_linear, cons
 int gr_sasrec_fused_launch(const gr_sasrec_params* p, const int64_t* seqs, int64_t B, int32_t n,
                            float* out, int32_t last_only, int32_t* err, hipStream_t st);
 int gr_attn_mfma_launch(const float* qkv, float* out, int64_t B, int n, int H, int hd, float scale,
-                        hipStream_t st);
+                        int last_tile_only, hipStream_t st);
 int gr_score_launch(const float* h, int64_t B, int32_t d, const float* table, int64_t rows,
                     float* logits, int64_t ld, hipStream_t st);
 int gr_linear_launch(const float* x, int64_t m, int32_t k, const float* w, int32_t n,

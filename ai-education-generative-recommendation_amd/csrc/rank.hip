@@ -6,6 +6,7 @@
 //              ids = column + id_offset (a shard's first catalog row)
 // One workgroup per row; the row is streamed once with 16-byte loads where alignment allows.
 #include "gr_common.h"
+#include "topk_list.h"
 
 namespace gr {
 
@@ -60,75 +61,6 @@ __global__ __launch_bounds__(256) void count_gt_kernel(const float* __restrict__
   }
 }
 
-// (value, column) order: larger value first, then smaller column.
-__device__ __forceinline__ bool better(float va, int64_t ia, float vb, int64_t ib) {
-  return va > vb || (va == vb && ia < ib);
-}
-
-// Per-thread sorted candidate list of KMAX entries (best first); NaN never enters.
-template <int KMAX>
-struct TopList {
-  float v[KMAX];
-  int64_t i[KMAX];
-  __device__ void init() {
-#pragma unroll
-    for (int q = 0; q < KMAX; ++q) {
-      v[q] = -__builtin_inff();
-      i[q] = INT64_MAX;
-    }
-  }
-  __device__ __forceinline__ void push(float cv, int64_t ci) {
-    if (!better(cv, ci, v[KMAX - 1], i[KMAX - 1])) return;
-#pragma unroll
-    for (int q = 0; q < KMAX; ++q) {   // insertion: carry the displaced entry down the list
-      if (better(cv, ci, v[q], i[q])) {
-        const float tv = v[q];
-        const int64_t ti = i[q];
-        v[q] = cv;
-        i[q] = ci;
-        cv = tv;
-        ci = ti;
-      }
-    }
-  }
-  // k rounds of a block-wide arg-best over the heads of the per-thread lists; emit(q, v, i)
-  template <typename E>
-  __device__ void block_select(int k, E&& emit) {
-    __shared__ float sv[256];
-    __shared__ int64_t si[256];
-    __shared__ int sw[256];
-    int head = 0;
-    for (int q = 0; q < k; ++q) {
-      float hv = -__builtin_inff();
-      int64_t hi = INT64_MAX;
-#pragma unroll
-      for (int u = 0; u < KMAX; ++u)
-        if (u == head) {
-          hv = v[u];
-          hi = i[u];
-        }
-      sv[threadIdx.x] = hv;
-      si[threadIdx.x] = hi;
-      sw[threadIdx.x] = threadIdx.x;
-      __syncthreads();
-      for (int s = 128; s > 0; s >>= 1) {
-        if (threadIdx.x < s) {
-          const int o = threadIdx.x + s;
-          if (better(sv[o], si[o], sv[threadIdx.x], si[threadIdx.x])) {
-            sv[threadIdx.x] = sv[o];
-            si[threadIdx.x] = si[o];
-            sw[threadIdx.x] = sw[o];
-          }
-        }
-        __syncthreads();
-      }
-      if (threadIdx.x == 0) emit(q, sv[0], si[0]);
-      if (threadIdx.x == sw[0]) ++head;
-      __syncthreads();
-    }
-  }
-};
-
 // Phase 1: local top-k of one segment (+ the strict count against thr when given); candidates
 // [row][segment][k] to the workspace.
 template <int KMAX>
@@ -160,24 +92,6 @@ __global__ __launch_bounds__(256) void topk_seg_kernel(const float* __restrict__
   tl.block_select(k, [&](int q, float v, int64_t i) {
     cv[base + q] = v;
     ci[base + q] = i;
-  });
-}
-
-// Phase 2: merge the segments' candidates of one row (blockIdx.x) into the row's top-k.
-template <int KMAX>
-__global__ __launch_bounds__(256) void topk_merge_kernel(int segs, int k, int64_t id_offset,
-                                                         const float* __restrict__ cv,
-                                                         const int64_t* __restrict__ ci,
-                                                         float* __restrict__ vals,
-                                                         int64_t* __restrict__ ids) {
-  const int64_t b = blockIdx.x;
-  TopList<KMAX> tl;
-  tl.init();
-  const int64_t n = (int64_t)segs * k;
-  for (int64_t q = threadIdx.x; q < n; q += 256) tl.push(cv[b * n + q], ci[b * n + q]);
-  tl.block_select(k, [&](int q, float v, int64_t i) {
-    vals[b * k + q] = v;
-    ids[b * k + q] = i == INT64_MAX ? -1 : i + id_offset;
   });
 }
 
@@ -244,10 +158,10 @@ extern "C" int gr_topk_f32(const float* logits, int64_t B, int64_t cols, int64_t
   const dim3 g1(segs, (unsigned)B), g2((unsigned)B), blk(256);
   if (k <= 16) {
     hipLaunchKernelGGL(topk_seg_kernel<16>, g1, blk, 0, st, logits, cols, ld, segs, k, thresholds, cnt, cv, ci);
-    hipLaunchKernelGGL(topk_merge_kernel<16>, g2, blk, 0, st, segs, k, id_offset, cv, ci, vals_out, ids_out);
+    hipLaunchKernelGGL(topk_merge_kernel<16>, g2, blk, 0, st, (int64_t)segs * k, (int64_t)segs * k, k, id_offset, cv, ci, vals_out, ids_out);
   } else {
     hipLaunchKernelGGL(topk_seg_kernel<64>, g1, blk, 0, st, logits, cols, ld, segs, k, thresholds, cnt, cv, ci);
-    hipLaunchKernelGGL(topk_merge_kernel<64>, g2, blk, 0, st, segs, k, id_offset, cv, ci, vals_out, ids_out);
+    hipLaunchKernelGGL(topk_merge_kernel<64>, g2, blk, 0, st, (int64_t)segs * k, (int64_t)segs * k, k, id_offset, cv, ci, vals_out, ids_out);
   }
   return check_launch("gr_topk_f32");
 }

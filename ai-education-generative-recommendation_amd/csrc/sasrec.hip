@@ -38,6 +38,19 @@ __global__ __launch_bounds__(256) void embed_kernel(const int64_t* __restrict__ 
   *reinterpret_cast<f32x4*>(x + row * d + c) = a + p;
 }
 
+// Row n-1 of every sequence of a [B, n, d] activation -> compact [B, d] (the last-position rows a
+// last_only forward carries through its final block).
+__global__ __launch_bounds__(256) void gather_last_kernel(const float* __restrict__ src, int64_t B,
+                                                          int n, int d, float* __restrict__ dst) {
+  const int d4 = d >> 2;
+  const int64_t f = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (f >= B * d4) return;
+  const int64_t b = f / d4;
+  const int c = (int)(f % d4) * 4;
+  *reinterpret_cast<f32x4*>(dst + b * d + c) =
+      *reinterpret_cast<const f32x4*>(src + (b * n + n - 1) * d + c);
+}
+
 // ---------------------------------------------------------------------------------- layernorm
 // One wave per row: mean, biased variance, (x - mean) * rsqrt(var + eps) * w + b (F.layer_norm).
 // Input row r is read at in + (r * in_stride + in_offset) * d (in_stride = n, in_offset = n-1
@@ -257,8 +270,27 @@ static int run_layernorm(const float* in, int64_t rows, int d, int64_t stride, i
   return check_launch("sasrec layernorm");
 }
 
+// Rows the final layernorm reads after run_forward: `rows` (B*n for a full forward, B when the
+// final block ran on the last positions only) at x + (r * stride + off) * d.
+struct SasOut {
+  const float* x;
+  int64_t stride, off;
+};
+
+static int run_gather_last(const float* src, int64_t B, int n, int d, float* dst, hipStream_t st) {
+  const int64_t tot = B * (d / 4);
+  hipLaunchKernelGGL(gather_last_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, src, B,
+                     n, d, dst);
+  return check_launch("sasrec gather");
+}
+
+// last_only: the caller needs position n-1 only (model.py:104), so the FINAL block's attention
+// runs for the query tile holding it and its out-proj / FFN / residuals on the B last rows —
+// each of those rows computed by the same kernels with the same per-row instruction sequence as
+// the full forward (bitwise equal).  Earlier blocks still produce every position (they are the
+// final block's keys and values).
 static int run_forward(const gr_sasrec_params* p, const int64_t* seqs, int64_t B, int32_t n,
-                       const SasWs& w, int32_t* err, hipStream_t st) {
+                       const SasWs& w, int32_t* err, int last_only, SasOut* fin, hipStream_t st) {
   const int d = p->d, H = p->n_heads, hd = d / H;
   const int64_t rows = B * n;
   {
@@ -275,13 +307,17 @@ static int run_forward(const gr_sasrec_params* p, const int64_t* seqs, int64_t B
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)att_lds) != hipSuccess)
       return fail(GR_ERR_HIP, "sasrec attention: cannot raise the LDS limit");
   }
+  *fin = SasOut{w.x, n, n - 1};
+  // the pruned final block keeps [B, d] x / h and [B, mlp] f in the (then free) FFN buffer
+  const bool prune = last_only && n >= 2 && (int64_t)n * p->mlp >= 2LL * d + p->mlp;
   for (int i = 0; i < p->n_blocks; ++i) {
+    const bool last_blk = prune && i == p->n_blocks - 1;
     int rc = run_layernorm(w.x, rows, d, 1, 0, p->attn_ln_w[i], p->attn_ln_b[i], p->eps, w.h, st);
     if (rc) return rc;
     rc = gr_linear_launch(w.h, rows, d, p->in_proj_w[i], 3 * d, p->in_proj_b[i], nullptr, 0,
                           GR_ACT_NONE, w.qkv, 3 * d, st);
     if (rc) return rc;
-    rc = gr_attn_mfma_launch(w.qkv, w.o, B, n, H, hd, scale, st);   // matrix cores (attn.hip)
+    rc = gr_attn_mfma_launch(w.qkv, w.o, B, n, H, hd, scale, last_blk ? 1 : 0, st);   // attn.hip
     if (rc == GR_ERR_UNSUPPORTED) {                                   // other head widths
       clear_error();
       hipLaunchKernelGGL(causal_attn_kernel, dim3((unsigned)(B * H), (unsigned)((n + ATT_QT - 1) / ATT_QT)),
@@ -289,6 +325,21 @@ static int run_forward(const gr_sasrec_params* p, const int64_t* seqs, int64_t B
       rc = check_launch("sasrec attention");
     }
     if (rc) return rc;
+    if (last_blk) {
+      float* xl = w.f;                 // [B, d] residual stream of the last positions
+      float* hl = w.f + B * d;         // [B, d] layernorm output
+      float* fl = w.f + 2 * B * d;     // [B, mlp] FFN hidden
+      float* ol = w.h;                 // [B, d] attention output rows
+      rc = run_gather_last(w.o, B, n, d, ol, st);
+      if (!rc) rc = run_gather_last(w.x, B, n, d, xl, st);
+      if (!rc) rc = gr_linear_launch(ol, B, d, p->out_proj_w[i], d, p->out_proj_b[i], xl, d, GR_ACT_NONE, xl, d, st);
+      if (!rc) rc = run_layernorm(xl, B, d, 1, 0, p->ffn_ln_w[i], p->ffn_ln_b[i], p->eps, hl, st);
+      if (!rc) rc = gr_linear_launch(hl, B, d, p->ffn1_w[i], p->mlp, p->ffn1_b[i], nullptr, 0, GR_ACT_RELU, fl, p->mlp, st);
+      if (!rc) rc = gr_linear_launch(fl, B, p->mlp, p->ffn2_w[i], d, p->ffn2_b[i], xl, d, GR_ACT_NONE, xl, d, st);
+      if (rc) return rc;
+      *fin = SasOut{xl, 1, 0};
+      break;
+    }
     rc = gr_linear_launch(w.o, rows, d, p->out_proj_w[i], d, p->out_proj_b[i], w.x, d, GR_ACT_NONE,
                           w.x, d, st);
     if (rc) return rc;
@@ -340,9 +391,10 @@ extern "C" int gr_sasrec_forward_f32(const gr_sasrec_params* p, const int64_t* s
     if (rc != GR_ERR_UNSUPPORTED) return rc;
     return fail(GR_ERR_UNSUPPORTED, "sasrec: fused path refused a shape fused_ok accepted");
   }
-  rc = run_forward(p, seqs, B, n, w, err_flag, st);
+  SasOut fin;
+  rc = run_forward(p, seqs, B, n, w, err_flag, last_only, &fin, st);
   if (rc) return rc;
-  if (last_only) return run_layernorm(w.x, B, p->d, n, n - 1, p->last_ln_w, p->last_ln_b, p->eps, out, st);
+  if (last_only) return run_layernorm(fin.x, B, p->d, fin.stride, fin.off, p->last_ln_w, p->last_ln_b, p->eps, out, st);
   return run_layernorm(w.x, B * n, p->d, 1, 0, p->last_ln_w, p->last_ln_b, p->eps, out, st);
 }
 
@@ -362,9 +414,10 @@ extern "C" int gr_sasrec_predict_f32(const gr_sasrec_params* p, const int64_t* s
     if (rc == GR_ERR_UNSUPPORTED)
       return fail(GR_ERR_UNSUPPORTED, "sasrec: fused path refused a shape fused_ok accepted");
   } else {
-    rc = run_forward(p, seqs, B, n, w, err_flag, st);
+    SasOut fin;
+    rc = run_forward(p, seqs, B, n, w, err_flag, 1, &fin, st);
     if (rc) return rc;
-    rc = run_layernorm(w.x, B, p->d, n, n - 1, p->last_ln_w, p->last_ln_b, p->eps, w.h, st);
+    rc = run_layernorm(fin.x, B, p->d, fin.stride, fin.off, p->last_ln_w, p->last_ln_b, p->eps, w.h, st);
   }
   if (rc) return rc;
   rc = gr_score_launch(w.h, B, p->d, p->item_emb, p->item_rows, logits, p->item_rows, st);

@@ -1,0 +1,417 @@
+// Fused full-catalog top-k + strict rank count: the
+// `logits = h . table^T` of SASRec/model.py:107, the column-0 mask of SASRec/evaluate.py:27, the
+// strict `>` count of evaluate.py:32 and a per-user top-k (value descending, ties to the lower
+// column) — without writing the [B, rows] logits (4 MB per user at 1M items) and without reading
+// them back.
+//
+// Every logit is the scoring kernel's exact fp32 chain (score.hip): per 32-deep group g, step s
+// takes features 32g + 8(s>>2) + (s&3) + 4h (h = lane half).  Here the operands are swapped —
+// table rows are the MFMA A operand and users the B operand — so the accumulator holds
+// S^T[item][user]: lane (r, h) of user tile ut owns user 64w + 32ut + r and register v the item
+// 32it + (v&3) + 8(v>>2) + 4h of the chunk.  a0*b0 + a1*b1 with the factors swapped is the same
+// fp32 value, so each logit is bitwise what gr_score_f32 writes.
+//
+// Top-k.  Each lane keeps, per user tile, a sorted register list of KC >= k (value, column)
+// entries.  A lane meets its items in increasing column order, so an item that does not beat the
+// list's last value strictly can never enter the user's top-k (KC entries >= it have lower
+// columns); each lane's list is one candidate segment of the user, and a merge kernel takes the
+// top-k of all segments.  A wave executes an insertion whenever ANY of its lanes needs one, so on
+// its own this would cost more than the matrix work; a per-user threshold T_S keeps insertions
+// rare: pass 1 scores a strided SAMPLE of the chunks (every s-th) and keeps only the running max
+// of KC position buckets per lane (one v_max per logit; the maxima are values of distinct items),
+// T_S = the k-th largest of those maxima over the user's lanes (merge kernel).  k items >= T_S
+// exist, so pass 2 — every chunk, counts included — inserts only items >= T_S: about k*s per
+// user over the whole catalog.
+#include <cmath>
+#include <cstring>
+
+#include "gr_common.h"
+#include "topk_list.h"
+
+namespace gr {
+
+constexpr int TK_CHUNK = 64;     // items per chunk (two 32-item MFMA tiles)
+constexpr float TK_MASK = -1e9f; // evaluate.py:27
+
+template <int KC>
+struct LaneList {
+  float v[KC];
+  int c[KC];
+  __device__ __forceinline__ void init() {
+#pragma unroll
+    for (int q = 0; q < KC; ++q) {
+      v[q] = -INFINITY;
+      c[q] = -1;
+    }
+  }
+  // Insert (x, col) given that every entry has a lower column: strict '>' places x after equal
+  // values; once placed, the rest of the list shifts down by one.  A no-op when x does not beat
+  // the last entry.
+  __device__ __forceinline__ void insert(float x, int col) {
+    bool moved = false;
+#pragma unroll
+    for (int q = 0; q < KC; ++q) {
+      const bool b = moved || x > v[q];
+      const float tv = v[q];
+      const int tc = c[q];
+      v[q] = b ? x : tv;
+      c[q] = b ? col : tc;
+      x = b ? tv : x;
+      col = b ? tc : col;
+      moved = b;
+    }
+  }
+};
+
+// The largest float below t (t > -inf, not NaN): x > prev_below(t)  <=>  x >= t.
+__device__ __forceinline__ float prev_below(float t) {
+  if (t == 0.f) return -__int_as_float(1);
+  const int b = __float_as_int(t);
+  return __int_as_float(t > 0.f ? b - 1 : b + 1);
+}
+
+// Chunk set of a pass: mode 0 = every chunk (exact lists), 1 = the sample (chunks 0, s, 2s, ...;
+// bucket maxima only).
+__device__ __forceinline__ int64_t phys_chunk(int64_t v, int mode, int s) {
+  return mode == 1 ? v * s : v;
+}
+
+template <int D, int KC>
+__global__ __launch_bounds__(256, 1) void score_topk_kernel(
+    const float* __restrict__ h, int64_t B, const float* __restrict__ table, int64_t rows,
+    const float* __restrict__ thr, int mask_col0, unsigned long long* __restrict__ cnt_out,
+    const float* __restrict__ tinit, int tstride, int64_t vchunks, int mode, int s,
+    float* __restrict__ cv, int64_t* __restrict__ ci, int64_t seg_stride, int seg_off, int ublocks,
+    int slices, int ablate) {
+  constexpr int KG = D / 32;
+  constexpr int P = D + 4;
+  constexpr int LV = TK_CHUNK * D / 4 / 256;
+  __shared__ __attribute__((aligned(16))) float tab[2][TK_CHUNK * P];
+  const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, hh = lane >> 5;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wgid = xcd_remap(blockIdx.x, gridDim.x);
+  const int ub = wgid % ublocks, sl = wgid / ublocks;
+  const int64_t v_begin = vchunks * sl / slices, v_end = vchunks * (sl + 1) / slices;
+  const int64_t u0 = ((int64_t)ub * 4 + w) * 64;
+
+  // B operand: the users (lane r = user), as in the scoring kernel's A operand
+  f32x4 hf[2][KG][4];
+  float th[2], ts[2];
+#pragma unroll
+  for (int ut = 0; ut < 2; ++ut) {
+    const int64_t u = u0 + ut * 32 + r;
+    const int64_t uc = u < B ? u : B - 1;
+#pragma unroll
+    for (int g = 0; g < KG; ++g)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const f32x4 v = *reinterpret_cast<const f32x4*>(h + uc * D + 32 * g + 8 * q + 4 * hh);
+        hf[ut][g][q] = u < B ? v : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    th[ut] = thr ? thr[uc] : 0.f;
+    ts[ut] = tinit ? tinit[uc * tstride] : -INFINITY;
+  }
+  LaneList<KC> ll[2];
+  ll[0].init();
+  ll[1].init();
+  // pass test x > Tm  <=>  x > (list's last value) && x >= T_S
+  auto tm_of = [&](int ut) {
+    const float to = ll[ut].v[KC - 1];
+    return ts[ut] > to ? prev_below(ts[ut]) : to;
+  };
+  float Tm[2] = {tm_of(0), tm_of(1)};
+  int cgt[2] = {0, 0};
+
+  f32x4 st[LV];
+  auto gload = [&](int64_t c) {
+#pragma unroll
+    for (int i = 0; i < LV; ++i) {
+      const int f = tid + 256 * i, row = f / (D / 4), col = (f % (D / 4)) * 4;
+      int64_t item = c * TK_CHUNK + row;
+      item = item < rows ? item : rows - 1;
+      st[i] = *reinterpret_cast<const f32x4*>(table + item * D + col);
+    }
+  };
+  auto swrite = [&](int b) {
+#pragma unroll
+    for (int i = 0; i < LV; ++i) {
+      const int f = tid + 256 * i, row = f / (D / 4), col = (f % (D / 4)) * 4;
+      *reinterpret_cast<f32x4*>(&tab[b][row * P + col]) = st[i];
+    }
+  };
+  if (v_begin < v_end) {
+    gload(phys_chunk(v_begin, mode, s));
+    swrite(0);
+  }
+  __syncthreads();
+  int buf = 0;
+#pragma unroll 1
+  for (int64_t vc = v_begin; vc < v_end; ++vc) {
+    if (vc + 1 < v_end) gload(phys_chunk(vc + 1, mode, s));
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int ut = 0; ut < 2; ++ut)
+#pragma unroll
+      for (int it = 0; it < 2; ++it)
+#pragma unroll
+        for (int v = 0; v < 16; ++v) acc[ut][it][v] = 0.f;
+    const float* tb = &tab[buf][r * P + 4 * hh];
+#pragma unroll
+    for (int g = 0; g < KG; ++g)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        f32x4 bt[2];
+#pragma unroll
+        for (int it = 0; it < 2; ++it) bt[it] = *reinterpret_cast<const f32x4*>(tb + it * 32 * P + 32 * g + 8 * q);
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4)
+#pragma unroll
+          for (int it = 0; it < 2; ++it)
+#pragma unroll
+            for (int ut = 0; ut < 2; ++ut) acc[ut][it] = mfma32(bt[it][s4], hf[ut][g][q][s4], acc[ut][it]);
+      }
+    const int c0 = (int)(phys_chunk(vc, mode, s) * TK_CHUNK);
+    if (c0 + TK_CHUNK > rows || (mask_col0 && c0 == 0)) {   // catalog ends: masks
+#pragma unroll
+      for (int it = 0; it < 2; ++it)
+#pragma unroll
+        for (int v = 0; v < 16; ++v) {
+          const int col = c0 + 32 * it + (v & 3) + 8 * (v >> 2) + 4 * hh;
+#pragma unroll
+          for (int ut = 0; ut < 2; ++ut) {
+            if (mask_col0 && col == 0) acc[ut][it][v] = TK_MASK;
+            if (col >= rows) acc[ut][it][v] = __int_as_float(0x7fc00000);   // NaN: fails every test
+          }
+        }
+    }
+    if (mode == 1) {   // sample pass: bucket maxima (bucket = position mod KC), nothing else
+#pragma unroll
+      for (int ut = 0; ut < 2; ++ut)
+#pragma unroll
+        for (int it = 0; it < 2; ++it)
+#pragma unroll
+          for (int v = 0; v < 16; ++v) {
+            float& bm = ll[ut].v[(16 * it + v) % KC];
+            bm = fmaxf(bm, acc[ut][it][v]);
+          }
+      if (vc + 1 < v_end) swrite(buf ^ 1);
+      __syncthreads();
+      buf ^= 1;
+      continue;
+    }
+#pragma unroll
+    for (int ut = 0; ut < 2; ++ut) {
+      float mx = -INFINITY;
+#pragma unroll
+      for (int it = 0; it < 2; ++it)
+#pragma unroll
+        for (int v = 0; v < 16; ++v) {
+          const float x = acc[ut][it][v];
+          cgt[ut] += x > th[ut] ? 1 : 0;
+          mx = fmaxf(mx, x);
+        }
+      if (ablate == 1) continue;
+      if (__any(mx > Tm[ut])) {
+#pragma unroll
+        for (int it = 0; it < 2; ++it)
+#pragma unroll
+          for (int v = 0; v < 16; ++v) {
+            const float x = acc[ut][it][v];
+            if (x > Tm[ut]) ll[ut].insert(x, c0 + 32 * it + (v & 3) + 8 * (v >> 2) + 4 * hh);
+          }
+        Tm[ut] = tm_of(ut);
+      }
+    }
+    if (vc + 1 < v_end) swrite(buf ^ 1);
+    __syncthreads();
+    buf ^= 1;
+  }
+  // strict counts: the two lane halves of a user, one atomic per (user, slice)
+#pragma unroll
+  for (int ut = 0; ut < 2; ++ut) {
+    const int x = cgt[ut] + __shfl_xor(cgt[ut], 32);
+    const int64_t u = u0 + ut * 32 + r;
+    if (cnt_out && hh == 0 && u < B && x) atomicAdd(&cnt_out[u], (unsigned long long)x);
+  }
+  // candidate segment (pass, slice, half) of each user: the lane's sorted list
+#pragma unroll
+  for (int ut = 0; ut < 2; ++ut) {
+    const int64_t u = u0 + ut * 32 + r;
+    if (u >= B) continue;
+    const int64_t base = u * seg_stride + (int64_t)(seg_off + 2 * sl + hh) * KC;
+#pragma unroll
+    for (int q = 0; q < KC; ++q) {   // (the sample pass's bucket maxima carry no column)
+      cv[base + q] = ll[ut].v[q];
+      ci[base + q] = mode == 1 ? (int64_t)q : ll[ut].c[q] < 0 ? INT64_MAX : (int64_t)ll[ut].c[q];
+    }
+  }
+}
+
+static int cu_count() {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
+      cus = 256;
+  }
+  return cus;
+}
+
+// Launch plan: user blocks of 256, one workgroup per CU per pass.  The sample stride s trades the
+// sample pass's extra matrix work (1/s) against pass 2's insertions (about k*s per user); below
+// 4 chunks per slice the catalog is too short to pay for a second launch.
+struct TopkPlan {
+  int64_t ublocks, chunks;
+  int s;                       // 0: no sample pass
+  int64_t v1, slices1;         // the sample pass (s > 0)
+  int64_t slices2;             // the full pass
+  int kc;
+  int64_t seg_per_user() const { return 2 * (slices1 + slices2); }
+};
+
+static int64_t slices_for(int64_t ublocks, int64_t vchunks) {
+  int64_t sl = (cu_count() + ublocks - 1) / ublocks;
+  if (sl > vchunks) sl = vchunks;
+  return sl < 1 ? 1 : sl;
+}
+
+static int kc_for(int k) { return k <= 4 ? 4 : k <= 10 ? 10 : 16; }
+
+static TopkPlan topk_plan(int64_t B, int64_t rows, int k) {
+  TopkPlan p;
+  p.ublocks = (B + 255) / 256;
+  p.chunks = (rows + TK_CHUNK - 1) / TK_CHUNK;
+  p.kc = kc_for(k);
+  p.slices2 = slices_for(p.ublocks, p.chunks);
+  const int64_t per_slice = p.chunks / p.slices2;
+  p.s = 0;
+  p.v1 = p.slices1 = 0;
+  if (per_slice >= 4 && option("topk_sample") != 0) {
+    const int64_t s = per_slice / 4;
+    p.s = (int)(s < 2 ? 2 : s > 16 ? 16 : s);
+    p.v1 = (p.chunks + p.s - 1) / p.s;
+    p.slices1 = slices_for(p.ublocks, p.v1);
+  }
+  return p;
+}
+
+struct TopkWs {
+  size_t cv, ci, v1, i1, total;
+};
+static TopkWs topk_ws(int64_t B, const TopkPlan& p, int k) {
+  TopkWs w;
+  const size_t cand = (size_t)B * p.seg_per_user() * p.kc;
+  w.cv = align_up(cand * sizeof(float), 256);
+  w.ci = align_up(cand * sizeof(int64_t), 256);
+  w.v1 = align_up((size_t)B * k * sizeof(float), 256);
+  w.i1 = align_up((size_t)B * k * sizeof(int64_t), 256);
+  w.total = w.cv + w.ci + w.v1 + w.i1 + 256;
+  return w;
+}
+
+template <int KC>
+static void launch_pass(int d, dim3 grid, hipStream_t st, const float* h, int64_t B, const float* table,
+                        int64_t rows, const float* thr, int mask_col0, unsigned long long* cnt,
+                        const float* tinit, int tstride, int64_t vchunks, int mode, int s, float* cv,
+                        int64_t* ci, int64_t seg_stride, int seg_off, int ub, int sl, int ablate) {
+  const dim3 blk(256);
+  switch (d) {
+    case 32: hipLaunchKernelGGL((score_topk_kernel<32, KC>), grid, blk, 0, st, h, B, table, rows, thr, mask_col0, cnt, tinit, tstride, vchunks, mode, s, cv, ci, seg_stride, seg_off, ub, sl, ablate); break;
+    case 64: hipLaunchKernelGGL((score_topk_kernel<64, KC>), grid, blk, 0, st, h, B, table, rows, thr, mask_col0, cnt, tinit, tstride, vchunks, mode, s, cv, ci, seg_stride, seg_off, ub, sl, ablate); break;
+    default: hipLaunchKernelGGL((score_topk_kernel<128, KC>), grid, blk, 0, st, h, B, table, rows, thr, mask_col0, cnt, tinit, tstride, vchunks, mode, s, cv, ci, seg_stride, seg_off, ub, sl, ablate); break;
+  }
+}
+
+template <int KC>
+static void launch_merge(hipStream_t st, int64_t B, int64_t row_stride, int64_t n, int k, int64_t id_offset,
+                         const float* cv, const int64_t* ci, float* vals, int64_t* ids) {
+  hipLaunchKernelGGL(topk_merge_kernel<KC>, dim3((unsigned)B), dim3(256), 0, st, row_stride, n, k,
+                     id_offset, cv, ci, vals, ids);
+}
+
+}  // namespace gr
+
+extern "C" size_t gr_score_topk_workspace_bytes(int64_t B, int32_t d, int64_t rows, int32_t k) {
+  (void)d;
+  if (B < 1 || rows < 1 || k < 1 || k > 16) return 256;
+  const gr::TopkPlan p = gr::topk_plan(B, rows, k);
+  return gr::topk_ws(B, p, k).total;
+}
+
+extern "C" int gr_score_topk_f32(const float* h, int64_t B, int32_t d, const float* table,
+                                 int64_t rows, int64_t id_offset, int32_t mask_col0, int32_t k,
+                                 const float* thresholds, int64_t* counts_out, float* vals_out,
+                                 int64_t* ids_out, void* workspace, size_t workspace_bytes,
+                                 void* stream) {
+  using namespace gr;
+  clear_error();
+  if (B < 0 || rows < 0 || k < 1) return fail(GR_ERR_ARG, "gr_score_topk_f32: bad shape");
+  if (B == 0) return GR_OK;
+  if (!h || !table || !vals_out || !ids_out) return fail(GR_ERR_ARG, "gr_score_topk_f32: null pointer");
+  if ((thresholds == nullptr) != (counts_out == nullptr))
+    return fail(GR_ERR_ARG, "gr_score_topk_f32: thresholds and counts_out go together");
+  if (d != 32 && d != 64 && d != 128)
+    return fail(GR_ERR_UNSUPPORTED, "gr_score_topk_f32: d must be 32, 64 or 128");
+  if (k > 16) return fail(GR_ERR_UNSUPPORTED, "gr_score_topk_f32: k > 16");
+  if (rows >= (1LL << 31) - 4096) return fail(GR_ERR_UNSUPPORTED, "gr_score_topk_f32: rows >= 2^31");
+  if (B > 65535) return fail(GR_ERR_UNSUPPORTED, "gr_score_topk_f32: B > 65535");
+  if (!aligned16(h) || !aligned16(table)) return fail(GR_ERR_ARG, "gr_score_topk_f32: h / table not 16-byte aligned");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (counts_out && hipMemsetAsync(counts_out, 0, (size_t)B * sizeof(int64_t), st) != hipSuccess)
+    return fail(GR_ERR_HIP, "gr_score_topk_f32: memset failed");
+  if (rows == 0) {   // nothing to rank: every entry is padding
+    if (hipMemsetAsync(ids_out, 0xff, (size_t)B * k * sizeof(int64_t), st) != hipSuccess)
+      return fail(GR_ERR_HIP, "gr_score_topk_f32: memset failed");
+    const float ninf = -INFINITY;
+    uint32_t bits;
+    memcpy(&bits, &ninf, 4);
+    if (hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(vals_out), (int)bits, (size_t)B * k, st) != hipSuccess)
+      return fail(GR_ERR_HIP, "gr_score_topk_f32: memset failed");
+    return GR_OK;
+  }
+  const TopkPlan p = topk_plan(B, rows, k);
+  const TopkWs wl = topk_ws(B, p, k);
+  if (!workspace || workspace_bytes < wl.total)
+    return fail(GR_ERR_WORKSPACE, "gr_score_topk_f32: workspace too small (need " + std::to_string(wl.total) + " bytes)");
+  if (p.ublocks * p.slices2 > 0x7fffffffLL)
+    return fail(GR_ERR_UNSUPPORTED, "gr_score_topk_f32: grid too large");
+  char* base = reinterpret_cast<char*>(align_up(reinterpret_cast<uintptr_t>(workspace), 256));
+  auto* cv = reinterpret_cast<float*>(base);
+  auto* ci = reinterpret_cast<int64_t*>(base + wl.cv);
+  auto* v1 = reinterpret_cast<float*>(base + wl.cv + wl.ci);
+  auto* i1 = reinterpret_cast<int64_t*>(base + wl.cv + wl.ci + wl.v1);
+  auto* cnt = reinterpret_cast<unsigned long long*>(counts_out);
+  const int ablate = (int)option("topk_ablate");   // diagnostic only (gr_set_option)
+  const int64_t seg_stride = p.seg_per_user() * p.kc;
+  const int ub = (int)p.ublocks;
+  auto run = [&](auto kc_tag) -> int {
+    constexpr int KC = decltype(kc_tag)::value;
+    const float* tinit = nullptr;
+    int rc;
+    if (p.s) {   // sample pass -> T_S = the k-th largest bucket maximum per user
+      launch_pass<KC>(d, dim3((unsigned)(p.ublocks * p.slices1)), st, h, B, table, rows, nullptr, mask_col0,
+                      nullptr, nullptr, 0, p.v1, 1, p.s, cv, ci, seg_stride, 0, ub, (int)p.slices1, ablate);
+      rc = check_launch("gr_score_topk_f32 (sample pass)");
+      if (rc) return rc;
+      launch_merge<KC>(st, B, seg_stride, 2 * p.slices1 * KC, k, 0, cv, ci, v1, i1);
+      rc = check_launch("gr_score_topk_f32 (sample merge)");
+      if (rc) return rc;
+      tinit = v1 + (k - 1);
+    }
+    launch_pass<KC>(d, dim3((unsigned)(p.ublocks * p.slices2)), st, h, B, table, rows, thresholds, mask_col0,
+                    cnt, tinit, k, p.chunks, 0, 1, cv, ci, seg_stride, (int)(2 * p.slices1), ub,
+                    (int)p.slices2, ablate);
+    rc = check_launch("gr_score_topk_f32 (pass)");
+    if (rc) return rc;
+    // final merge over the full pass's segments only (the sample's maxima are not candidates)
+    launch_merge<KC>(st, B, seg_stride, 2 * p.slices2 * KC, k, id_offset, cv + 2 * p.slices1 * KC,
+                     ci + 2 * p.slices1 * KC, vals_out, ids_out);
+    return check_launch("gr_score_topk_f32 (merge)");
+  };
+  switch (p.kc) {
+    case 4: return run(std::integral_constant<int, 4>{});
+    case 10: return run(std::integral_constant<int, 10>{});
+    default: return run(std::integral_constant<int, 16>{});
+  }
+}

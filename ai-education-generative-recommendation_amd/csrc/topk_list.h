@@ -1,0 +1,115 @@
+// Per-thread top-k candidate lists and the per-row merge shared by the top-k kernels
+// (rank.hip: over materialised logits; score_topk.hip: fused into the scoring chain).
+#pragma once
+#include "gr_common.h"
+
+namespace gr {
+
+// (value, column) order: larger value first, then smaller column.
+__device__ __forceinline__ bool better(float va, int64_t ia, float vb, int64_t ib) {
+  return va > vb || (va == vb && ia < ib);
+}
+
+// Per-thread sorted candidate list of KMAX entries (best first); NaN never enters.
+template <int KMAX>
+struct TopList {
+  float v[KMAX];
+  int64_t i[KMAX];
+  __device__ void init() {
+#pragma unroll
+    for (int q = 0; q < KMAX; ++q) {
+      v[q] = -__builtin_inff();
+      i[q] = INT64_MAX;
+    }
+  }
+  __device__ __forceinline__ void push(float cv, int64_t ci) {
+    if (!better(cv, ci, v[KMAX - 1], i[KMAX - 1])) return;
+#pragma unroll
+    for (int q = 0; q < KMAX; ++q) {   // insertion: carry the displaced entry down the list
+      if (better(cv, ci, v[q], i[q])) {
+        const float tv = v[q];
+        const int64_t ti = i[q];
+        v[q] = cv;
+        i[q] = ci;
+        cv = tv;
+        ci = ti;
+      }
+    }
+  }
+  // k rounds of a block-wide arg-best over the heads of the per-thread lists; emit(q, v, i).
+  // Per round: a 64-lane shuffle arg-best in each wave, one barrier, then every thread picks the
+  // best of the 4 wave winners (slots double-buffered by round parity, so one barrier suffices).
+  // Equal (value, id) pairs resolve to the lower thread: the order is deterministic.
+  template <typename E>
+  __device__ void block_select(int k, E&& emit) {
+    __shared__ float sv[2][4];
+    __shared__ int64_t si[2][4];
+    __shared__ int sw[2][4];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    int head = 0;
+    for (int q = 0; q < k; ++q) {
+      float bv = -__builtin_inff();
+      int64_t bi = INT64_MAX;
+#pragma unroll
+      for (int u = 0; u < KMAX; ++u)
+        if (u == head) {
+          bv = v[u];
+          bi = i[u];
+        }
+      int bt = threadIdx.x;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        const float ov = __shfl_xor(bv, o);
+        const int64_t oi = __shfl_xor(bi, o);
+        const int ot = __shfl_xor(bt, o);
+        if (better(ov, oi, bv, bi) || (ov == bv && oi == bi && ot < bt)) {
+          bv = ov;
+          bi = oi;
+          bt = ot;
+        }
+      }
+      const int par = q & 1;
+      if (lane == 0) {
+        sv[par][wv] = bv;
+        si[par][wv] = bi;
+        sw[par][wv] = bt;
+      }
+      __syncthreads();
+      bv = sv[par][0];
+      bi = si[par][0];
+      bt = sw[par][0];
+#pragma unroll
+      for (int w = 1; w < 4; ++w) {
+        const float ov = sv[par][w];
+        const int64_t oi = si[par][w];
+        const int ot = sw[par][w];
+        if (better(ov, oi, bv, bi) || (ov == bv && oi == bi && ot < bt)) {
+          bv = ov;
+          bi = oi;
+          bt = ot;
+        }
+      }
+      if (threadIdx.x == 0) emit(q, bv, bi);
+      if (threadIdx.x == bt) ++head;
+    }
+  }
+};
+
+// Merge the first n candidates of row blockIdx.x (cv / ci + row * row_stride) into the row's top-k.
+template <int KMAX>
+__global__ __launch_bounds__(256) void topk_merge_kernel(int64_t row_stride, int64_t n, int k, int64_t id_offset,
+                                                         const float* __restrict__ cv,
+                                                         const int64_t* __restrict__ ci,
+                                                         float* __restrict__ vals,
+                                                         int64_t* __restrict__ ids) {
+  const int64_t b = blockIdx.x;
+  TopList<KMAX> tl;
+  tl.init();
+  for (int64_t q = threadIdx.x; q < n; q += 256) tl.push(cv[b * row_stride + q], ci[b * row_stride + q]);
+  tl.block_select(k, [&](int q, float v, int64_t i) {
+    vals[b * k + q] = v;
+    ids[b * k + q] = i == INT64_MAX ? -1 : i + id_offset;
+  });
+}
+
+}  // namespace gr

@@ -65,6 +65,11 @@ def sharded_rank_topk(h, table_shard, row_offset, targets, k=10, group=None, mas
     """Catalog-sharded scoring: every rank holds ``table_shard`` = rows [row_offset, ...) of the
     item table and the same ``h`` [B, d] / global ``targets`` [B].  Returns (rank [B] int64,
     top values [B, k], top ids [B, k]) identical on every rank."""
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    rows = table_shard.shape[0]
+    if (scorer is None and counter is None and topk_fn is None and h.is_cuda and rows > 0
+            and 1 <= k <= 16 and h.shape[1] in (32, 64, 128)):
+        return _sharded_rank_topk_fused(h, table_shard, row_offset, targets, k, group, mask_row0, world)
     s_fn, c_fn, t_fn = _default_ops()
     scorer, counter, topk_fn = scorer or s_fn, counter or c_fn, topk_fn or t_fn
     logits = scorer(h, table_shard)
@@ -75,7 +80,6 @@ def sharded_rank_topk(h, table_shard, row_offset, targets, k=10, group=None, mas
     own = (t >= row_offset) & (t < row_offset + rows)
     local = torch.where(own, t - row_offset, torch.zeros_like(t))
     ts = torch.where(own, logits.gather(1, local.unsqueeze(1)).squeeze(1), torch.zeros_like(t, dtype=logits.dtype))
-    world = dist.get_world_size(group) if dist.is_initialized() else 1
     if world > 1:
         dist.all_reduce(ts, op=dist.ReduceOp.SUM, group=group)
     kk = min(k, rows) if rows > 0 else 0
@@ -88,19 +92,46 @@ def sharded_rank_topk(h, table_shard, row_offset, targets, k=10, group=None, mas
         else:
             v = torch.empty((logits.shape[0], 0), dtype=logits.dtype, device=logits.device)
             i = torch.empty((logits.shape[0], 0), dtype=torch.int64, device=logits.device)
-    if world > 1:
-        dist.all_reduce(cnt, op=dist.ReduceOp.SUM, group=group)
     if kk < k:
         pad = k - kk
         v = torch.cat([v, torch.full((v.shape[0], pad), float("-inf"), dtype=v.dtype, device=v.device)], 1)
         i = torch.cat([i, torch.full((i.shape[0], pad), -1, dtype=i.dtype, device=i.device)], 1)
+    return _exchange(cnt, v, i, k, group, world)
+
+
+def _exchange(cnt, v, i, k, group, world):
+    """Steps 2-3 of the module docstring: global counts and the merged top-k."""
     if world > 1:
+        dist.all_reduce(cnt, op=dist.ReduceOp.SUM, group=group)
         vs = [torch.empty_like(v) for _ in range(world)]
         is_ = [torch.empty_like(i) for _ in range(world)]
         dist.all_gather(vs, v.contiguous(), group=group)
         dist.all_gather(is_, i.contiguous(), group=group)
         v, i = merge_topk(torch.cat(vs, 1), torch.cat(is_, 1), k)
     return cnt + 1, v, i
+
+
+def _sharded_rank_topk_fused(h, table_shard, row_offset, targets, k, group, mask_row0, world):
+    """The same exchange with the shard's logits never materialised: the target logit comes from
+    ``score_pairs`` and the counts + local top-k from one ``score_topk`` pass over the shard
+    (bitwise the values of the unfused path: all three kernels share one fp32 chain)."""
+    from . import ops
+    rows = table_shard.shape[0]
+    m0 = bool(mask_row0 and row_offset == 0)
+    t = targets.reshape(-1).to(torch.int64)
+    own = (t >= row_offset) & (t < row_offset + rows)
+    local = torch.where(own, t - row_offset, torch.zeros_like(t))
+    ts = torch.where(own, ops.score_pairs(h, table_shard, local, mask_col0=m0),
+                     torch.zeros(t.shape, dtype=torch.float32, device=h.device))
+    if world > 1:
+        dist.all_reduce(ts, op=dist.ReduceOp.SUM, group=group)
+    kk = min(k, rows)
+    v, i, cnt = ops.score_topk(h, table_shard, kk, row_offset, thresholds=ts, mask_col0=m0)
+    if kk < k:
+        pad = k - kk
+        v = torch.cat([v, torch.full((v.shape[0], pad), float("-inf"), dtype=v.dtype, device=v.device)], 1)
+        i = torch.cat([i, torch.full((i.shape[0], pad), -1, dtype=i.dtype, device=i.device)], 1)
+    return _exchange(cnt, v, i, k, group, world)
 
 
 def hr_ndcg(ranks, top_k=10):

@@ -137,6 +137,30 @@ def score_rank(h, table, targets, mask_col0=True):
     return score_count_gt(h, table, score_pairs(h, table, targets, mask_col0), mask_col0) + 1
 
 
+def score_topk(h, table, k, id_offset=0, thresholds=None, mask_col0=True):
+    """Top-k of ``h @ table.T`` per user without writing the logits: (values [B,k] descending,
+    ids [B,k] = column + id_offset; ties -> lower id), column 0 taken as -1e9 when ``mask_col0``
+    (SASRec/evaluate.py:27).  With ``thresholds`` also the strict counts ``#{j : l[b,j] > thr[b]}``.
+    Same values, bit for bit, as ``topk(score(h, table))`` after the column-0 mask."""
+    L.require_gpu(h, table)
+    h, t = L.as_f32(h), L.as_f32(table)
+    B, d = h.shape
+    rows = t.shape[0]
+    dev = h.device
+    vals = torch.empty((B, k), dtype=torch.float32, device=dev)
+    ids = torch.empty((B, k), dtype=torch.int64, device=dev)
+    th = L.as_f32(thresholds.reshape(-1)) if thresholds is not None else None
+    cnt = torch.empty(B, dtype=torch.int64, device=dev) if th is not None else None
+    nbytes = L.lib().gr_score_topk_workspace_bytes(B, d, rows, k)
+    wsp = L.workspace(nbytes, dev)
+    with torch.cuda.device(dev):
+        L.check(L.lib().gr_score_topk_f32(L.ptr(h), B, d, L.ptr(t), rows, id_offset,
+                                          1 if mask_col0 else 0, k, L.ptr(th), L.ptr(cnt),
+                                          L.ptr(vals), L.ptr(ids), L.ptr(wsp), nbytes,
+                                          L.stream_of(dev)), "gr_score_topk_f32")
+    return (vals, ids) if th is None else (vals, ids, cnt)
+
+
 def rq_quantize(z, codebooks, with_gap=False):
     """Residual quantization of latents (RQ-VAE/models/rq.py:39-56, use_sk=False).
 

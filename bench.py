@@ -273,13 +273,21 @@ def bench_sas_c5(a, world, rank, dev):
 
     steps, warm = max(2, min(a.steps, 10)), 2
     wall, dev_ms = timed(step, steps, warm, world)
+    h = model.last_hidden(seqs)
+    ts = torch.zeros(B, device=dev)
+    topk_ms = kernel_ms(lambda: ops.score_topk(h, shard, 10, lo, thresholds=ts, mask_col0=(lo == 0)))
+    fwd_ms = kernel_ms(lambda: model.last_hidden(seqs[ulo:uhi]))
     return {"metric": "seqs_scored/s", "value": B * steps / wall, "unit": "seqs/s", "scaling": "strong",
             "ms_per_step": wall / steps * 1e3, "steps": steps,
             "config": {"workload": "sas_c5: SASRec d 128, n 200, 2 blocks, 1M-item catalog, rank + top-10",
                        "users_per_step": B, "catalog_rows": items + 1, "rows_per_rank": hi - lo,
                        "parallelism": f"catalog-sharded x{world}: RCCL all-gather h + top-k, all-reduce counts"
                        if world > 1 else "single shard"},
-            "call": {"device_ms_rank0": dev_ms, "flop_per_user": sas_flop_per_user(d, n, items)}}
+            "roofline": roofline("score_topk_kernel<128,10> (sample + full pass + merges)", 2 * d * (hi - lo) * B, topk_ms),
+            "call": {"device_ms_rank0": dev_ms, "flop_per_user": sas_flop_per_user(d, n, items),
+                     "forward_ms": fwd_ms, "score_topk_ms": topk_ms,
+                     "note": "rank + top-10 fused into the scoring pass (gr_score_topk_f32): the "
+                             "[B, rows] logits are never written"}}
 
 
 def main():

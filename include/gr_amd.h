@@ -52,6 +52,10 @@ const char* gr_last_error(void);
  *                   (the workspace query follows the option in force when it is called)
  *   "score_ablate"  0 (default).  DIAGNOSTIC ONLY, outputs invalid otherwise: 1 = the scoring
  *                   kernel skips the logits stores, 2 = it skips the matrix work
+ *   "topk_ablate"   0 (default).  DIAGNOSTIC ONLY, outputs invalid otherwise: the fused score +
+ *                   top-k kernel skips 1 = all top-k work (counts stay valid)
+ *   "topk_sample"   1 (default): gr_score_topk_f32 prunes with a threshold from a strided sample
+ *                   pass when the catalog is long enough; 0: one pass.  Identical results.
  * gr_set_option returns GR_ERR_ARG for an unknown name/value; gr_get_option returns -1 for an
  * unknown name. */
 int gr_set_option(const char* name, int64_t value);
@@ -213,6 +217,20 @@ int gr_score_pairs_f32(const float* h, int64_t B, int32_t d, const float* table,
 int gr_score_count_gt_f32(const float* h, int64_t B, int32_t d, const float* table, int64_t rows,
                           const float* thresholds, int32_t mask_col0, int64_t* counts_out,
                           void* stream);
+
+/* Fused top-k (+ strict counts) over the full catalog or a catalog shard without materialising
+ * logits (SASRec/model.py:107 + evaluate.py:27-32; the per-shard candidate lists of SURVEY §8(e)).
+ * Logits are l = h . table^T evaluated with exactly gr_score_f32's instruction sequence, column 0
+ * taken as -1e9 when mask_col0.  vals_out[B, k] / ids_out[B, k]: the k largest, value descending,
+ * ties to the lower column, ids = column + id_offset (-1 / -inf pad rows with fewer than k
+ * columns).  thresholds / counts_out (both or neither): counts_out[b] = #{j : l[b, j] > thr[b]}.
+ * d in {32, 64, 128}, 1 <= k <= 16, rows < 2^31, B <= 65535.  Replaces gr_score_f32 + gr_topk_f32
+ * (which read the logits back) when only the top-k / ranks are needed. */
+size_t gr_score_topk_workspace_bytes(int64_t B, int32_t d, int64_t rows, int32_t k);
+int gr_score_topk_f32(const float* h, int64_t B, int32_t d, const float* table, int64_t rows,
+                      int64_t id_offset, int32_t mask_col0, int32_t k, const float* thresholds,
+                      int64_t* counts_out, float* vals_out, int64_t* ids_out, void* workspace,
+                      size_t workspace_bytes, void* stream);
 
 #ifdef __cplusplus
 }

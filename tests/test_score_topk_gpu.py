@@ -1,0 +1,125 @@
+"""Fused scoring + top-k + strict counts without logits (gr_score_topk_f32; SURVEY §8(e) C5,
+§8f row 2) against the materialised path on the same device.
+
+Bar: bit-exact.  Values and ids equal ``topk(score(h, table))`` after the evaluate.py:27 column-0
+mask (the fused kernel shares the scoring kernel's fp32 chain), ties to the lower column, counts
+equal ``(logits > thr).sum(1)``.  Shapes cover ragged users / rows, rows < k, exact ties, a
+catalog whose logits rise with the column (every item displaces the running top-k: the append
+buffers overflow and fold every chunk) and one where they fall."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _reference(h, t, k, id_offset, thr, mask_col0):
+    from gr_amd import ops
+    lg = ops.score(h, t)
+    if mask_col0:
+        lg[:, 0] = -1e9
+    cnt = (lg > thr[:, None]).sum(1)
+    kk = min(k, lg.shape[1])
+    o = torch.argsort(lg, dim=1, descending=True, stable=True)[:, :kk]
+    v, i = lg.gather(1, o), o + id_offset
+    if kk < k:
+        v = torch.cat([v, torch.full((v.shape[0], k - kk), float("-inf"), device=v.device)], 1)
+        i = torch.cat([i, torch.full((i.shape[0], k - kk), -1, dtype=i.dtype, device=i.device)], 1)
+    return v, i, cnt
+
+
+def _check(h, t, k, id_offset=0, mask_col0=True, seed=0):
+    """Both plans (sample-thresholded two passes where the catalog is long enough, and one pass)
+    against the materialised reference."""
+    from gr_amd import _lib, ops
+    g = torch.Generator(device=h.device).manual_seed(seed)
+    thr = torch.randn(h.shape[0], generator=g, device=h.device)
+    rv, ri, rc = _reference(h, t, k, id_offset, thr, mask_col0)
+    try:
+        for sample in (1, 0):
+            _lib.set_option("topk_sample", sample)
+            v, i, c = ops.score_topk(h, t, k, id_offset, thresholds=thr, mask_col0=mask_col0)
+            assert torch.equal(i, ri)
+            assert torch.equal(v, rv)
+            assert torch.equal(c, rc)
+            v2, i2 = ops.score_topk(h, t, k, id_offset, mask_col0=mask_col0)   # without counts
+            assert torch.equal(v2, rv) and torch.equal(i2, ri)
+    finally:
+        _lib.set_option("topk_sample", 1)
+
+
+@pytest.mark.parametrize("B,d,rows,k", [(1, 64, 70, 10), (300, 64, 100001, 10), (64, 128, 5000, 16),
+                                        (257, 32, 1000, 1), (70, 64, 64, 10), (5, 128, 7, 10),
+                                        (513, 128, 20011, 10), (33, 32, 1, 3), (512, 128, 300007, 10),
+                                        (100, 32, 150001, 4), (40, 64, 262145, 16)])
+def test_score_topk_random(B, d, rows, k, dev):
+    g = torch.Generator().manual_seed(B * 7 + d + rows)
+    h = torch.randn(B, d, generator=g).to(dev)
+    t = torch.randn(rows, d, generator=g).to(dev)
+    _check(h, t, k, id_offset=0, mask_col0=True, seed=rows)
+    _check(h, t, k, id_offset=12345, mask_col0=False, seed=rows + 1)
+
+
+def test_score_topk_ties(dev):
+    """Duplicated table rows (exact logit ties inside and across lanes, chunks and slices) and a
+    constant catalog: the lower column must win every tie."""
+    g = torch.Generator().manual_seed(3)
+    d, rows = 64, 30001
+    t = torch.randn(rows, d, generator=g)
+    t[rows // 2:] = t[: rows - rows // 2].clone()
+    t[100:164] = t[7]
+    h = torch.randn(40, d, generator=g)
+    _check(h.to(dev), t.to(dev), 16)
+    _check(h.to(dev), torch.ones(4097, d).to(dev), 10)
+
+
+@pytest.mark.parametrize("direction", [1.0, -1.0])
+def test_score_topk_monotone_catalog(direction, dev):
+    """Logits strictly monotone in the column for every user: rising = worst case (each new item
+    enters every lane's list), falling = best case (nothing after the first chunk)."""
+    d, rows, B = 32, 200000, 96
+    t = torch.zeros(rows, d)
+    t[:, 0] = direction * torch.arange(rows, dtype=torch.float32) / rows
+    t[:, 1] = 1.0
+    g = torch.Generator().manual_seed(4)
+    h = torch.rand(B, d, generator=g) + 0.5
+    _check(h.to(dev), t.to(dev), 10)
+
+
+def test_sharded_fused_equals_full_catalog(dev):
+    """Catalog shards scored by the fused kernel (8 sequential shards on one GPU): counts summed
+    over shards + 1 and the merged top-k equal the full-catalog rank / top-k bit for bit."""
+    from gr_amd import dist as D, ops
+    g = torch.Generator().manual_seed(11)
+    B, d, rows, k = 200, 128, 40001, 10
+    table = torch.randn(rows, d, generator=g).to(dev)
+    h = torch.randn(B, d, generator=g).to(dev)
+    tg = torch.randint(0, rows, (B,), generator=g).to(dev)
+    full = ops.score(h, table)
+    ref_rank = ops.rank(full, tg)
+    full[:, 0] = -1e9
+    o = torch.argsort(full, dim=1, descending=True, stable=True)[:, :k]
+    ts = ops.score_pairs(h, table, tg)            # global target logits (column-0 masked)
+    cnt = torch.zeros(B, dtype=torch.int64, device=dev)
+    vs, is_ = [], []
+    for r in range(8):
+        lo, hi = D.shard_range(rows, r, 8)
+        v, i, c = ops.score_topk(h, table[lo:hi], k, lo, thresholds=ts, mask_col0=(lo == 0))
+        cnt += c
+        vs.append(v)
+        is_.append(i)
+    v, i = D.merge_topk(torch.cat(vs, 1), torch.cat(is_, 1), k)
+    assert torch.equal(cnt + 1, ref_rank)
+    assert torch.equal(i, o) and torch.equal(v, full.gather(1, o))
+    # the module-level entry point (world size 1) takes the fused path
+    rk, v1, i1 = D.sharded_rank_topk(h, table, 0, tg, k=k)
+    assert torch.equal(rk, ref_rank) and torch.equal(i1, o) and torch.equal(v1, v)
+
+
+def test_score_topk_rejects_bad_args(dev):
+    from gr_amd import ops
+    h = torch.randn(4, 64, device=dev)
+    t = torch.randn(100, 64, device=dev)
+    with pytest.raises(RuntimeError, match="k > 16"):
+        ops.score_topk(h, t, 17)
+    with pytest.raises(RuntimeError, match="d must be"):
+        ops.score_topk(torch.randn(4, 48, device=dev), torch.randn(100, 48, device=dev), 5)
