@@ -2,112 +2,188 @@
 // than the fused kernel's 64 tokens, e.g. config C5: n = 200, d = 128): the
 // `softmax(mask + (q * sqrt(1/hd)) k^T) v` of torch functional.py:6578-6594 for one head.
 //
-// One wavefront per (sequence, head, 32-query tile); a workgroup holds the 4 query tiles of one
-// (sequence, head) so their key/value reads share L1.  Orientation as in the fused kernel
-// (sasrec_fused.hip): S^T[key][query] = K . Q^T with the key rows as the A operand (float4 loads
-// of k rows) and the scaled query rows as the B operand; lane = query, so the softmax is a
-// per-lane reduction over registers plus one exchange of the two lane halves.  Keys are walked in
-// 32-key tiles up to the diagonal with an online softmax (running max / sum per query, O
-// rescaled), and O^T[f][query] += V^T . P^T takes value rows as the A operand (lane = feature:
-// 32 consecutive floats of one value row per register, coalesced) and P^T straight from the S^T
-// registers.  fp32 throughout (v_mfma_f32_32x32x2_f32); exp via v_exp_f32.
+// One workgroup (4 waves) per (sequence, head).  Key / value rows are streamed through LDS in
+// 32-key tiles (double-buffered, the next tile prefetched into registers while the current one is
+// consumed), shared by every query tile of the sequence; the 4 waves own 4 consecutive 32-query
+// tiles per round.
+// Orientation as in the fused kernel (sasrec_fused.hip): S^T[key][query] = K . Q^T with the key
+// rows as the A operand (ds_read_b128 of a K row) and the scaled query rows as the B operand; lane
+// = query, so the softmax is a per-lane reduction over registers plus one exchange of the two lane
+// halves.  Keys are walked up to the diagonal with an online softmax (running max / sum per query,
+// O rescaled), and O^T[f][query] += V^T . P^T takes value rows as the A operand (lane = feature,
+// one ds_read_b32 feeding both query tiles) and P^T straight from the S^T registers.  fp32
+// throughout (v_mfma_f32_32x32x2_f32); exp via v_exp_f32.  Each output row sees exactly the same
+// instruction sequence whichever tiles are launched, so a last-tile-only launch (the final block of
+// a last-position forward) reproduces the full launch's rows bit for bit.
 #include <cmath>
 
 #include "gr_common.h"
 
 namespace gr {
 
+constexpr int AT_KT = 32;   // keys per tile
+
 template <int HD>
-__global__ __launch_bounds__(256) void attn_mfma_kernel(const float* __restrict__ qkv,
-                                                        float* __restrict__ out, int n, int H,
-                                                        float scale, int qt_from) {
-  constexpr int FT = HD / 32;            // feature tiles of the head
-  const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
-  const int w = threadIdx.x >> 6;
+struct AttnTile {                  // one 32-query tile owned by a wave
+  f32x4 qf[HD / 32][4];            // B operand: scaled q[32qt + r][32it + 8g + 4h .. +3]
+  f32x16 O[HD / 32];               // O^T[feature][query]
+  float m, l;                      // running max / sum of this lane's query
+};
+
+template <int HD>
+__global__ __launch_bounds__(256, 1) void attn_mfma_kernel(const float* __restrict__ qkv,
+                                                           float* __restrict__ out, int n, int H,
+                                                           float scale, int qt_lo) {
+  constexpr int FT = HD / 32;
+  constexpr int KP = HD + 4;   // K row pitch: conflict-free ds_read_b128 of 16 rows
+  constexpr int VP = HD + 8;   // V row pitch: the two lane halves (4 rows apart) on disjoint banks
+  constexpr int LV = AT_KT * HD / 4 / 256;   // float4 per thread per tile, each of K and V
+  __shared__ __attribute__((aligned(16))) float ks[2][AT_KT * KP];
+  __shared__ __attribute__((aligned(16))) float vs[2][AT_KT * VP];
+  const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, h = lane >> 5;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int bh = blockIdx.x, b = bh / H, hh = bh % H;
-  const int qt = qt_from + blockIdx.y * 4 + w;   // this wave's query tile
-  if (qt * 32 >= n) return;              // whole wave; no barrier in the kernel
   const int d = H * HD;
   const int64_t rs = 3LL * d;
   const float* base = qkv + (int64_t)b * n * rs + hh * HD;
   const float* Qb = base;
   const float* Kb = base + d;
   const float* Vb = base + 2 * d;
+  const int T = (n + 31) / 32;
 
-  // B operand: scaled query rows, lane (r, h): q[32qt + r][32it + 8g + 4h .. +3]
-  const int qi = qt * 32 + r;
-  const int qc = qi < n ? qi : n - 1;
-  f32x4 qf[FT][4];
+  // rounds of 4 query tiles, one per wave, taken from the end (the first round streams every key
+  // tile with all 4 waves busy for most of them; the short causal tail comes last)
+  for (int t1 = T; t1 > qt_lo; t1 -= 4) {
+    const int t0 = t1 - 4 > qt_lo ? t1 - 4 : qt_lo;
+    const int nt = t1 - t0;
+    int myq[2] = {w < nt ? t0 + w : -1, -1};
+    AttnTile<HD> at[1];
 #pragma unroll
-  for (int it = 0; it < FT; ++it)
+    for (int u = 0; u < 1; ++u) {
+      const int qt = myq[u] < 0 ? t0 : myq[u];
+      const int qi = qt * 32 + r;
+      const int qc = qi < n ? qi : n - 1;
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      f32x4 v = *reinterpret_cast<const f32x4*>(Qb + (int64_t)qc * rs + 32 * it + 8 * g + 4 * h);
-      qf[it][g] = v * scale;             // q * sqrt(1/hd) (functional.py:6578)
+      for (int it = 0; it < FT; ++it)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const f32x4 v = *reinterpret_cast<const f32x4*>(Qb + (int64_t)qc * rs + 32 * it + 8 * g + 4 * h);
+          at[u].qf[it][g] = v * scale;   // q * sqrt(1/hd) (functional.py:6578)
+        }
+#pragma unroll
+      for (int ft = 0; ft < FT; ++ft)
+#pragma unroll
+        for (int v = 0; v < 16; ++v) at[u].O[ft][v] = 0.f;
+      at[u].m = -INFINITY;
+      at[u].l = 0.f;
     }
-  f32x16 O[FT];
+    const int qmax = t0 + nt - 1;   // the last key tile any wave of this round needs
+    f32x4 pk[LV], pv[LV];
+    auto gload = [&](int kt) {
 #pragma unroll
-  for (int ft = 0; ft < FT; ++ft)
-#pragma unroll
-    for (int v = 0; v < 16; ++v) O[ft][v] = 0.f;
-  float m = -INFINITY, l = 0.f;          // running max / sum of this lane's query
-  for (int kt = 0; kt <= qt; ++kt) {
-    // S^T tile [32 keys x 32 queries]
-    const int kj = kt * 32 + r;          // A operand row = key
-    const int kc = kj < n ? kj : n - 1;
-    f32x16 S;
-#pragma unroll
-    for (int v = 0; v < 16; ++v) S[v] = 0.f;
-#pragma unroll
-    for (int it = 0; it < FT; ++it)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const f32x4 kv = *reinterpret_cast<const f32x4*>(Kb + (int64_t)kc * rs + 32 * it + 8 * g + 4 * h);
-#pragma unroll
-        for (int s = 0; s < 4; ++s) S = mfma32(kv[s], qf[it][g][s], S);
+      for (int i = 0; i < LV; ++i) {
+        const int f = tid + 256 * i, row = f / (HD / 4), col = (f % (HD / 4)) * 4;
+        int key = kt * AT_KT + row;
+        key = key < n ? key : n - 1;
+        pk[i] = *reinterpret_cast<const f32x4*>(Kb + (int64_t)key * rs + col);
+        pv[i] = *reinterpret_cast<const f32x4*>(Vb + (int64_t)key * rs + col);
       }
-    // causal / padding mask: register v holds key 32kt + (v&3) + 8(v>>2) + 4h for query qi
-    float tmax = -INFINITY;
+    };
+    auto swrite = [&](int bf) {
 #pragma unroll
-    for (int v = 0; v < 16; ++v) {
-      const int key = kt * 32 + (v & 3) + 8 * (v >> 2) + 4 * h;
-      if (key > qi || key >= n) S[v] = -INFINITY;
-      tmax = fmaxf(tmax, S[v]);
-    }
-    tmax = fmaxf(tmax, __shfl_xor(tmax, 32));
-    const float mn = fmaxf(m, tmax);
-    const float alpha = __expf(m - mn);  // 0 on the first tile (m = -inf)
-    float ts = 0.f;
-#pragma unroll
-    for (int v = 0; v < 16; ++v) {
-      const float e = __expf(S[v] - mn);
-      S[v] = e;
-      ts += e;
-    }
-    ts += __shfl_xor(ts, 32);
-    l = l * alpha + ts;
-    m = mn;
-#pragma unroll
-    for (int ft = 0; ft < FT; ++ft) O[ft] *= alpha;
-    // O^T[f][q] += V^T[f][key] P^T[key][q]: A = value rows (lane = feature), B = S^T registers
-#pragma unroll
-    for (int ft = 0; ft < FT; ++ft)
-#pragma unroll
-      for (int s = 0; s < 16; ++s) {
-        const int key = kt * 32 + (s & 3) + 8 * (s >> 2) + 4 * h;
-        const float vv = key < n ? Vb[(int64_t)key * rs + 32 * ft + r] : 0.f;
-        O[ft] = mfma32(vv, S[s], O[ft]);
+      for (int i = 0; i < LV; ++i) {
+        const int f = tid + 256 * i, row = f / (HD / 4), col = (f % (HD / 4)) * 4;
+        *reinterpret_cast<f32x4*>(&ks[bf][row * KP + col]) = pk[i];
+        *reinterpret_cast<f32x4*>(&vs[bf][row * VP + col]) = pv[i];
       }
+    };
+    // one key tile against the wave's query tiles U0 .. U0+NU-1
+    auto tile_step = [&](auto u0_tag, auto nu_tag, int kt, int bf) {
+      constexpr int U0 = decltype(u0_tag)::value, NU = decltype(nu_tag)::value;
+      f32x16 S[NU];
+#pragma unroll
+      for (int u = 0; u < NU; ++u)
+#pragma unroll
+        for (int v = 0; v < 16; ++v) S[u][v] = 0.f;
+      const float* kr = &ks[bf][r * KP + 4 * h];
+#pragma unroll
+      for (int it = 0; it < FT; ++it)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const f32x4 kv = *reinterpret_cast<const f32x4*>(kr + 32 * it + 8 * g);
+#pragma unroll
+          for (int s4 = 0; s4 < 4; ++s4)
+#pragma unroll
+            for (int u = 0; u < NU; ++u) S[u] = mfma32(kv[s4], at[U0 + u].qf[it][g][s4], S[u]);
+        }
+#pragma unroll
+      for (int u = 0; u < NU; ++u) {
+        AttnTile<HD>& A = at[U0 + u];
+        const int qi = myq[U0 + u] * 32 + r;
+        // causal / padding mask: register v holds key 32kt + (v&3) + 8(v>>2) + 4h for query qi
+        float tmax = -INFINITY;
+#pragma unroll
+        for (int v = 0; v < 16; ++v) {
+          const int key = kt * 32 + (v & 3) + 8 * (v >> 2) + 4 * h;
+          if (key > qi || key >= n) S[u][v] = -INFINITY;
+          tmax = fmaxf(tmax, S[u][v]);
+        }
+        tmax = fmaxf(tmax, __shfl_xor(tmax, 32));
+        const float mn = fmaxf(A.m, tmax);
+        const float alpha = __expf(A.m - mn);   // 0 on the first tile (m = -inf)
+        float ts = 0.f;
+#pragma unroll
+        for (int v = 0; v < 16; ++v) {
+          const float e = __expf(S[u][v] - mn);
+          S[u][v] = e;
+          ts += e;
+        }
+        ts += __shfl_xor(ts, 32);
+        A.l = A.l * alpha + ts;
+        A.m = mn;
+#pragma unroll
+        for (int ft = 0; ft < FT; ++ft) A.O[ft] *= alpha;
+      }
+      // O^T[f][q] += V^T[f][key] P^T[key][q]: A = value rows (lane = feature), B = S^T registers
+#pragma unroll
+      for (int ft = 0; ft < FT; ++ft)
+#pragma unroll
+        for (int s = 0; s < 16; ++s) {
+          const int key = (s & 3) + 8 * (s >> 2) + 4 * h;
+          const float vv = kt * 32 + key < n ? vs[bf][key * VP + 32 * ft + r] : 0.f;
+#pragma unroll
+          for (int u = 0; u < NU; ++u) at[U0 + u].O[ft] = mfma32(vv, S[u][s], at[U0 + u].O[ft]);
+        }
+    };
+    gload(0);
+    swrite(0);
+    __syncthreads();
+    for (int kt = 0; kt <= qmax; ++kt) {
+      const int bf = kt & 1;
+      if (kt + 1 <= qmax) gload(kt + 1);
+      const bool act0 = myq[0] >= kt, act1 = myq[1] >= kt;   // wave-uniform
+      using I0 = std::integral_constant<int, 0>;
+      using I1 = std::integral_constant<int, 1>;
+      (void)act1;
+      if (act0) tile_step(I0{}, I1{}, kt, bf);
+      if (kt + 1 <= qmax) swrite(bf ^ 1);
+      __syncthreads();
+    }
+#pragma unroll
+    for (int u = 0; u < 1; ++u) {
+      if (myq[u] < 0) continue;
+      const int qi = myq[u] * 32 + r;
+      if (qi >= n) continue;
+      const float inv = 1.0f / at[u].l;
+      float* orow = out + ((int64_t)b * n + qi) * d + hh * HD;
+#pragma unroll
+      for (int ft = 0; ft < FT; ++ft)
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+          *reinterpret_cast<f32x4*>(orow + 32 * ft + 8 * g + 4 * h) =
+              f32x4{at[u].O[ft][4 * g], at[u].O[ft][4 * g + 1], at[u].O[ft][4 * g + 2], at[u].O[ft][4 * g + 3]} * inv;
+    }
   }
-  if (qi >= n) return;
-  const float inv = 1.0f / l;
-  float* orow = out + ((int64_t)b * n + qi) * d + hh * HD;
-#pragma unroll
-  for (int ft = 0; ft < FT; ++ft)
-#pragma unroll
-    for (int g = 0; g < 4; ++g)
-      *reinterpret_cast<f32x4*>(orow + 32 * ft + 8 * g + 4 * h) =
-          f32x4{O[ft][4 * g], O[ft][4 * g + 1], O[ft][4 * g + 2], O[ft][4 * g + 3]} * inv;
 }
 
 }  // namespace gr
@@ -121,13 +197,12 @@ int gr_attn_mfma_launch(const float* qkv, float* out, int64_t B, int n, int H, i
   if (hd != 32 && hd != 64 && hd != 128) return GR_ERR_UNSUPPORTED;
   if (!aligned16(qkv) || !aligned16(out)) return GR_ERR_UNSUPPORTED;
   if (B * H > 0x7fffffffLL) return GR_ERR_UNSUPPORTED;
-  const int qt_from = last_tile_only ? (n - 1) / 32 : 0;
-  const dim3 g((unsigned)(B * H), last_tile_only ? 1u : (unsigned)((n + 127) / 128)),
-      blk(last_tile_only ? 64 : 256);
+  const int qt_lo = last_tile_only ? (n - 1) / 32 : 0;
+  const dim3 g((unsigned)(B * H)), blk(256);
   switch (hd) {
-    case 32: hipLaunchKernelGGL(attn_mfma_kernel<32>, g, blk, 0, st, qkv, out, n, H, scale, qt_from); break;
-    case 64: hipLaunchKernelGGL(attn_mfma_kernel<64>, g, blk, 0, st, qkv, out, n, H, scale, qt_from); break;
-    default: hipLaunchKernelGGL(attn_mfma_kernel<128>, g, blk, 0, st, qkv, out, n, H, scale, qt_from); break;
+    case 32: hipLaunchKernelGGL(attn_mfma_kernel<32>, g, blk, 0, st, qkv, out, n, H, scale, qt_lo); break;
+    case 64: hipLaunchKernelGGL(attn_mfma_kernel<64>, g, blk, 0, st, qkv, out, n, H, scale, qt_lo); break;
+    default: hipLaunchKernelGGL(attn_mfma_kernel<128>, g, blk, 0, st, qkv, out, n, H, scale, qt_lo); break;
   }
   return check_launch("sasrec attention (mfma)");
 }
