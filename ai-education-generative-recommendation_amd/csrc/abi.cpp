@@ -15,7 +15,8 @@ static std::atomic<int64_t> g_rq_fused{1};
 // sas_fused (1: register-resident fused SASRec forward when n <= 64 and d <= 64, 0: layer-wise).
 static std::atomic<int64_t> g_sas_fused{1};
 // score_ablate (diagnostic, results INVALID when != 0): 1 = scoring kernel skips its logits
-// stores, 2 = skips its matrix work.  Used by scripts/ab_score.py to split the kernel's time.
+// stores, 2 = skips its matrix work, 3 = skips the matrix work and the logits ring writes, 4 = as
+// 3 and the store waves store constants (no ring reads).  scripts/ab_score.py splits the time.
 static std::atomic<int64_t> g_score_ablate{0};
 // topk_ablate (diagnostic, results INVALID when != 0): the fused score + top-k kernel skips 1 = all
 // top-k work (counts only), 2 = the appends and folds (keeps the per-chunk max test).
@@ -23,6 +24,15 @@ static std::atomic<int64_t> g_topk_ablate{0};
 // topk_sample (1: gr_score_topk_f32 takes its threshold from a strided sample pass when the
 // catalog is long enough, 0: always one pass).  Same results either way; used for A/B timing.
 static std::atomic<int64_t> g_topk_sample{1};
+// score_flags (1: the scoring kernel's compute and store waves hand chunks over through LDS words,
+// 0: one workgroup barrier per chunk).  Same results either way; used for A/B timing.
+static std::atomic<int64_t> g_score_flags{1};
+// score_ubmajor (1: the workgroups one XCD runs share a user block and sweep the catalog, 0: they
+// share a catalog slice across all user blocks).  Same results; A/B timing.
+static std::atomic<int64_t> g_score_ubmajor{1};
+// score_impl (0: compute / store wave specialisation with the LDS ring, 1: direct accumulator
+// stores, two workgroups per CU).  Same results; A/B timing.
+static std::atomic<int64_t> g_score_impl{0};
 
 int64_t option(const char* name) {
   if (!strcmp(name, "rq_fused")) return g_rq_fused.load();
@@ -30,6 +40,9 @@ int64_t option(const char* name) {
   if (!strcmp(name, "score_ablate")) return g_score_ablate.load();
   if (!strcmp(name, "topk_ablate")) return g_topk_ablate.load();
   if (!strcmp(name, "topk_sample")) return g_topk_sample.load();
+  if (!strcmp(name, "score_flags")) return g_score_flags.load();
+  if (!strcmp(name, "score_ubmajor")) return g_score_ubmajor.load();
+  if (!strcmp(name, "score_impl")) return g_score_impl.load();
   return -1;
 }
 }  // namespace gr
@@ -39,9 +52,12 @@ extern "C" int gr_set_option(const char* name, int64_t value) {
   if (!name) return gr::fail(GR_ERR_ARG, "gr_set_option: null name");
   if (!strcmp(name, "rq_fused") && (value == 0 || value == 1)) { gr::g_rq_fused = value; return GR_OK; }
   if (!strcmp(name, "sas_fused") && (value == 0 || value == 1)) { gr::g_sas_fused = value; return GR_OK; }
-  if (!strcmp(name, "score_ablate") && value >= 0 && value <= 2) { gr::g_score_ablate = value; return GR_OK; }
+  if (!strcmp(name, "score_ablate") && value >= 0 && value <= 4) { gr::g_score_ablate = value; return GR_OK; }
   if (!strcmp(name, "topk_ablate") && value >= 0 && value <= 2) { gr::g_topk_ablate = value; return GR_OK; }
   if (!strcmp(name, "topk_sample") && (value == 0 || value == 1)) { gr::g_topk_sample = value; return GR_OK; }
+  if (!strcmp(name, "score_flags") && (value == 0 || value == 1)) { gr::g_score_flags = value; return GR_OK; }
+  if (!strcmp(name, "score_ubmajor") && (value == 0 || value == 1)) { gr::g_score_ubmajor = value; return GR_OK; }
+  if (!strcmp(name, "score_impl") && (value == 0 || value == 1)) { gr::g_score_impl = value; return GR_OK; }
   return gr::fail(GR_ERR_ARG, std::string("gr_set_option: unknown option or value: ") + name);
 }
 

@@ -39,25 +39,76 @@ __device__ __forceinline__ int line_shift(uint32_t pbase, int ul, int64_t ld) {
   return (int)((32u - ((pbase + (uint32_t)((int64_t)ul * ld)) & 31u)) & 31u);
 }
 
-template <int D>
-__global__ __launch_bounds__(128 * ScCW<D>::value, 2) void score_kernel(const float* __restrict__ h, int64_t B,
+// Intra-workgroup hand-off through LDS words (FLAGS variant): a wave publishes after its own LDS
+// traffic has retired (lgkmcnt(0)), one lane writes the word; a waiting wave polls with relaxed
+// loads and s_sleep.  Global stores stay in flight across a publish (no vmcnt wait).
+__device__ __forceinline__ void lds_publish_add(int* w, int v, int lane) {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  if (lane == 0) __hip_atomic_fetch_add(w, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_publish_set(int* w, int v, int lane) {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  if (lane == 0) __hip_atomic_store(w, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_wait_ge(int* w, int target) {
+  while (__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < target)
+    __builtin_amdgcn_s_sleep(1);
+  asm volatile("" ::: "memory");
+}
+// every one of the 4 words w[0..3] >= target (per-wave progress counters: a sum could be met by
+// one wave running ahead while another has not finished its part)
+__device__ __forceinline__ void lds_wait_all_ge(int* w, int target) {
+  while (true) {
+    const int a = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    const int b = __hip_atomic_load(w + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    const int c = __hip_atomic_load(w + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    const int d = __hip_atomic_load(w + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (min(min(a, b), min(c, d)) >= target) break;
+    __builtin_amdgcn_s_sleep(1);
+  }
+  asm volatile("" ::: "memory");
+}
+
+// Store waves per workgroup (64 logits rows each).  8 waves of 32 rows were measured 1.6x slower
+// at d = 64: the compute waves spill at 3 waves per SIMD.
+template <int D, bool FLAGS> struct ScSW { static constexpr int value = 4; };
+
+template <int D, bool FLAGS>
+__global__ __launch_bounds__(64 * (ScCW<D>::value + ScSW<D, FLAGS>::value), 1) void score_kernel(const float* __restrict__ h, int64_t B,
                                                    const float* __restrict__ table, int64_t rows,
                                                    float* __restrict__ out, int64_t ld,
-                                                   int ublocks, int slices, int ablate) {
+                                                   int ublocks, int slices, int ablate, int ubmajor) {
   constexpr int KG = D / 32;                       // 32-deep k groups
   constexpr int P = D + 4;                         // LDS table row pitch (floats)
   constexpr int CW = ScCW<D>::value, SC_USERS = 64 * CW;
+  constexpr int SWN = ScSW<D, FLAGS>::value;       // store waves
+  constexpr int RPW = SC_USERS / SWN;              // logits rows per store wave
+  constexpr int SI = RPW / 8;                      // store instructions (8 rows each) per line
   constexpr int LV = SC_CHUNK * D / 4 / (64 * CW);  // float4 per store-wave thread per chunk load
   constexpr int RW = SC_RING * SC_CHUNK;           // ring width per user row (items)
   __shared__ __attribute__((aligned(16))) float tab[2][SC_CHUNK * P];
   __shared__ __attribute__((aligned(16))) float ring[SC_USERS * RW];
+  // FLAGS variant: the compute waves stage the table themselves (so the store waves issue no
+  // vector-memory loads, and no vmcnt wait for a load ever drains their stores), and the roles
+  // hand over through LDS words instead of one barrier per chunk: [w] table chunks compute wave w
+  // has staged (its quarter), [CW + w] table chunks it has consumed, [2CW + w] chunks of logits it
+  // has put in the ring, [3CW + sw] lines store wave sw has taken out of the ring.
+  static_assert(ScCW<D>::value == 4, "4 compute waves");
+  __shared__ __attribute__((aligned(16))) int sy[3 * ScCW<D>::value + ScSW<D, FLAGS>::value];
   const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, hh = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wgid = xcd_remap(blockIdx.x, gridDim.x);
-  const int ub = wgid % ublocks, sl = wgid / ublocks;
+  // slice-major within an XCD: the 32 workgroups an XCD runs share one user block and sweep the
+  // catalog (logits rows of one block, whole row range), not one column band of every row
+  const int ub = ubmajor ? wgid / slices : wgid % ublocks;
+  const int sl = ubmajor ? wgid % slices : wgid / ublocks;
   const int64_t chunks = (rows + SC_CHUNK - 1) / SC_CHUNK;
   const int64_t c_begin = chunks * sl / slices, c_end = chunks * (sl + 1) / slices;
   if (c_begin >= c_end) return;   // whole workgroup: uniform
+  if (FLAGS) {
+    if (tid < 3 * CW + SWN) sy[tid] = 0;
+    __syncthreads();
+  }
   const int64_t s_lo = c_begin * SC_CHUNK;
   const int64_t s_hi = c_end * SC_CHUNK < rows ? c_end * SC_CHUNK : rows;
   const int64_t ubase = (int64_t)ub * SC_USERS;   // first user of the workgroup
@@ -95,13 +146,39 @@ __global__ __launch_bounds__(128 * ScCW<D>::value, 2) void score_kernel(const fl
         const int p = r - line_shift(pbase, ul, ld);
         rpos[ut][v] = ul * RW + (p < 0 ? p + RW : p);
       }
-    __syncthreads();   // table chunk c_begin staged by the store waves
+    f32x4 cst[LV];   // FLAGS: this wave's quarter of the next table chunk, loaded a chunk ahead
+    auto cgload = [&](int64_t c) {
+#pragma unroll
+      for (int i = 0; i < LV; ++i) {
+        const int f = tid + 64 * CW * i, row = f / (D / 4), col = (f % (D / 4)) * 4;
+        int64_t item = c * SC_CHUNK + row;
+        item = item < rows ? item : rows - 1;   // past-the-end items are never stored
+        cst[i] = *reinterpret_cast<const f32x4*>(table + item * D + col);
+      }
+    };
+    auto cswrite = [&](int b) {
+#pragma unroll
+      for (int i = 0; i < LV; ++i) {
+        const int f = tid + 64 * CW * i, row = f / (D / 4), col = (f % (D / 4)) * 4;
+        *reinterpret_cast<f32x4*>(&tab[b][row * P + col]) = cst[i];
+      }
+    };
+    if (FLAGS) {
+      cgload(c_begin);
+      cswrite(0);
+      lds_publish_set(&sy[wave], 1, lane);   // table chunk 0: this wave's quarter staged
+      if (c_begin + 1 < c_end) cgload(c_begin + 1);
+    } else {
+      __syncthreads();   // table chunk c_begin staged by the store waves
+    }
     auto run = [&](auto nomfma_sel) {
       constexpr bool NOMFMA = decltype(nomfma_sel)::value;
       int cm = (int)((c_begin * SC_CHUNK) % RW);   // 32k mod RW
 #pragma unroll 1
       for (int64_t k = c_begin; k < c_end; ++k) {
         const int kb = (int)((k - c_begin) & 1);
+        const int j = (int)(k - c_begin);
+        if (FLAGS) lds_wait_all_ge(&sy[0], j + 1);   // table chunk j staged by every compute wave
         f32x16 acc[2];
 #pragma unroll
         for (int ut = 0; ut < 2; ++ut)
@@ -121,25 +198,39 @@ __global__ __launch_bounds__(128 * ScCW<D>::value, 2) void score_kernel(const fl
                 else acc[ut] = mfma32(hf[ut][g][q][s], bt[s], acc[ut]);
               }
           }
+        if (FLAGS) {
+          lds_publish_set(&sy[CW + wave], j + 1, lane);   // done reading table chunk j
+          if (k + 1 < c_end) {   // stage chunk j+1 into the buffer chunk j-1 used
+            lds_wait_all_ge(&sy[CW], j);                  // ... once every wave is done with j-1
+            cswrite((j + 1) & 1);
+            lds_publish_set(&sy[wave], j + 2, lane);
+            if (k + 2 < c_end) cgload(k + 2);             // a whole chunk period ahead
+          }
+          // its ring slots drained by the store waves of its rows
+#pragma unroll
+          for (int q = 0; q < SWN / CW; ++q) lds_wait_ge(&sy[3 * CW + wave * (SWN / CW) + q], j + 2 - SC_RING);
+        }
         // logits tile -> ring (row-shifted); a position past the row's RW wraps back by RW
 #pragma unroll
-        for (int ut = 0; ut < 2; ++ut)
+        for (int ut = 0; ut < 2 && ablate < 3; ++ut)
 #pragma unroll
           for (int v = 0; v < 16; ++v) {
             const int ul_end = (wave * 64 + ut * 32 + (v & 3) + 8 * (v >> 2) + 4 * hh + 1) * RW;
             const int p = rpos[ut][v] + cm;
             ring[p >= ul_end ? p - RW : p] = acc[ut][v];
           }
-        __syncthreads();
+        if (FLAGS) lds_publish_set(&sy[2 * CW + wave], j + 1, lane);
+        else __syncthreads();
         cm = cm + SC_CHUNK == RW ? 0 : cm + SC_CHUNK;
       }
-      __syncthreads();   // the store waves' final iteration
+      if (!FLAGS) __syncthreads();   // the store waves' final iteration
     };
-    if (ablate == 2) run(std::true_type{});
+    if (ablate >= 2) run(std::true_type{});
     else run(std::false_type{});
   } else {
     // ------------------------------------------------------------------ store waves
     const int sw = wave - CW, stid = tid - 64 * CW;
+    const int cw_of = sw / (SWN / CW);   // the compute wave whose rows this store wave writes
     // table chunks are loaded two chunks ahead (register double buffer): the HBM / L2 latency
     // spans a whole chunk period instead of being exposed before every barrier
     f32x4 st[2][LV];
@@ -159,20 +250,22 @@ __global__ __launch_bounds__(128 * ScCW<D>::value, 2) void score_kernel(const fl
         *reinterpret_cast<f32x4*>(&tab[b][row * P + col]) = st[sb][i];
       }
     };
-    gload(c_begin, 0);
-    if (c_begin + 1 < c_end) gload(c_begin + 1, 1);
-    swrite(0, 0);
-    // Store instruction i covers local rows 64 sw + 8i + (lane >> 3); lane part e = lane & 7
+    if (!FLAGS) {
+      gload(c_begin, 0);
+      if (c_begin + 1 < c_end) gload(c_begin + 1, 1);
+      swrite(0, 0);
+    }
+    // Store instruction i covers local rows RPW sw + 8i + (lane >> 3); lane part e = lane & 7
     // holds items 4e..4e+3 of the row's line [32c - 32 + a, 32c + a) for chunk c: 8 rows x one
     // whole, aligned 128-byte line per instruction (dwordx4 per lane).  Descriptor 32 items before
     // the workgroup's first row (offsets stay non-negative), chunk as the scalar soffset.
     const auto rs = __builtin_amdgcn_make_buffer_rsrc(out + ubase * ld - SC_CHUNK, 0, -1, 0x00020000);
     const int e = lane & 7;
-    int voff[8], lrow[8], ashift[8];
+    int voff[SI], lrow[SI], ashift[SI];
     uint32_t row_mask = 0;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int ul = 64 * sw + 8 * i + (lane >> 3);
+    for (int i = 0; i < SI; ++i) {
+      const int ul = RPW * sw + 8 * i + (lane >> 3);
       ashift[i] = line_shift(pbase, ul, ld);
       voff[i] = (int)(((int64_t)ul * ld + ashift[i] + 4 * e) * 4);
       lrow[i] = ul * RW + 4 * e;
@@ -181,7 +274,7 @@ __global__ __launch_bounds__(128 * ScCW<D>::value, 2) void score_kernel(const fl
     const bool all_rows = ubase + SC_USERS <= B;
     // items [lo, hi) of chunk-c's line, per item (slice ends, the tail, partial user blocks)
     auto store_items = [&](int i, int64_t c, int64_t lo, int64_t hi, int pos) {
-      const int ul = 64 * sw + 8 * i + (lane >> 3);
+      const int ul = RPW * sw + 8 * i + (lane >> 3);
       if (!((row_mask >> i) & 1u)) return;
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
@@ -194,34 +287,40 @@ __global__ __launch_bounds__(128 * ScCW<D>::value, 2) void score_kernel(const fl
         }
       }
     };
-    __syncthreads();
+    if (!FLAGS) __syncthreads();
     // ring position of the line read at iteration k (the line ending in chunk k-1): 32(k-2) mod RW
     int lm = (int)((((c_begin - 2) * SC_CHUNK) % RW + RW) % RW);
     auto iter = [&](int64_t k, auto par_sel) {   // par = (k - c_begin) & 1: register buffer of chunk k+1
       constexpr int par = decltype(par_sel)::value;
-      if (k + 2 < c_end) gload(k + 2, par);   // chunk k+2 into the buffer chunk k just freed
+      if (!FLAGS && k + 2 < c_end) gload(k + 2, par);   // chunk k+2 into the buffer chunk k freed
+      const int j = (int)(k - c_begin);
+      if (FLAGS && k > c_begin) lds_wait_ge(&sy[2 * CW + cw_of], j);   // chunk k-1 in the ring
       if (k > c_begin && ablate != 1) {   // the line ending inside chunk c = k-1 (k-2 still held)
         const int64_t c = k - 1, c0 = c * SC_CHUNK;
         const int soff = (int)(c0 * 4);
         if (all_rows && c0 - SC_CHUNK >= s_lo && c0 + SC_CHUNK <= s_hi) {   // steady state
 #pragma unroll
-          for (int i = 0; i < 8; ++i) {
-            const f32x4 v = *reinterpret_cast<const f32x4*>(&ring[lrow[i] + lm]);
+          for (int i = 0; i < SI; ++i) {
+            const f32x4 v = ablate == 4 ? f32x4{1.f, 2.f, 3.f, 4.f}
+                                        : *reinterpret_cast<const f32x4*>(&ring[lrow[i] + lm]);
             __builtin_amdgcn_raw_buffer_store_b128(
                 __builtin_bit_cast(HIP_vector_type<unsigned int, 4>::Native_vec_, v), rs, voff[i], soff, 0);
           }
         } else {
 #pragma unroll 1
-          for (int i = 0; i < 8; ++i) store_items(i, c, s_lo, s_hi < c0 + SC_CHUNK ? s_hi : c0 + SC_CHUNK, lm);
+          for (int i = 0; i < SI; ++i) store_items(i, c, s_lo, s_hi < c0 + SC_CHUNK ? s_hi : c0 + SC_CHUNK, lm);
         }
         if (k == c_end) {   // the tail after the slice's last whole line: [32c + a, s_hi)
           const int lt = lm + SC_CHUNK == RW ? 0 : lm + SC_CHUNK;
 #pragma unroll 1
-          for (int i = 0; i < 8; ++i) store_items(i, c + 1, s_lo, s_hi, lt);
+          for (int i = 0; i < SI; ++i) store_items(i, c + 1, s_lo, s_hi, lt);
         }
       }
-      if (k + 1 < c_end) swrite(par ^ 1, par ^ 1);
-      __syncthreads();
+      if (FLAGS && k > c_begin) lds_publish_set(&sy[3 * CW + sw], j, lane);   // line k-1 taken
+      if (!FLAGS) {
+        if (k + 1 < c_end) swrite(par ^ 1, par ^ 1);
+        __syncthreads();
+      }
       lm = lm + SC_CHUNK == RW ? 0 : lm + SC_CHUNK;
     };
     int64_t k = c_begin;
@@ -232,6 +331,120 @@ __global__ __launch_bounds__(128 * ScCW<D>::value, 2) void score_kernel(const fl
     }
     if (k <= c_end) iter(k, std::integral_constant<int, 0>{});
   }
+}
+
+// Direct-store variant (option score_impl = 1): no store waves and no ring.  Each of the 4 waves
+// scores 64 users against the chunk and writes its accumulators as they stand: register v of lane
+// (r, h) is row (v&3) + 8(v>>2) + 4h, column r, so one dword store per register covers two rows x
+// 32 consecutive logits (two 128-B segments, unaligned when the row stride is odd: the next
+// chunk's stores complete the lines in L2).  Two workgroups per CU, so one wave's MFMAs run while
+// another's stores drain.
+template <int D>
+__global__ __launch_bounds__(256, 2) void score_direct_kernel(const float* __restrict__ h, int64_t B,
+                                                            const float* __restrict__ table, int64_t rows,
+                                                            float* __restrict__ out, int64_t ld,
+                                                            int ublocks, int slices) {
+  constexpr int KG = D / 32;
+  constexpr int P = D + 4;
+  constexpr int LV = SC_CHUNK * D / 4 / 256;
+  __shared__ __attribute__((aligned(16))) float tab[2][SC_CHUNK * P];
+  const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, hh = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wgid = xcd_remap(blockIdx.x, gridDim.x);
+  const int ub = wgid / slices, sl = wgid % slices;
+  const int64_t chunks = (rows + SC_CHUNK - 1) / SC_CHUNK;
+  const int64_t c_begin = chunks * sl / slices, c_end = chunks * (sl + 1) / slices;
+  if (c_begin >= c_end) return;
+  const int64_t u0 = (int64_t)ub * 256 + wave * 64;
+  f32x4 hf[2][KG][4];
+#pragma unroll
+  for (int ut = 0; ut < 2; ++ut) {
+    const int64_t u = u0 + ut * 32 + r;
+    const int64_t uc = u < B ? u : B - 1;
+#pragma unroll
+    for (int g = 0; g < KG; ++g)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const f32x4 v = *reinterpret_cast<const f32x4*>(h + uc * D + 32 * g + 8 * q + 4 * hh);
+        hf[ut][g][q] = u < B ? v : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+  }
+  // row pointers of the lane's 32 rows (register v of user tile ut), column r
+  const bool full_rows = u0 + 64 <= B;
+  f32x4 st[LV];
+  auto gload = [&](int64_t c) {
+#pragma unroll
+    for (int i = 0; i < LV; ++i) {
+      const int f = tid + 256 * i, row = f / (D / 4), col = (f % (D / 4)) * 4;
+      int64_t item = c * SC_CHUNK + row;
+      item = item < rows ? item : rows - 1;
+      st[i] = *reinterpret_cast<const f32x4*>(table + item * D + col);
+    }
+  };
+  auto swrite = [&](int b) {
+#pragma unroll
+    for (int i = 0; i < LV; ++i) {
+      const int f = tid + 256 * i, row = f / (D / 4), col = (f % (D / 4)) * 4;
+      *reinterpret_cast<f32x4*>(&tab[b][row * P + col]) = st[i];
+    }
+  };
+  gload(c_begin);
+  swrite(0);
+  if (c_begin + 1 < c_end) gload(c_begin + 1);
+  __syncthreads();
+  float* obase = out + u0 * ld + r;
+  // software pipeline: the logits of chunk k-1 (prev) are stored one register at a time between
+  // the MFMAs of chunk k, so the wave's stores trickle out at a steady rate instead of a burst
+  f32x16 prev[2];
+  int64_t pk = -1;   // chunk held in prev (-1: none)
+  auto store_one = [&](int t) {   // register t of prev: user tile t >> 4, register t & 15
+    const int ut = t >> 4, v = t & 15;
+    const int rl = 32 * ut + (v & 3) + 8 * (v >> 2) + 4 * hh;
+    const int64_t col = pk * SC_CHUNK + r;
+    float* op = obase + pk * SC_CHUNK + (int64_t)rl * ld;
+    if (full_rows && pk * SC_CHUNK + SC_CHUNK <= rows) __builtin_nontemporal_store(prev[ut][v], op);
+    else if (u0 + rl < B && col < rows) *op = prev[ut][v];
+  };
+  constexpr int STEPS = KG * 16;             // (g, q, s) steps of a chunk, 2 MFMAs each
+  constexpr int PER = 32 / STEPS > 0 ? 32 / STEPS : 1;   // stores per step
+  constexpr int EVERY = STEPS / 32 > 0 ? STEPS / 32 : 1;  // steps per store
+#pragma unroll 1
+  for (int64_t k = c_begin; k < c_end; ++k) {
+    const int kb = (int)((k - c_begin) & 1);
+    const bool have_prev = pk >= 0;
+    f32x16 acc[2];
+#pragma unroll
+    for (int ut = 0; ut < 2; ++ut)
+#pragma unroll
+      for (int v = 0; v < 16; ++v) acc[ut][v] = 0.f;
+    const float* tb = &tab[kb][r * P + 4 * hh];
+#pragma unroll
+    for (int g = 0; g < KG; ++g)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const f32x4 bt = *reinterpret_cast<const f32x4*>(tb + 32 * g + 8 * q);
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) {
+          const int step = (g * 4 + q) * 4 + s4;
+#pragma unroll
+          for (int ut = 0; ut < 2; ++ut) acc[ut] = mfma32(hf[ut][g][q][s4], bt[s4], acc[ut]);
+          if (have_prev && step % EVERY == 0) {
+#pragma unroll
+            for (int e = 0; e < PER; ++e) store_one((step / EVERY) * PER + e);
+          }
+        }
+      }
+    if (k + 1 < c_end) {
+      swrite(kb ^ 1);
+      if (k + 2 < c_end) gload(k + 2);
+    }
+    prev[0] = acc[0];
+    prev[1] = acc[1];
+    pk = k;
+    __syncthreads();
+  }
+#pragma unroll
+  for (int t = 0; t < 32; ++t) store_one(t);
 }
 
 }  // namespace gr
@@ -260,12 +473,32 @@ int gr_score_launch(const float* h, int64_t B, int32_t d, const float* table, in
   if (slices > chunks) slices = chunks;
   if (slices < 1) slices = 1;
   if (ublocks * slices > 0x7fffffffLL) return fail(GR_ERR_UNSUPPORTED, "gr_score_f32: grid too large");
-  const dim3 g((unsigned)(ublocks * slices)), b(128 * cw);
+  const dim3 g((unsigned)(ublocks * slices));
   const int ablate = (int)option("score_ablate");   // diagnostic only (gr_set_option)
-  switch (d) {
-    case 32: hipLaunchKernelGGL(score_kernel<32>, g, b, 0, st, h, B, table, rows, logits, ld, (int)ublocks, (int)slices, ablate); break;
-    case 64: hipLaunchKernelGGL(score_kernel<64>, g, b, 0, st, h, B, table, rows, logits, ld, (int)ublocks, (int)slices, ablate); break;
-    default: hipLaunchKernelGGL(score_kernel<128>, g, b, 0, st, h, B, table, rows, logits, ld, (int)ublocks, (int)slices, ablate); break;
+  const bool flags = option("score_flags") != 0 && d <= 64;   // d = 128 spills at 2 waves / SIMD
+  const int ubmajor = (int)option("score_ubmajor");
+  if (option("score_impl") == 1) {
+    int64_t sl2 = (2 * cus + ublocks - 1) / ublocks;
+    if (sl2 > chunks) sl2 = chunks;
+    if (sl2 < 1) sl2 = 1;
+    const dim3 g2((unsigned)(ublocks * sl2));
+    switch (d) {
+      case 32: hipLaunchKernelGGL(score_direct_kernel<32>, g2, dim3(256), 0, st, h, B, table, rows, logits, ld, (int)ublocks, (int)sl2); break;
+      case 64: hipLaunchKernelGGL(score_direct_kernel<64>, g2, dim3(256), 0, st, h, B, table, rows, logits, ld, (int)ublocks, (int)sl2); break;
+      default: hipLaunchKernelGGL(score_direct_kernel<128>, g2, dim3(256), 0, st, h, B, table, rows, logits, ld, (int)ublocks, (int)sl2); break;
+    }
+    return check_launch("gr_score_f32 (direct)");
   }
+#define GR_SC_LAUNCH(DD)                                                                           \
+  if (flags) hipLaunchKernelGGL((score_kernel<DD, true>), g, dim3(64 * (cw + ScSW<DD, true>::value)), \
+                                0, st, h, B, table, rows, logits, ld, (int)ublocks, (int)slices, ablate, ubmajor); \
+  else hipLaunchKernelGGL((score_kernel<DD, false>), g, dim3(64 * (cw + ScSW<DD, false>::value)), 0, \
+                          st, h, B, table, rows, logits, ld, (int)ublocks, (int)slices, ablate, ubmajor);
+  switch (d) {
+    case 32: GR_SC_LAUNCH(32) break;
+    case 64: GR_SC_LAUNCH(64) break;
+    default: GR_SC_LAUNCH(128) break;
+  }
+#undef GR_SC_LAUNCH
   return check_launch("gr_score_f32");
 }

@@ -51,7 +51,13 @@ const char* gr_last_error(void);
  *                   multiples of 8), mlp <= 128, num_blocks <= 8; 0: the layer-wise pipeline
  *                   (the workspace query follows the option in force when it is called)
  *   "score_ablate"  0 (default).  DIAGNOSTIC ONLY, outputs invalid otherwise: 1 = the scoring
- *                   kernel skips the logits stores, 2 = it skips the matrix work
+ *                   kernel skips the logits stores, 2 = it skips the matrix work, 3 = also the
+ *                   logits ring writes, 4 = also the ring reads (constants stored)
+ *   "score_flags"   1 (default): the scoring kernel (d <= 64) hands chunks between its compute and
+ *                   store waves through LDS words; 0: one barrier per chunk.  Identical results.
+ *   "score_ubmajor" 1 (default): one XCD's workgroups share a user block; 0: a catalog slice.
+ *   "score_impl"    0 (default): compute / store wave specialisation with an LDS ring; 1: the
+ *                   compute waves store their accumulators directly (A/B only; identical results).
  *   "topk_ablate"   0 (default).  DIAGNOSTIC ONLY, outputs invalid otherwise: the fused score +
  *                   top-k kernel skips 1 = all top-k work (counts stay valid)
  *   "topk_sample"   1 (default): gr_score_topk_f32 prunes with a threshold from a strided sample

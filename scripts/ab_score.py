@@ -31,11 +31,21 @@ for suf in (sys.argv[1:] or [""]):
     call = lambda: fn(h.data_ptr(), B, D, t.data_ptr(), ROWS, out.data_ptr(), LD, st)
     for _ in range(3):
         assert call() == 0
+    lib.gr_set_option.argtypes = [ctypes.c_char_p, ctypes.c_int64]
+    if os.environ.get("AB_FLAGS") is not None:
+        assert lib.gr_set_option(b"score_flags", int(os.environ["AB_FLAGS"])) == 0
+        suf = (suf or "") + f"flags{os.environ['AB_FLAGS']}"
+    if os.environ.get("AB_IMPL") is not None:
+        assert lib.gr_set_option(b"score_impl", int(os.environ["AB_IMPL"])) == 0
+        suf = (suf or "") + f"impl{os.environ['AB_IMPL']}"
+    if os.environ.get("AB_UBM") is not None:
+        assert lib.gr_set_option(b"score_ubmajor", int(os.environ["AB_UBM"])) == 0
+        suf = (suf or "") + f"ubm{os.environ['AB_UBM']}"
     abl = int(os.environ.get("AB_ABLATE", 0))
     if abl:
         lib.gr_set_option.argtypes = [ctypes.c_char_p, ctypes.c_int64]
         assert lib.gr_set_option(b"score_ablate", abl) == 0
-        suf = f"ablate{abl}"
+        suf = (suf or "") + f"ablate{abl}"
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     for _ in range(20):

@@ -123,3 +123,31 @@ def test_score_topk_rejects_bad_args(dev):
         ops.score_topk(h, t, 17)
     with pytest.raises(RuntimeError, match="d must be"):
         ops.score_topk(torch.randn(4, 48, device=dev), torch.randn(100, 48, device=dev), 5)
+
+
+@pytest.mark.parametrize("B,d,rows,ld", [(300, 64, 100001, 100001), (2048, 64, 20001, 20032), (77, 32, 5003, 5003),
+                                         (129, 128, 9000, 9001)])
+def test_score_kernel_variants_identical(B, d, rows, ld, dev):
+    """Every scoring-kernel variant (LDS-word or barrier hand-off, XCD mapping, direct stores)
+    writes the same bits, ragged users / rows and odd row strides included."""
+    from gr_amd import _lib, ops
+    g = torch.Generator().manual_seed(B + rows)
+    h = torch.randn(B, d, generator=g).to(dev)
+    t = torch.randn(rows, d, generator=g).to(dev)
+    outs = []
+    try:
+        for opts in [dict(), dict(score_flags=0), dict(score_ubmajor=0), dict(score_impl=1)]:
+            for k, v in opts.items():
+                _lib.set_option(k, v)
+            buf = torch.full((B, ld), 7.0, device=dev)
+            ops.score(h, t, out=buf[:, :rows])
+            outs.append(buf)
+            for k in opts:
+                _lib.set_option(k, {"score_flags": 1, "score_ubmajor": 1, "score_impl": 0}[k])
+    finally:
+        _lib.set_option("score_flags", 1)
+        _lib.set_option("score_ubmajor", 1)
+        _lib.set_option("score_impl", 0)
+    for o in outs[1:]:
+        assert torch.equal(o, outs[0])
+    assert (outs[0][:, rows:] == 7.0).all()   # nothing written past the row's columns
