@@ -125,12 +125,16 @@ def traffic_of(kernel):
     return (t["bytes_per_launch"], t["source"]) if t else (None, None)
 
 
-def roofline(kernel, flop, ms, bound="mfma"):
+def roofline(kernel, flop, ms, bound="mfma", launches=1, note=None):
+    """``kernel`` names the dominant kernel (the profiles/traffic.json key); ``launches`` = its
+    launches per timed call (traffic is per call, like ``achieved``)."""
     ach = flop / (ms * 1e-3) / 1e12
     tr, src = traffic_of(kernel)
+    if tr is not None:
+        tr *= launches
     return {"bound": bound, "achieved": ach, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
             "frac": ach / FP32_PEAK_TFLOPS, "traffic": tr, "traffic_source": src, "kernel": kernel,
-            "flop_per_launch": flop, "kernel_ms": ms}
+            "flop_per_launch": flop, "kernel_ms": ms, **({"note": note} if note else {})}
 
 
 def cpu_threads():
@@ -240,7 +244,7 @@ def bench_sas_c3(a, world, rank, dev):
            "config": {"workload": "sas_c3: SASRec predict, 2 blocks, d 64, n 50, H 1, mlp 64, "
                                   "100k-item full-catalog logits written", "users_per_rank_per_step": a.sas_batch,
                       "parallelism": f"user-sharded x{world}, no collective"},
-           "roofline": roofline("score_kernel<64>", 2 * d * (items + 1) * a.sas_batch, score_ms),
+           "roofline": roofline("score_kernel<64,true>", 2 * d * (items + 1) * a.sas_batch, score_ms),
            "call": {"device_ms": dev_ms, "flop_per_user": fl,
                     "frac_of_fp32_peak": fl * a.sas_batch / (dev_ms * 1e-3) / 1e12 / FP32_PEAK_TFLOPS,
                     "forward_ms": fwd_ms, "score_ms": score_ms,
@@ -283,7 +287,9 @@ def bench_sas_c5(a, world, rank, dev):
                        "users_per_step": B, "catalog_rows": items + 1, "rows_per_rank": hi - lo,
                        "parallelism": f"catalog-sharded x{world}: RCCL all-gather h + top-k, all-reduce counts"
                        if world > 1 else "single shard"},
-            "roofline": roofline("score_topk_kernel<128,10> (sample + full pass + merges)", 2 * d * (hi - lo) * B, topk_ms),
+            "roofline": roofline("score_topk_kernel<128,10>", 2 * d * (hi - lo) * B, topk_ms, launches=2,
+                                 note="one gr_score_topk_f32 call: sample pass + exact pass + 2 merge "
+                                      "kernels; flop counts the exact pass only"),
             "call": {"device_ms_rank0": dev_ms, "flop_per_user": sas_flop_per_user(d, n, items),
                      "forward_ms": fwd_ms, "score_topk_ms": topk_ms,
                      "note": "rank + top-10 fused into the scoring pass (gr_score_topk_f32): the "
