@@ -107,6 +107,9 @@ __global__ __launch_bounds__(256) void linear_f32_kernel(
   }
 
   // Epilogue: bias, activation, residual; D register v -> row (v&3)+8(v>>2)+4h, column r.
+  // `residual` may alias `y` element for element (in-place residual add), so the compiler cannot
+  // move a residual load above an earlier y store: every residual of the tile is loaded first
+  // (all loads in flight together), then the outputs are stored.
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     const int col = n0 + wn * (BN / WN) + j * 32 + r;
@@ -114,6 +117,14 @@ __global__ __launch_bounds__(256) void linear_f32_kernel(
     const float bv = (bias != nullptr && cok) ? bias[col] : 0.f;
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
+      float rv[16];
+      if (RES) {
+#pragma unroll
+        for (int v = 0; v < 16; ++v) {
+          const int64_t row = m0 + wm * (BM / WM) + i * 32 + (v & 3) + 8 * (v >> 2) + 4 * h;
+          rv[v] = (cok && row < M) ? residual[row * ldr + col] : 0.f;
+        }
+      }
 #pragma unroll
       for (int v = 0; v < 16; ++v) {
         const int64_t row = m0 + wm * (BM / WM) + i * 32 + (v & 3) + 8 * (v >> 2) + 4 * h;
@@ -121,7 +132,7 @@ __global__ __launch_bounds__(256) void linear_f32_kernel(
           float o = acc[i][j][v];
           if (bias != nullptr) o = o + bv;
           if (ACT == GR_ACT_RELU) o = (o < 0.f) ? 0.f : o;  // NaN propagates like torch.relu
-          if (RES) o = residual[row * ldr + col] + o;
+          if (RES) o = rv[v] + o;
           y[row * ldy + col] = o;
         }
       }
