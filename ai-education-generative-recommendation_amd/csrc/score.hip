@@ -30,7 +30,10 @@ constexpr int SC_CHUNK = 32;   // items per chunk (one 32-item MFMA tile)
 // compute waves per workgroup (64 users each) and as many store waves.  4: one compute and one
 // store wave on every SIMD.  (2, with two workgroups per CU, measured 1.3x slower at C3: the
 // dispatcher may stack both workgroups' compute waves on the same two SIMDs.)
-template <int D> struct ScCW { static constexpr int value = 4; };
+// Compute waves per workgroup (256 users: 64 per wave as two 32-user MFMA tiles).  8 waves of 32
+// users (two per SIMD, so one wave's ring epilogue overlaps the other's MFMAs) measured no faster
+// at d = 64 (375 vs 372 us at C3); the kernel keeps the generality (UT tiles per wave).
+template <int D, bool FLAGS = false> struct ScCW { static constexpr int value = 4; };
 constexpr int SC_RING = 3;     // chunks of logits staged in LDS
 
 // Line alignment of a logits row: the first item of a 128-byte line in row ul (mod 32), given the
@@ -55,15 +58,15 @@ __device__ __forceinline__ void lds_wait_ge(int* w, int target) {
     __builtin_amdgcn_s_sleep(1);
   asm volatile("" ::: "memory");
 }
-// every one of the 4 words w[0..3] >= target (per-wave progress counters: a sum could be met by
+// every one of the N words w[0..N) >= target (per-wave progress counters: a sum could be met by
 // one wave running ahead while another has not finished its part)
+template <int N>
 __device__ __forceinline__ void lds_wait_all_ge(int* w, int target) {
   while (true) {
-    const int a = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    const int b = __hip_atomic_load(w + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    const int c = __hip_atomic_load(w + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    const int d = __hip_atomic_load(w + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    if (min(min(a, b), min(c, d)) >= target) break;
+    int m = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#pragma unroll
+    for (int i = 1; i < N; ++i) m = min(m, __hip_atomic_load(w + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+    if (m >= target) break;
     __builtin_amdgcn_s_sleep(1);
   }
   asm volatile("" ::: "memory");
@@ -74,17 +77,21 @@ __device__ __forceinline__ void lds_wait_all_ge(int* w, int target) {
 template <int D, bool FLAGS> struct ScSW { static constexpr int value = 4; };
 
 template <int D, bool FLAGS>
-__global__ __launch_bounds__(64 * (ScCW<D>::value + ScSW<D, FLAGS>::value), 1) void score_kernel(const float* __restrict__ h, int64_t B,
+__global__ __launch_bounds__(64 * (ScCW<D, FLAGS>::value + ScSW<D, FLAGS>::value), 1) void score_kernel(const float* __restrict__ h, int64_t B,
                                                    const float* __restrict__ table, int64_t rows,
                                                    float* __restrict__ out, int64_t ld,
                                                    int ublocks, int slices, int ablate, int ubmajor) {
   constexpr int KG = D / 32;                       // 32-deep k groups
   constexpr int P = D + 4;                         // LDS table row pitch (floats)
-  constexpr int CW = ScCW<D>::value, SC_USERS = 64 * CW;
+  constexpr int CW = ScCW<D, FLAGS>::value, SC_USERS = 256;   // compute waves; users per workgroup
+  constexpr int UT = SC_USERS / (32 * CW);                     // 32-user MFMA tiles per compute wave
+  constexpr int UPW = 32 * UT;                                 // users per compute wave
   constexpr int SWN = ScSW<D, FLAGS>::value;       // store waves
   constexpr int RPW = SC_USERS / SWN;              // logits rows per store wave
   constexpr int SI = RPW / 8;                      // store instructions (8 rows each) per line
-  constexpr int LV = SC_CHUNK * D / 4 / (64 * CW);  // float4 per store-wave thread per chunk load
+  constexpr int LV = SC_CHUNK * D / 4 / 256;        // float4 per staging thread per chunk (256 threads)
+  constexpr int LVC = SC_CHUNK * D / 4 / (64 * CW);  // ... per compute-wave thread (FLAGS staging)
+  static_assert(LVC >= 1, "table chunk too small for the compute waves to stage");
   constexpr int RW = SC_RING * SC_CHUNK;           // ring width per user row (items)
   __shared__ __attribute__((aligned(16))) float tab[2][SC_CHUNK * P];
   __shared__ __attribute__((aligned(16))) float ring[SC_USERS * RW];
@@ -93,8 +100,7 @@ __global__ __launch_bounds__(64 * (ScCW<D>::value + ScSW<D, FLAGS>::value), 1) v
   // hand over through LDS words instead of one barrier per chunk: [w] table chunks compute wave w
   // has staged (its quarter), [CW + w] table chunks it has consumed, [2CW + w] chunks of logits it
   // has put in the ring, [3CW + sw] lines store wave sw has taken out of the ring.
-  static_assert(ScCW<D>::value == 4, "4 compute waves");
-  __shared__ __attribute__((aligned(16))) int sy[3 * ScCW<D>::value + ScSW<D, FLAGS>::value];
+  __shared__ __attribute__((aligned(16))) int sy[3 * ScCW<D, FLAGS>::value + ScSW<D, FLAGS>::value];
   const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, hh = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wgid = xcd_remap(blockIdx.x, gridDim.x);
@@ -121,10 +127,10 @@ __global__ __launch_bounds__(64 * (ScCW<D>::value + ScSW<D, FLAGS>::value), 1) v
 
   if (wave < CW) {
     // ------------------------------------------------------------------ compute waves
-    const int64_t u0 = ubase + wave * 64;
-    f32x4 hf[2][KG][4];   // lane (r, hh) of user tile ut: h[u][32g + 8q + 4hh .. +3]
+    const int64_t u0 = ubase + wave * UPW;
+    f32x4 hf[UT][KG][4];   // lane (r, hh) of user tile ut: h[u][32g + 8q + 4hh .. +3]
 #pragma unroll
-    for (int ut = 0; ut < 2; ++ut) {
+    for (int ut = 0; ut < UT; ++ut) {
       const int64_t u = u0 + ut * 32 + r;
       const int64_t uc = u < B ? u : B - 1;   // clamped load, zeroed below
 #pragma unroll
@@ -137,19 +143,19 @@ __global__ __launch_bounds__(64 * (ScCW<D>::value + ScSW<D, FLAGS>::value), 1) v
     }
     // ring position of item r of chunk 0 for each of the lane's 32 rows (register v of user
     // tile ut holds row 64 wave + 32 ut + rho(v) + 4 hh): (r - a) mod RW
-    int rpos[2][16];
+    int rpos[UT][16];
 #pragma unroll
-    for (int ut = 0; ut < 2; ++ut)
+    for (int ut = 0; ut < UT; ++ut)
 #pragma unroll
       for (int v = 0; v < 16; ++v) {
-        const int ul = wave * 64 + ut * 32 + (v & 3) + 8 * (v >> 2) + 4 * hh;
+        const int ul = wave * UPW + ut * 32 + (v & 3) + 8 * (v >> 2) + 4 * hh;
         const int p = r - line_shift(pbase, ul, ld);
         rpos[ut][v] = ul * RW + (p < 0 ? p + RW : p);
       }
-    f32x4 cst[LV];   // FLAGS: this wave's quarter of the next table chunk, loaded a chunk ahead
+    f32x4 cst[LVC];   // FLAGS: this wave's share of the next table chunk, loaded a chunk ahead
     auto cgload = [&](int64_t c) {
 #pragma unroll
-      for (int i = 0; i < LV; ++i) {
+      for (int i = 0; i < LVC; ++i) {
         const int f = tid + 64 * CW * i, row = f / (D / 4), col = (f % (D / 4)) * 4;
         int64_t item = c * SC_CHUNK + row;
         item = item < rows ? item : rows - 1;   // past-the-end items are never stored
@@ -158,7 +164,7 @@ __global__ __launch_bounds__(64 * (ScCW<D>::value + ScSW<D, FLAGS>::value), 1) v
     };
     auto cswrite = [&](int b) {
 #pragma unroll
-      for (int i = 0; i < LV; ++i) {
+      for (int i = 0; i < LVC; ++i) {
         const int f = tid + 64 * CW * i, row = f / (D / 4), col = (f % (D / 4)) * 4;
         *reinterpret_cast<f32x4*>(&tab[b][row * P + col]) = cst[i];
       }
@@ -178,10 +184,10 @@ __global__ __launch_bounds__(64 * (ScCW<D>::value + ScSW<D, FLAGS>::value), 1) v
       for (int64_t k = c_begin; k < c_end; ++k) {
         const int kb = (int)((k - c_begin) & 1);
         const int j = (int)(k - c_begin);
-        if (FLAGS) lds_wait_all_ge(&sy[0], j + 1);   // table chunk j staged by every compute wave
-        f32x16 acc[2];
+        if (FLAGS) lds_wait_all_ge<CW>(&sy[0], j + 1);   // table chunk j staged by every compute wave
+        f32x16 acc[UT];
 #pragma unroll
-        for (int ut = 0; ut < 2; ++ut)
+        for (int ut = 0; ut < UT; ++ut)
 #pragma unroll
           for (int v = 0; v < 16; ++v) acc[ut][v] = 0.f;
         const float* tb = &tab[kb][r * P + 4 * hh];
@@ -193,7 +199,7 @@ __global__ __launch_bounds__(64 * (ScCW<D>::value + ScSW<D, FLAGS>::value), 1) v
 #pragma unroll
             for (int s = 0; s < 4; ++s)
 #pragma unroll
-              for (int ut = 0; ut < 2; ++ut) {
+              for (int ut = 0; ut < UT; ++ut) {
                 if (NOMFMA) acc[ut][4 * q + s] += bt[s];   // diagnostic: no matrix work
                 else acc[ut] = mfma32(hf[ut][g][q][s], bt[s], acc[ut]);
               }
@@ -201,21 +207,20 @@ __global__ __launch_bounds__(64 * (ScCW<D>::value + ScSW<D, FLAGS>::value), 1) v
         if (FLAGS) {
           lds_publish_set(&sy[CW + wave], j + 1, lane);   // done reading table chunk j
           if (k + 1 < c_end) {   // stage chunk j+1 into the buffer chunk j-1 used
-            lds_wait_all_ge(&sy[CW], j);                  // ... once every wave is done with j-1
+            lds_wait_all_ge<CW>(&sy[CW], j);              // ... once every wave is done with j-1
             cswrite((j + 1) & 1);
             lds_publish_set(&sy[wave], j + 2, lane);
             if (k + 2 < c_end) cgload(k + 2);             // a whole chunk period ahead
           }
-          // its ring slots drained by the store waves of its rows
-#pragma unroll
-          for (int q = 0; q < SWN / CW; ++q) lds_wait_ge(&sy[3 * CW + wave * (SWN / CW) + q], j + 2 - SC_RING);
+          // its ring slots drained by the store wave of its rows
+          lds_wait_ge(&sy[3 * CW + wave * UPW / RPW], j + 2 - SC_RING);
         }
         // logits tile -> ring (row-shifted); a position past the row's RW wraps back by RW
 #pragma unroll
-        for (int ut = 0; ut < 2 && ablate < 3; ++ut)
+        for (int ut = 0; ut < UT && ablate < 3; ++ut)
 #pragma unroll
           for (int v = 0; v < 16; ++v) {
-            const int ul_end = (wave * 64 + ut * 32 + (v & 3) + 8 * (v >> 2) + 4 * hh + 1) * RW;
+            const int ul_end = (wave * UPW + ut * 32 + (v & 3) + 8 * (v >> 2) + 4 * hh + 1) * RW;
             const int p = rpos[ut][v] + cm;
             ring[p >= ul_end ? p - RW : p] = acc[ut][v];
           }
@@ -230,14 +235,15 @@ __global__ __launch_bounds__(64 * (ScCW<D>::value + ScSW<D, FLAGS>::value), 1) v
   } else {
     // ------------------------------------------------------------------ store waves
     const int sw = wave - CW, stid = tid - 64 * CW;
-    const int cw_of = sw / (SWN / CW);   // the compute wave whose rows this store wave writes
+    constexpr int CPS = RPW / UPW;               // compute waves whose rows one store wave writes
+    const int cw_of = sw * CPS;                  // the first of them
     // table chunks are loaded two chunks ahead (register double buffer): the HBM / L2 latency
     // spans a whole chunk period instead of being exposed before every barrier
     f32x4 st[2][LV];
     auto gload = [&](int64_t c, int sb) {   // float4 f of the chunk = row f / (D/4), col 4 (f % (D/4))
 #pragma unroll
       for (int i = 0; i < LV; ++i) {
-        const int f = stid + 64 * CW * i, row = f / (D / 4), col = (f % (D / 4)) * 4;
+        const int f = stid + 256 * i, row = f / (D / 4), col = (f % (D / 4)) * 4;
         int64_t item = c * SC_CHUNK + row;
         item = item < rows ? item : rows - 1;   // past-the-end items are never stored
         st[sb][i] = *reinterpret_cast<const f32x4*>(table + item * D + col);
@@ -246,7 +252,7 @@ __global__ __launch_bounds__(64 * (ScCW<D>::value + ScSW<D, FLAGS>::value), 1) v
     auto swrite = [&](int b, int sb) {
 #pragma unroll
       for (int i = 0; i < LV; ++i) {
-        const int f = stid + 64 * CW * i, row = f / (D / 4), col = (f % (D / 4)) * 4;
+        const int f = stid + 256 * i, row = f / (D / 4), col = (f % (D / 4)) * 4;
         *reinterpret_cast<f32x4*>(&tab[b][row * P + col]) = st[sb][i];
       }
     };
@@ -294,7 +300,10 @@ __global__ __launch_bounds__(64 * (ScCW<D>::value + ScSW<D, FLAGS>::value), 1) v
       constexpr int par = decltype(par_sel)::value;
       if (!FLAGS && k + 2 < c_end) gload(k + 2, par);   // chunk k+2 into the buffer chunk k freed
       const int j = (int)(k - c_begin);
-      if (FLAGS && k > c_begin) lds_wait_ge(&sy[2 * CW + cw_of], j);   // chunk k-1 in the ring
+      if (FLAGS && k > c_begin) {   // chunk k-1 in the ring, from every compute wave of these rows
+#pragma unroll
+        for (int q = 0; q < CPS; ++q) lds_wait_ge(&sy[2 * CW + cw_of + q], j);
+      }
       if (k > c_begin && ablate != 1) {   // the line ending inside chunk c = k-1 (k-2 still held)
         const int64_t c = k - 1, c0 = c * SC_CHUNK;
         const int soff = (int)(c0 * 4);
@@ -490,9 +499,9 @@ int gr_score_launch(const float* h, int64_t B, int32_t d, const float* table, in
     return check_launch("gr_score_f32 (direct)");
   }
 #define GR_SC_LAUNCH(DD)                                                                           \
-  if (flags) hipLaunchKernelGGL((score_kernel<DD, true>), g, dim3(64 * (cw + ScSW<DD, true>::value)), \
+  if (flags) hipLaunchKernelGGL((score_kernel<DD, true>), g, dim3(64 * (ScCW<DD, true>::value + ScSW<DD, true>::value)), \
                                 0, st, h, B, table, rows, logits, ld, (int)ublocks, (int)slices, ablate, ubmajor); \
-  else hipLaunchKernelGGL((score_kernel<DD, false>), g, dim3(64 * (cw + ScSW<DD, false>::value)), 0, \
+  else hipLaunchKernelGGL((score_kernel<DD, false>), g, dim3(64 * (ScCW<DD, false>::value + ScSW<DD, false>::value)), 0, \
                           st, h, B, table, rows, logits, ld, (int)ublocks, (int)slices, ablate, ubmajor);
   switch (d) {
     case 32: GR_SC_LAUNCH(32) break;
