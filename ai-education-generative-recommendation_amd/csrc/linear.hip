@@ -19,7 +19,7 @@ constexpr int LIN_BK = 32;
 constexpr int LIN_PITCH = LIN_BK + 4;
 
 template <int BM, int BN, int WM, int WN, int ACT, bool RES, bool NMAJOR>
-__global__ __launch_bounds__(256) void linear_f32_kernel(
+__global__ __launch_bounds__(256, 2) void linear_f32_kernel(
     const float* __restrict__ x, const float* __restrict__ w, const float* __restrict__ bias,
     const float* residual, float* y, int64_t M, int N, int K, int64_t ldy, int64_t ldr,
     int tiles_m, int tiles_n) {
