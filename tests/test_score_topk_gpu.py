@@ -151,3 +151,52 @@ def test_score_kernel_variants_identical(B, d, rows, ld, dev):
     for o in outs[1:]:
         assert torch.equal(o, outs[0])
     assert (outs[0][:, rows:] == 7.0).all()   # nothing written past the row's columns
+
+
+def _gloo_gpu_worker(rank, world, port, data, out):
+    import os as _os
+    import torch.distributed as dist
+    _os.environ["MASTER_ADDR"] = "127.0.0.1"
+    _os.environ["MASTER_PORT"] = str(port)
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from gr_amd import dist as D
+    h, table, targets, k = (t.cuda() if torch.is_tensor(t) else t for t in data)
+    lo, hi = D.shard_range(table.shape[0], rank, world)
+    rk, v, i = D.sharded_rank_topk(h, table[lo:hi].contiguous(), lo, targets, k)   # fused HIP path
+    out[rank] = (rk.cpu(), v.cpu(), i.cpu())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_catalog_sharded_fused_multi_rank(world, dev):
+    """The catalog-sharded exchange over real ranks (gloo, every rank on this GPU) with the fused
+    HIP kernels: every rank returns the full-catalog rank / top-k bit for bit."""
+    import socket
+    import torch.multiprocessing as mp
+    from gr_amd import ops
+    g = torch.Generator().manual_seed(21 + world)
+    B, d, rows, k = 96, 64, 30011, 10
+    table = torch.randn(rows, d, generator=g)
+    table[25000] = table[17]            # an exact tie across shards: the lower id wins
+    h = torch.randn(B, d, generator=g)
+    tg = torch.randint(0, rows, (B,), generator=g)
+    tg[0] = 0
+    tg[1] = 25000
+    full = ops.score(h.to(dev), table.to(dev))
+    ref_rank = ops.rank(full, tg.to(dev)).cpu()
+    full[:, 0] = -1e9
+    o = torch.argsort(full, dim=1, descending=True, stable=True)[:, :k]
+    ref_v, ref_i = full.gather(1, o).cpu(), o.cpu()
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_gloo_gpu_worker, args=(world, port, (h, table, tg, k), out), nprocs=world, join=True)
+    for r in range(world):
+        rk, v, i = out[r]
+        assert torch.equal(rk, ref_rank)
+        assert torch.equal(i, ref_i) and torch.equal(v, ref_v)
