@@ -304,10 +304,18 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if a.gpus != world and world == 1 and a.gpus > 1:
         sys.exit("bench.py: --gpus N>1 must be launched with torch.distributed.run (one rank per GPU)")
+    # GR_BENCH_BACKEND=gloo is a rehearsal mode only (several ranks sharing one GPU to exercise the
+    # multi-rank code paths on a one-GPU box); real runs use RCCL ("nccl"), one GPU per rank.
+    backend = os.environ.get("GR_BENCH_BACKEND", "nccl")
+    if backend != "nccl":
+        local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     line, rq_model = bench_rq_c2(a, world, rank, dev)
     if "sasrec" not in skip:
