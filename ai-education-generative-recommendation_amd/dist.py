@@ -26,13 +26,15 @@ def shard_range(n, rank, world):
     return n * rank // world, n * (rank + 1) // world
 
 
-def all_gather_rows(t, group=None):
-    """Concatenate a [n_r, ...] tensor over ranks (n_r may differ by rank)."""
+def all_gather_rows(t, group=None, sizes=None):
+    """Concatenate a [n_r, ...] tensor over ranks (n_r may differ by rank).  ``sizes`` (every
+    rank's n_r, e.g. from ``shard_range``) skips the size exchange and its host synchronisation."""
     world = dist.get_world_size(group)
-    n = torch.tensor([t.shape[0]], dtype=torch.int64, device=t.device)
-    sizes = [torch.zeros_like(n) for _ in range(world)]
-    dist.all_gather(sizes, n, group=group)
-    sizes = [int(s.item()) for s in sizes]
+    if sizes is None:
+        n = torch.tensor([t.shape[0]], dtype=torch.int64, device=t.device)
+        sz = [torch.zeros_like(n) for _ in range(world)]
+        dist.all_gather(sz, n, group=group)
+        sizes = [int(s.item()) for s in sz]
     m = max(sizes)
     pad = torch.zeros((m - t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
     buf = torch.cat([t, pad])
@@ -100,14 +102,17 @@ def sharded_rank_topk(h, table_shard, row_offset, targets, k=10, group=None, mas
 
 
 def _exchange(cnt, v, i, k, group, world):
-    """Steps 2-3 of the module docstring: global counts and the merged top-k."""
+    """Steps 2-3 of the module docstring: global counts and the merged top-k.  The (value, id)
+    candidates travel as ONE int64 all-gather: [ids | value bits] per user."""
     if world > 1:
         dist.all_reduce(cnt, op=dist.ReduceOp.SUM, group=group)
-        vs = [torch.empty_like(v) for _ in range(world)]
-        is_ = [torch.empty_like(i) for _ in range(world)]
-        dist.all_gather(vs, v.contiguous(), group=group)
-        dist.all_gather(is_, i.contiguous(), group=group)
-        v, i = merge_topk(torch.cat(vs, 1), torch.cat(is_, 1), k)
+        kk = v.shape[1]
+        packed = torch.cat([i, v.contiguous().view(torch.int32).to(torch.int64)], 1)
+        parts = [torch.empty_like(packed) for _ in range(world)]
+        dist.all_gather(parts, packed, group=group)
+        ids = torch.cat([p_[:, :kk] for p_ in parts], 1)
+        vals = torch.cat([p_[:, kk:].to(torch.int32).view(torch.float32) for p_ in parts], 1)
+        v, i = merge_topk(vals, ids, k)
     return cnt + 1, v, i
 
 

@@ -267,12 +267,13 @@ def bench_sas_c5(a, world, rank, dev):
     seqs = synth.sequences(B, n, items, 5000, dev)            # same users on every rank
     targets = torch.randint(1, items + 1, (B,), generator=torch.Generator(device=dev).manual_seed(6), device=dev)
     ulo, uhi = D.shard_range(B, rank, world)
+    usizes = [D.shard_range(B, r_, world)[1] - D.shard_range(B, r_, world)[0] for r_ in range(world)]
     lo, hi = D.shard_range(items + 1, rank, world)
     shard = model.item_emb.weight.detach()[lo:hi]
 
     def step():
         hl = model.last_hidden(seqs[ulo:uhi])
-        h = D.all_gather_rows(hl) if world > 1 else hl
+        h = D.all_gather_rows(hl, sizes=usizes) if world > 1 else hl
         return D.sharded_rank_topk(h, shard, lo, targets, k=10)
 
     steps, warm = max(2, min(a.steps, 10)), 2

@@ -47,6 +47,9 @@ def _worker(rank, world, port, data, out):
     # user-sharded transformer output gathered back (variable shard sizes)
     ulo, uhi = D.shard_range(h.shape[0], rank, world)
     hg = D.all_gather_rows(h[ulo:uhi])
+    sizes = [D.shard_range(h.shape[0], r, world)[1] - D.shard_range(h.shape[0], r, world)[0]
+             for r in range(world)]
+    assert torch.equal(D.all_gather_rows(h[ulo:uhi], sizes=sizes), hg)   # known sizes: no exchange
     out[rank] = (rk, v, i, hg)
     dist.barrier()
     dist.destroy_process_group()
