@@ -70,6 +70,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="budget per CPU baseline leg")
     ap.add_argument("--skip", default="", help="comma list of legs to skip: sasrec,c4,c5")
+    ap.add_argument("--spinup-s", type=float, default=1.0,
+                    help="untimed seconds of each leg's workload before its warmup (clock ramp)")
     return ap.parse_args()
 
 
@@ -80,9 +82,38 @@ def sync_all(world):
     torch.cuda.synchronize()
 
 
+SPINUP_S = 1.0   # seconds of untimed work before each leg's warmup (set by --spinup-s)
+
+
+def spinup(fn, seconds=None, world=1):
+    """Run ``fn`` untimed for about ``seconds``: MI355X ramps its clocks over the first ~0.1-0.3 s of
+    sustained load (measured: the C3 scoring kernel averages 379 us over 20 launches from idle and
+    294 us in steady state), so every timed region starts at steady state.  The iteration count
+    comes from a short probe and is agreed over the ranks (max), so steps that contain collectives
+    stay matched."""
+    seconds = SPINUP_S if seconds is None else seconds
+    if seconds <= 0:
+        return
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    n = int(seconds / max((time.perf_counter() - t0) / 3, 1e-6)) + 1
+    if world > 1:
+        t = torch.tensor([n], dtype=torch.int64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        n = int(t.item())
+    for i in range(n):
+        fn()
+        if i % 8 == 7:
+            torch.cuda.synchronize()
+
+
 def timed(fn, steps, warmup, world):
-    """W untimed steps, then exactly K steps between barrier+synchronize; returns (max-over-ranks
-    wall seconds, mean device ms per step from HIP events on the launch stream)."""
+    """Spin-up, W untimed warmup steps, then exactly K steps between barrier+synchronize; returns
+    (max-over-ranks wall seconds, mean device ms per step from HIP events on the launch stream)."""
+    spinup(fn, world=world)
     for _ in range(warmup):
         fn()
     sync_all(world)
@@ -102,9 +133,10 @@ def timed(fn, steps, warmup, world):
     return wall, dev_ms
 
 
-def kernel_ms(fn, reps=10, warmup=2):
+def kernel_ms(fn, reps=50, warmup=2):
     """Mean device time of one launch of ``fn`` (HIP events on torch's current stream, which is the
-    stream every gr_amd op enqueues on)."""
+    stream every gr_amd op enqueues on), after a short spin-up (clock ramp)."""
+    spinup(fn, min(SPINUP_S, 0.3))
     for _ in range(warmup):
         fn()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -299,6 +331,8 @@ def bench_sas_c5(a, world, rank, dev):
 
 def main():
     a = parse()
+    global SPINUP_S
+    SPINUP_S = a.spinup_s
     skip = set(s for s in a.skip.split(",") if s)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

@@ -47,12 +47,13 @@ for suf in (sys.argv[1:] or [""]):
         assert lib.gr_set_option(b"score_ablate", abl) == 0
         suf = (suf or "") + f"ablate{abl}"
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    reps = int(os.environ.get("AB_REPS", 20))
     e0.record()
-    for _ in range(20):
+    for _ in range(reps):
         call()
     e1.record()
     torch.cuda.synchronize()
-    ms = e0.elapsed_time(e1) / 20
+    ms = e0.elapsed_time(e1) / reps
     print(f"ld={LD} {suf or 'product':12s} {ms * 1e3:8.1f} us  {2 * B * ROWS * D / ms / 1e9:7.1f} TF/s  "
           f"{B * ROWS * 4 / ms / 1e6:7.0f} GB/s logits", flush=True)
 # write-bandwidth reference: torch fill of the same logits buffer
