@@ -12,9 +12,12 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from gr_amd import _lib, ops  # noqa: E402
 
 
-def ms(fn, reps=10):
-    for _ in range(2):
+def ms(fn, reps=50):
+    import time
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < 0.5:   # clock ramp (bench.py spinup)
         fn()
+        torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     for _ in range(reps):
