@@ -31,8 +31,9 @@ static std::atomic<int64_t> g_score_flags{1};
 // share a catalog slice across all user blocks).  Same results; A/B timing.
 static std::atomic<int64_t> g_score_ubmajor{1};
 // score_impl (0: compute / store wave specialisation with the LDS ring, 1: direct accumulator
-// stores, two workgroups per CU).  Same results; A/B timing.
-static std::atomic<int64_t> g_score_impl{0};
+// stores, two workgroups per CU, 2: direct when the logits rows are 128-B line aligned, else the
+// ring).  Same results.
+static std::atomic<int64_t> g_score_impl{2};
 
 int64_t option(const char* name) {
   if (!strcmp(name, "rq_fused")) return g_rq_fused.load();
@@ -57,7 +58,7 @@ extern "C" int gr_set_option(const char* name, int64_t value) {
   if (!strcmp(name, "topk_sample") && (value == 0 || value == 1)) { gr::g_topk_sample = value; return GR_OK; }
   if (!strcmp(name, "score_flags") && (value == 0 || value == 1)) { gr::g_score_flags = value; return GR_OK; }
   if (!strcmp(name, "score_ubmajor") && (value == 0 || value == 1)) { gr::g_score_ubmajor = value; return GR_OK; }
-  if (!strcmp(name, "score_impl") && (value == 0 || value == 1)) { gr::g_score_impl = value; return GR_OK; }
+  if (!strcmp(name, "score_impl") && value >= 0 && value <= 2) { gr::g_score_impl = value; return GR_OK; }
   return gr::fail(GR_ERR_ARG, std::string("gr_set_option: unknown option or value: ") + name);
 }
 

@@ -56,8 +56,10 @@ const char* gr_last_error(void);
  *   "score_flags"   1 (default): the scoring kernel (d <= 64) hands chunks between its compute and
  *                   store waves through LDS words; 0: one barrier per chunk.  Identical results.
  *   "score_ubmajor" 1 (default): one XCD's workgroups share a user block; 0: a catalog slice.
- *   "score_impl"    0 (default): compute / store wave specialisation with an LDS ring; 1: the
- *                   compute waves store their accumulators directly (A/B only; identical results).
+ *   "score_impl"    2 (default): the compute waves store their accumulators directly when every
+ *                   logits row starts on a 128-byte line (row stride % 32 == 0, aligned base),
+ *                   else compute / store wave specialisation with an LDS ring; 0: always the ring;
+ *                   1: always direct.  Identical results.
  *   "topk_ablate"   0 (default).  DIAGNOSTIC ONLY, outputs invalid otherwise: the fused score +
  *                   top-k kernel skips 1 = all top-k work (counts stay valid)
  *   "topk_sample"   1 (default): gr_score_topk_f32 prunes with a threshold from a strided sample

@@ -136,18 +136,19 @@ def test_score_kernel_variants_identical(B, d, rows, ld, dev):
     t = torch.randn(rows, d, generator=g).to(dev)
     outs = []
     try:
-        for opts in [dict(), dict(score_flags=0), dict(score_ubmajor=0), dict(score_impl=1)]:
+        for opts in [dict(score_impl=0), dict(score_impl=0, score_flags=0), dict(score_impl=0, score_ubmajor=0),
+                     dict(score_impl=1), dict(score_impl=2)]:
             for k, v in opts.items():
                 _lib.set_option(k, v)
             buf = torch.full((B, ld), 7.0, device=dev)
             ops.score(h, t, out=buf[:, :rows])
             outs.append(buf)
             for k in opts:
-                _lib.set_option(k, {"score_flags": 1, "score_ubmajor": 1, "score_impl": 0}[k])
+                _lib.set_option(k, {"score_flags": 1, "score_ubmajor": 1, "score_impl": 2}[k])
     finally:
         _lib.set_option("score_flags", 1)
         _lib.set_option("score_ubmajor", 1)
-        _lib.set_option("score_impl", 0)
+        _lib.set_option("score_impl", 2)
     for o in outs[1:]:
         assert torch.equal(o, outs[0])
     assert (outs[0][:, rows:] == 7.0).all()   # nothing written past the row's columns
