@@ -30,8 +30,11 @@ struct AttnTile {                  // one 32-query tile owned by a wave
   float m, l;                      // running max / sum of this lane's query
 };
 
+// Two workgroups per CU: at hd = 128 that caps the kernel at 256 VGPRs (a few spill), and still
+// measured 85 vs 114 us per C5 call (steady state) — the second workgroup's MFMAs fill the gaps
+// of the first's barriers and softmax.
 template <int HD>
-__global__ __launch_bounds__(256, 1) void attn_mfma_kernel(const float* __restrict__ qkv,
+__global__ __launch_bounds__(256, 2) void attn_mfma_kernel(const float* __restrict__ qkv,
                                                            float* __restrict__ out, int n, int H,
                                                            float scale, int qt_lo) {
   constexpr int FT = HD / 32;
