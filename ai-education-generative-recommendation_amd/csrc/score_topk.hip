@@ -76,8 +76,12 @@ __device__ __forceinline__ int64_t phys_chunk(int64_t v, int mode, int s) {
   return mode == 1 ? v * s : v;
 }
 
+// Users per wave: TK_UT 32-user MFMA tiles.  One tile per wave keeps the kernel within 256 VGPRs,
+// so two workgroups share each CU and one wave's list insertions / counts overlap another's MFMAs.
+template <int D> struct TkUT { static constexpr int value = 1; };
+
 template <int D, int KC>
-__global__ __launch_bounds__(256, 1) void score_topk_kernel(
+__global__ __launch_bounds__(256, 2) void score_topk_kernel(
     const float* __restrict__ h, int64_t B, const float* __restrict__ table, int64_t rows,
     const float* __restrict__ thr, int mask_col0, unsigned long long* __restrict__ cnt_out,
     const float* __restrict__ tinit, int tstride, int64_t vchunks, int mode, int s,
@@ -92,13 +96,14 @@ __global__ __launch_bounds__(256, 1) void score_topk_kernel(
   const int wgid = xcd_remap(blockIdx.x, gridDim.x);
   const int ub = wgid % ublocks, sl = wgid / ublocks;
   const int64_t v_begin = vchunks * sl / slices, v_end = vchunks * (sl + 1) / slices;
-  const int64_t u0 = ((int64_t)ub * 4 + w) * 64;
+  constexpr int UT = TkUT<D>::value;
+  const int64_t u0 = ((int64_t)ub * 4 + w) * (32 * UT);
 
   // B operand: the users (lane r = user), as in the scoring kernel's A operand
-  f32x4 hf[2][KG][4];
-  float th[2], ts[2];
+  f32x4 hf[UT][KG][4];
+  float th[UT], ts[UT];
 #pragma unroll
-  for (int ut = 0; ut < 2; ++ut) {
+  for (int ut = 0; ut < UT; ++ut) {
     const int64_t u = u0 + ut * 32 + r;
     const int64_t uc = u < B ? u : B - 1;
 #pragma unroll
@@ -111,16 +116,21 @@ __global__ __launch_bounds__(256, 1) void score_topk_kernel(
     th[ut] = thr ? thr[uc] : 0.f;
     ts[ut] = tinit ? tinit[uc * tstride] : -INFINITY;
   }
-  LaneList<KC> ll[2];
-  ll[0].init();
-  ll[1].init();
+  LaneList<KC> ll[UT];
+#pragma unroll
+  for (int ut = 0; ut < UT; ++ut) ll[ut].init();
   // pass test x > Tm  <=>  x > (list's last value) && x >= T_S
   auto tm_of = [&](int ut) {
     const float to = ll[ut].v[KC - 1];
     return ts[ut] > to ? prev_below(ts[ut]) : to;
   };
-  float Tm[2] = {tm_of(0), tm_of(1)};
-  int cgt[2] = {0, 0};
+  float Tm[UT];
+  int cgt[UT];
+#pragma unroll
+  for (int ut = 0; ut < UT; ++ut) {
+    Tm[ut] = tm_of(ut);
+    cgt[ut] = 0;
+  }
 
   f32x4 st[LV];
   auto gload = [&](int64_t c) {
@@ -148,9 +158,9 @@ __global__ __launch_bounds__(256, 1) void score_topk_kernel(
 #pragma unroll 1
   for (int64_t vc = v_begin; vc < v_end; ++vc) {
     if (vc + 1 < v_end) gload(phys_chunk(vc + 1, mode, s));
-    f32x16 acc[2][2];
+    f32x16 acc[UT][2];
 #pragma unroll
-    for (int ut = 0; ut < 2; ++ut)
+    for (int ut = 0; ut < UT; ++ut)
 #pragma unroll
       for (int it = 0; it < 2; ++it)
 #pragma unroll
@@ -168,7 +178,7 @@ __global__ __launch_bounds__(256, 1) void score_topk_kernel(
 #pragma unroll
           for (int it = 0; it < 2; ++it)
 #pragma unroll
-            for (int ut = 0; ut < 2; ++ut) acc[ut][it] = mfma32(bt[it][s4], hf[ut][g][q][s4], acc[ut][it]);
+            for (int ut = 0; ut < UT; ++ut) acc[ut][it] = mfma32(bt[it][s4], hf[ut][g][q][s4], acc[ut][it]);
       }
     const int c0 = (int)(phys_chunk(vc, mode, s) * TK_CHUNK);
     if (c0 + TK_CHUNK > rows || (mask_col0 && c0 == 0)) {   // catalog ends: masks
@@ -178,7 +188,7 @@ __global__ __launch_bounds__(256, 1) void score_topk_kernel(
         for (int v = 0; v < 16; ++v) {
           const int col = c0 + 32 * it + (v & 3) + 8 * (v >> 2) + 4 * hh;
 #pragma unroll
-          for (int ut = 0; ut < 2; ++ut) {
+          for (int ut = 0; ut < UT; ++ut) {
             if (mask_col0 && col == 0) acc[ut][it][v] = TK_MASK;
             if (col >= rows) acc[ut][it][v] = __int_as_float(0x7fc00000);   // NaN: fails every test
           }
@@ -186,7 +196,7 @@ __global__ __launch_bounds__(256, 1) void score_topk_kernel(
     }
     if (mode == 1) {   // sample pass: bucket maxima (bucket = position mod KC), nothing else
 #pragma unroll
-      for (int ut = 0; ut < 2; ++ut)
+      for (int ut = 0; ut < UT; ++ut)
 #pragma unroll
         for (int it = 0; it < 2; ++it)
 #pragma unroll
@@ -200,7 +210,7 @@ __global__ __launch_bounds__(256, 1) void score_topk_kernel(
       continue;
     }
 #pragma unroll
-    for (int ut = 0; ut < 2; ++ut) {
+    for (int ut = 0; ut < UT; ++ut) {
       float mx = -INFINITY;
 #pragma unroll
       for (int it = 0; it < 2; ++it)
@@ -228,14 +238,14 @@ __global__ __launch_bounds__(256, 1) void score_topk_kernel(
   }
   // strict counts: the two lane halves of a user, one atomic per (user, slice)
 #pragma unroll
-  for (int ut = 0; ut < 2; ++ut) {
+  for (int ut = 0; ut < UT; ++ut) {
     const int x = cgt[ut] + __shfl_xor(cgt[ut], 32);
     const int64_t u = u0 + ut * 32 + r;
     if (cnt_out && hh == 0 && u < B && x) atomicAdd(&cnt_out[u], (unsigned long long)x);
   }
   // candidate segment (pass, slice, half) of each user: the lane's sorted list
 #pragma unroll
-  for (int ut = 0; ut < 2; ++ut) {
+  for (int ut = 0; ut < UT; ++ut) {
     const int64_t u = u0 + ut * 32 + r;
     if (u >= B) continue;
     const int64_t base = u * seg_stride + (int64_t)(seg_off + 2 * sl + hh) * KC;
@@ -270,20 +280,26 @@ struct TopkPlan {
   int64_t seg_per_user() const { return 2 * (slices1 + slices2); }
 };
 
-static int64_t slices_for(int64_t ublocks, int64_t vchunks) {
-  int64_t sl = (cu_count() + ublocks - 1) / ublocks;
+static int64_t slices_for(int64_t ublocks, int64_t vchunks, int d) {
+  const int per_cu = (d == 128 ? TkUT<128>::value : d == 64 ? TkUT<64>::value : TkUT<32>::value) == 1 ? 2 : 1;
+  int64_t sl = (per_cu * cu_count() + ublocks - 1) / ublocks;
   if (sl > vchunks) sl = vchunks;
   return sl < 1 ? 1 : sl;
 }
 
 static int kc_for(int k) { return k <= 4 ? 4 : k <= 10 ? 10 : 16; }
 
-static TopkPlan topk_plan(int64_t B, int64_t rows, int k) {
+static int users_per_wg(int d) {
+  return 128 * (d == 128 ? TkUT<128>::value : d == 64 ? TkUT<64>::value : TkUT<32>::value);
+}
+
+static TopkPlan topk_plan(int64_t B, int64_t rows, int k, int d) {
   TopkPlan p;
-  p.ublocks = (B + 255) / 256;
+  const int uw = users_per_wg(d);
+  p.ublocks = (B + uw - 1) / uw;
   p.chunks = (rows + TK_CHUNK - 1) / TK_CHUNK;
   p.kc = kc_for(k);
-  p.slices2 = slices_for(p.ublocks, p.chunks);
+  p.slices2 = slices_for(p.ublocks, p.chunks, d);
   const int64_t per_slice = p.chunks / p.slices2;
   p.s = 0;
   p.v1 = p.slices1 = 0;
@@ -291,7 +307,7 @@ static TopkPlan topk_plan(int64_t B, int64_t rows, int k) {
     const int64_t s = per_slice / 4;
     p.s = (int)(s < 2 ? 2 : s > 16 ? 16 : s);
     p.v1 = (p.chunks + p.s - 1) / p.s;
-    p.slices1 = slices_for(p.ublocks, p.v1);
+    p.slices1 = slices_for(p.ublocks, p.v1, d);
   }
   return p;
 }
@@ -335,7 +351,7 @@ static void launch_merge(hipStream_t st, int64_t B, int64_t row_stride, int64_t 
 extern "C" size_t gr_score_topk_workspace_bytes(int64_t B, int32_t d, int64_t rows, int32_t k) {
   (void)d;
   if (B < 1 || rows < 1 || k < 1 || k > 16) return 256;
-  const gr::TopkPlan p = gr::topk_plan(B, rows, k);
+  const gr::TopkPlan p = gr::topk_plan(B, rows, k, d);
   return gr::topk_ws(B, p, k).total;
 }
 
@@ -370,7 +386,7 @@ extern "C" int gr_score_topk_f32(const float* h, int64_t B, int32_t d, const flo
       return fail(GR_ERR_HIP, "gr_score_topk_f32: memset failed");
     return GR_OK;
   }
-  const TopkPlan p = topk_plan(B, rows, k);
+  const TopkPlan p = topk_plan(B, rows, k, d);
   const TopkWs wl = topk_ws(B, p, k);
   if (!workspace || workspace_bytes < wl.total)
     return fail(GR_ERR_WORKSPACE, "gr_score_topk_f32: workspace too small (need " + std::to_string(wl.total) + " bytes)");
