@@ -11,7 +11,7 @@
 // have produced and the target never counts itself (SURVEY §7 hard part 3).
 //
 // count_gt is the scoring kernel with the logits stream replaced by a compare-and-count epilogue:
-// MFMA-bound (12.8 Mflop per user at C3) and reads only the table.  Workgroup = 4 waves x 64 users,
+// MFMA-bound (12.8 Mflop per user at C3) and reads only the table.  Workgroup = 4 waves x 32 users,
 // one contiguous catalog slice walked in 64-item chunks (table chunk staged in LDS, prefetched into
 // registers one chunk ahead); per-lane counters, reduced over the 32 item lanes at the end, one
 // atomic add per (user, slice).
@@ -59,8 +59,12 @@ __global__ __launch_bounds__(64) void score_pairs_kernel(const float* __restrict
   if (u < B && ((r >> 2) & 1) == hh) out[u] = (mask_col0 && t == 0) ? RK_MASK : d;
 }
 
+// One 32-user MFMA tile per wave (128 users per workgroup) and two workgroups per CU: one wave's
+// compare-and-count epilogue overlaps another's MFMAs (as in score_topk.hip).
+constexpr int RK_UT = 1;
+
 template <int D>
-__global__ __launch_bounds__(256, (D <= 32 ? 2 : 1)) void score_count_kernel(const float* __restrict__ h, int64_t B,
+__global__ __launch_bounds__(256, 2) void score_count_kernel(const float* __restrict__ h, int64_t B,
                                                             const float* __restrict__ table,
                                                             int64_t rows,
                                                             const float* __restrict__ thr,
@@ -78,12 +82,13 @@ __global__ __launch_bounds__(256, (D <= 32 ? 2 : 1)) void score_count_kernel(con
   const int64_t chunks = (rows + RK_CHUNK - 1) / RK_CHUNK;
   const int64_t c_begin = chunks * sl / slices, c_end = chunks * (sl + 1) / slices;
   if (c_begin >= c_end) return;
-  const int64_t u0 = ((int64_t)ub * 4 + w) * 64;
+  constexpr int UT = RK_UT;
+  const int64_t u0 = ((int64_t)ub * 4 + w) * (32 * UT);
 
-  f32x4 hf[2][KG][4];
-  float th[2][16];
+  f32x4 hf[UT][KG][4];
+  float th[UT][16];
 #pragma unroll
-  for (int ut = 0; ut < 2; ++ut) {
+  for (int ut = 0; ut < UT; ++ut) {
     const int64_t u = u0 + ut * 32 + r;
     const int64_t uc = u < B ? u : B - 1;
 #pragma unroll
@@ -119,18 +124,18 @@ __global__ __launch_bounds__(256, (D <= 32 ? 2 : 1)) void score_count_kernel(con
   gload(c_begin);
   swrite(0);
   __syncthreads();
-  int cnt[2][16];
+  int cnt[UT][16];
 #pragma unroll
-  for (int ut = 0; ut < 2; ++ut)
+  for (int ut = 0; ut < UT; ++ut)
 #pragma unroll
     for (int v = 0; v < 16; ++v) cnt[ut][v] = 0;
   int buf = 0;
 #pragma unroll 1
   for (int64_t c = c_begin; c < c_end; ++c) {
     if (c + 1 < c_end) gload(c + 1);
-    f32x16 acc[2][2];
+    f32x16 acc[UT][2];
 #pragma unroll
-    for (int ut = 0; ut < 2; ++ut)
+    for (int ut = 0; ut < UT; ++ut)
 #pragma unroll
       for (int it = 0; it < 2; ++it)
 #pragma unroll
@@ -148,12 +153,12 @@ __global__ __launch_bounds__(256, (D <= 32 ? 2 : 1)) void score_count_kernel(con
 #pragma unroll
           for (int it = 0; it < 2; ++it)
 #pragma unroll
-            for (int ut = 0; ut < 2; ++ut) acc[ut][it] = mfma32(hf[ut][g][q][s], bt[it][s], acc[ut][it]);
+            for (int ut = 0; ut < UT; ++ut) acc[ut][it] = mfma32(hf[ut][g][q][s], bt[it][s], acc[ut][it]);
       }
     const int64_t c0 = c * RK_CHUNK;
     if (c0 + RK_CHUNK <= rows && !(mask_col0 && c0 == 0)) {   // steady state: no column masks
 #pragma unroll
-      for (int ut = 0; ut < 2; ++ut)
+      for (int ut = 0; ut < UT; ++ut)
 #pragma unroll
         for (int it = 0; it < 2; ++it)
 #pragma unroll
@@ -165,7 +170,7 @@ __global__ __launch_bounds__(256, (D <= 32 ? 2 : 1)) void score_count_kernel(con
         const bool ok = col < rows;
         const bool m0 = mask_col0 && col == 0;
 #pragma unroll
-        for (int ut = 0; ut < 2; ++ut)
+        for (int ut = 0; ut < UT; ++ut)
 #pragma unroll
           for (int v = 0; v < 16; ++v) {
             const float l = m0 ? RK_MASK : acc[ut][it][v];
@@ -179,7 +184,7 @@ __global__ __launch_bounds__(256, (D <= 32 ? 2 : 1)) void score_count_kernel(con
   }
   // reduce over the 32 item lanes of each half, one atomic per (user, slice)
 #pragma unroll
-  for (int ut = 0; ut < 2; ++ut)
+  for (int ut = 0; ut < UT; ++ut)
 #pragma unroll
     for (int v = 0; v < 16; ++v) {
       int x = cnt[ut][v];
@@ -239,9 +244,9 @@ extern "C" int gr_score_count_gt_f32(const float* h, int64_t B, int32_t d, const
   if (hipMemsetAsync(counts_out, 0, (size_t)B * sizeof(int64_t), st) != hipSuccess)
     return fail(GR_ERR_HIP, "gr_score_count_gt_f32: memset failed");
   if (rows == 0) return GR_OK;
-  const int64_t ublocks = (B + 255) / 256;
+  const int64_t ublocks = (B + 128 * RK_UT - 1) / (128 * RK_UT);
   const int64_t chunks = (rows + RK_CHUNK - 1) / RK_CHUNK;
-  const int64_t per_cu = d <= 32 ? 2 : 1;   // resident workgroups per CU (registers)
+  const int64_t per_cu = 2;   // resident workgroups per CU (registers, LDS)
   int64_t slices = (per_cu * cu_count() + ublocks - 1) / ublocks;
   if (slices > chunks) slices = chunks;
   if (slices < 1) slices = 1;
