@@ -57,6 +57,8 @@ SIGNATURES = {
                                              _i32, _vp, _sz, _vp, _vp]),
     "gr_sasrec_predict_f32": (ctypes.c_int, [ctypes.POINTER(SasrecParams), _vp, _i64, _i32, _vp,
                                              _vp, _sz, _vp, _vp]),
+    "gr_sasrec_predict_ld_f32": (ctypes.c_int, [ctypes.POINTER(SasrecParams), _vp, _i64, _i32, _vp,
+                                                _i64, _vp, _sz, _vp, _vp]),
     "gr_score_f32": (ctypes.c_int, [_vp, _i64, _i32, _vp, _i64, _vp, _i64, _vp]),
     "gr_rank_f32": (ctypes.c_int, [_vp, _i64, _i64, _i64, _vp, _i32, _vp, _vp]),
     "gr_count_gt_f32": (ctypes.c_int, [_vp, _i64, _i64, _i64, _vp, _vp, _vp]),

@@ -398,17 +398,19 @@ extern "C" int gr_sasrec_forward_f32(const gr_sasrec_params* p, const int64_t* s
   return run_layernorm(w.x, B * n, p->d, 1, 0, p->last_ln_w, p->last_ln_b, p->eps, out, st);
 }
 
-extern "C" int gr_sasrec_predict_f32(const gr_sasrec_params* p, const int64_t* seqs, int64_t B,
-                                     int32_t n, float* logits, void* workspace,
-                                     size_t workspace_bytes, int32_t* err_flag, void* stream) {
+extern "C" int gr_sasrec_predict_ld_f32(const gr_sasrec_params* p, const int64_t* seqs, int64_t B,
+                                        int32_t n, float* logits, int64_t ld, void* workspace,
+                                        size_t workspace_bytes, int32_t* err_flag, void* stream) {
   using namespace gr;
   clear_error();
+  if (p && ld < p->item_rows)
+    return fail(GR_ERR_ARG, "gr_sasrec_predict_ld_f32: ld < item_rows");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   SasWs w;
   int rc = sas_prepare(p, B, n, workspace, workspace_bytes, &w);
   if (rc) return rc;
   if (B == 0) return GR_OK;
-  if (!seqs || !logits) return fail(GR_ERR_ARG, "gr_sasrec_predict_f32: null seqs / logits");
+  if (!seqs || !logits) return fail(GR_ERR_ARG, "gr_sasrec_predict: null seqs / logits");
   if (fused_ok(p, n)) {
     rc = gr_sasrec_fused_launch(p, seqs, B, n, w.h, 1, err_flag, st);
     if (rc == GR_ERR_UNSUPPORTED)
@@ -420,11 +422,18 @@ extern "C" int gr_sasrec_predict_f32(const gr_sasrec_params* p, const int64_t* s
     rc = run_layernorm(fin.x, B, p->d, fin.stride, fin.off, p->last_ln_w, p->last_ln_b, p->eps, w.h, st);
   }
   if (rc) return rc;
-  rc = gr_score_launch(w.h, B, p->d, p->item_emb, p->item_rows, logits, p->item_rows, st);
+  rc = gr_score_launch(w.h, B, p->d, p->item_emb, p->item_rows, logits, ld, st);
   if (rc != GR_ERR_UNSUPPORTED) return rc;
   clear_error();
   return gr_linear_launch(w.h, B, p->d, p->item_emb, (int32_t)p->item_rows, nullptr, nullptr, 0,
-                          GR_ACT_NONE, logits, p->item_rows, st);
+                          GR_ACT_NONE, logits, ld, st);
+}
+
+extern "C" int gr_sasrec_predict_f32(const gr_sasrec_params* p, const int64_t* seqs, int64_t B,
+                                     int32_t n, float* logits, void* workspace,
+                                     size_t workspace_bytes, int32_t* err_flag, void* stream) {
+  return gr_sasrec_predict_ld_f32(p, seqs, B, n, logits, p ? p->item_rows : 0, workspace,
+                                  workspace_bytes, err_flag, stream);
 }
 
 extern "C" int gr_rank_f32(const float* logits, int64_t B, int64_t cols, int64_t ld,

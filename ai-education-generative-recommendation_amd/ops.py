@@ -43,7 +43,7 @@ def score(h, table, out=None):
     t = L.as_f32(table)
     B, d = h.shape
     rows = t.shape[0]
-    y = out if out is not None else torch.empty((B, rows), dtype=torch.float32, device=h.device)
+    y = out if out is not None else logits_buffer(B, rows, h.device)
     with torch.cuda.device(h.device):
         L.check(L.lib().gr_score_f32(L.ptr(h), B, d, L.ptr(t), rows, L.ptr(y), y.stride(0),
                                      L.stream_of(h.device)), "gr_score_f32")
@@ -366,18 +366,38 @@ def sasrec_forward(binding, log_seqs, last_only=False):
     return out
 
 
+LOGITS_ROW_ALIGN = 32  # floats: one 128-byte line
+
+
+def logits_buffer(B, rows, device):
+    """A fresh ``[B, rows]`` fp32 logits tensor whose rows are ``rows`` rounded up to 32 floats apart
+    (a view of a ``[B, ld]`` allocation), so every row starts on a 128-byte line and the scoring
+    kernel stores whole lines straight from its accumulators.  The reference's callers
+    (evaluate.py:27-32, train.py:45-48: in-place ``[:, 0]`` mask, ``gather``, ``>`` + ``sum``) work on
+    it unchanged; ``.contiguous()`` gives a packed copy."""
+    ld = -(-rows // LOGITS_ROW_ALIGN) * LOGITS_ROW_ALIGN
+    return torch.empty((B, ld), dtype=torch.float32, device=device)[:, :rows]
+
+
 def sasrec_predict(binding, log_seqs, out=None):
+    """model.py:98-108 through ``gr_sasrec_predict_ld_f32``.  ``out`` (optional) may be any
+    ``[B, item_rows]`` fp32 tensor with unit column stride; by default a row-padded
+    :func:`logits_buffer` is returned."""
     ids = _sas_ids(log_seqs, binding)
     B, n = ids.shape
     dev = ids.device
     rows = binding.p.item_rows
-    logits = out if out is not None else torch.empty((B, rows), dtype=torch.float32, device=dev)
+    logits = out if out is not None else logits_buffer(B, rows, dev)
+    if (logits.shape != (B, rows) or logits.dtype != torch.float32 or logits.device != dev
+            or (B > 1 and logits.stride(1) != 1) or logits.stride(0) < rows):
+        raise ValueError("sasrec_predict: out must be fp32 [B, item_rows] on the ids' device with unit column stride")
+    ld = logits.stride(0) if B > 1 else rows
     nbytes = binding.workspace_bytes(B, n)
     wsp = L.workspace(nbytes, dev)
     err = torch.zeros(1, dtype=torch.int32, device=dev)
     with torch.cuda.device(dev):
-        L.check(L.lib().gr_sasrec_predict_f32(ctypes.byref(binding.p), L.ptr(ids), B, n,
-                                              L.ptr(logits), L.ptr(wsp), nbytes, L.ptr(err),
-                                              L.stream_of(dev)), "gr_sasrec_predict_f32")
+        L.check(L.lib().gr_sasrec_predict_ld_f32(ctypes.byref(binding.p), L.ptr(ids), B, n,
+                                                 L.ptr(logits), ld, L.ptr(wsp), nbytes, L.ptr(err),
+                                                 L.stream_of(dev)), "gr_sasrec_predict_ld_f32")
     _check_err(err)
     return logits

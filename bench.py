@@ -261,7 +261,7 @@ def bench_sas_c3(a, world, rank, dev):
     p = synth.sasrec_params(d, n, 2, 1, 64, dev)
     model = synth.sasrec_model(items, p, dev)
     seqs = synth.sequences(a.sas_batch, n, items, 2000 + rank, dev)
-    out = torch.empty((a.sas_batch, items + 1), dtype=torch.float32, device=dev)
+    out = ops.logits_buffer(a.sas_batch, items + 1, dev)  # what predict() returns: rows 128-B aligned
     binding = ops.SasrecBinding(model)
     wall, dev_ms = timed(lambda: ops.sasrec_predict(binding, seqs, out=out), a.steps, a.warmup, world)
     h = model.last_hidden(seqs)
@@ -276,7 +276,7 @@ def bench_sas_c3(a, world, rank, dev):
            "config": {"workload": "sas_c3: SASRec predict, 2 blocks, d 64, n 50, H 1, mlp 64, "
                                   "100k-item full-catalog logits written", "users_per_rank_per_step": a.sas_batch,
                       "parallelism": f"user-sharded x{world}, no collective"},
-           "roofline": roofline("score_kernel<64,true>", 2 * d * (items + 1) * a.sas_batch, score_ms),
+           "roofline": roofline("score_direct_kernel<64>", 2 * d * (items + 1) * a.sas_batch, score_ms),
            "call": {"device_ms": dev_ms, "flop_per_user": fl,
                     "frac_of_fp32_peak": fl * a.sas_batch / (dev_ms * 1e-3) / 1e12 / FP32_PEAK_TFLOPS,
                     "forward_ms": fwd_ms, "score_ms": score_ms,

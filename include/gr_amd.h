@@ -181,6 +181,14 @@ int gr_sasrec_predict_f32(const gr_sasrec_params* p, const int64_t* seqs, int64_
                           float* logits, void* workspace, size_t workspace_bytes,
                           int32_t* err_flag, void* stream);
 
+/* Same, logits rows ld floats apart (ld >= item_rows).  SASRec.predict allocates ld = item_rows
+ * rounded up to 32 floats, so every row starts on a 128-byte line and the scoring kernel stores
+ * whole lines straight from its accumulators; the caller gets the [B, item_rows]
+ * view, on which evaluate.py:27-32 (in-place column-0 mask, gather, '>' count) work unchanged. */
+int gr_sasrec_predict_ld_f32(const gr_sasrec_params* p, const int64_t* seqs, int64_t B, int32_t n,
+                             float* logits, int64_t ld, void* workspace, size_t workspace_bytes,
+                             int32_t* err_flag, void* stream);
+
 /* Full-catalog (or catalog-shard) scoring logits[B, rows] = h[B, d] . table[rows, d]^T
  * (SASRec/model.py:107).  ld = row stride of logits. */
 int gr_score_f32(const float* h, int64_t B, int32_t d, const float* table, int64_t rows,

@@ -90,6 +90,29 @@ def test_predict_returns_fresh_writable_tensor(dev):
     assert not torch.equal(a[:, 0], b[:, 0]) and torch.equal(a[:, 1:], b[:, 1:])
 
 
+@pytest.mark.parametrize("name", ["sas_csv_c1", "sas_syn_c3"])
+def test_predict_row_padded_layout(name, dev, sas_path):
+    """predict() returns a [B, N+1] view whose rows are 32-float aligned (direct-store scoring); the
+    values are bitwise those written into a packed buffer, and evaluate.py:27-32 runs on the view."""
+    from gr_amd import ops
+    m, out, meta = build(name, dev)
+    seqs = torch.from_numpy(out["seqs"]).to(dev)
+    targets = torch.from_numpy(out["targets"]).to(dev)
+    a = m.predict(seqs)
+    rows = meta["item_num"] + 1
+    assert a.shape == (len(seqs), rows) and a.stride(1) == 1
+    assert a.stride(0) % 32 == 0 and a.data_ptr() % 128 == 0
+    packed = torch.empty((len(seqs), rows), device=dev)
+    ops.sasrec_predict(m._binding(seqs), seqs, out=packed)
+    assert torch.equal(a, packed)
+    lg, lp = a.clone(), packed.clone()
+    a[:, 0] = -1e9
+    packed[:, 0] = -1e9
+    ra = (a > a.gather(1, targets.unsqueeze(1))).sum(1) + 1
+    rp = (packed > packed.gather(1, targets.unsqueeze(1))).sum(1) + 1
+    assert torch.equal(ra, rp) and torch.equal(ops.rank(lg, targets), ra)
+
+
 def test_deterministic_and_batch_invariant(dev, sas_path):
     m, out, meta = build("sas_syn_c3", dev)
     seqs = torch.from_numpy(out["seqs"]).to(dev)
