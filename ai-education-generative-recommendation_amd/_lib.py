@@ -60,6 +60,10 @@ SIGNATURES = {
     "gr_sasrec_predict_ld_f32": (ctypes.c_int, [ctypes.POINTER(SasrecParams), _vp, _i64, _i32, _vp,
                                                 _i64, _vp, _sz, _vp, _vp]),
     "gr_score_f32": (ctypes.c_int, [_vp, _i64, _i32, _vp, _i64, _vp, _i64, _vp]),
+    "gr_sampled_bce_fwd_f32": (ctypes.c_int, [_vp, _i64, _i32, _i32, _vp, _i64, _vp, _vp, _i32, _f32,
+                                              _vp, _vp, _vp, _vp, _vp]),
+    "gr_sampled_bce_bwd_f32": (ctypes.c_int, [_vp, _i64, _i32, _i32, _vp, _i64, _vp, _vp, _i32, _vp,
+                                              _vp, _vp, _vp, _vp]),
     "gr_rank_f32": (ctypes.c_int, [_vp, _i64, _i64, _i64, _vp, _i32, _vp, _vp]),
     "gr_count_gt_f32": (ctypes.c_int, [_vp, _i64, _i64, _i64, _vp, _vp, _vp]),
     "gr_topk_workspace_bytes": (_sz, [_i64, _i64, _i32]),

@@ -401,3 +401,67 @@ def sasrec_predict(binding, log_seqs, out=None):
                                                  L.stream_of(dev)), "gr_sasrec_predict_ld_f32")
     _check_err(err)
     return logits
+
+
+# --------------------------------------------------------------------------------------------
+# Training-side scoring (SASRec/train.py:131-160)
+
+class _SampledBCE(torch.autograd.Function):
+    """``(batch_loss, batch_valid_t)`` of train.py:134-158 with the score matrix never formed;
+    differentiable in ``feats`` and ``table`` (gr_sampled_bce_fwd_f32 / gr_sampled_bce_bwd_f32)."""
+
+    @staticmethod
+    def forward(ctx, feats, table, targets, negs, eps):
+        B, n, d = feats.shape
+        rows = table.shape[0]
+        J = negs.shape[1]
+        dev = feats.device
+        row_loss = torch.empty(B * n, dtype=torch.float32, device=dev)
+        coef = torch.empty(B * n * (J + 1), dtype=torch.float32, device=dev)
+        sums = torch.empty(2, dtype=torch.float32, device=dev)
+        err = torch.zeros(1, dtype=torch.int32, device=dev)
+        with torch.cuda.device(dev):
+            L.check(L.lib().gr_sampled_bce_fwd_f32(L.ptr(feats), B, n, d, L.ptr(table), rows,
+                                                   L.ptr(targets), L.ptr(negs), J, float(eps),
+                                                   L.ptr(row_loss), L.ptr(coef), L.ptr(sums),
+                                                   L.ptr(err), L.stream_of(dev)),
+                    "gr_sampled_bce_fwd_f32")
+        _check_err(err)
+        ctx.save_for_backward(feats, table, targets, negs, coef)
+        valid = sums[1]
+        ctx.mark_non_differentiable(valid)
+        return sums[0], valid
+
+    @staticmethod
+    def backward(ctx, g_loss, g_valid):
+        feats, table, targets, negs, coef = ctx.saved_tensors
+        B, n, d = feats.shape
+        rows = table.shape[0]
+        dev = feats.device
+        g = g_loss.to(device=dev, dtype=torch.float32).reshape(1).contiguous()
+        dfeats = torch.empty_like(feats)
+        dtable = torch.empty_like(table)
+        with torch.cuda.device(dev):
+            L.check(L.lib().gr_sampled_bce_bwd_f32(L.ptr(feats), B, n, d, L.ptr(table), rows,
+                                                   L.ptr(targets), L.ptr(negs), negs.shape[1],
+                                                   L.ptr(coef), L.ptr(g), L.ptr(dfeats),
+                                                   L.ptr(dtable), L.stream_of(dev)),
+                    "gr_sampled_bce_bwd_f32")
+        return dfeats, dtable, None, None, None
+
+
+def sampled_bce_loss(seq_features, item_emb_weight, target_o_t, neg_samples, eps):
+    """train.py:134-158 in one fused op: returns ``(batch_loss, batch_valid_t)`` as device scalars,
+    equal to the reference's ``(pos_loss + neg_loss).sum()`` and ``mask.sum()`` over the
+    ``[B, n, item_num+1]`` score matrix it forms (this op never forms it).  ``batch_loss`` is
+    differentiable in ``seq_features`` [B, n, d] and ``item_emb_weight`` [item_num+1, d]; the caller
+    divides by ``batch_valid_t`` (train.py:161-164) and calls ``backward()`` as before."""
+    L.require_gpu(seq_features, item_emb_weight, target_o_t, neg_samples)
+    if seq_features.dim() != 3 or item_emb_weight.dim() != 2 or seq_features.shape[2] != item_emb_weight.shape[1]:
+        raise RuntimeError("sampled_bce_loss: seq_features [B, n, d] and item_emb_weight [rows, d] expected")
+    B, n, _ = seq_features.shape
+    if tuple(target_o_t.shape) != (B, n) or neg_samples.dim() != 2 or neg_samples.shape[0] != B:
+        raise RuntimeError("sampled_bce_loss: target_o_t [B, n] and neg_samples [B, num_neg] expected")
+    return _SampledBCE.apply(L.as_f32(seq_features), L.as_f32(item_emb_weight),
+                             target_o_t.to(torch.int64).contiguous(),
+                             neg_samples.to(torch.int64).contiguous(), eps)

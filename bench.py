@@ -69,7 +69,8 @@ def parse():
     ap.add_argument("--c5-items", type=int, default=1_000_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="budget per CPU baseline leg")
-    ap.add_argument("--skip", default="", help="comma list of legs to skip: sasrec,c4,c5")
+    ap.add_argument("--train-batch", type=int, default=128, help="sas_train leg: users per rank per step")
+    ap.add_argument("--skip", default="", help="comma list of legs to skip: sasrec,c4,c5,train")
     ap.add_argument("--spinup-s", type=float, default=1.0,
                     help="untimed seconds of each leg's workload before its warmup (clock ramp)")
     return ap.parse_args()
@@ -329,6 +330,77 @@ def bench_sas_c5(a, world, rank, dev):
                              "[B, rows] logits are never written"}}
 
 
+def sas_train_bytes(B, n, d, rows, J):
+    """Algorithmic HBM bytes of one training-side scoring step (forward + backward of
+    gr_sampled_bce_*): every operand read or written once (features twice: forward and backward),
+    the gathered table rows once per pass, the dense dM written once plus a read-modify-write of
+    the touched rows."""
+    P = B * n
+    fwd = P * d * 4 + (P + B * J) * d * 4 + P * 8 + B * J * 8 + P * (J + 2) * 4
+    bwd = 2 * P * d * 4 + P * (J + 1) * 4 + (P + B * J) * d * 4 + P * d * 4 + rows * d * 4 \
+        + 2 * (P + B * J) * d * 4
+    return fwd + bwd
+
+
+def bench_sas_train(a, world, rank, dev):
+    """the training-side scoring of SASRec/train.py:131-167 at C3 shapes with the
+    reference's training batch (main.py: batch_size 128, num_neg_samples 10, loss_eps 1e-24):
+    forward + backward of ops.sampled_bce_loss (no [B, n, N+1] score matrix), user-sharded."""
+    B, n, d, items, J = a.train_batch, 50, 64, 100_000, 10
+    g = torch.Generator(device=dev).manual_seed(3000 + rank)
+    feats = (0.3 * torch.randn(B, n, d, generator=g, device=dev)).requires_grad_(True)
+    table = (0.3 * torch.randn(items + 1, d, generator=g, device=dev)).requires_grad_(True)
+    lens = torch.randint(3, n + 1, (B,), generator=g, device=dev)
+    targets = torch.randint(1, items + 1, (B, n), generator=g, device=dev)
+    targets[torch.arange(n, device=dev)[None, :] < (n - lens)[:, None]] = 0
+    negs = torch.randint(1, items + 1, (B, J), generator=g, device=dev)
+
+    def step():
+        bl, valid = ops.sampled_bce_loss(feats, table, targets, negs, 1e-24)
+        feats.grad = table.grad = None
+        (bl / valid).backward()
+
+    def dense_step():   # train.py:134-167 as written, in torch on the same GPU (rocBLAS GEMMs)
+        sm = torch.matmul(feats, table.t())
+        mask = (targets != 0).float()
+        ne = negs.unsqueeze(1).expand(-1, n, -1)
+        ps = torch.gather(sm, 2, targets.unsqueeze(-1)).squeeze(-1)
+        ns = torch.gather(sm, 2, ne)
+        pl = -torch.log(torch.sigmoid(ps) + 1e-24) * mask
+        nl = (-torch.log(1 - torch.sigmoid(ns) + 1e-24) * mask.unsqueeze(-1)).sum(-1)
+        feats.grad = table.grad = None
+        ((pl + nl).sum() / mask.sum()).backward()
+
+    wall, dev_ms = timed(step, a.steps, a.warmup, world)
+    dense_ms = kernel_ms(dense_step, reps=10)
+    nbytes = sas_train_bytes(B, n, d, items + 1, J)
+    res = {"metric": "train_seqs_scored/s", "value": B * world * a.steps / wall, "unit": "seqs/s",
+           "ms_per_step": wall / a.steps * 1e3, "scaling": "weak",
+           "config": {"workload": f"sas_train: SASRec train.py:131-167 scoring + sampled BCE, forward + "
+                                  f"backward, B {B}, n {n}, d {d}, {items}-item table, {J} negatives",
+                      "users_per_rank_per_step": B, "parallelism": f"user-sharded x{world}, no collective"},
+           "roofline": {"bound": "hbm", "achieved": nbytes / (dev_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
+                        "unit": "GB/s", "frac": nbytes / (dev_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                        "traffic": None, "kernel": "whole step (gr_sampled_bce fwd + bwd, 4 kernels + dM fill)",
+                        "bytes_per_step": nbytes, "step_device_ms": dev_ms},
+           "reference_formulation_gpu": {"note": "train.py:134-167 as written ([B, n, N+1] score matrix, "
+                                                 "gathers, dense backward) in torch on the same GPU",
+                                         "ms_per_step": dense_ms, "speedup": dense_ms / dev_ms}}
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        from oracle import sasrec_oracle
+        torch.set_num_threads(cpu_threads())
+        f, w, t, ng = feats.detach().cpu(), table.detach().cpu(), targets.cpu(), negs.cpu()
+        t0, k = time.perf_counter(), 0
+        while k == 0 or (time.perf_counter() - t0 < min(a.cpu_seconds, 10.0) and k < 20):
+            sasrec_oracle.train_loss_grads(f, w, t, ng, 1e-24)
+            k += 1
+        el = time.perf_counter() - t0
+        res["cpu_baseline"] = {"value": B * k / el, "unit": "seqs/s", "cores": cpu_threads(), "kind": "port",
+                               "sample": f"oracle/sasrec_oracle.train_loss_grads (train.py:134-167 in torch CPU), "
+                                         f"{k} steps of B {B} ({el:.1f} s)"}
+    return res
+
+
 def main():
     a = parse()
     global SPINUP_S
@@ -359,6 +431,8 @@ def main():
         line["rq_c4"] = bench_rq_c4(a, world, rank, dev)
     if "c5" not in skip:
         line["sasrec_c5"] = bench_sas_c5(a, world, rank, dev)
+    if "train" not in skip:
+        line["sasrec_train"] = bench_sas_train(a, world, rank, dev)
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         line["cpu_baseline"] = cpu_rq_baseline(rq_model, a.cpu_seconds)
         if "sasrec" not in skip:

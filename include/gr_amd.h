@@ -248,6 +248,28 @@ int gr_score_topk_f32(const float* h, int64_t B, int32_t d, const float* table, 
                       int64_t* counts_out, float* vals_out, int64_t* ids_out, void* workspace,
                       size_t workspace_bytes, void* stream);
 
+/* ------------------------------------------------------------------------------------------ */
+/* Training-side scoring (SASRec/train.py:131-160) without the [B, n, rows]
+ * score matrix.  feats[B, n, d] = model.forward(input_seqs), table[rows, d] = item_emb.weight,
+ * targets[B, n] = o_t (0 = padding, masked), negs[B, num_neg] (shared by the user's n positions,
+ * train.py:143-150).  With S = feats . table^T:
+ *   row_loss[b*n+t] = m*(-log(sigmoid(S[b,t,o_t]) + eps)) + sum_j m*(-log(1 - sigmoid(S[b,t,neg_j]) + eps)),
+ *   m = (o_t != 0);  sums[0] = batch_loss = sum of row_loss, sums[1] = mask.sum()  (train.py:155-158).
+ * coef[B*n*(1+num_neg)] receives d row_loss / d S at the gathered entries (target first), the
+ * saved state for the backward.  err_flag (optional device int32) is set for an id outside [0, rows). */
+int gr_sampled_bce_fwd_f32(const float* feats, int64_t B, int32_t n, int32_t d, const float* table,
+                           int64_t rows, const int64_t* targets, const int64_t* negs,
+                           int32_t num_neg, float eps, float* row_loss, float* coef, float* sums,
+                           int32_t* err_flag, void* stream);
+
+/* Backward of batch_loss scaled by *grad_scale (device fp32 scalar, e.g. 1/valid of
+ * `loss = batch_loss / batch_valid_t`): dfeats[B, n, d] (written) and dtable[rows, d] (zeroed,
+ * then the gathered rows accumulated with fp32 atomics, so the summation order is not fixed). */
+int gr_sampled_bce_bwd_f32(const float* feats, int64_t B, int32_t n, int32_t d, const float* table,
+                           int64_t rows, const int64_t* targets, const int64_t* negs,
+                           int32_t num_neg, const float* coef, const float* grad_scale,
+                           float* dfeats, float* dtable, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -9,6 +9,8 @@ restatement then agrees within rounding only (compare with a tolerance).
 """
 import math
 
+import numpy as np
+
 import torch
 import torch.nn.functional as F
 
@@ -75,3 +77,41 @@ def predict(log_seqs, sd, num_blocks, num_heads, eps):
     """SASRec.predict (SASRec/model.py:98-108): ``LN_last(x)[:, -1, :] @ item_emb.weight.t()``."""
     feats = forward(log_seqs, sd, num_blocks, num_heads, eps)
     return feats[:, -1, :].matmul(sd['item_emb.weight'].t())
+
+
+def neg_samples(seq, item_num, num_neg, rng=np.random):
+    """train.py:15-30 get_neg_samples: per row, ``num_neg`` distinct items drawn uniformly from
+    ``[1, item_num]`` minus the row's non-zero history (``np.random.choice(..., replace=False)``)."""
+    out = []
+    for s in np.asarray(seq):
+        valid = np.setdiff1d(np.arange(1, item_num + 1), s[s != 0])
+        out.append(rng.choice(valid, num_neg, replace=False))
+    return torch.tensor(np.array(out), dtype=torch.long)
+
+
+def train_loss(seq_features, item_emb_weight, target_o_t, negs, eps):
+    """train.py:134-158 verbatim in torch (CPU fp32): the full score matrix ``[B, n, N+1]``, the
+    target / negative gathers, the masked BCE terms.  Returns ``(batch_loss, batch_valid_t)``;
+    autograd through it gives the reference's gradients."""
+    score_matrix = torch.matmul(seq_features, item_emb_weight.t())
+    mask = (target_o_t != 0).float()
+    seq_len = score_matrix.shape[1]
+    neg_expanded = negs.unsqueeze(1).expand(-1, seq_len, -1)
+    pos_scores = torch.gather(score_matrix, dim=2, index=target_o_t.unsqueeze(-1)).squeeze(-1)
+    neg_scores = torch.gather(score_matrix, dim=2, index=neg_expanded)
+    pos_loss = -torch.log(torch.sigmoid(pos_scores) + eps) * mask
+    neg_loss = (-torch.log(1 - torch.sigmoid(neg_scores) + eps) * mask.unsqueeze(-1)).sum(dim=-1)
+    return (pos_loss + neg_loss).sum(), mask.sum()
+
+
+def train_loss_grads(seq_features, item_emb_weight, target_o_t, negs, eps):
+    """``loss = batch_loss / batch_valid_t; loss.backward()`` (train.py:161-167) on the restatement:
+    returns ``(batch_loss, valid, d seq_features, d item_emb_weight)``."""
+    f = seq_features.detach().clone().requires_grad_(True)
+    w = item_emb_weight.detach().clone().requires_grad_(True)
+    bl, valid = train_loss(f, w, target_o_t, negs, eps)
+    loss = bl / valid.item() if valid.item() > 0 else torch.zeros((), requires_grad=True)
+    loss.backward()
+    gf = f.grad if f.grad is not None else torch.zeros_like(f)
+    gw = w.grad if w.grad is not None else torch.zeros_like(w)
+    return bl.detach(), valid, gf, gw
