@@ -15,19 +15,6 @@
 
 namespace gr {
 
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
-}
-
-__device__ __forceinline__ float row_dot(const float* __restrict__ a, const float* __restrict__ b,
-                                         int d, int lane) {
-  float s = 0.f;
-  for (int k = lane; k < d; k += 64) s = fmaf(a[k], b[k], s);
-  return wave_sum(s);
-}
-
 __device__ __forceinline__ int64_t checked_row(int64_t r, int64_t rows, int32_t* err) {
   if (r < 0 || r >= rows) {
     if (err) *err = 1;
@@ -39,6 +26,15 @@ __device__ __forceinline__ int64_t checked_row(int64_t r, int64_t rows, int32_t*
 // train.py:147-156 for one position: pos = S[b,t,o_t], neg_j = S[b,t,neg[b,j]], m = (o_t != 0);
 //   loss = -log(sigmoid(pos) + eps) * m + sum_j -log(1 - sigmoid(neg_j) + eps) * m
 // and d loss / d S at each gathered entry (autograd's chain: mask, log, sigmoid).
+// The position's rows (target first, then the negatives) go in groups of RB: all RB row segments
+// are loaded before any arithmetic and the RB wave reductions run interleaved, so one group costs
+// about one memory round trip and one 6-step butterfly instead of RB of each.
+constexpr int BCE_RB = 16;
+
+__device__ __forceinline__ int64_t bce_row(int i, int64_t tg, const int64_t* __restrict__ nb) {
+  return i == 0 ? tg : nb[i - 1];
+}
+
 __global__ __launch_bounds__(256) void bce_fwd_kernel(const float* __restrict__ feats, int64_t P,
                                                      int n, int d, const float* __restrict__ table,
                                                      int64_t rows, const int64_t* __restrict__ targets,
@@ -52,42 +48,89 @@ __global__ __launch_bounds__(256) void bce_fwd_kernel(const float* __restrict__ 
   const float* h = feats + p * d;
   const int64_t tg = checked_row(targets[p], rows, err);
   const float m = targets[p] != 0 ? 1.f : 0.f;
-  const float sp = row_dot(h, table + tg * d, d, lane);
-  const float gp = 1.f / (1.f + expf(-sp));
-  const float lp = -logf(gp + eps) * m;
-  // d/ds [-log(sigmoid(s) + eps) * m] = (-m / (sigmoid + eps)) * sigmoid * (1 - sigmoid)
-  const float cp = (-m / (gp + eps)) * ((1.f - gp) * gp);
-  float ln = 0.f;
+  const int64_t* nb = negs + b * J;
   float* c = coef + p * (J + 1);
-  if (lane == 0) c[0] = cp;
-  for (int j = 0; j < J; ++j) {
-    const int64_t r = checked_row(negs[b * J + j], rows, err);
-    const float s = row_dot(h, table + r * d, d, lane);
-    const float g = 1.f / (1.f + expf(-s));
-    ln += -logf(1.f - g + eps) * m;
-    // d/ds [-log(1 - sigmoid(s) + eps) * m] = (m / (1 - sigmoid + eps)) * sigmoid * (1 - sigmoid)
-    if (lane == 0) c[1 + j] = (m / (1.f - g + eps)) * ((1.f - g) * g);
+  float lpos = 0.f, lneg = 0.f;   // pos_loss and neg_loss (summed over j) of train.py:155-156
+  for (int g0 = 0; g0 < J + 1; g0 += BCE_RB) {
+    int64_t r[BCE_RB];
+#pragma unroll
+    for (int i = 0; i < BCE_RB; ++i)
+      r[i] = g0 + i < J + 1 ? checked_row(bce_row(g0 + i, tg, nb), rows, err) : tg;
+    float s[BCE_RB];
+#pragma unroll
+    for (int i = 0; i < BCE_RB; ++i) s[i] = 0.f;
+    for (int k = lane; k < d; k += 64) {
+      const float hk = h[k];
+      float v[BCE_RB];
+#pragma unroll
+      for (int i = 0; i < BCE_RB; ++i) v[i] = table[r[i] * d + k];
+#pragma unroll
+      for (int i = 0; i < BCE_RB; ++i) s[i] = fmaf(hk, v[i], s[i]);
+    }
+    // Reduce-scatter of the 16 partial dot products over the wave (recursive halving: 8 + 4 + 2 + 1
+    // exchanges, then 2 butterfly steps inside each 4-lane group): lane l ends with the full dot
+    // product of row g0 + (l >> 2), 17 cross-lane moves instead of 16 x 6.
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const bool up = lane & 32;
+      const float keep = up ? s[i + 8] : s[i];
+      s[i] = keep + __shfl_xor(up ? s[i] : s[i + 8], 32, 64);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const bool up = lane & 16;
+      const float keep = up ? s[i + 4] : s[i];
+      s[i] = keep + __shfl_xor(up ? s[i] : s[i + 4], 16, 64);
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const bool up = lane & 8;
+      const float keep = up ? s[i + 2] : s[i];
+      s[i] = keep + __shfl_xor(up ? s[i] : s[i + 2], 8, 64);
+    }
+    {
+      const bool up = lane & 4;
+      const float keep = up ? s[1] : s[0];
+      s[0] = keep + __shfl_xor(up ? s[0] : s[1], 4, 64);
+    }
+    s[0] += __shfl_xor(s[0], 2, 64);
+    s[0] += __shfl_xor(s[0], 1, 64);
+    const int q = g0 + (lane >> 2);
+    const float sg = 1.f / (1.f + expf(-s[0]));
+    if (q == 0) {
+      // d/ds [-log(sigmoid(s) + eps) * m] = (-m / (sigmoid + eps)) * sigmoid * (1 - sigmoid)
+      if (lane == 0) {
+        lpos = -logf(sg + eps) * m;
+        c[0] = (-m / (sg + eps)) * ((1.f - sg) * sg);
+      }
+    } else if (q <= J && (lane & 3) == 0) {
+      lneg += -logf(1.f - sg + eps) * m;
+      // d/ds [-log(1 - sigmoid(s) + eps) * m] = (m / (1 - sigmoid + eps)) * sigmoid * (1 - sigmoid)
+      c[q] = (m / (1.f - sg + eps)) * ((1.f - sg) * sg);
+    }
   }
-  if (lane == 0) row_loss[p] = lp + ln;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) lneg += __shfl_xor(lneg, o, 64);
+  if (lane == 0) row_loss[p] = lpos + lneg;
 }
 
 // batch_loss = sum of the position losses (float64 accumulation, fixed order: deterministic) and
 // the number of valid positions, mask.sum() (train.py:157-158).
-__global__ __launch_bounds__(256) void bce_sum_kernel(const float* __restrict__ row_loss,
-                                                     const int64_t* __restrict__ targets, int64_t P,
-                                                     float* __restrict__ sums) {
-  __shared__ double sl[256];
-  __shared__ long long sv[256];
+__global__ __launch_bounds__(1024) void bce_sum_kernel(const float* __restrict__ row_loss,
+                                                      const int64_t* __restrict__ targets, int64_t P,
+                                                      float* __restrict__ sums) {
+  __shared__ double sl[1024];
+  __shared__ long long sv[1024];
   double a = 0.0;
   long long v = 0;
-  for (int64_t i = threadIdx.x; i < P; i += 256) {
+  for (int64_t i = threadIdx.x; i < P; i += 1024) {
     a += (double)row_loss[i];
     v += targets[i] != 0;
   }
   sl[threadIdx.x] = a;
   sv[threadIdx.x] = v;
   __syncthreads();
-  for (int s = 128; s > 0; s >>= 1) {
+  for (int s = 512; s > 0; s >>= 1) {
     if ((int)threadIdx.x < s) {
       sl[threadIdx.x] += sl[threadIdx.x + s];
       sv[threadIdx.x] += sv[threadIdx.x + s];
@@ -120,6 +163,7 @@ __global__ __launch_bounds__(256) void bce_bwd_pos_kernel(const float* __restric
   const float* h = feats + p * d;
   for (int k = lane; k < d; k += 64) {
     float acc = cp * table[tg * d + k];
+#pragma unroll 8
     for (int j = 0; j < J; ++j) {
       const int64_t r = checked_row(negs[b * J + j], rows, nullptr);
       acc = fmaf(g * c[1 + j], table[r * d + k], acc);
@@ -146,6 +190,7 @@ __global__ __launch_bounds__(256) void bce_bwd_neg_kernel(const float* __restric
   const int64_t r = checked_row(negs[q], rows, nullptr);
   for (int k = lane; k < d; k += 64) {
     float acc = 0.f;
+#pragma unroll 8
     for (int t = 0; t < n; ++t) {
       const int64_t p = b * n + t;
       acc = fmaf(coef[p * (J + 1) + 1 + j], feats[p * d + k], acc);
@@ -186,7 +231,7 @@ extern "C" int gr_sampled_bce_fwd_f32(const float* feats, int64_t B, int32_t n, 
     rc = check_launch("gr_sampled_bce_fwd_f32");
     if (rc) return rc;
   }
-  hipLaunchKernelGGL(bce_sum_kernel, dim3(1), dim3(256), 0, st, row_loss, targets, P, sums);
+  hipLaunchKernelGGL(bce_sum_kernel, dim3(1), dim3(1024), 0, st, row_loss, targets, P, sums);
   return check_launch("gr_sampled_bce_fwd_f32 (sum)");
 }
 
