@@ -14,9 +14,12 @@ dev = torch.device("cuda:0")
 g = torch.Generator(device=dev).manual_seed(0)
 
 
-def ms(fn, reps=20):
-    for _ in range(3):
+def ms(fn, reps=50):
+    import time
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < 0.3:   # clock ramp
         fn()
+        torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     for _ in range(reps):
@@ -28,7 +31,7 @@ def ms(fn, reps=20):
 
 for L, K in [(3, 256), (1, 256), (4, 1024)]:
     cbs = [torch.randn((K, 32), generator=g, device=dev) * 0.3 for _ in range(L)]
-    for n in (25_000, 100_000, 400_000):
+    for n in (25_000, 50_000, 100_000, 200_000, 400_000):
         z = torch.randn((n, 32), generator=g, device=dev)
         t = ms(lambda: ops.rq_quantize(z, cbs))
         fl = 2.0 * n * L * K * 32
