@@ -465,3 +465,30 @@ def sampled_bce_loss(seq_features, item_emb_weight, target_o_t, neg_samples, eps
     return _SampledBCE.apply(L.as_f32(seq_features), L.as_f32(item_emb_weight),
                              target_o_t.to(torch.int64).contiguous(),
                              neg_samples.to(torch.int64).contiguous(), eps)
+
+
+_NEG_CALLS = itertools.count()
+
+
+def neg_samples(seq, item_num, num_neg=1, seed=None):
+    """train.py:15-30 ``get_neg_samples(seq, item_num, num_neg)`` on the GPU: ``[B, num_neg]`` int64,
+    per row distinct items uniform over ``[1, item_num]`` minus the row's non-zero history (the
+    reference's distribution; not numpy's random stream).  ``seed`` defaults to a fresh value per
+    call drawn from torch's global generator, so ``torch.manual_seed`` makes runs repeatable."""
+    L.require_gpu(seq)
+    s = seq.to(torch.int64).contiguous()
+    if s.dim() != 2:
+        raise RuntimeError("neg_samples: seq must be [B, n]")
+    B, n = s.shape
+    if seed is None:
+        seed = int(torch.randint(0, 2 ** 62, (1,)).item()) ^ next(_NEG_CALLS)
+    out = torch.empty((B, num_neg), dtype=torch.int64, device=s.device)
+    err = torch.zeros(1, dtype=torch.int32, device=s.device)
+    with torch.cuda.device(s.device):
+        L.check(L.lib().gr_neg_samples(L.ptr(s), B, n, int(item_num), int(num_neg), int(seed) & (2 ** 64 - 1),
+                                       L.ptr(out), L.ptr(err), L.stream_of(s.device)), "gr_neg_samples")
+    if CHECK:
+        torch.cuda.synchronize(s.device)
+        if int(err.item()) != 0:
+            raise ValueError("Cannot take a larger sample than population when 'replace=False'")
+    return out

@@ -25,6 +25,7 @@ import os
 import sys
 import time
 
+import numpy as np
 import torch
 import torch.distributed as dist
 
@@ -353,10 +354,13 @@ def bench_sas_train(a, world, rank, dev):
     lens = torch.randint(3, n + 1, (B,), generator=g, device=dev)
     targets = torch.randint(1, items + 1, (B, n), generator=g, device=dev)
     targets[torch.arange(n, device=dev)[None, :] < (n - lens)[:, None]] = 0
-    negs = torch.randint(1, items + 1, (B, J), generator=g, device=dev)
+    inputs = torch.roll(targets, 1, dims=1)          # s_t = o_{t-1}, the train-mode pairs
+    inputs[:, 0] = 0
+    negs = ops.neg_samples(inputs, items, J)
 
-    def step():
-        bl, valid = ops.sampled_bce_loss(feats, table, targets, negs, 1e-24)
+    def step():   # train.py:142 (negatives) + 134-167 (scores, loss, backward); the transformer is the caller's
+        ng = ops.neg_samples(inputs, items, J)
+        bl, valid = ops.sampled_bce_loss(feats, table, targets, ng, 1e-24)
         feats.grad = table.grad = None
         (bl / valid).backward()
 
@@ -381,23 +385,29 @@ def bench_sas_train(a, world, rank, dev):
                       "users_per_rank_per_step": B, "parallelism": f"user-sharded x{world}, no collective"},
            "roofline": {"bound": "hbm", "achieved": nbytes / (dev_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
                         "unit": "GB/s", "frac": nbytes / (dev_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                        "traffic": None, "kernel": "whole step (gr_sampled_bce fwd + bwd, 4 kernels + dM fill)",
+                        "traffic": None, "kernel": "whole step (gr_neg_samples + gr_sampled_bce fwd + bwd: 5 kernels + dM fill)",
                         "bytes_per_step": nbytes, "step_device_ms": dev_ms},
            "reference_formulation_gpu": {"note": "train.py:134-167 as written ([B, n, N+1] score matrix, "
-                                                 "gathers, dense backward) in torch on the same GPU",
+                                                 "gathers, dense backward) in torch on the same GPU, "
+                                                 "negatives precomputed (the reference draws them on the host)",
                                          "ms_per_step": dense_ms, "speedup": dense_ms / dev_ms}}
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         from oracle import sasrec_oracle
         torch.set_num_threads(cpu_threads())
-        f, w, t, ng = feats.detach().cpu(), table.detach().cpu(), targets.cpu(), negs.cpu()
-        t0, k = time.perf_counter(), 0
+        f, w, t, si = feats.detach().cpu(), table.detach().cpu(), targets.cpu(), inputs.cpu().numpy()
+        rng = np.random.RandomState(0)
+        t0, k, neg_s = time.perf_counter(), 0, 0.0
         while k == 0 or (time.perf_counter() - t0 < min(a.cpu_seconds, 10.0) and k < 20):
+            t1 = time.perf_counter()
+            ng = sasrec_oracle.neg_samples(si, items, J, rng)
+            neg_s += time.perf_counter() - t1
             sasrec_oracle.train_loss_grads(f, w, t, ng, 1e-24)
             k += 1
         el = time.perf_counter() - t0
         res["cpu_baseline"] = {"value": B * k / el, "unit": "seqs/s", "cores": cpu_threads(), "kind": "port",
-                               "sample": f"oracle/sasrec_oracle.train_loss_grads (train.py:134-167 in torch CPU), "
-                                         f"{k} steps of B {B} ({el:.1f} s)"}
+                               "sample": f"oracle get_neg_samples (train.py:15-30, numpy) + train_loss_grads "
+                                         f"(train.py:134-167, torch CPU), {k} steps of B {B} ({el:.1f} s, "
+                                         f"{neg_s / k * 1e3:.0f} ms/step of it negative sampling)"}
     return res
 
 

@@ -270,6 +270,15 @@ int gr_sampled_bce_bwd_f32(const float* feats, int64_t B, int32_t n, int32_t d, 
                            int32_t num_neg, const float* coef, const float* grad_scale,
                            float* dfeats, float* dtable, void* stream);
 
+/* Negative items for SASRec training (SASRec/train.py:15-30 get_neg_samples): out[b, 0..num_neg)
+ * = num_neg distinct items drawn uniformly from [1, item_num] minus the non-zero items of
+ * seqs[b, 0..n) (the reference's np.random.choice(setdiff1d(...), num_neg, replace=False): same
+ * distribution, own counter-based random stream keyed by seed).  num_neg <= 1024.  err_flag
+ * (optional device int32) is set when a row has fewer than num_neg valid items (the reference
+ * raises ValueError there). */
+int gr_neg_samples(const int64_t* seqs, int64_t B, int32_t n, int64_t item_num, int32_t num_neg,
+                   uint64_t seed, int64_t* out, int32_t* err_flag, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

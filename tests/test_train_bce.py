@@ -135,3 +135,60 @@ def test_sampled_bce_bad_ids_flagged(dev):
             ops.sampled_bce_loss(f, w, tg, ng, 1e-24)
     finally:
         ops.CHECK = old
+
+
+# ------------------------------------------------------------------ negative sampling (train.py:15-30)
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B,n,items,J", [(128, 50, 100000, 10), (64, 20, 30, 10), (7, 200, 300, 64), (3, 5, 12, 4)])
+def test_neg_samples_constraints(B, n, items, J, dev):
+    """Every row: num_neg distinct items in [1, item_num], none in the row's non-zero history
+    (the setdiff1d + replace=False contract of get_neg_samples)."""
+    from gr_amd import ops
+    g = torch.Generator().manual_seed(B + n)
+    seq = torch.randint(1, items + 1, (B, n), generator=g)
+    seq[:, : n // 3] = 0                                     # left padding
+    if items >= J + n:
+        seq[0] = torch.randperm(items, generator=g)[:n] + 1  # a full history of distinct items
+    out = ops.neg_samples(seq.to(dev), items, J, seed=7).cpu().numpy()
+    assert out.shape == (B, J)
+    for s, ng in zip(seq.numpy(), out):
+        assert len(set(ng.tolist())) == J
+        assert ng.min() >= 1 and ng.max() <= items
+        assert not set(ng.tolist()) & set(s[s != 0].tolist())
+
+
+@pytest.mark.gpu
+def test_neg_samples_uniform_and_seeded(dev):
+    """Distribution = uniform over the valid set (chi-square over 20000 rows), random order,
+    repeatable for a given seed."""
+    from gr_amd import ops
+    items, J, B = 20, 3, 20000
+    seq = torch.zeros((B, 4), dtype=torch.long)
+    seq[:, 0], seq[:, 1] = 5, 17                             # history {5, 17}: 18 valid items
+    a = ops.neg_samples(seq.to(dev), items, J, seed=123)
+    assert torch.equal(a, ops.neg_samples(seq.to(dev), items, J, seed=123))
+    assert not torch.equal(a, ops.neg_samples(seq.to(dev), items, J, seed=124))
+    cnt = np.bincount(a.cpu().numpy().ravel(), minlength=items + 1)
+    assert cnt[0] == 0 and cnt[5] == 0 and cnt[17] == 0
+    valid = [i for i in range(1, items + 1) if i not in (5, 17)]
+    exp = B * J / len(valid)
+    chi2 = sum((cnt[i] - exp) ** 2 / exp for i in valid)
+    assert chi2 < 45.0          # 17 dof: p ~ 3e-4
+    first = np.bincount(a[:, 0].cpu().numpy(), minlength=items + 1)[valid]   # each position uniform too
+    assert (first.max() - first.min()) < 0.25 * first.mean()
+
+
+@pytest.mark.gpu
+def test_neg_samples_population_too_small(dev):
+    from gr_amd import ops
+    seq = torch.tensor([[1, 2, 3, 4], [0, 0, 0, 1]], device=dev)
+    old = ops.CHECK
+    ops.CHECK = True
+    try:
+        with pytest.raises(ValueError):
+            ops.neg_samples(seq, 6, 3)                       # row 0 has 2 valid items
+    finally:
+        ops.CHECK = old
+    with pytest.raises(RuntimeError):
+        ops.neg_samples(seq, 2, 3)                           # num_neg > item_num
