@@ -259,8 +259,15 @@ def rq_encode_sk(x, weights, biases, codebooks, sk_eps, sk_iters, group_sizes=No
     independent row groups in ONE launch: ``group_sizes`` partitions the rows of ``x`` into
     consecutive groups, each one reference call (default: the whole batch is one group)."""
     L.require_gpu(x, *weights, *codebooks)
-    n = x.shape[0]
-    z = rq_mlp(x, weights, biases)
+    return rq_quantize_sk(rq_mlp(x, weights, biases), codebooks, sk_eps, sk_iters, group_sizes)
+
+
+def rq_quantize_sk(z, codebooks, sk_eps, sk_iters, group_sizes=None):
+    """ResidualVectorQuantizer.forward(z, use_sk=True) indices (rq.py:39-56, vq.py:63-84): per level,
+    Sinkhorn over the group's distances where ``sk_eps[l] > 0``, plain argmin otherwise."""
+    L.require_gpu(z, *codebooks)
+    z = L.as_f32(z)
+    n = z.shape[0]
     cbs = [L.as_f32(c) for c in codebooks]
     e = z.shape[1]
     Ks = [c.shape[0] for c in cbs]
@@ -268,7 +275,7 @@ def rq_encode_sk(x, weights, biases, codebooks, sk_eps, sk_iters, group_sizes=No
     if sum(sizes) != n or any(s < 1 for s in sizes):
         raise RuntimeError("rq_encode_sk: group sizes must be positive and sum to the batch")
     ptr = torch.tensor([0] + list(itertools.accumulate(sizes)), dtype=torch.int64)
-    dev = x.device
+    dev = z.device
     ptr = ptr.to(dev)
     lib = L.lib()
     ks_c = L.i32_array(Ks)

@@ -7,8 +7,11 @@ load unchanged and ``RQ-VAE/infer.py`` / ``generate_code.py`` can swap the impor
     from models.rqvae import RQVAE            ->   from gr_amd.rqvae import RQVAE
 
 ``get_indices(xs, use_sk=False)`` (rqvae.py:67-71) is one C-ABI call, ``gr_rq_encode_f32``.
+``forward(x, use_sk)`` (rqvae.py:60-65, the training call of RQ-VAE/train.py:113) is differentiable,
+with every level's codebook assignment (argmin or Sinkhorn) on the kernels.
 """
 import torch
+import torch.nn.functional as F
 from torch import nn
 from torch.nn.init import xavier_normal_
 
@@ -73,6 +76,17 @@ class MLPLayers(nn.Module):
     def linears(self):
         return [m for m in self.mlp_layers if isinstance(m, nn.Linear)]
 
+    def eval_forward(self, x):
+        """layers.py:42-43 in eval mode on ``gr_linear_f32`` layer by layer (any widths; ReLU after
+        every Linear but the last) — the decoder of the no-grad forward."""
+        if self.use_bn:
+            raise NotImplementedError("gr_amd: BatchNorm MLPs are not supported")
+        lin = self.linears()
+        for i, m in enumerate(lin):
+            x = ops.linear(x, m.weight.detach(), m.bias.detach(),
+                           act="relu" if i + 1 < len(lin) else "none")
+        return x
+
     def forward(self, x):
         if self.use_bn:
             raise NotImplementedError("gr_amd: BatchNorm encoders are not supported (bn=False in "
@@ -112,6 +126,15 @@ class VectorQuantizer(nn.Module):
         z_q = self.embedding(indices)
         return z_q.view(shape) if shape is not None else z_q
 
+    def init_emb(self, data):
+        """vq.py:39-47 + layers.py:69-82: codebook <- scikit-learn KMeans(n_e, max_iter) centres of the
+        first training batch's latents (host, once; the reference's own call)."""
+        from sklearn.cluster import KMeans
+        centers = KMeans(n_clusters=self.n_e, max_iter=self.kmeans_iters).fit(
+            data.detach().cpu().numpy()).cluster_centers_
+        self.embedding.weight.data.copy_(torch.from_numpy(centers).to(self.embedding.weight.device))
+        self.initted = True
+
 
 class ResidualVectorQuantizer(nn.Module):
     """Module tree of RQ-VAE/models/rq.py:13-30."""
@@ -137,6 +160,33 @@ class ResidualVectorQuantizer(nn.Module):
 
     def codebooks(self):
         return [q.embedding.weight.detach() for q in self.vq_layers]
+
+    def quantize_forward(self, x, use_sk=True, training=False):
+        """rq.py:39-56 with vq.py:63-99 per level: indices from the kernels (one launch per level:
+        the next level's residual depends on this level's assignment, and a level's k-means init
+        on the residual it sees, vq.py:66-67), values and losses under autograd."""
+        losses, idxs = [], []
+        x_q = 0
+        residual = x
+        for q in self.vq_layers:
+            latent = residual.reshape(-1, self.e_dim)
+            if not q.initted and training:
+                q.init_emb(latent.detach())
+            cb = q.embedding.weight.detach()
+            eps = q.sk_epsilon if use_sk else 0.0
+            if eps > 0:
+                idx = ops.rq_quantize_sk(latent.detach(), [cb], [eps], q.sk_iters)[:, 0]
+            else:
+                idx = ops.rq_quantize(latent.detach(), [cb])[:, 0]
+            xq = q.embedding(idx).view(residual.shape)
+            commitment_loss = F.mse_loss(xq.detach(), residual)
+            codebook_loss = F.mse_loss(xq, residual.detach())
+            losses.append(codebook_loss + q.beta * commitment_loss)
+            xq = residual + (xq - residual).detach()
+            residual = residual - xq
+            x_q = x_q + xq
+            idxs.append(idx.view(residual.shape[:-1]))
+        return x_q, torch.stack(losses).mean(), torch.stack(idxs, dim=-1)
 
 
 class RQVAE(nn.Module):
@@ -168,9 +218,29 @@ class RQVAE(nn.Module):
         self.decoder = MLPLayers(layers=self.decode_layer_dims, dropout=dropout_prob, bn=bn)
 
     def forward(self, x, use_sk=True):
-        """Training forward (rqvae.py:60-65) is outside the ported hot path."""
-        raise NotImplementedError("gr_amd RQVAE implements the encode path (get_indices); the "
-                                  "training forward with the decoder is out of scope")
+        """rqvae.py:60-65 -> ``(out, rq_loss, indices)``, differentiable (the RQ-VAE/train.py:113 call;
+        SURVEY §8f row 4).  The codebook assignment of every level — vq.py:69-84: the fp32 distance
+        matrix and its argmin, or the batch-coupled Sinkhorn when ``use_sk`` and ``sk_epsilon > 0``
+        (main.py trains with eps 0.01 at every level) — runs on the gfx950 kernels, on the residual
+        exactly as the reference forms it; the straight-through values, the codebook / commitment
+        losses (vq.py:88-95) and the encoder / decoder MLPs stay under autograd (torch modules,
+        dropout active in train mode).  With grad disabled in eval mode, the encoder and decoder
+        also run on the kernels (``gr_rq_mlp_f32`` / ``gr_linear_f32``)."""
+        fast = not torch.is_grad_enabled() and not self.training
+        z = self.encoder(x) if fast else self.encoder.mlp_layers(x)
+        x_q, rq_loss, indices = self.rq.quantize_forward(z, use_sk, self.training)
+        out = self.decoder.eval_forward(x_q) if fast else self.decoder.mlp_layers(x_q)
+        return out, rq_loss, indices
+
+    def compute_loss(self, out, quant_loss, xs=None):
+        """rqvae.py:73-84: reconstruction (mse or l1, mean) + quant_loss_weight * quant_loss."""
+        if self.loss_type == "mse":
+            loss_recon = F.mse_loss(out, xs, reduction="mean")
+        elif self.loss_type == "l1":
+            loss_recon = F.l1_loss(out, xs, reduction="mean")
+        else:
+            raise ValueError("incompatible loss type")
+        return loss_recon + self.quant_loss_weight * quant_loss, loss_recon
 
     def _check_encode(self, xs, use_sk):
         if self.bn:
