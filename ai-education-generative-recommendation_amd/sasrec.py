@@ -53,10 +53,35 @@ class SASRec(nn.Module):
             raise IndexError(f"sequence length {n} exceeds max_len {self.pos_emb.weight.shape[0]}")
         return ops.SasrecBinding(self)
 
-    @torch.no_grad()
     def forward(self, log_seqs):
-        """model.py:49-96: ``[B, n]`` item ids -> ``[B, n, d]`` final hidden states (eval mode)."""
-        return ops.sasrec_forward(self._binding(log_seqs), log_seqs)
+        """model.py:49-96: ``[B, n]`` item ids -> ``[B, n, d]`` final hidden states.
+
+        Eval mode (or grad disabled): one C-ABI call, ``gr_sasrec_forward_f32``, no autograd graph.
+        Train mode with grad enabled (the SASRec/train.py:131 call): the same blocks as torch modules
+        under autograd, dropout active — the transformer's backward is not a kernel here; the
+        step's scoring, loss and negative sampling are (``ops.sampled_bce_loss``,
+        ``ops.neg_samples``)."""
+        if self.training and torch.is_grad_enabled():
+            return self._forward_autograd(log_seqs)
+        with torch.no_grad():
+            return ops.sasrec_forward(self._binding(log_seqs), log_seqs)
+
+    def _forward_autograd(self, log_seqs):
+        """model.py:58-96 as module calls: E[s] + P[0..n), then per block a pre-LN causal
+        self-attention residual and a pre-LN FFN residual, then the last LayerNorm.  The reference's
+        W_Q / W_K / W_V outputs (model.py:63-65) feed nothing and are not computed."""
+        n = log_seqs.shape[1]
+        if n > self.pos_emb.weight.shape[0]:
+            raise IndexError(f"sequence length {n} exceeds max_len {self.pos_emb.weight.shape[0]}")
+        pos = torch.arange(n, device=log_seqs.device)
+        x = self.item_emb(log_seqs) + self.pos_emb(pos).unsqueeze(0)
+        causal = torch.ones((n, n), dtype=torch.bool, device=log_seqs.device).triu(1)
+        for ln_a, mha, ln_f, ffn in zip(self.attention_layernorms, self.attention_layers,
+                                        self.forward_layernorms, self.forward_layers):
+            h = ln_a(x)
+            x = x + mha(h, h, h, attn_mask=causal)[0]
+            x = x + ffn(ln_f(x))
+        return self.last_layernorm(x)
 
     @torch.no_grad()
     def last_hidden(self, log_seqs):

@@ -10,7 +10,9 @@ last n of seq[1:], both left-padded with 0); negatives follow get_neg_samples (t
 seeded RandomState.  The loss block itself (train.py:134-167) is inline in the reference's train()
 (its module imports h5py, absent here), so it runs from the oracle's verbatim restatement
 (oracle/sasrec_oracle.train_loss).  Stored: features, item table, targets, negatives, batch loss,
-valid count and the gradients of ``loss = batch_loss / valid`` w.r.t. features and table.
+valid count and the gradients of ``loss = batch_loss / valid`` w.r.t. features and table; the model's
+state dict and the gradient of every parameter for the whole step (forward under autograd, loss,
+backward through the reference model).
 """
 import json
 import os
@@ -64,12 +66,20 @@ def make(SASRec, name, item_num, d, n, B, J, seed, mlp=64, heads=1, blocks=2, ep
         feats = model(torch.from_numpy(seqs)).detach()
     table = model.item_emb.weight.detach().clone()
     bl, valid, gf, gw = sasrec_oracle.train_loss_grads(feats, table, tg, negs, eps)
+    sd = {k: v.detach().clone() for k, v in model.state_dict().items()}
+    # the whole train.py:131-167 step through the reference model: forward (autograd), loss, backward
+    model.zero_grad()
+    f2 = model.forward(torch.from_numpy(seqs))
+    bl2, valid2 = sasrec_oracle.train_loss(f2, model.item_emb.weight, tg, negs, eps)
+    (bl2 / valid2.item()).backward()
+    pgrads = {f"pgrad/{k}": p.grad.detach().numpy() for k, p in model.named_parameters() if p.grad is not None}
     meta = dict(name=name, item_num=item_num, d=d, n=n, B=B, num_neg=J, eps=eps, seed=seed,
-                torch=torch.__version__)
+                params=params, torch=torch.__version__)
     np.savez_compressed(os.path.join(HERE, f"{name}.npz"), meta=json.dumps(meta),
                         feats=feats.numpy(), table=table.numpy(), targets=tgts, negs=negs.numpy(),
                         seqs=seqs, batch_loss=np.float32(bl.item()), valid=np.float32(valid.item()),
-                        dfeats=gf.numpy(), dtable=gw.numpy())
+                        dfeats=gf.numpy(), dtable=gw.numpy(), **{f"sd/{k}": v.numpy() for k, v in sd.items()},
+                        **pgrads)
     print(name, "batch_loss", bl.item(), "valid", valid.item())
 
 

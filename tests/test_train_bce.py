@@ -192,3 +192,40 @@ def test_neg_samples_population_too_small(dev):
         ops.CHECK = old
     with pytest.raises(RuntimeError):
         ops.neg_samples(seq, 2, 3)                           # num_neg > item_num
+
+
+# ------------------------------------------------------------------ the whole train.py:131-167 step
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", FIXTURES)
+def test_full_training_step_matches_reference(name, dev):
+    """Drop-in SASRec in train mode (forward under autograd, dropout 0 for determinism) +
+    ops.sampled_bce_loss + backward: every parameter gradient equals the reference model's
+    (make_golden_train.py) within 1e-5 of its tensor's largest magnitude."""
+    from gr_amd import SASRec, ops
+    sd, out, meta = gl.load(name)
+    p = dict(meta["params"], device=str(dev))
+    m = SASRec(meta["item_num"], p)
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
+    m = m.to(dev).train()
+    seqs = torch.from_numpy(out["seqs"]).to(dev)
+    f = m(seqs)
+    assert f.requires_grad
+    assert _scaled_err(f, out["feats"]) <= TOL
+    bl, valid = ops.sampled_bce_loss(f, m.item_emb.weight, torch.from_numpy(out["targets"]).to(dev),
+                                     torch.from_numpy(out["negs"]).to(dev), meta["eps"])
+    (bl / valid.item()).backward()
+    worst = 0.0
+    for k, prm in m.named_parameters():
+        key = f"pgrad/{k}"
+        if key not in out:
+            assert prm.grad is None or torch.count_nonzero(prm.grad) == 0, k
+            continue
+        err = _scaled_err(prm.grad, out[key])
+        worst = max(worst, err)
+        assert err <= TOL, (k, err)
+    print(f"\n{name}: worst scaled parameter-grad error {worst:.3g}")
+    # eval mode afterwards runs the kernels again, on the same weights
+    m.eval()
+    with torch.no_grad():
+        assert _scaled_err(m(seqs), out["feats"]) <= TOL
