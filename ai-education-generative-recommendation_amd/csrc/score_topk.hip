@@ -269,7 +269,10 @@ static int cu_count() {
 }
 
 // Launch plan: user blocks of 256, one workgroup per CU per pass.  The sample stride s trades the
-// sample pass's extra matrix work (1/s) against pass 2's insertions (about k*s per user); below
+// sample pass's extra matrix work (1/s) against pass 2's insertions (about k*s per user).  s = 16
+// at every catalog length: at 125k rows (one shard of C5 over 8 GPUs) strides 2..32 measured
+// 3 -> 254 us, 8 -> 234, 16 -> 232, 32 -> 231 (profiles/r01o_ab_topk_stride_125k.txt), at 1M
+// rows 1208 us for all of them — the insertions stay cheap while the sample pass shrinks.  Below
 // 4 chunks per slice the catalog is too short to pay for a second launch.
 struct TopkPlan {
   int64_t ublocks, chunks;
@@ -304,8 +307,7 @@ static TopkPlan topk_plan(int64_t B, int64_t rows, int k, int d) {
   p.s = 0;
   p.v1 = p.slices1 = 0;
   if (per_slice >= 4 && option("topk_sample") != 0) {
-    const int64_t s = per_slice / 4;
-    p.s = (int)(s < 2 ? 2 : s > 16 ? 16 : s);
+    p.s = 16;
     p.v1 = (p.chunks + p.s - 1) / p.s;
     p.slices1 = slices_for(p.ublocks, p.v1, d);
   }
