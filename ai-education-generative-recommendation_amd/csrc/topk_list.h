@@ -105,7 +105,29 @@ __global__ __launch_bounds__(256) void topk_merge_kernel(int64_t row_stride, int
   const int64_t b = blockIdx.x;
   TopList<KMAX> tl;
   tl.init();
-  for (int64_t q = threadIdx.x; q < n; q += 256) tl.push(cv[b * row_stride + q], ci[b * row_stride + q]);
+  // Candidates in batches of MB loads issued together, then pushed in the same order (q = tid,
+  // tid + 256, ...): a load per push would wait out one memory latency per candidate, because
+  // the compiler does not move loads across push's early return.  Slots past n push (-inf, max),
+  // which no list accepts.
+  constexpr int MB = 8;
+  const float* rv = cv + b * row_stride;
+  const int64_t* ri = ci + b * row_stride;
+  for (int64_t q0 = threadIdx.x; q0 < n; q0 += 256 * MB) {
+    float v[MB];
+    int64_t id[MB];
+#pragma unroll
+    for (int u = 0; u < MB; ++u) {
+      const int64_t q = q0 + 256 * u;
+      const int64_t qc = q < n ? q : q0;
+      v[u] = rv[qc];
+      id[u] = ri[qc];
+    }
+#pragma unroll
+    for (int u = 0; u < MB; ++u) {
+      const bool ok = q0 + 256 * u < n;
+      tl.push(ok ? v[u] : -__builtin_inff(), ok ? id[u] : INT64_MAX);
+    }
+  }
   tl.block_select(k, [&](int q, float v, int64_t i) {
     vals[b * k + q] = v;
     ids[b * k + q] = i == INT64_MAX ? -1 : i + id_offset;
