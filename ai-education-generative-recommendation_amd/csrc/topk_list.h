@@ -10,6 +10,16 @@ __device__ __forceinline__ bool better(float va, int64_t ia, float vb, int64_t i
   return va > vb || (va == vb && ia < ib);
 }
 
+// Order-preserving key of (value, id) for block_select: larger key = better entry.  -0 and +0
+// share a key (better() compares them equal); ids are -1 .. 2^32 - 3 (columns) or INT64_MAX (empty
+// slot, below every real id).  NaN never reaches a list.
+__device__ __forceinline__ uint64_t sel_key(float v, int64_t id) {
+  uint32_t u = __float_as_uint(v == 0.f ? 0.f : v);
+  u = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+  const uint32_t lo = id == INT64_MAX ? 0u : 0xFFFFFFFEu - (uint32_t)(id + 1);
+  return ((uint64_t)u << 32) | lo;
+}
+
 // Per-thread sorted candidate list of KMAX entries (best first); NaN never enters.
 template <int KMAX>
 struct TopList {
@@ -36,61 +46,50 @@ struct TopList {
       }
     }
   }
-  // k rounds of a block-wide arg-best over the heads of the per-thread lists; emit(q, v, i).
-  // Per round: a 64-lane shuffle arg-best in each wave, one barrier, then every thread picks the
-  // best of the 4 wave winners (slots double-buffered by round parity, so one barrier suffices).
-  // Equal (value, id) pairs resolve to the lower thread: the order is deterministic.
+  // k rounds of a block-wide arg-best over the heads of the per-thread lists; emit(q, v, i) is
+  // called by the winning thread with its own entry.  The (value desc, id asc) order is one
+  // unsigned 64-bit key (sel_key), so a round is a 6-step 64-bit max in each wave, one barrier,
+  // the best of the 4 wave maxima (slots double-buffered by round parity), and a ballot for the
+  // lowest lane holding it: equal (value, id) pairs resolve to the lower thread, as before.
   template <typename E>
   __device__ void block_select(int k, E&& emit) {
-    __shared__ float sv[2][4];
-    __shared__ int64_t si[2][4];
-    __shared__ int sw[2][4];
+    __shared__ uint64_t sm[2][4];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     int head = 0;
     for (int q = 0; q < k; ++q) {
-      float bv = -__builtin_inff();
-      int64_t bi = INT64_MAX;
+      float hv = -__builtin_inff();
+      int64_t hi = INT64_MAX;
 #pragma unroll
       for (int u = 0; u < KMAX; ++u)
         if (u == head) {
-          bv = v[u];
-          bi = i[u];
+          hv = v[u];
+          hi = i[u];
         }
-      int bt = threadIdx.x;
+      const uint64_t key = sel_key(hv, hi);
+      uint64_t m = key;
 #pragma unroll
       for (int o = 32; o > 0; o >>= 1) {
-        const float ov = __shfl_xor(bv, o);
-        const int64_t oi = __shfl_xor(bi, o);
-        const int ot = __shfl_xor(bt, o);
-        if (better(ov, oi, bv, bi) || (ov == bv && oi == bi && ot < bt)) {
-          bv = ov;
-          bi = oi;
-          bt = ot;
-        }
+        const uint64_t om = __shfl_xor(m, o);
+        m = om > m ? om : m;
       }
       const int par = q & 1;
-      if (lane == 0) {
-        sv[par][wv] = bv;
-        si[par][wv] = bi;
-        sw[par][wv] = bt;
-      }
+      if (lane == 0) sm[par][wv] = m;
       __syncthreads();
-      bv = sv[par][0];
-      bi = si[par][0];
-      bt = sw[par][0];
+      uint64_t M = sm[par][0];
+      int wf = 0;
 #pragma unroll
-      for (int w = 1; w < 4; ++w) {
-        const float ov = sv[par][w];
-        const int64_t oi = si[par][w];
-        const int ot = sw[par][w];
-        if (better(ov, oi, bv, bi) || (ov == bv && oi == bi && ot < bt)) {
-          bv = ov;
-          bi = oi;
-          bt = ot;
+      for (int w = 1; w < 4; ++w)
+        if (sm[par][w] > M) {   // strict: the first wave holding the maximum
+          M = sm[par][w];
+          wf = w;
+        }
+      if (wv == wf) {
+        const uint64_t bal = __ballot(key == M);
+        if (lane == __ffsll((unsigned long long)bal) - 1) {
+          emit(q, hv, hi);
+          ++head;
         }
       }
-      if (threadIdx.x == 0) emit(q, bv, bi);
-      if (threadIdx.x == bt) ++head;
     }
   }
 };
