@@ -188,3 +188,35 @@ def test_full_size_c2_properties(dev, rq_path):
     diff = (a[sample.to(dev)].cpu().numpy() != ref.numpy()).any(1)
     tie = near_tie_rows({"dbest": dbest.numpy(), "gap": gaps.numpy(), "znorm": (zs ** 2).sum(1).numpy()})
     assert not (diff & ~tie).any()
+
+
+def test_full_size_c4_properties(dev, rq_path):
+    """Config 4 size (10M items, 4x1024 codebooks, 30.7 GB of input in HBM): the input spans
+    7.68e9 floats, so rows past 2^31 elements exercise 64-bit addressing.  Range, determinism, and
+    agreement with the oracle on a strided sample plus the last 64 rows (near-ties excepted)."""
+    from gr_amd import synth
+    n = 10_000_000
+    m = synth.rqvae_model(4, 1024, dev, seed=4)
+    x = synth.items(n, 4000, dev)
+    a = m.get_indices(x)
+    assert a.shape == (n, 4) and a.dtype == torch.int64
+    assert int(a.min()) >= 0 and int(a.max()) < 1024
+    tail = slice(n - 4096, n)
+    # the same rows re-encoded as their own batch (offset 0): only batch-size-dependent launch
+    # plans may differ, and those only on near-ties
+    assert (m.get_indices(x[tail]) != a[tail]).any(1).sum().item() <= 4
+    sample = torch.cat([torch.arange(0, n, 5003), torch.arange(n - 64, n)])
+    lin = m.encoder.linears()
+    ws = [l.weight.detach().cpu() for l in lin]
+    bs = [l.bias.detach().cpu() for l in lin]
+    cbs = [q.cpu() for q in m.rq.codebooks()]
+    xs = x[sample.to(dev)].cpu()
+    del x
+    zs = rq_oracle.mlp_encode(xs, ws, bs)
+    ref, res, gaps = rq_oracle.rq_quantize(zs, cbs, return_detail=True)
+    dbest = torch.stack([rq_oracle.vq_level(r, c)[2].min(1).values for r, c in zip(res, cbs)], -1)
+    diff = (a[sample.to(dev)].cpu().numpy() != ref.numpy()).any(1)
+    tie = near_tie_rows({"dbest": dbest.numpy(), "gap": gaps.numpy(), "znorm": (zs ** 2).sum(1).numpy()})
+    print(f"C4 sample {len(sample)} rows: {int(diff.sum())} differ, all certified near-ties: "
+          f"{not (diff & ~tie).any()}")
+    assert not (diff & ~tie).any()
