@@ -50,7 +50,8 @@ def _check(h, t, k, id_offset=0, mask_col0=True, seed=0):
 @pytest.mark.parametrize("B,d,rows,k", [(1, 64, 70, 10), (300, 64, 100001, 10), (64, 128, 5000, 16),
                                         (257, 32, 1000, 1), (70, 64, 64, 10), (5, 128, 7, 10),
                                         (513, 128, 20011, 10), (33, 32, 1, 3), (512, 128, 300007, 10),
-                                        (100, 32, 150001, 4), (40, 64, 262145, 16)])
+                                        (100, 32, 150001, 4), (40, 64, 262145, 16),
+                                        (512, 128, 1000001, 10)])   # C5 full size: 512 users x 1M-item catalog
 def test_score_topk_random(B, d, rows, k, dev):
     g = torch.Generator().manual_seed(B * 7 + d + rows)
     h = torch.randn(B, d, generator=g).to(dev)
