@@ -34,6 +34,9 @@ static std::atomic<int64_t> g_score_ubmajor{1};
 // stores, two workgroups per CU, 2: direct when the logits rows are 128-B line aligned, else the
 // ring).  Same results.
 static std::atomic<int64_t> g_score_impl{2};
+// topk_wg_per_cu (0: the launch plan's own rule; 1..4: catalog slices sized for that many
+// workgroups per CU).  Same results; A/B timing.
+static std::atomic<int64_t> g_topk_wg_per_cu{0};
 
 int64_t option(const char* name) {
   if (!strcmp(name, "rq_fused")) return g_rq_fused.load();
@@ -44,6 +47,7 @@ int64_t option(const char* name) {
   if (!strcmp(name, "score_flags")) return g_score_flags.load();
   if (!strcmp(name, "score_ubmajor")) return g_score_ubmajor.load();
   if (!strcmp(name, "score_impl")) return g_score_impl.load();
+  if (!strcmp(name, "topk_wg_per_cu")) return g_topk_wg_per_cu.load();
   return -1;
 }
 }  // namespace gr
@@ -59,6 +63,7 @@ extern "C" int gr_set_option(const char* name, int64_t value) {
   if (!strcmp(name, "score_flags") && (value == 0 || value == 1)) { gr::g_score_flags = value; return GR_OK; }
   if (!strcmp(name, "score_ubmajor") && (value == 0 || value == 1)) { gr::g_score_ubmajor = value; return GR_OK; }
   if (!strcmp(name, "score_impl") && value >= 0 && value <= 2) { gr::g_score_impl = value; return GR_OK; }
+  if (!strcmp(name, "topk_wg_per_cu") && value >= 0 && value <= 4) { gr::g_topk_wg_per_cu = value; return GR_OK; }
   return gr::fail(GR_ERR_ARG, std::string("gr_set_option: unknown option or value: ") + name);
 }
 

@@ -284,7 +284,9 @@ struct TopkPlan {
 };
 
 static int64_t slices_for(int64_t ublocks, int64_t vchunks, int d) {
-  const int per_cu = (d == 128 ? TkUT<128>::value : d == 64 ? TkUT<64>::value : TkUT<32>::value) == 1 ? 2 : 1;
+  const int64_t forced = option("topk_wg_per_cu");
+  const int per_cu = forced > 0 ? (int)forced
+                   : (d == 128 ? TkUT<128>::value : d == 64 ? TkUT<64>::value : TkUT<32>::value) == 1 ? 2 : 1;
   int64_t sl = (per_cu * cu_count() + ublocks - 1) / ublocks;
   if (sl > vchunks) sl = vchunks;
   return sl < 1 ? 1 : sl;

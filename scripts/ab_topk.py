@@ -43,6 +43,10 @@ for B, rows, d in SHAPES:
         _lib.set_option("topk_sample", smp)
         res[f"topk sample{smp}"] = ms(lambda: ops.score_topk(h, t, 10, thresholds=thr))
     _lib.set_option("topk_sample", 1)
+    for wpc in (1, 2, 3, 4):
+        _lib.set_option("topk_wg_per_cu", wpc)
+        res[f"topk wg/cu {wpc}"] = ms(lambda: ops.score_topk(h, t, 10, thresholds=thr))
+    _lib.set_option("topk_wg_per_cu", 0)
     _lib.set_option("topk_ablate", 1)
     res["topk no-topk"] = ms(lambda: ops.score_topk(h, t, 10, thresholds=thr))
     _lib.set_option("topk_ablate", 0)
