@@ -51,11 +51,12 @@ __global__ __launch_bounds__(256) void neg_sample_kernel(const int64_t* __restri
     taken += __popcll(m);
     __builtin_amdgcn_wave_barrier();   // LDS writes of this round precede the next round's reads
   }
-  if (taken < J) {
-    if (lane == 0 && err) *err = 1;
-    return;
-  }
-  for (int q = lane; q < J; q += 64) out[row * J + q] = tk[q];
+  // A row that cannot be filled (population < J) gets -1 ids and raises the sticky error code 2
+  // (ops.check_errors -> ValueError, numpy's choice(replace=False) error); the fused BCE op flags
+  // a -1 id as out of range, so it never reads row 0 in its place unnoticed.
+  const bool full = taken >= J;
+  if (!full && lane == 0 && err) *err = 2;
+  for (int q = lane; q < J; q += 64) out[row * J + q] = full ? tk[q] : -1;
 }
 
 }  // namespace gr

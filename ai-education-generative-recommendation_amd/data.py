@@ -10,8 +10,9 @@ exactly the tensors the reference's datasets hand to the models.
 
 Sources: h5 (the reference's format; needs ``h5py``, which is optional and imported lazily),
 ``.npz`` with the same dataset names, plain ``.npy`` embeddings, or an interaction CSV such as
-stu-major/interaction_records.csv (``student_id``, ``class_id`` columns in file order; rows without
-a student are skipped, Baseline/data_process.py:22-27 orders them by (student_id, id)).
+stu-major/interaction_records.csv (``student_id``, ``class_id``; rows without a student are
+skipped and the rest ordered by (student_id, id) exactly as Baseline/data_process.py:22-27's
+``ORDER BY student_id, id`` builds the reference's h5 file, so users come out in that order).
 Batches are built on the host as whole tensors (no per-item Python ``__getitem__`` calls) and moved
 to the GPU by the caller, as in SASRec/evaluate.py:21-23.
 """
@@ -50,14 +51,22 @@ def read_interactions(path):
             return [(u, [int(i) for i in row[:n]]) for u, row, n in zip(users, z["item_id_list"], lens)]
         raise KeyError(f"{path}: expected user_id / item_id_list / item_len arrays")
     if ext == ".csv":
-        out = []
+        rows = []
         with open(path, encoding="utf-8-sig", newline="") as f:
-            for row in csv.DictReader(f):
+            for k, row in enumerate(csv.DictReader(f)):
                 s = (row.get("student_id") or "").strip()
                 if s:
-                    out.append((s, [int(row["class_id"])]))
-        return out
+                    rid = int(row["id"]) if (row.get("id") or "").strip() else k
+                    rows.append((s, rid, int(row["class_id"])))
+        return [(s, [c]) for s, _, c in reference_order(rows)]
     raise ValueError(f"unsupported interaction file: {path}")
+
+
+def reference_order(rows):
+    """Stable sort of (student_id, id, ...) interaction rows by ``ORDER BY student_id, id``
+    (Baseline/data_process.py:22-27): SQLite compares TEXT student ids bytewise (BINARY collation on
+    UTF-8), then the integer row id."""
+    return sorted(rows, key=lambda r: (str(r[0]).encode("utf-8"), int(r[1])))
 
 
 class SASRecDataset:

@@ -46,11 +46,15 @@ def hr_ndcg(ranks, top_k):
     return float(np.mean(ht)), float(np.mean(ndcg))
 
 
-def multi_k(ranks, topk_list):
-    """SASRec/train.py:33-56: {k: HR@k}, {k: NDCG@k} for every k of ``topk_list``."""
+def multi_k(ranks, topk_list, targets=None):
+    """SASRec/train.py:33-56: {k: HR@k}, {k: NDCG@k} for every k of ``topk_list``.  With ``targets``
+    the users whose target is 0 are dropped first (train.py:42-45 ``valid_mask``)."""
     hits = {k: [] for k in topk_list}
     ndcgs = {k: [] for k in topk_list}
-    for r in np.asarray(ranks):
+    ranks = np.asarray(ranks)
+    if targets is not None:
+        ranks = ranks[np.asarray(targets) != 0]
+    for r in ranks:
         for k in topk_list:
             hits[k].append(1 if r <= k else 0)
             ndcgs[k].append(1 / np.log2(r + 1) if r <= k else 0)
@@ -72,21 +76,45 @@ def evaluate(params, dataset=None, model=None, materialize=False, save_csv=True)
         model = SASRec(dataset.item_num, params).to(device)
         model.load_state_dict(torch.load(params["ckpt"], map_location=device, weights_only=True))
     model.eval()
-    ranks = []
+    ranks, tgts = [], []
     for input_ids, target in dataset.batches(params.get("eval_batch_size", 128)):
         ranks.append(rank_batch(model, input_ids.to(device), target.to(device), materialize))
+        tgts.append(target)
+    if device.type == "cuda":
+        ops.check_errors(device)     # out-of-range ids flagged by the kernels (IndexError)
     ranks = torch.cat(ranks).cpu().numpy() if ranks else np.zeros(0, np.int64)
+    tgts = torch.cat(tgts).numpy() if tgts else np.zeros(0, np.int64)
     top_k = params.get("top_k", 10)
     hit, ndcg = hr_ndcg(ranks, top_k)
     results = {f"Hit@{top_k}": hit, f"NDCG@{top_k}": ndcg}
-    if params.get("topk_list"):
-        hk, nk = multi_k(ranks, params["topk_list"])
+    if params.get("topk_list"):        # train.py:33-56 semantics: target-0 users dropped
+        hk, nk = multi_k(ranks, params["topk_list"], tgts)
         for k in params["topk_list"]:
             results.setdefault(f"Hit@{k}", hk[k])
             results.setdefault(f"NDCG@{k}", nk[k])
     if save_csv and params.get("params_path"):
         save_results_to_csv(params, results)
     return results, ranks
+
+
+@torch.no_grad()
+def train_evaluate(model, test_loader, params, device):
+    """SASRec/train.py:33-56 ``evaluate(model, test_loader, params, device)``: users with target 0
+    dropped (``valid_mask``, :42-45), strict ranks from the fused kernels, HR@k / NDCG@k for every
+    k of ``params['topk_list']``.  Leaves the model in train mode like the reference (:53)."""
+    model.eval()
+    ranks = []
+    for input_ids, target_item in test_loader:
+        input_ids = input_ids.to(device)
+        target_item = target_item.to(device)
+        valid = target_item != 0
+        if not bool(valid.any()):
+            continue
+        ranks.append(rank_batch(model, input_ids[valid], target_item[valid]))
+    ops.check_errors(torch.device(device))
+    model.train()
+    r = torch.cat(ranks).cpu().numpy() if ranks else np.zeros(0, np.int64)
+    return multi_k(r, params["topk_list"])
 
 
 def save_results_to_csv(params, results):

@@ -11,9 +11,38 @@ import torch
 
 from . import _lib as L
 
-# GR_AMD_CHECK=1 synchronises after SASRec calls and raises on out-of-range item ids (the
-# reference raises IndexError there; the kernels only flag it to stay asynchronous).
+# Input errors the kernels detect (an item id outside the table, a row whose negatives cannot be
+# drawn) are OR-ed into a per-device sticky error word instead of synchronising the stream.
+# ``check_errors()`` synchronises and raises (evaluate() calls it once per evaluation; a training
+# loop calls it once per epoch).  GR_AMD_CHECK=1 checks after every call instead.
 CHECK = os.environ.get("GR_AMD_CHECK", "0") == "1"
+ERR_BAD_ID = 1        # item id outside [0, rows): the reference raises IndexError (nn.Embedding / gather)
+ERR_NEG_POPULATION = 2  # get_neg_samples population smaller than num_neg: numpy raises ValueError
+_ERR = {}
+
+
+def err_flag(device):
+    """The device's sticky error word (int32, 0 = clean); kernels only ever write a nonzero code."""
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    t = _ERR.get(idx)
+    if t is None:
+        t = torch.zeros(1, dtype=torch.int32, device=torch.device("cuda", idx))
+        _ERR[idx] = t
+    return t
+
+
+def check_errors(device=None):
+    """Synchronise ``device`` and raise the error the kernels flagged since the last check (then
+    clear it): IndexError for out-of-range item ids, ValueError for an unfillable negative row."""
+    devs = [device] if device is not None else [torch.device("cuda", i) for i in list(_ERR)]
+    for d in devs:
+        t = err_flag(torch.device(d))
+        code = int(t.item())              # .item() synchronises the stream the flag was written on
+        if code:
+            t.zero_()
+            if code == ERR_NEG_POPULATION:
+                raise ValueError("Cannot take a larger sample than population when 'replace=False'")
+            raise IndexError("index out of range in self (item id outside the embedding table)")
 
 
 def linear(x, weight, bias=None, act="none", residual=None, out=None):
@@ -108,7 +137,7 @@ def score_pairs(h, table, ids, mask_col0=True):
     ids = ids.reshape(-1).to(torch.int64).contiguous()
     B, d = h.shape
     out = torch.empty(B, dtype=torch.float32, device=h.device)
-    err = torch.zeros(1, dtype=torch.int32, device=h.device)
+    err = err_flag(h.device)
     with torch.cuda.device(h.device):
         L.check(L.lib().gr_score_pairs_f32(L.ptr(h), B, d, L.ptr(t), t.shape[0], L.ptr(ids),
                                            1 if mask_col0 else 0, L.ptr(out), L.ptr(err),
@@ -190,38 +219,86 @@ def rq_quantize(z, codebooks, with_gap=False):
     return (idx, best, gap) if with_gap else idx
 
 
-def rq_encode(x, weights, biases, codebooks, with_gap=False, with_z=False):
+class RqBinding:
+    """The encoder weights / biases and codebooks of one RQ-VAE as the ctypes arrays
+    ``gr_rq_encode_f32`` takes (device pointers, dims, K per level), built once per parameter set
+    (:func:`rq_binding`) so a ``get_indices`` call at the reference's batch 64 (RQ-VAE/infer.py:84-95)
+    pays only the launch."""
+
+    def __init__(self, weights, biases, codebooks):
+        weights, biases, codebooks = ([t.detach() for t in ts] for ts in (weights, biases, codebooks))
+        self.ws = [L.as_f32(w) for w in weights]
+        self.bs = [L.as_f32(b) for b in biases]
+        self.cbs = [L.as_f32(c) for c in codebooks]
+        L.require_gpu(*self.ws, *self.cbs)
+        self.direct = all(a.data_ptr() == b.data_ptr() for a, b in
+                          zip(self.ws + self.bs + self.cbs, list(weights) + list(biases) + list(codebooks)))
+        self.in_dim = self.ws[0].shape[1]
+        self.dims = [self.in_dim] + [w.shape[0] for w in self.ws]
+        for i, w in enumerate(self.ws):
+            if w.shape[1] != self.dims[i]:
+                raise RuntimeError(f"rq_encode: Linear {i} expects {w.shape[1]} inputs, got {self.dims[i]}")
+        self.Ks = [c.shape[0] for c in self.cbs]
+        self.dims_c, self.ks_c = L.i32_array(self.dims), L.i32_array(self.Ks)
+        self.w_arr, self.b_arr, self.c_arr = L.ptr_array(self.ws), L.ptr_array(self.bs), L.ptr_array(self.cbs)
+        self.device = self.ws[0].device
+        self._ws_bytes = {}
+
+    def workspace_bytes(self, n):
+        nb = self._ws_bytes.get(n)
+        if nb is None:
+            nb = L.lib().gr_rq_encode_workspace_bytes(n, len(self.ws), self.dims_c, len(self.cbs), self.ks_c)
+            if nb == 0:
+                raise RuntimeError("rq_encode: bad encoder description")
+            if len(self._ws_bytes) < 64:
+                self._ws_bytes[n] = nb
+        return nb
+
+
+def rq_binding(owner, weights_fn):
+    """Cached :class:`RqBinding` on ``owner`` (an RQVAE): rebuilt when any parameter's storage moved
+    (``.to()``, ``param.data = ...``); in-place updates (``load_state_dict``, optimiser steps) are
+    seen through the same pointers.  ``weights_fn() -> (weights, biases, codebooks)``, the LIVE
+    parameters (not detached copies: their pointers are the cache key)."""
+    c = owner.__dict__.get("_gr_rq_binding")
+    if c is not None:
+        tensors, key, b = c
+        if b.direct and tuple(t.data_ptr() for t in tensors) == key:
+            return b
+    ws, bs, cbs = weights_fn()
+    tensors = list(ws) + list(bs) + list(cbs)
+    b = RqBinding(ws, bs, cbs)
+    owner.__dict__["_gr_rq_binding"] = (tensors, tuple(t.data_ptr() for t in tensors), b)
+    return b
+
+
+def rq_encode(x, weights=None, biases=None, codebooks=None, with_gap=False, with_z=False, binding=None):
     """RQVAE.get_indices(xs, use_sk=False): encoder MLP + residual quantization (rqvae.py:67-71).
 
     Returns ``idx`` [n, L] int64, plus ``best`` and ``gap`` [n, L] (best distance and second-best
-    minus best) and the encoder output ``z`` when requested.
+    minus best) and the encoder output ``z`` when requested.  ``binding`` (an :class:`RqBinding`)
+    replaces ``weights`` / ``biases`` / ``codebooks``.
     """
-    L.require_gpu(x, *weights, *codebooks)
+    b = binding if binding is not None else RqBinding(weights, biases, codebooks)
+    L.require_gpu(x)
     x2 = L.as_f32(x)
+    if x2.dim() != 2 or x2.shape[1] != b.in_dim:
+        raise RuntimeError(f"rq_encode: expected [n, {b.in_dim}] inputs, got {tuple(x2.shape)}")
+    if x2.device != b.device:
+        raise RuntimeError(f"rq_encode: inputs on {x2.device}, parameters on {b.device}")
     n = x2.shape[0]
-    ws = [L.as_f32(w) for w in weights]
-    bs = [L.as_f32(b) for b in biases]
-    cbs = [L.as_f32(c) for c in codebooks]
-    dims = [x2.shape[1]] + [w.shape[0] for w in ws]
-    for i, w in enumerate(ws):
-        if w.shape[1] != dims[i]:
-            raise RuntimeError(f"rq_encode: Linear {i} expects {w.shape[1]} inputs, got {dims[i]}")
-    Ks = [c.shape[0] for c in cbs]
-    dev = x.device
-    lib = L.lib()
-    dims_c, ks_c = L.i32_array(dims), L.i32_array(Ks)
-    nbytes = lib.gr_rq_encode_workspace_bytes(n, len(ws), dims_c, len(cbs), ks_c)
-    if nbytes == 0:
-        raise RuntimeError("rq_encode: bad encoder description")
+    dev = x2.device
+    nbytes = b.workspace_bytes(n)
     wsp = L.workspace(nbytes, dev)
-    idx = torch.empty((n, len(cbs)), dtype=torch.int64, device=dev)
-    gap = torch.empty((n, len(cbs)), dtype=torch.float32, device=dev) if with_gap else None
-    best = torch.empty((n, len(cbs)), dtype=torch.float32, device=dev) if with_gap else None
-    z = torch.empty((n, dims[-1]), dtype=torch.float32, device=dev) if with_z else None
+    nl = len(b.cbs)
+    idx = torch.empty((n, nl), dtype=torch.int64, device=dev)
+    gap = torch.empty((n, nl), dtype=torch.float32, device=dev) if with_gap else None
+    best = torch.empty((n, nl), dtype=torch.float32, device=dev) if with_gap else None
+    z = torch.empty((n, b.dims[-1]), dtype=torch.float32, device=dev) if with_z else None
     with torch.cuda.device(dev):
-        L.check(lib.gr_rq_encode_f32(L.ptr(x2), n, len(ws), dims_c, L.ptr_array(ws), L.ptr_array(bs),
-                                     len(cbs), ks_c, L.ptr_array(cbs), L.ptr(idx), L.ptr(best), L.ptr(gap),
-                                     L.ptr(z), L.ptr(wsp), nbytes, L.stream_of(dev)),
+        L.check(L.lib().gr_rq_encode_f32(L.ptr(x2), n, len(b.ws), b.dims_c, b.w_arr, b.b_arr,
+                                         nl, b.ks_c, b.c_arr, L.ptr(idx), L.ptr(best), L.ptr(gap),
+                                         L.ptr(z), L.ptr(wsp), nbytes, L.stream_of(dev)),
                 "gr_rq_encode_f32")
     out = [idx]
     if with_gap:
@@ -293,11 +370,13 @@ def rq_quantize_sk(z, codebooks, sk_eps, sk_iters, group_sizes=None):
 class SasrecBinding:
     """Device-pointer view of a SASRec module's parameters (``gr_sasrec_params``).
 
-    Rebuilt on every call (cheap), so in-place weight updates and ``load_state_dict`` are seen.
+    Built once per parameter set and cached on the module (:func:`sasrec_binding`); the pointers
+    are the parameters' own storage, so in-place weight updates and ``load_state_dict`` are seen.
     """
 
     def __init__(self, model):
         self.keep = []
+        self.direct = True           # every pointer is the parameter's own storage (no copies)
         f = self._f
         nb = model.num_blocks
         p = L.SasrecParams()
@@ -327,9 +406,10 @@ class SasrecBinding:
 
     def _f(self, t):
         L.require_gpu(t)
-        t = L.as_f32(t.detach())
-        self.keep.append(t)
-        return t.data_ptr()
+        t2 = L.as_f32(t.detach())
+        self.direct &= t2.data_ptr() == t.data_ptr()
+        self.keep.append(t2)
+        return t2.data_ptr()
 
     def _arr(self, ts):
         a = (ctypes.c_void_p * max(1, len(ts)))(*[self._f(t) for t in ts])
@@ -338,6 +418,23 @@ class SasrecBinding:
 
     def workspace_bytes(self, B, n):
         return L.lib().gr_sasrec_workspace_bytes(ctypes.byref(self.p), B, n)
+
+
+def sasrec_binding(model):
+    """Cached :class:`SasrecBinding` of ``model``: reused while every parameter's storage pointer
+    is unchanged (checked per call, ~5 us for SASRec's 34 tensors); rebuilt after ``.to()`` or a
+    ``param.data = ...`` swap, and on every call when a parameter is not contiguous fp32 (then the
+    binding holds copies).  This is what makes a ``predict`` at the reference's eval batch of 128
+    (SASRec/evaluate.py:13, 26) cost one launch on the host."""
+    c = model.__dict__.get("_gr_sas_binding")
+    if c is not None:
+        params, key, b = c
+        if b.direct and tuple(q.data_ptr() for q in params) == key:
+            return b
+    params = list(model.parameters())
+    b = SasrecBinding(model)
+    model.__dict__["_gr_sas_binding"] = (params, tuple(q.data_ptr() for q in params), b)
+    return b
 
 
 def _sas_ids(log_seqs, binding):
@@ -351,9 +448,7 @@ def _sas_ids(log_seqs, binding):
 
 def _check_err(err):
     if CHECK:
-        torch.cuda.synchronize(err.device)
-        if int(err.item()) != 0:
-            raise IndexError("index out of range in self (item id outside the embedding table)")
+        check_errors(err.device)
 
 
 def sasrec_forward(binding, log_seqs, last_only=False):
@@ -364,7 +459,7 @@ def sasrec_forward(binding, log_seqs, last_only=False):
     out = torch.empty((B, d) if last_only else (B, n, d), dtype=torch.float32, device=dev)
     nbytes = binding.workspace_bytes(B, n)
     wsp = L.workspace(nbytes, dev)
-    err = torch.zeros(1, dtype=torch.int32, device=dev)
+    err = err_flag(dev)
     with torch.cuda.device(dev):
         L.check(L.lib().gr_sasrec_forward_f32(ctypes.byref(binding.p), L.ptr(ids), B, n, L.ptr(out),
                                               1 if last_only else 0, L.ptr(wsp), nbytes, L.ptr(err),
@@ -401,7 +496,7 @@ def sasrec_predict(binding, log_seqs, out=None):
     ld = logits.stride(0) if B > 1 else rows
     nbytes = binding.workspace_bytes(B, n)
     wsp = L.workspace(nbytes, dev)
-    err = torch.zeros(1, dtype=torch.int32, device=dev)
+    err = err_flag(dev)
     with torch.cuda.device(dev):
         L.check(L.lib().gr_sasrec_predict_ld_f32(ctypes.byref(binding.p), L.ptr(ids), B, n,
                                                  L.ptr(logits), ld, L.ptr(wsp), nbytes, L.ptr(err),
@@ -426,7 +521,7 @@ class _SampledBCE(torch.autograd.Function):
         row_loss = torch.empty(B * n, dtype=torch.float32, device=dev)
         coef = torch.empty(B * n * (J + 1), dtype=torch.float32, device=dev)
         sums = torch.empty(2, dtype=torch.float32, device=dev)
-        err = torch.zeros(1, dtype=torch.int32, device=dev)
+        err = err_flag(dev)
         with torch.cuda.device(dev):
             L.check(L.lib().gr_sampled_bce_fwd_f32(L.ptr(feats), B, n, d, L.ptr(table), rows,
                                                    L.ptr(targets), L.ptr(negs), J, float(eps),
@@ -481,7 +576,13 @@ def neg_samples(seq, item_num, num_neg=1, seed=None):
     """train.py:15-30 ``get_neg_samples(seq, item_num, num_neg)`` on the GPU: ``[B, num_neg]`` int64,
     per row distinct items uniform over ``[1, item_num]`` minus the row's non-zero history (the
     reference's distribution; not numpy's random stream).  ``seed`` defaults to a fresh value per
-    call drawn from torch's global generator, so ``torch.manual_seed`` makes runs repeatable."""
+    call drawn from torch's global generator, so ``torch.manual_seed`` makes runs repeatable.
+
+    A row whose population (``item_num`` minus its distinct history) is smaller than ``num_neg``
+    raises ValueError, as numpy's ``choice(replace=False)`` does.  That can only happen when
+    ``n + num_neg > item_num`` (the history holds at most ``n`` distinct items), and only then does
+    this call synchronise to check; otherwise every candidate is accepted with probability
+    >= 1/2 and the kernel's 4096 rounds of 64 draws cannot fall short.  Unfilled rows hold -1."""
     L.require_gpu(seq)
     s = seq.to(torch.int64).contiguous()
     if s.dim() != 2:
@@ -490,12 +591,10 @@ def neg_samples(seq, item_num, num_neg=1, seed=None):
     if seed is None:
         seed = int(torch.randint(0, 2 ** 62, (1,)).item()) ^ next(_NEG_CALLS)
     out = torch.empty((B, num_neg), dtype=torch.int64, device=s.device)
-    err = torch.zeros(1, dtype=torch.int32, device=s.device)
+    err = err_flag(s.device)
     with torch.cuda.device(s.device):
         L.check(L.lib().gr_neg_samples(L.ptr(s), B, n, int(item_num), int(num_neg), int(seed) & (2 ** 64 - 1),
                                        L.ptr(out), L.ptr(err), L.stream_of(s.device)), "gr_neg_samples")
-    if CHECK:
-        torch.cuda.synchronize(s.device)
-        if int(err.item()) != 0:
-            raise ValueError("Cannot take a larger sample than population when 'replace=False'")
+    if CHECK or 2 * (n + num_neg) > item_num:
+        check_errors(s.device)
     return out

@@ -258,11 +258,19 @@ class RQVAE(nn.Module):
         ``use_sk=True`` with a level whose ``sk_epsilon > 0`` assigns that level by Sinkhorn over the
         whole batch (vq.py:76-84), as the reference does; the batch is one group."""
         self._check_encode(xs, use_sk)
-        lin = self.encoder.linears()
-        ws, bs = [m.weight.detach() for m in lin], [m.bias.detach() for m in lin]
         if use_sk and any(q.sk_epsilon > 0 for q in self.rq.vq_layers):
+            lin = self.encoder.linears()
+            ws, bs = [m.weight.detach() for m in lin], [m.bias.detach() for m in lin]
             return ops.rq_encode_sk(xs, ws, bs, self.rq.codebooks(), self.sk_eps(), self.rq.sk_iters)
-        return ops.rq_encode(xs, ws, bs, self.rq.codebooks())
+        return ops.rq_encode(xs, binding=self.encode_binding())
+
+    def encode_binding(self):
+        """The cached device-pointer view of the encoder and codebooks (ops.rq_binding)."""
+        return ops.rq_binding(self, self._encode_params)
+
+    def _encode_params(self):
+        lin = self.encoder.linears()
+        return [m.weight for m in lin], [m.bias for m in lin], [q.embedding.weight for q in self.rq.vq_layers]
 
     def sk_eps(self):
         return [float(q.sk_epsilon) for q in self.rq.vq_layers]
@@ -284,8 +292,5 @@ class RQVAE(nn.Module):
         certificate (``near_tie_bound``): it may legitimately differ from a CPU run of the reference.
         Every unflagged row is the reference's answer."""
         self._check_encode(xs, False)
-        lin = self.encoder.linears()
-        idx, best, gap, z = ops.rq_encode(xs, [m.weight.detach() for m in lin],
-                                          [m.bias.detach() for m in lin], self.rq.codebooks(),
-                                          with_gap=True, with_z=True)
+        idx, best, gap, z = ops.rq_encode(xs, binding=self.encode_binding(), with_gap=True, with_z=True)
         return idx, near_tie_rows(best, gap, (z * z).sum(1))

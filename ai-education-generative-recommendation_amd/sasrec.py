@@ -51,7 +51,7 @@ class SASRec(nn.Module):
         n = log_seqs.shape[-1]
         if n > self.pos_emb.weight.shape[0]:
             raise IndexError(f"sequence length {n} exceeds max_len {self.pos_emb.weight.shape[0]}")
-        return ops.SasrecBinding(self)
+        return ops.sasrec_binding(self)
 
     def forward(self, log_seqs):
         """model.py:49-96: ``[B, n]`` item ids -> ``[B, n, d]`` final hidden states.

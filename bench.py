@@ -69,9 +69,9 @@ def parse():
     ap.add_argument("--c5-batch", type=int, default=512)
     ap.add_argument("--c5-items", type=int, default=1_000_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="budget per CPU baseline leg")
     ap.add_argument("--train-batch", type=int, default=128, help="sas_train leg: users per rank per step")
-    ap.add_argument("--skip", default="", help="comma list of legs to skip: sasrec,c4,c5,train")
+    ap.add_argument("--legs", default="", help="comma list of legs to run (default all): " + ",".join(LEGS))
+    ap.add_argument("--skip", default="", help="comma list of legs to skip")
     ap.add_argument("--spinup-s", type=float, default=1.0,
                     help="untimed seconds of each leg's workload before its warmup (clock ramp)")
     return ap.parse_args()
@@ -176,41 +176,54 @@ def cpu_threads():
     return max(1, min(n, int(os.environ.get("OMP_NUM_THREADS", n))))
 
 
-def cpu_rq_baseline(model, budget_s):
-    """Oracle restatement of get_indices (oracle/rq_oracle.py) on host cores: 100k-item batches of
-    the same synthetic workload, repeated until ~budget_s."""
-    from oracle import rq_oracle
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_median(fn, units, unit, sample, warm=3, reps=10):
+    """the CPU restatement timed with 3 warmups then the median of 10 calls, on
+    ``cpu_threads()`` host threads; returns the cpu_baseline object (``units`` per call)."""
     torch.set_num_threads(cpu_threads())
+    for _ in range(warm):
+        fn()
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        fn()
+        ts.append(time.perf_counter() - t0)
+    med = float(np.median(ts))
+    return {"value": units / med, "unit": unit, "cores": torch.get_num_threads(), "kind": "port",
+            "cpu": cpu_model(), "timing": f"{warm} warmups + median of {reps} calls "
+            f"(median {med * 1e3:.1f} ms, min {min(ts) * 1e3:.1f}, max {max(ts) * 1e3:.1f})", "sample": sample}
+
+
+def cpu_rq_baseline(model, n_items, tag):
+    """Oracle restatement of get_indices (oracle/rq_oracle.py) on host cores, one call of
+    ``n_items`` synthetic items of the same workload."""
+    from oracle import rq_oracle
     lin = model.encoder.linears()
     ws = [l.weight.detach().cpu() for l in lin]
     bs = [l.bias.detach().cpu() for l in lin]
     cbs = [c.cpu() for c in model.rq.codebooks()]
-    x = synth.items(100_000, 12345, "cuda").cpu()
-    rq_oracle.get_indices(x[:4096], ws, bs, cbs)
-    n, t0 = 0, time.perf_counter()
-    while time.perf_counter() - t0 < budget_s or n == 0:
-        rq_oracle.get_indices(x, ws, bs, cbs)
-        n += x.shape[0]
-    dt = time.perf_counter() - t0
-    return {"value": n / dt, "unit": "items/s", "cores": torch.get_num_threads(), "kind": "port",
-            "sample": f"oracle/rq_oracle.get_indices on {n} synthetic C2 items (100k per call, "
-                      f"{dt:.1f} s, fp32 torch CPU)"}
+    x = synth.items(n_items, 12345, "cuda").cpu()
+    return cpu_median(lambda: rq_oracle.get_indices(x, ws, bs, cbs), n_items, "items/s",
+                      f"oracle/rq_oracle.get_indices, {tag}: batch of {n_items} synthetic items (fp32 torch CPU)")
 
 
-def cpu_sas_baseline(model, budget_s, n, items):
+def cpu_sas_baseline(model, B, n, items, tag):
+    """Oracle restatement of predict (oracle/sasrec_oracle.py) on host cores, one call of B users."""
     from oracle import sasrec_oracle
-    torch.set_num_threads(cpu_threads())
     sd = {k: v.detach().cpu() for k, v in model.state_dict().items()}
-    seqs = synth.sequences(128, n, items, 777, "cuda").cpu()
-    sasrec_oracle.predict(seqs[:8], sd, model.num_blocks, model.num_heads, 1e-8)
-    cnt, t0 = 0, time.perf_counter()
-    while time.perf_counter() - t0 < budget_s or cnt == 0:
-        sasrec_oracle.predict(seqs, sd, model.num_blocks, model.num_heads, 1e-8)
-        cnt += seqs.shape[0]
-    dt = time.perf_counter() - t0
-    return {"value": cnt / dt, "unit": "seqs/s", "cores": torch.get_num_threads(), "kind": "port",
-            "sample": f"oracle/sasrec_oracle.predict, {cnt} users in batches of 128 "
-                      f"(d {model.d}, n {n}, {items} items, {dt:.1f} s)"}
+    seqs = synth.sequences(B, n, items, 777, "cuda").cpu()
+    return cpu_median(lambda: sasrec_oracle.predict(seqs, sd, model.num_blocks, model.num_heads, 1e-8),
+                      B, "seqs/s", f"oracle/sasrec_oracle.predict, {tag}: batch of {B} users "
+                      f"(d {model.d}, n {n}, {items}-item catalog, logits [B, {items + 1}])")
 
 
 def bench_rq_c2(a, world, rank, dev):
@@ -249,13 +262,16 @@ def bench_rq_c4(a, world, rank, dev):
     x = synth.items(hi - lo, 4000 + rank, dev)
     steps, warm = max(2, min(a.steps, 5)), 1
     wall, dev_ms = timed(lambda: model.get_indices(x), steps, warm, world)
-    return {"metric": "items_encoded/s", "value": a.c4_items * steps / wall, "unit": "items/s",
+    enc_ms = kernel_ms(lambda: ops.rq_encode(x, binding=model.encode_binding()), reps=3)
+    res = {"metric": "items_encoded/s", "value": a.c4_items * steps / wall, "unit": "items/s",
             "scaling": "strong", "ms_per_step": wall / steps * 1e3, "steps": steps,
             "config": {"workload": "rq_c4: RQ-VAE get_indices, 4x1024 codebooks, in 768 -> [256,128] -> e 32",
                        "catalog_items": a.c4_items, "items_per_rank": hi - lo,
                        "parallelism": f"item-sharded x{world}, no collective"},
             "call": {"device_ms": dev_ms, "flop_per_item": rq_flop_per_item(L, K),
-                     "frac_of_fp32_peak": rq_flop_per_item(L, K) * (hi - lo) / (dev_ms * 1e-3) / 1e12 / FP32_PEAK_TFLOPS}}
+                     "frac_of_fp32_peak": rq_flop_per_item(L, K) * (hi - lo) / (dev_ms * 1e-3) / 1e12 / FP32_PEAK_TFLOPS,
+                     "encode_call_ms_50rep_mean": enc_ms}}
+    return res, model
 
 
 def bench_sas_c3(a, world, rank, dev):
@@ -263,9 +279,10 @@ def bench_sas_c3(a, world, rank, dev):
     p = synth.sasrec_params(d, n, 2, 1, 64, dev)
     model = synth.sasrec_model(items, p, dev)
     seqs = synth.sequences(a.sas_batch, n, items, 2000 + rank, dev)
-    out = ops.logits_buffer(a.sas_batch, items + 1, dev)  # what predict() returns: rows 128-B aligned
-    binding = ops.SasrecBinding(model)
-    wall, dev_ms = timed(lambda: ops.sasrec_predict(binding, seqs, out=out), a.steps, a.warmup, world)
+    # timed through the drop-in surface: model.predict(seqs) allocates its fresh [B, N+1] logits
+    # (rows 128-B aligned, ops.logits_buffer) every call, as the reference's evaluate.py:26 sees it
+    wall, dev_ms = timed(lambda: model.predict(seqs), a.steps, a.warmup, world)
+    out = ops.logits_buffer(a.sas_batch, items + 1, dev)
     h = model.last_hidden(seqs)
     table = model.item_emb.weight.detach()
     score_ms = kernel_ms(lambda: ops.score(h, table, out=out))
@@ -316,7 +333,7 @@ def bench_sas_c5(a, world, rank, dev):
     ts = torch.zeros(B, device=dev)
     topk_ms = kernel_ms(lambda: ops.score_topk(h, shard, 10, lo, thresholds=ts, mask_col0=(lo == 0)))
     fwd_ms = kernel_ms(lambda: model.last_hidden(seqs[ulo:uhi]))
-    return {"metric": "seqs_scored/s", "value": B * steps / wall, "unit": "seqs/s", "scaling": "strong",
+    res = {"metric": "seqs_scored/s", "value": B * steps / wall, "unit": "seqs/s", "scaling": "strong",
             "ms_per_step": wall / steps * 1e3, "steps": steps,
             "config": {"workload": "sas_c5: SASRec d 128, n 200, 2 blocks, 1M-item catalog, rank + top-10",
                        "users_per_step": B, "catalog_rows": items + 1, "rows_per_rank": hi - lo,
@@ -329,6 +346,7 @@ def bench_sas_c5(a, world, rank, dev):
                      "forward_ms": fwd_ms, "score_topk_ms": topk_ms,
                      "note": "rank + top-10 fused into the scoring pass (gr_score_topk_f32): the "
                              "[B, rows] logits are never written"}}
+    return res, model, h, targets
 
 
 def sas_train_bytes(B, n, d, rows, J):
@@ -393,29 +411,116 @@ def bench_sas_train(a, world, rank, dev):
                                          "ms_per_step": dense_ms, "speedup": dense_ms / dev_ms}}
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         from oracle import sasrec_oracle
-        torch.set_num_threads(cpu_threads())
         f, w, t, si = feats.detach().cpu(), table.detach().cpu(), targets.cpu(), inputs.cpu().numpy()
         rng = np.random.RandomState(0)
-        t0, k, neg_s = time.perf_counter(), 0, 0.0
-        while k == 0 or (time.perf_counter() - t0 < min(a.cpu_seconds, 10.0) and k < 20):
-            t1 = time.perf_counter()
+
+        def cpu_step():
             ng = sasrec_oracle.neg_samples(si, items, J, rng)
-            neg_s += time.perf_counter() - t1
             sasrec_oracle.train_loss_grads(f, w, t, ng, 1e-24)
-            k += 1
-        el = time.perf_counter() - t0
-        res["cpu_baseline"] = {"value": B * k / el, "unit": "seqs/s", "cores": cpu_threads(), "kind": "port",
-                               "sample": f"oracle get_neg_samples (train.py:15-30, numpy) + train_loss_grads "
-                                         f"(train.py:134-167, torch CPU), {k} steps of B {B} ({el:.1f} s, "
-                                         f"{neg_s / k * 1e3:.0f} ms/step of it negative sampling)"}
+        res["cpu_baseline"] = cpu_median(cpu_step, B, "seqs/s",
+                                         f"oracle get_neg_samples (train.py:15-30, numpy) + train_loss_grads "
+                                         f"(train.py:134-167, torch CPU), one step of B {B}")
     return res
+
+
+def bench_c5_shard(a, model, h, targets, dev, shards=8):
+    """The per-GPU work of the 8-GPU C5 point, timed on one GPU: 512 users against one catalog
+    shard of 125,001 rows (rows [lo, hi) of the 1M-item table; the first shard, which also masks
+    row 0): the owner's target logits (gr_score_pairs_f32) + fused score + top-10 + strict counts
+    (gr_score_topk_f32).  The collectives around it (all-reduce of B floats and B counts,
+    all-gather of B x 10 candidates) are latency-bound and not included."""
+    from gr_amd import dist as D
+    d, B, k = h.shape[1], h.shape[0], 10
+    lo, hi = D.shard_range(model.item_emb.weight.shape[0], 0, shards)
+    shard = model.item_emb.weight.detach()[lo:hi]
+    t = targets.reshape(-1)
+    own = (t >= lo) & (t < hi)
+    loc = torch.where(own, t - lo, torch.zeros_like(t))
+
+    def step():
+        ts = ops.score_pairs(h, shard, loc, mask_col0=(lo == 0))
+        return ops.score_topk(h, shard, k, lo, thresholds=ts, mask_col0=(lo == 0))
+
+    wall, dev_ms = timed(step, a.steps, a.warmup, 1)
+    ts = ops.score_pairs(h, shard, loc, mask_col0=(lo == 0))
+    topk_ms = kernel_ms(lambda: ops.score_topk(h, shard, k, lo, thresholds=ts, mask_col0=(lo == 0)))
+    cnt_ms = kernel_ms(lambda: ops.score_count_gt(h, shard, ts, mask_col0=(lo == 0)))
+    flop = 2 * d * (hi - lo) * B
+    return {"metric": "seqs_scored/s", "value": B * a.steps / wall, "unit": "seqs/s",
+            "ms_per_step": wall / a.steps * 1e3, "scaling": "per-rank shard of the 8-GPU C5 point",
+            "config": {"workload": f"c5_shard: {B} users x one {hi - lo}-row catalog shard (1/{shards} of "
+                                   f"{model.item_emb.weight.shape[0]}), d {d}, target logit + rank + top-{k}",
+                       "rows": hi - lo, "users": B},
+            "roofline": roofline("score_topk_kernel<128,10>", flop, topk_ms, launches=2,
+                                 note="one gr_score_topk_f32 call on the shard (all its launches); flop "
+                                      "counts the scoring GEMM once"),
+            "call": {"device_ms": dev_ms, "score_topk_ms": topk_ms, "score_count_ms": cnt_ms,
+                     "frac_of_fp32_peak_step": flop / (dev_ms * 1e-3) / 1e12 / FP32_PEAK_TFLOPS}}
+
+
+def _call_pattern(fn, units, reps=200):
+    """Per-call cost of a small drop-in call at the reference's own batch size: host time to issue
+    one call (no sync), device time of one call (HIP events), and the pipelined wall time per call
+    (``reps`` calls back to back, one sync at the end)."""
+    spinup(fn, 0.3)
+    torch.cuda.synchronize()
+    host = []
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        t1 = time.perf_counter()
+        fn()
+        host.append(time.perf_counter() - t1)
+    torch.cuda.synchronize()
+    wall = (time.perf_counter() - t0) / reps
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(50)]
+    for s_, e_ in ev:
+        torch.cuda.synchronize()
+        s_.record()
+        fn()
+        e_.record()
+    torch.cuda.synchronize()
+    dev_us = float(np.median([s_.elapsed_time(e_) for s_, e_ in ev])) * 1e3
+    return {"value": units / wall, "us_per_call": wall * 1e6, "host_us_per_call": float(np.median(host)) * 1e6,
+            "device_us_per_call": dev_us}
+
+
+def bench_calls(rq_model, sas_model, sas_n, sas_items, dev, cpu=True):
+    """the drop-in methods at the reference's own call sizes, host overhead
+    included: ``model.get_indices(x[:64])`` (RQ-VAE/infer.py:84-95, batch 64) and
+    ``model.predict(seqs[:128])`` + the evaluate tail (SASRec/evaluate.py:13, 26-32, batch 128)."""
+    from gr_amd import evaluate as E
+    out = {}
+    x = synth.items(64, 77, dev)
+    r = _call_pattern(lambda: rq_model.get_indices(x), 64)
+    r.update(unit="items/s", workload="RQVAE.get_indices(x[64, 768]) at C2 weights")
+    if cpu:
+        r["cpu_baseline"] = cpu_rq_baseline(rq_model, 64, "batch 64 (infer.py:84)")
+    out["rq_get_indices_b64"] = r
+    if sas_model is not None:
+        seqs = synth.sequences(128, sas_n, sas_items, 78, dev)
+        tg = torch.randint(1, sas_items + 1, (128,), generator=torch.Generator(device=dev).manual_seed(9), device=dev)
+        r = _call_pattern(lambda: sas_model.predict(seqs), 128)
+        r.update(unit="seqs/s", workload=f"SASRec.predict(seqs[128, {sas_n}]) at C3 weights, logits written")
+        if cpu:
+            r["cpu_baseline"] = cpu_sas_baseline(sas_model, 128, sas_n, sas_items, "batch 128 (evaluate.py:13)")
+        out["sas_predict_b128"] = r
+        r = _call_pattern(lambda: E.rank_batch(sas_model, seqs, tg), 128)
+        r.update(unit="seqs/s", workload="evaluate.rank_batch at batch 128: forward + target logit + strict "
+                                         "count (evaluate.py:26-32 without the logits)")
+        out["sas_rank_b128"] = r
+    return out
+
+
+LEGS = ["c2", "calls", "sasrec", "c4", "c5", "shard", "train"]
 
 
 def main():
     a = parse()
     global SPINUP_S
     SPINUP_S = a.spinup_s
+    legs = [l for l in (a.legs.split(",") if a.legs else LEGS) if l]
     skip = set(s for s in a.skip.split(",") if s)
+    legs = [l for l in legs if l not in skip]
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -433,20 +538,43 @@ def main():
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group(backend)
+    cpu = rank == 0 and world == 1 and not a.no_cpu_baseline
 
-    line, rq_model = bench_rq_c2(a, world, rank, dev)
-    if "sasrec" not in skip:
-        line["sasrec"], sas_model, (sn, sitems) = bench_sas_c3(a, world, rank, dev)
-    if "c4" not in skip:
-        line["rq_c4"] = bench_rq_c4(a, world, rank, dev)
-    if "c5" not in skip:
-        line["sasrec_c5"] = bench_sas_c5(a, world, rank, dev)
-    if "train" not in skip:
+    if "c2" in legs:
+        line, rq_model = bench_rq_c2(a, world, rank, dev)
+        if cpu:
+            line["cpu_baseline"] = cpu_rq_baseline(rq_model, 100_000, "C2")
+    else:   # a partial run (per-leg profiling): the headline leg is not measured
+        line = {"metric": METRIC, "value": None, "unit": "items/s", "n_gpus": world, "legs": legs,
+                "note": "partial run (--legs): the C2 headline was not measured"}
+        rq_model = synth.rqvae_model(3, 256, dev) if "calls" in legs else None
+    sas_model, sn, sitems = None, 50, 100_000
+    if "sasrec" in legs or "calls" in legs:
+        sres, sas_model, (sn, sitems) = bench_sas_c3(a, world, rank, dev)
+        if "sasrec" in legs:
+            line["sasrec"] = sres
+            if cpu:
+                line["sasrec"]["cpu_baseline"] = cpu_sas_baseline(sas_model, 1024, sn, sitems, "C3")
+    if "calls" in legs and world == 1:
+        line["calls"] = bench_calls(rq_model, sas_model, sn, sitems, dev, cpu)
+    if "c4" in legs:
+        line["rq_c4"], c4_model = bench_rq_c4(a, world, rank, dev)
+        if cpu:
+            line["rq_c4"]["cpu_baseline"] = cpu_rq_baseline(c4_model, 20_000, "C4 sample")
+        del c4_model
+        torch.cuda.empty_cache()
+    if "c5" in legs or "shard" in legs:
+        c5, c5_model, h5, t5 = bench_sas_c5(a, world, rank, dev)
+        if "c5" in legs:
+            line["sasrec_c5"] = c5
+            if cpu:
+                line["sasrec_c5"]["cpu_baseline"] = cpu_sas_baseline(c5_model, 128, 200, a.c5_items, "C5")
+        if "shard" in legs and world == 1:
+            line["c5_shard"] = bench_c5_shard(a, c5_model, h5, t5, dev)
+        del c5_model, h5
+        torch.cuda.empty_cache()
+    if "train" in legs:
         line["sasrec_train"] = bench_sas_train(a, world, rank, dev)
-    if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        line["cpu_baseline"] = cpu_rq_baseline(rq_model, a.cpu_seconds)
-        if "sasrec" not in skip:
-            line["sasrec"]["cpu_baseline"] = cpu_sas_baseline(sas_model, a.cpu_seconds, sn, sitems)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -274,8 +274,8 @@ int gr_sampled_bce_bwd_f32(const float* feats, int64_t B, int32_t n, int32_t d, 
  * = num_neg distinct items drawn uniformly from [1, item_num] minus the non-zero items of
  * seqs[b, 0..n) (the reference's np.random.choice(setdiff1d(...), num_neg, replace=False): same
  * distribution, own counter-based random stream keyed by seed).  num_neg <= 1024.  err_flag
- * (optional device int32) is set when a row has fewer than num_neg valid items (the reference
- * raises ValueError there). */
+ * (optional device int32) is set to 2 when a row has fewer than num_neg valid items (the reference
+ * raises ValueError there); that row's ids are all -1. */
 int gr_neg_samples(const int64_t* seqs, int64_t B, int32_t n, int64_t item_num, int32_t num_neg,
                    uint64_t seed, int64_t* out, int32_t* err_flag, void* stream);
 

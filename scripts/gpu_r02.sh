@@ -1,0 +1,53 @@
+#!/bin/bash
+# Round-2 GPU session: parity tests (with the audit JSON), smoke, bench, and one rocprofv3
+# kernel-trace run PER BENCH LEG (so no kernel name mixes launch shapes across configs), each split
+# by launch shape with scripts/trace_stats.py.  Every GPU step has its own time limit; a fault /
+# abort / timeout (exit codes other than 0 and 1) ends the script at once.
+# Usage: scripts/gpu_r02.sh TAG [steps...]   steps: tests smoke bench legs pmc
+set -u
+ROOT=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
+TAG=${1:-run}; shift || true
+STEPS=${*:-tests smoke bench legs}
+OUT=$ROOT/gpurun_out/$TAG
+mkdir -p "$OUT"
+cd "$ROOT"
+export HSA_ENABLE_IPC_MODE_LEGACY=0
+
+step() {  # name, timeout, command...
+  local name=$1 t=$2; shift 2
+  echo "== $name ($(date +%T))"
+  timeout -k 10 "$t" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "== $name rc=$rc"
+  tail -n 12 "$OUT/$name.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "!! $name ended with $rc: stopping"; exit $rc; fi
+  return 0
+}
+
+for s in $STEPS; do
+  case $s in
+    tests) GR_PARITY_OUT=$OUT/parity_counts.json step pytest_gpu 1500 \
+             python -u -m pytest tests -m gpu -v -rs --timeout 400 --timeout-method thread ;;
+    quick) GR_PARITY_OUT=$OUT/parity_counts.json step pytest_quick 900 \
+             python -u -m pytest tests -m gpu -v -rs --timeout 300 --timeout-method thread -k "${GR_TESTS_K:-not full_size}" ;;
+    smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) step bench 900 python bench.py ;;
+    legs)
+      export TMPDIR=/tmp
+      for leg in ${GR_LEGS:-c2 calls sasrec c4 c5 shard train}; do
+        cd /tmp
+        step prof_$leg 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$leg" -o run -- \
+            python3 "$ROOT/bench.py" --legs $leg --steps 10 --warmup 3 --no-cpu-baseline --spinup-s 0.5
+        cd "$ROOT"
+        python3 scripts/trace_stats.py "$OUT/prof_$leg/run_kernel_trace.csv" --leg $leg > "$OUT/trace_$leg.csv" || true
+      done ;;
+    pmc)  # HBM traffic per kernel: FETCH_SIZE and WRITE_SIZE in separate passes
+      export TMPDIR=/tmp
+      cd /tmp
+      step pmcb_FETCH 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmcb_FETCH" -o run -- python3 "$ROOT/bench.py" --steps 3 --warmup 1 --no-cpu-baseline --skip c4,calls --spinup-s 0.2 && \
+      step pmcb_WRITE 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmcb_WRITE" -o run -- python3 "$ROOT/bench.py" --steps 3 --warmup 1 --no-cpu-baseline --skip c4,calls --spinup-s 0.2 && \
+      python3 "$ROOT/scripts/pmc_traffic.py" "$OUT/pmcb_FETCH" "$OUT/pmcb_WRITE" "$TAG" > "$OUT/traffic.json"
+      cd "$ROOT" ;;
+  esac
+done
+echo "== done"

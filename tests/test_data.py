@@ -8,23 +8,39 @@ import pytest
 import torch
 
 import golden_lib as gl
-from gr_amd.data import EmbDataset, SASRecDataset, read_interactions
+from gr_amd.data import EmbDataset, SASRecDataset, read_interactions, reference_order
 from gr_amd.evaluate import hr_ndcg, multi_k, save_results_to_csv
 
 
 def c1_records():
+    """The config-1 interactions in the reference's h5 order (ORDER BY student_id, id)."""
     z = np.load(os.path.join(gl.HERE, "interactions_c1.npz"), allow_pickle=False)
-    return [(s, [int(c)]) for s, c in zip(z["student_id"], z["class_id"])]
+    rows = reference_order(list(zip(z["student_id"].tolist(), z["row_id"].tolist(), z["class_id"].tolist())))
+    return [(s, [int(c)]) for s, _, c in rows]
+
+
+def c1_fixture_perm(user_ids):
+    """Row permutation from the C1 fixture (users in first-seen FILE order, make_golden.py) to
+    ``user_ids``: per-user outputs are compared after it."""
+    z = np.load(os.path.join(gl.HERE, "interactions_c1.npz"), allow_pickle=False)
+    seen = {}
+    for s in z["student_id"].tolist():
+        seen[s] = seen.get(s, 0) + 1
+    file_users = [u for u, c in seen.items() if c >= 3]
+    return np.array([file_users.index(u) for u in user_ids])
 
 
 def test_sasrec_test_dataset_matches_config1_fixture():
     """stu-major interactions -> per-user test sequences: the inputs / targets / item_num the C1
-    golden fixture was generated with (SASRec/data_vision.py:16-38, 74-87)."""
+    golden fixture was generated with (SASRec/data_vision.py:16-38, 74-87), users in the order of
+    the reference's h5 file (Baseline/data_process.py:22-27)."""
     _, out, meta = gl.load("sas_csv_c1")
     ds = SASRecDataset(c1_records(), max_len=20, mode="test", params={"min_seq_len": 3})
     inp, tgt = ds.tensors()
     assert ds.item_num == meta["item_num"]
-    assert np.array_equal(inp.numpy(), out["seqs"]) and np.array_equal(tgt.numpy(), out["targets"])
+    assert ds.user_ids == sorted(ds.user_ids, key=lambda u: u.encode())
+    perm = c1_fixture_perm(ds.user_ids)
+    assert np.array_equal(inp.numpy(), out["seqs"][perm]) and np.array_equal(tgt.numpy(), out["targets"][perm])
     x, t = ds[3]
     assert torch.equal(x, inp[3]) and int(t) == int(tgt[3])
     b = list(ds.batches(5))
@@ -53,6 +69,13 @@ def test_interaction_and_embedding_csv_readers(tmp_path):
         w.writerow([2, "", 4, json.dumps(vec)])
         w.writerow([3, "b", 5, json.dumps([1.0] * 4)])
     assert read_interactions(str(p)) == [("a", [3]), ("b", [5])]
+    q = tmp_path / "unordered.csv"      # SQL ORDER BY student_id, id: bytewise ids, then row id
+    with open(q, "w", newline="", encoding="utf-8") as f:
+        w = csv.writer(f)
+        w.writerow(["id", "student_id", "class_id"])
+        for rid, sid, cid in [(5, "b", 1), (2, "a", 2), (9, "B", 3), (1, "b", 4), (3, "a", 5)]:
+            w.writerow([rid, sid, cid])
+    assert read_interactions(str(q)) == [("B", [3]), ("a", [2]), ("a", [5]), ("b", [4]), ("b", [1])]
     e = EmbDataset(str(p))
     assert e.embeddings.shape == (2, 4) and e.dim == 4 and e.embeddings.dtype == np.float32
     np.save(tmp_path / "e.npy", np.arange(12, dtype=np.float32).reshape(3, 4))
@@ -86,3 +109,12 @@ def test_metrics_match_reference_tail(tmp_path):
     rows = list(csv.reader(open(params["params_path"])))
     assert rows[0] == ["task_id", "d", "top_k", "Hit@10", "NDCG@10"] and len(rows) == 3
     assert rows[1][3] == f"{hit:.6f}"
+
+
+def test_multi_k_drops_target_zero_users():
+    """train.py:42-45: users with target 0 are removed before ranking (valid_mask)."""
+    ranks = np.array([1, 3, 10, 11, 2], np.int64)
+    targets = np.array([5, 0, 7, 0, 9], np.int64)
+    hk, nk = multi_k(ranks, [2, 10], targets)
+    assert hk[2] == np.mean([1, 0, 1]) and hk[10] == 1.0
+    assert nk[10] == np.mean([1.0, 1 / np.log2(11), 1 / np.log2(3)])

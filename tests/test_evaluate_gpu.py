@@ -61,17 +61,57 @@ def test_evaluate_harness_config1(dev, tmp_path):
     checkpoint from the fixture's state dict (weights_only load), fused and materialised ranks."""
     from gr_amd.data import SASRecDataset
     from gr_amd.evaluate import evaluate
+    from test_data import c1_fixture_perm, c1_records
     sd, out, meta = gl.load("sas_csv_c1")
-    z = np.load(os.path.join(gl.HERE, "interactions_c1.npz"), allow_pickle=False)
-    recs = [(s, [int(c)]) for s, c in zip(z["student_id"], z["class_id"])]
+    recs = c1_records()
     params = dict(meta["params"], device=str(dev), eval_batch_size=5, top_k=10, topk_list=[2, 5, 10, 20],
                   min_seq_len=3, ckpt=str(tmp_path / "c1.pt"), params_path=str(tmp_path / "res.csv"),
                   task_id="c1")
     torch.save({k: torch.from_numpy(v) for k, v in sd.items()}, params["ckpt"])
     ds = SASRecDataset(recs, max_len=params["max_len"], mode="test", params=params)
     res, ranks = evaluate(params, dataset=ds)
-    assert np.array_equal(ranks, out["ranks"])
+    assert np.array_equal(ranks, out["ranks"][c1_fixture_perm(ds.user_ids)])
     assert res["Hit@10"] == meta["hr10"]
     res2, ranks2 = evaluate(params, dataset=ds, materialize=True, save_csv=False)
     assert np.array_equal(ranks2, ranks) and res2 == res
     assert os.path.exists(params["params_path"])
+
+
+def test_train_evaluate_valid_mask(dev):
+    """SASRec/train.py:33-56 on the GPU kernels: target-0 users dropped, multi-k metrics over the
+    rest equal to the fixture ranks' (certified users)."""
+    from gr_amd import SASRec
+    from gr_amd.evaluate import multi_k, train_evaluate
+    sd, out, meta = gl.load("sas_syn_c3")
+    m = SASRec(meta["item_num"], dict(meta["params"], device=str(dev)))
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
+    m = m.to(dev)
+    seqs = torch.from_numpy(out["seqs"])
+    tg = torch.from_numpy(out["targets"]).clone()
+    tg[::3] = 0
+    loader = [(seqs[i:i + 50], tg[i:i + 50]) for i in range(0, len(seqs), 50)]
+    params = {"topk_list": [2, 5, 10, 20]}
+    hk, nk = train_evaluate(m, loader, params, dev)
+    assert m.training
+    keep = tg.numpy() != 0
+    assert (out["margin"][keep] > 1e-5).all()
+    ref_h, ref_n = multi_k(out["ranks"][keep], params["topk_list"])
+    assert hk == ref_h and nk == ref_n
+
+
+def test_bad_ids_raise_without_check_mode(dev):
+    """with GR_AMD_CHECK off (the default), an out-of-range item id still raises
+    IndexError at the end of evaluate() (sticky device error word, one sync per evaluation)."""
+    from gr_amd import SASRec, ops
+    from gr_amd.data import SASRecDataset
+    from gr_amd.evaluate import evaluate
+    assert not ops.CHECK
+    sd, out, meta = gl.load("sas_csv_c1")
+    m = SASRec(meta["item_num"], dict(meta["params"], device=str(dev)))
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
+    recs = [("u1", [1, 2, 3]), ("u2", [4, meta["item_num"] + 5, 6])]
+    ds = SASRecDataset(recs, max_len=meta["params"]["max_len"], mode="test", params={"min_seq_len": 3})
+    params = dict(meta["params"], device=str(dev), top_k=10)
+    with pytest.raises(IndexError):
+        evaluate(params, dataset=ds, model=m.to(dev), save_csv=False)
+    ops.check_errors(dev)          # the flag was cleared by the raise

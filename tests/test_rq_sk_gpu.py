@@ -25,7 +25,7 @@ def model_of(name, dev, eps):
 
 
 @pytest.mark.parametrize("name", CASES)
-def test_grouped_sinkhorn_reencode_matches_reference(name, dev):
+def test_grouped_sinkhorn_reencode_matches_reference(name, dev, parity_log):
     """Every collision round's groups, all in one launch, against the reference's per-group calls."""
     x, _, _, _, out, meta = _case(name)
     L = meta["L"]
@@ -34,7 +34,8 @@ def test_grouped_sinkhorn_reencode_matches_reference(name, dev):
     sizes = np.diff(ptr)
     got = m.get_indices_groups(x[torch.from_numpy(rows)].to(dev), sizes.tolist()).cpu().numpy()
     bad = (got != out["round_out"]).any(1)
-    print(f"\n{name}: {bad.sum()} / {len(bad)} re-encoded rows differ")
+    parity_log(kind="rq_sinkhorn_reencode", fixture=name, levels="last level Sinkhorn (infer.py:109-110)",
+               rows=len(bad), groups=len(sizes), rows_differ=int(bad.sum()), cap=max(1, len(bad) // 500))
     assert bad.sum() <= max(1, len(bad) // 500)
     # a single group through the drop-in get_indices(use_sk=True) = the same rows of the launch
     r0 = torch.from_numpy(rows[ptr[0]:ptr[1]])
@@ -42,17 +43,18 @@ def test_grouped_sinkhorn_reencode_matches_reference(name, dev):
 
 
 @pytest.mark.parametrize("name", CASES)
-def test_sinkhorn_every_level_matches_reference(name, dev):
+def test_sinkhorn_every_level_matches_reference(name, dev, parity_log):
     x, _, _, _, out, meta = _case(name)
     m = model_of(name, dev, [0.01] * meta["L"])
     rows, ptr = out["all_rows"], out["all_ptr"]
     got = m.get_indices_groups(x[torch.from_numpy(rows)].to(dev), np.diff(ptr).tolist()).cpu().numpy()
     bad = (got != out["all_out"]).any(1)
-    print(f"\n{name}: {bad.sum()} / {len(bad)} rows differ")
+    parity_log(kind="rq_sinkhorn_reencode", fixture=name, levels="every level Sinkhorn", rows=len(bad),
+               groups=len(ptr) - 1, rows_differ=int(bad.sum()), cap=max(1, len(bad) // 500))
     assert bad.sum() <= max(1, len(bad) // 500)
 
 
-def test_infer_code_emission_matches_reference(dev, tmp_path):
+def test_infer_code_emission_matches_reference(dev, tmp_path, parity_log):
     """RQ-VAE/infer.py end to end on the config-1 items: codes, 30 collision rounds, dedup digit,
     .npy + mapping json."""
     import json
@@ -60,6 +62,10 @@ def test_infer_code_emission_matches_reference(dev, tmp_path):
     x, _, _, _, out, meta = _case("rq_sk_csv_3x8")
     m = model_of("rq_sk_csv_3x8", dev, [0.01] * meta["L"])
     codes, final, stats = generate_codes(m, x, dev)
+    parity_log(kind="rq_code_emission", fixture="rq_sk_csv_3x8", rows=len(final),
+               rows_differ_codes=int((codes != out["codes"]).any(1).sum()),
+               rows_differ_final=int((final != out["final"]).any(1).sum()),
+               rounds=stats["rounds"], ref_rounds=meta["rounds"])
     assert np.array_equal(codes, out["codes"]) and np.array_equal(final, out["final"])
     assert stats["rounds"] == meta["rounds"]
     f = str(tmp_path / "codes.npy")

@@ -293,3 +293,17 @@ def test_segmented_topk_count_vs_torch(B, cols, ld, dev):
     assert torch.equal(i.cpu(), o + 7) and torch.equal(v.cpu(), lg.gather(1, o))
     assert torch.equal(c.cpu(), (lg > thr[:, None]).sum(1))
     assert torch.equal(ops.count_gt(lgd, thr.to(dev)).cpu(), (lg > thr[:, None]).sum(1))
+
+
+def test_binding_cache_sees_weight_changes(dev):
+    """The cached SasrecBinding follows in-place updates and storage swaps."""
+    m, out, meta = build("sas_syn_c3", dev)
+    seqs = torch.from_numpy(out["seqs"][:16]).to(dev)
+    a = m.predict(seqs).clone()
+    with torch.no_grad():
+        m.last_layernorm.weight.mul_(2.0)                    # in place
+    b = m.predict(seqs).clone()
+    assert not torch.equal(a, b)
+    m.last_layernorm.weight.data = m.last_layernorm.weight.data / 2.0   # new storage
+    c = m.predict(seqs)
+    assert torch.equal(a, c)

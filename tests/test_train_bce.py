@@ -194,6 +194,25 @@ def test_neg_samples_population_too_small(dev):
         ops.neg_samples(seq, 2, 3)                           # num_neg > item_num
 
 
+@pytest.mark.gpu
+def test_neg_samples_population_too_small_default_mode(dev):
+    """with GR_AMD_CHECK off (the default) an unfillable row still raises ValueError
+    (the call synchronises whenever n + num_neg could exceed half the catalog), and the row holds
+    -1 ids, never uninitialised memory."""
+    from gr_amd import ops
+    assert not ops.CHECK
+    seq = torch.tensor([[1, 2, 3, 4], [0, 0, 0, 1]], device=dev)
+    with pytest.raises(ValueError):
+        ops.neg_samples(seq, 6, 3)
+    ops.check_errors(dev)                                    # cleared by the raise
+    out = ops.neg_samples(seq[1:], 6, 3)                     # row 1 alone: 5 valid items
+    assert ((out >= 2) & (out <= 6)).all() and len(set(out[0].tolist())) == 3
+    big = torch.randint(1, 100_000, (64, 50), device=dev)    # the common case: no sync, no error
+    out = ops.neg_samples(big, 100_000, 10)
+    ops.check_errors(dev)
+    assert (out >= 1).all()
+
+
 # ------------------------------------------------------------------ the whole train.py:131-167 step
 
 @pytest.mark.gpu
