@@ -134,6 +134,59 @@ __device__ __forceinline__ void layernorm(f32x16 (&y)[DT][TT], const f32x16 (&x)
   }
 }
 
+// Cross-lane hand-off through the wave's own LDS slice: LDS operations of one wave execute in
+// order, so only the compiler must be kept from reordering / forwarding across the point.
+__device__ __forceinline__ void wave_lds_sync() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+__device__ __forceinline__ float half_max(float v) {   // max over the 32 lanes of a half
+#pragma unroll
+  for (int o = 16; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+  return v;
+}
+
+__device__ __forceinline__ float half_sum(float v) {
+#pragma unroll
+  for (int o = 16; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+// y = bias[row] + W[row, 0..k) . v  (v broadcast from LDS, 16-B aligned, k % 4 == 0).
+__device__ __forceinline__ float gemv_row(const float* W, const float* bias, int row, int k,
+                                          const float* v) {
+  float acc = 0.f;
+  const float* w = W + (int64_t)row * k;
+  for (int c = 0; c < k; c += 4) {
+    const f32x4 a = *reinterpret_cast<const f32x4*>(w + c);
+    const f32x4 x = *reinterpret_cast<const f32x4*>(v + c);
+    acc = fmaf(a[0], x[0], acc);
+    acc = fmaf(a[1], x[1], acc);
+    acc = fmaf(a[2], x[2], acc);
+    acc = fmaf(a[3], x[3], acc);
+  }
+  return acc + bias[row];
+}
+
+// LayerNorm of one token whose d features sit one per lane (lanes >= d hold 0 and are ignored).
+__device__ __forceinline__ float ln_lane(float x, bool on, const float* w, const float* b, int f,
+                                         int d, float eps) {
+  const float inv_d = 1.0f / (float)d;
+  const float mean = wave_sum(on ? x : 0.f) * inv_d;
+  const float t = on ? x - mean : 0.f;
+  const float var = wave_sum(t * t) * inv_d;
+  const float rstd = 1.0f / sqrtf(var + eps);
+  return on ? (x - mean) * rstd * w[f] + b[f] : 0.f;
+}
+
 }  // namespace sf
 
 struct SasBlockPtrs {
@@ -160,8 +213,11 @@ __global__ __launch_bounds__(256) void sasrec_fused_kernel(const SasFusedArgs a,
   if (b >= B) return;   // whole wave; the kernel has no barrier
   const int d = a.d, n = a.n, mlp = a.mlp;
   const int hd = d / a.heads;
-  __shared__ __attribute__((aligned(16))) float sm[4 * DT * TT * 16 * 64];
-  float* xs = sm + (threadIdx.x >> 6) * (DT * TT * 16 * 64);
+  // per wave: the parked X (DT*TT*16*64 floats) + 1024 floats of scratch for the last-position tail
+  constexpr int SLICE = DT * TT * 16 * 64 + 1024;
+  __shared__ __attribute__((aligned(16))) float sm[4 * SLICE];
+  float* xs = sm + (threadIdx.x >> 6) * SLICE;
+  float* sc = xs + DT * TT * 16 * 64;
 
   // ---- embedding gather: X^T = (M[s] + P[pos])^T  (model.py:58-60)
   f32x16 X[DT][TT];
@@ -204,6 +260,22 @@ __global__ __launch_bounds__(256) void sasrec_fused_kernel(const SasFusedArgs a,
     {
       f32x16 Hn[DT][TT];
       layernorm<EXACT, DT, TT>(Hn, X, P.ln_a_w, P.ln_a_b, d, a.eps, h);
+      const bool tail = last_only && blk == a.nb - 1;
+      if (tail) {   // position n-1 of LN_a(x) and of x, for the single-query tail below
+        const int tl = (n - 1) >> 5, rl = (n - 1) & 31;
+#pragma unroll
+        for (int tt = 0; tt < TT; ++tt) {
+          if (tt != tl || r != rl) continue;
+#pragma unroll
+          for (int ft = 0; ft < DT; ++ft)
+#pragma unroll
+            for (int v = 0; v < 16; ++v) {
+              const int f = 32 * ft + (v & 3) + 8 * (v >> 2) + 4 * h;
+              sc[f] = Hn[ft][tt][v];
+              sc[64 + f] = X[ft][tt][v];
+            }
+        }
+      }
       // X is parked in this wave's LDS slice during attention (registers are the limit); the
       // empty asm keeps the compiler from forwarding the stored values instead of reloading
 #pragma unroll
@@ -241,6 +313,93 @@ __global__ __launch_bounds__(256) void sasrec_fused_kernel(const SasFusedArgs a,
         }
       }
       __builtin_amdgcn_sched_barrier(0);
+      if (tail) {
+        // ---- final block when only position n-1 is needed (model.py:104): the rest of the
+        // block is one query row, so it runs as lane-parallel GEMVs instead of 32-token MFMA
+        // tiles (K and V above still cover every key).  One feature per lane (d <= 64).
+        float* hl = sc;            // LN_a(x)[n-1]          [64]
+        float* xl = sc + 64;       // x[n-1]                [64]
+        float* qs = sc + 128;      // q (scaled)            [64]
+        float* os = sc + 192;      // attention output      [64]
+        float* ls = sc + 256;      // LN_f(x)               [64]
+        float* fs = sc + 320;      // relu(W1 . + b1)       [128]
+        float* ps = sc + 448;      // softmax rows per head [8][64]
+        const int f = lane;
+        const bool fon = f < d;
+        wave_lds_sync();
+        // q = (Wq h + bq) * sqrt(1/hd)   (functional.py:6578)
+        if (fon) qs[f] = gemv_row(P.w_in, P.b_in, f, d, hl) * a.scale;
+        wave_lds_sync();
+        // scores of every key against the one query, softmax per head over keys 0..n-1
+#pragma unroll 1
+        for (int hh = 0; hh < (SINGLE ? 1 : a.heads); ++hh) {
+          const int f_lo = SINGLE ? 0 : hh * hd, f_hi = SINGLE ? d : f_lo + hd;
+          float sv[TT];
+#pragma unroll
+          for (int tt = 0; tt < TT; ++tt) {
+            float acc = 0.f;
+#pragma unroll
+            for (int ft = 0; ft < DT; ++ft)
+#pragma unroll
+              for (int q = 0; q < 4; ++q) {
+                const int c = 32 * ft + 8 * q + 4 * h;
+                const f32x4 qq = *reinterpret_cast<const f32x4*>(qs + c);
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                  acc = (c + i >= f_lo && c + i < f_hi) ? fmaf(K[ft][tt][4 * q + i], qq[i], acc) : acc;
+              }
+            acc += swap_halves(acc);
+            sv[tt] = (32 * tt + r < n) ? acc : -INFINITY;
+          }
+          float m = sv[0];
+#pragma unroll
+          for (int tt = 1; tt < TT; ++tt) m = fmaxf(m, sv[tt]);
+          m = half_max(m);
+          float sum = 0.f;
+#pragma unroll
+          for (int tt = 0; tt < TT; ++tt) {
+            sv[tt] = __expf(sv[tt] - m);
+            sum += sv[tt];
+          }
+          const float inv = 1.0f / half_sum(sum);
+          if (h == 0) {
+#pragma unroll
+            for (int tt = 0; tt < TT; ++tt) ps[hh * 64 + 32 * tt + r] = sv[tt] * inv;
+          }
+        }
+        wave_lds_sync();
+        // o[f] = sum_j p_head(f)[j] V[j][f]
+#pragma unroll
+        for (int ft = 0; ft < DT; ++ft) {
+          const int fo = 32 * ft + r;
+          const float* pr = ps + (SINGLE ? 0 : (fo < d ? fo / hd : 0)) * 64;
+          float acc = 0.f;
+#pragma unroll
+          for (int tt = 0; tt < TT; ++tt)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              const f32x4 pp = *reinterpret_cast<const f32x4*>(pr + 32 * tt + 8 * q + 4 * h);
+#pragma unroll
+              for (int i = 0; i < 4; ++i) acc = fmaf(V[tt][ft][4 * q + i], pp[i], acc);
+            }
+          acc += swap_halves(acc);
+          if (h == 0 && fo < d) os[fo] = acc;
+        }
+        wave_lds_sync();
+        // out_proj + residual, LN_f, FFN + residual, last LayerNorm (model.py:84-96)
+        const float x1 = fon ? xl[f] + gemv_row(P.w_o, P.b_o, f, d, os) : 0.f;
+        const float l1 = ln_lane(x1, fon, P.ln_f_w, P.ln_f_b, f, d, a.eps);
+        if (fon) ls[f] = l1;
+        wave_lds_sync();
+#pragma unroll
+        for (int m0 = 0; m0 < 128; m0 += 64)
+          if (m0 + lane < mlp) fs[m0 + lane] = fmaxf(gemv_row(P.w1, P.b1, m0 + lane, d, ls), 0.f);
+        wave_lds_sync();
+        const float x2 = fon ? x1 + gemv_row(P.w2, P.b2, f, mlp, fs) : 0.f;
+        const float y = ln_lane(x2, fon, a.ln_w, a.ln_b, f, d, a.eps);
+        if (fon) out[b * d + f] = y;
+        return;
+      }
       const bool narrow = !SINGLE && hd < 32;   // heads narrower than a feature tile: step masks
       // one query tile at a time: Q^T tile, per-head S^T -> P^T -> O^T, out_proj, residual
 #pragma unroll

@@ -18,13 +18,15 @@ from torch.nn.init import xavier_normal_
 from . import ops
 
 # Near-tie certificate (SURVEY §7 hard part 1).  The encoder output of any fp32 implementation
-# differs from the reference's CPU/MKL bits by |dz| <= Z_TAU |z| (per row; Z_TAU = 3x the largest
-# ratio measured on the golden fixtures).  That moves every level's residual by ~dz, so
+# differs from the reference's CPU/MKL bits by |dz| <= Z_TAU |z| (per row).  Z_TAU = 3x the largest
+# ratio measured on HELD-OUT fixtures that no certified test uses (tests/golden/make_golden_calib.py:
+# 20,480 rows, two encoder shapes, both kernel paths; max 1.165e-6, profiles/r02_parity_counts.json,
+# tests/test_rq_calib_gpu.py).  That moves every level's residual by ~dz, so
 # d = |r - c|^2 moves by <= 2 sqrt(d) |dz|; the fp32 evaluation (|r|^2 + |c|^2) - 2 r.c rounds at
 # ~eps (|r| + |c|)^2 <= eps (|z| + sqrt(d))^2.  A level whose best/second-best gap is below the sum
 # of both bounds (for the two distances) can legitimately resolve either way; every other row
 # must match the reference bit for bit.
-Z_TAU = 2e-6
+Z_TAU = 3.5e-6
 D_EPS = 2.4e-7     # 4 x 2^-24
 
 

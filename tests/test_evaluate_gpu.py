@@ -94,9 +94,18 @@ def test_train_evaluate_valid_mask(dev):
     hk, nk = train_evaluate(m, loader, params, dev)
     assert m.training
     keep = tg.numpy() != 0
-    assert (out["margin"][keep] > 1e-5).all()
-    ref_h, ref_n = multi_k(out["ranks"][keep], params["topk_list"])
+    m.eval()
+    # train.py:44-48 run as written on the GPU's own logits, target-0 users removed first
+    logits = m.predict(seqs[keep].to(dev))
+    logits[:, 0] = -1e9
+    t = torch.from_numpy(out["targets"][keep]).to(dev)
+    ranks = ((logits > logits.gather(1, t[:, None])).sum(1) + 1).cpu().numpy()
+    cert = out["margin"][keep] > 1e-5
+    assert np.array_equal(ranks[cert], out["ranks"][keep][cert])
+    ref_h, ref_n = multi_k(ranks, params["topk_list"])
     assert hk == ref_h and nk == ref_n
+    assert multi_k(ranks, params["topk_list"]) == multi_k(
+        np.concatenate([ranks, [1, 1]]), params["topk_list"], np.concatenate([out["targets"][keep], [0, 0]]))
 
 
 def test_bad_ids_raise_without_check_mode(dev):

@@ -42,12 +42,12 @@ def near_tie_rows(out):
     return cert(out["dbest"], out["gap"], out["znorm"])
 
 
-# Cap on rows that may differ from the reference per fixture (all of them must also be certified
-# near-ties).  The data-derived fixtures allow 1 row per 1000; the reference's own uniform(+-1/K)
-# init (rq_syn_randinit_3x256) is the near-tie stress case: its codebook entries are ~1e-3 against
-# |z| ~ 1e1, so distances differ in the last bits only (exact reference ties: gap 0.0), and the
-# cap there is 1 row in 100.
-DIFF_CAP = {"rq_csv_3x8": 0, "rq_syn_3x256": 8, "rq_syn_4x1024": 8, "rq_syn_randinit_3x256": 20}
+# Cap on rows that may differ from the reference per fixture (every such row must also be a
+# certified near-tie).  Measured on MI355X (profiles/r02_parity_counts.json): 0 / 80, 0 / 8192,
+# 2 / 8192 and 0 / 2048 rows differ on both kernel paths; the caps leave room for two more rows
+# where the fixture has differing rows at all.  rq_syn_randinit_3x256 is the reference's own
+# uniform(+-1/K) init, the near-tie stress case (exact reference ties, gap 0.0, in 106 rows).
+DIFF_CAP = {"rq_csv_3x8": 0, "rq_syn_3x256": 2, "rq_syn_4x1024": 4, "rq_syn_randinit_3x256": 2}
 
 
 @pytest.mark.parametrize("name", RQ)
@@ -96,7 +96,7 @@ def test_quantize_on_reference_latents(dev, parity_log):
     np.testing.assert_allclose(g[~diff], out["gap"][~diff], rtol=0, atol=1e-5 * out["znorm"].max())
 
 
-def test_encoder_latents_close_to_reference(dev, rq_path):
+def test_encoder_latents_close_to_reference(dev, rq_path, parity_log):
     from gr_amd import ops
     x, sd, out, meta = gl.rq_inputs("rq_syn_3x256")
     m = build_model(meta, sd, dev)
@@ -108,8 +108,8 @@ def test_encoder_latents_close_to_reference(dev, rq_path):
     assert err < 1e-5, err
     from gr_amd.rqvae import Z_TAU
     row = np.linalg.norm(z.cpu().numpy().astype(np.float64) - zr, axis=1) / np.linalg.norm(zr, axis=1)
-    print(f"\nper-row |dz|/|z|: median {np.median(row):.3g}  p99.9 {np.quantile(row, 0.999):.3g}  "
-          f"max {row.max():.3g}  (Z_TAU {Z_TAU:g})")
+    parity_log(kind="z_tau_out_of_sample", fixture="rq_syn_3x256", path="fused" if rq_path else "layerwise",
+               rows=len(row), max_row_ratio=float(row.max()), median_row_ratio=float(np.median(row)), z_tau=Z_TAU)
     assert row.max() <= Z_TAU
     # the encoder alone through the drop-in module (layer-wise kernels)
     z2 = m.encoder(torch.from_numpy(x).to(dev)).cpu().numpy()

@@ -1,9 +1,10 @@
 """RQVAE.get_indices(use_sk=True) (Sinkhorn collision re-encode) and the infer.py code emission on
 the GPU vs the reference's golden fixtures (tests/golden/make_golden_sk.py).
 
-Bar: semantic IDs equal to the reference's.  The Sinkhorn runs in float64 like the reference; its
-inputs are the fp32 distances, so a row can only move where the reference itself sits on a near-tie
-(reported; the count is asserted small)."""
+Bar: semantic IDs equal to the reference's, every row.  The Sinkhorn runs in float64 like the
+reference; its inputs are the fp32 distances, so a row could in principle move where the reference
+itself sits on a near-tie, but none does on these fixtures (40,447 re-encoded rows in 10,493
+groups: 0 differ, profiles/r02_parity_counts.json), and the tests hold that exactly."""
 import numpy as np
 import pytest
 import torch
@@ -35,8 +36,8 @@ def test_grouped_sinkhorn_reencode_matches_reference(name, dev, parity_log):
     got = m.get_indices_groups(x[torch.from_numpy(rows)].to(dev), sizes.tolist()).cpu().numpy()
     bad = (got != out["round_out"]).any(1)
     parity_log(kind="rq_sinkhorn_reencode", fixture=name, levels="last level Sinkhorn (infer.py:109-110)",
-               rows=len(bad), groups=len(sizes), rows_differ=int(bad.sum()), cap=max(1, len(bad) // 500))
-    assert bad.sum() <= max(1, len(bad) // 500)
+               rows=len(bad), groups=len(sizes), rows_differ=int(bad.sum()), cap=0)
+    assert bad.sum() == 0
     # a single group through the drop-in get_indices(use_sk=True) = the same rows of the launch
     r0 = torch.from_numpy(rows[ptr[0]:ptr[1]])
     assert np.array_equal(m.get_indices(x[r0].to(dev), use_sk=True).cpu().numpy(), got[:ptr[1]])
@@ -50,8 +51,8 @@ def test_sinkhorn_every_level_matches_reference(name, dev, parity_log):
     got = m.get_indices_groups(x[torch.from_numpy(rows)].to(dev), np.diff(ptr).tolist()).cpu().numpy()
     bad = (got != out["all_out"]).any(1)
     parity_log(kind="rq_sinkhorn_reencode", fixture=name, levels="every level Sinkhorn", rows=len(bad),
-               groups=len(ptr) - 1, rows_differ=int(bad.sum()), cap=max(1, len(bad) // 500))
-    assert bad.sum() <= max(1, len(bad) // 500)
+               groups=len(ptr) - 1, rows_differ=int(bad.sum()), cap=0)
+    assert bad.sum() == 0
 
 
 def test_infer_code_emission_matches_reference(dev, tmp_path, parity_log):

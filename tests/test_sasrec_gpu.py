@@ -77,8 +77,11 @@ def test_forward_matches_reference(name, dev, sas_path):
     feats = m.forward(seqs).cpu().numpy()
     assert feats.shape == out["forward"].shape
     assert np.abs(feats - out["forward"]).max() < 5e-5
+    # last_hidden (predict's path) runs the final block for position n-1 alone: same math,
+    # another fp32 summation order than the full forward's last row
     last = m.last_hidden(seqs).cpu().numpy()
-    assert np.array_equal(last, feats[:, -1, :])
+    assert np.abs(last - out["forward"][:, -1, :]).max() < 5e-5
+    assert np.abs(last - feats[:, -1, :]).max() < 5e-5
 
 
 def test_predict_returns_fresh_writable_tensor(dev):
@@ -274,7 +277,7 @@ def test_fused_forward_vs_oracle(d, heads, mlp, n, blocks, B, dev):
     got = m.predict(seqs).cpu()
     err = ((got - ref).abs() / ref.abs().amax(1, keepdim=True)).max().item()
     assert err <= TOL, err
-    assert torch.equal(m.last_hidden(seqs).cpu(), got_f[:, -1, :])
+    assert (m.last_hidden(seqs).cpu() - ref_f[:, -1, :]).abs().max().item() < 5e-5
 
 
 @pytest.mark.parametrize("B,cols,ld", [(7, 100001, 100001), (33, 250000, 250003), (300, 5, 5), (2, 1, 1)])
