@@ -37,6 +37,12 @@ static std::atomic<int64_t> g_score_impl{2};
 // topk_wg_per_cu (0: the launch plan's own rule; 1..4: catalog slices sized for that many
 // workgroups per CU).  Same results; A/B timing.
 static std::atomic<int64_t> g_topk_wg_per_cu{0};
+// attn_pair (1: full-sequence attention launches use the paired-tile kernel, 0 (default): the rounds-of-4
+// kernel).  Same instruction sequence per row; A/B timing.
+static std::atomic<int64_t> g_attn_pair{0};
+// sas_rowtile (1: d = 128 layer-wise forwards fuse everything between attention launches into
+// row-tile kernels, sasrec_rowtile.hip; 0: one kernel per op).  A/B timing and a second path.
+static std::atomic<int64_t> g_sas_rowtile{1};
 
 int64_t option(const char* name) {
   if (!strcmp(name, "rq_fused")) return g_rq_fused.load();
@@ -48,6 +54,8 @@ int64_t option(const char* name) {
   if (!strcmp(name, "score_ubmajor")) return g_score_ubmajor.load();
   if (!strcmp(name, "score_impl")) return g_score_impl.load();
   if (!strcmp(name, "topk_wg_per_cu")) return g_topk_wg_per_cu.load();
+  if (!strcmp(name, "attn_pair")) return g_attn_pair.load();
+  if (!strcmp(name, "sas_rowtile")) return g_sas_rowtile.load();
   return -1;
 }
 }  // namespace gr
@@ -64,6 +72,8 @@ extern "C" int gr_set_option(const char* name, int64_t value) {
   if (!strcmp(name, "score_ubmajor") && (value == 0 || value == 1)) { gr::g_score_ubmajor = value; return GR_OK; }
   if (!strcmp(name, "score_impl") && value >= 0 && value <= 2) { gr::g_score_impl = value; return GR_OK; }
   if (!strcmp(name, "topk_wg_per_cu") && value >= 0 && value <= 4) { gr::g_topk_wg_per_cu = value; return GR_OK; }
+  if (!strcmp(name, "attn_pair") && (value == 0 || value == 1)) { gr::g_attn_pair = value; return GR_OK; }
+  if (!strcmp(name, "sas_rowtile") && (value == 0 || value == 1)) { gr::g_sas_rowtile = value; return GR_OK; }
   return gr::fail(GR_ERR_ARG, std::string("gr_set_option: unknown option or value: ") + name);
 }
 

@@ -189,6 +189,165 @@ __global__ __launch_bounds__(256, 2) void attn_mfma_kernel(const float* __restri
   }
 }
 
+// Full-sequence variant (every query tile; the first blocks of a forward): one workgroup per
+// (sequence, head) with ONE wave per SIMD (512-register budget, no spills), each wave owning a
+// PAIR of query tiles (T-1-p, p) so that every wave walks the same number of (query tile, key
+// tile) steps: at n = 200 (T = 7) the waves do 8, 8, 8 and 4 steps against 7, 6, 5, 4 then 3, 2,
+// 1 in two rounds of single tiles.  A key tile's K fragments (ds_read_b128) and V values
+// (ds_read_b32) each feed both tiles' MFMAs.  Per row the instruction sequence is the same as in
+// attn_mfma_kernel (same chains, same online-softmax order).
+template <int HD>
+__global__ __launch_bounds__(256, 1) void attn_pair_kernel(const float* __restrict__ qkv,
+                                                           float* __restrict__ out, int n, int H,
+                                                           float scale) {
+  constexpr int FT = HD / 32;
+  constexpr int KP = HD + 4;
+  constexpr int VP = HD + 8;
+  constexpr int LV = AT_KT * HD / 4 / 256;
+  __shared__ __attribute__((aligned(16))) float ks[2][AT_KT * KP];
+  __shared__ __attribute__((aligned(16))) float vs[2][AT_KT * VP];
+  const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, h = lane >> 5;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int bh = blockIdx.x, b = bh / H, hh = bh % H;
+  const int d = H * HD;
+  const int64_t rs = 3LL * d;
+  const float* base = qkv + (int64_t)b * n * rs + hh * HD;
+  const float* Qb = base;
+  const float* Kb = base + d;
+  const float* Vb = base + 2 * d;
+  const int T = (n + 31) / 32;
+  const int NP = (T + 1) / 2;   // pairs (T-1-p, p); the middle tile of an odd T pairs with none
+
+  for (int p0 = 0; p0 < NP; p0 += 4) {
+    const int pr = p0 + w;
+    // tiles of this wave: qa >= qb (qb = -1: none); waves past the last pair idle this round
+    const int qa = pr < NP ? T - 1 - pr : -1;
+    const int qb = (pr < NP && pr < T - 1 - pr) ? pr : -1;
+    const int myq[2] = {qa, qb};
+    AttnTile<HD> at[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int qt = myq[u] < 0 ? 0 : myq[u];
+      const int qi = qt * 32 + r;
+      const int qc = qi < n ? qi : n - 1;
+#pragma unroll
+      for (int it = 0; it < FT; ++it)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const f32x4 v = *reinterpret_cast<const f32x4*>(Qb + (int64_t)qc * rs + 32 * it + 8 * g + 4 * h);
+          at[u].qf[it][g] = v * scale;   // q * sqrt(1/hd) (functional.py:6578)
+        }
+#pragma unroll
+      for (int ft = 0; ft < FT; ++ft)
+#pragma unroll
+        for (int v = 0; v < 16; ++v) at[u].O[ft][v] = 0.f;
+      at[u].m = -INFINITY;
+      at[u].l = 0.f;
+    }
+    const int kmax = T - 1 - p0;   // the largest query tile of the round = the last key tile
+    f32x4 pk[LV], pv[LV];
+    auto gload = [&](int kt) {
+#pragma unroll
+      for (int i = 0; i < LV; ++i) {
+        const int f = tid + 256 * i, row = f / (HD / 4), col = (f % (HD / 4)) * 4;
+        int key = kt * AT_KT + row;
+        key = key < n ? key : n - 1;
+        pk[i] = *reinterpret_cast<const f32x4*>(Kb + (int64_t)key * rs + col);
+        pv[i] = *reinterpret_cast<const f32x4*>(Vb + (int64_t)key * rs + col);
+      }
+    };
+    auto swrite = [&](int bf) {
+#pragma unroll
+      for (int i = 0; i < LV; ++i) {
+        const int f = tid + 256 * i, row = f / (HD / 4), col = (f % (HD / 4)) * 4;
+        *reinterpret_cast<f32x4*>(&ks[bf][row * KP + col]) = pk[i];
+        *reinterpret_cast<f32x4*>(&vs[bf][row * VP + col]) = pv[i];
+      }
+    };
+    auto tile_step = [&](auto nu_tag, int kt, int bf) {
+      constexpr int NU = decltype(nu_tag)::value;
+      f32x16 S[NU];
+#pragma unroll
+      for (int u = 0; u < NU; ++u)
+#pragma unroll
+        for (int v = 0; v < 16; ++v) S[u][v] = 0.f;
+      const float* kr = &ks[bf][r * KP + 4 * h];
+#pragma unroll
+      for (int it = 0; it < FT; ++it)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const f32x4 kv = *reinterpret_cast<const f32x4*>(kr + 32 * it + 8 * g);
+#pragma unroll
+          for (int s4 = 0; s4 < 4; ++s4)
+#pragma unroll
+            for (int u = 0; u < NU; ++u) S[u] = mfma32(kv[s4], at[u].qf[it][g][s4], S[u]);
+        }
+#pragma unroll
+      for (int u = 0; u < NU; ++u) {
+        AttnTile<HD>& A = at[u];
+        const int qi = myq[u] * 32 + r;
+        float tmax = -INFINITY;
+#pragma unroll
+        for (int v = 0; v < 16; ++v) {
+          const int key = kt * 32 + (v & 3) + 8 * (v >> 2) + 4 * h;
+          if (key > qi || key >= n) S[u][v] = -INFINITY;
+          tmax = fmaxf(tmax, S[u][v]);
+        }
+        tmax = fmaxf(tmax, __shfl_xor(tmax, 32));
+        const float mn = fmaxf(A.m, tmax);
+        const float alpha = __expf(A.m - mn);
+        float ts = 0.f;
+#pragma unroll
+        for (int v = 0; v < 16; ++v) {
+          const float e = __expf(S[u][v] - mn);
+          S[u][v] = e;
+          ts += e;
+        }
+        ts += __shfl_xor(ts, 32);
+        A.l = A.l * alpha + ts;
+        A.m = mn;
+#pragma unroll
+        for (int ft = 0; ft < FT; ++ft) A.O[ft] *= alpha;
+      }
+#pragma unroll
+      for (int ft = 0; ft < FT; ++ft)
+#pragma unroll
+        for (int s = 0; s < 16; ++s) {
+          const int key = (s & 3) + 8 * (s >> 2) + 4 * h;
+          const float vv = kt * 32 + key < n ? vs[bf][key * VP + 32 * ft + r] : 0.f;
+#pragma unroll
+          for (int u = 0; u < NU; ++u) at[u].O[ft] = mfma32(vv, S[u][s], at[u].O[ft]);
+        }
+    };
+    gload(0);
+    swrite(0);
+    __syncthreads();
+    for (int kt = 0; kt <= kmax; ++kt) {
+      const int bf = kt & 1;
+      if (kt + 1 <= kmax) gload(kt + 1);
+      if (qb >= kt) tile_step(std::integral_constant<int, 2>{}, kt, bf);        // wave-uniform
+      else if (qa >= kt) tile_step(std::integral_constant<int, 1>{}, kt, bf);
+      if (kt + 1 <= kmax) swrite(bf ^ 1);
+      __syncthreads();
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      if (myq[u] < 0) continue;
+      const int qi = myq[u] * 32 + r;
+      if (qi >= n) continue;
+      const float inv = 1.0f / at[u].l;
+      float* orow = out + ((int64_t)b * n + qi) * d + hh * HD;
+#pragma unroll
+      for (int ft = 0; ft < FT; ++ft)
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+          *reinterpret_cast<f32x4*>(orow + 32 * ft + 8 * g + 4 * h) =
+              f32x4{at[u].O[ft][4 * g], at[u].O[ft][4 * g + 1], at[u].O[ft][4 * g + 2], at[u].O[ft][4 * g + 3]} * inv;
+    }
+    __syncthreads();   // the next round restages K / V
+  }
+}
+
 }  // namespace gr
 
 // Returns GR_ERR_UNSUPPORTED (message untouched) for head widths the kernel is not built for.
@@ -202,6 +361,14 @@ int gr_attn_mfma_launch(const float* qkv, float* out, int64_t B, int n, int H, i
   if (B * H > 0x7fffffffLL) return GR_ERR_UNSUPPORTED;
   const int qt_lo = last_tile_only ? (n - 1) / 32 : 0;
   const dim3 g((unsigned)(B * H)), blk(256);
+  if (!last_tile_only && option("attn_pair") != 0) {
+    switch (hd) {
+      case 32: hipLaunchKernelGGL(attn_pair_kernel<32>, g, blk, 0, st, qkv, out, n, H, scale); break;
+      case 64: hipLaunchKernelGGL(attn_pair_kernel<64>, g, blk, 0, st, qkv, out, n, H, scale); break;
+      default: hipLaunchKernelGGL(attn_pair_kernel<128>, g, blk, 0, st, qkv, out, n, H, scale); break;
+    }
+    return check_launch("sasrec attention (mfma, paired tiles)");
+  }
   switch (hd) {
     case 32: hipLaunchKernelGGL(attn_mfma_kernel<32>, g, blk, 0, st, qkv, out, n, H, scale, qt_lo); break;
     case 64: hipLaunchKernelGGL(attn_mfma_kernel<64>, g, blk, 0, st, qkv, out, n, H, scale, qt_lo); break;

@@ -275,6 +275,7 @@ static int run_layernorm(const float* in, int64_t rows, int d, int64_t stride, i
 struct SasOut {
   const float* x;
   int64_t stride, off;
+  bool done;   // the final hidden states were written by the last-position tail (LN included)
 };
 
 static int run_gather_last(const float* src, int64_t B, int n, int d, float* dst, hipStream_t st) {
@@ -289,10 +290,73 @@ static int run_gather_last(const float* src, int64_t B, int n, int d, float* dst
 // each of those rows computed by the same kernels with the same per-row instruction sequence as
 // the full forward (bitwise equal).  Earlier blocks still produce every position (they are the
 // final block's keys and values).
-static int run_forward(const gr_sasrec_params* p, const int64_t* seqs, int64_t B, int32_t n,
-                       const SasWs& w, int32_t* err, int last_only, SasOut* fin, hipStream_t st) {
+// d = 128 (C5): row-tile fusions (sasrec_rowtile.hip) between the attention launches —
+//   embed + LN_a0 | per block: in-proj, attention, post_attn (out-proj + residual + LN_f + FFN +
+//   residual + the next LayerNorm) | final block for position n-1: K/V projection + tail.
+// full_out (full forward only): the [B*n, d] output; the last block's post_attn writes
+// LN_last(X) straight into it.
+static int run_forward_rowtile(const gr_sasrec_params* p, const int64_t* seqs, int64_t B, int32_t n,
+                               const SasWs& w, int32_t* err, int last_only, SasOut* fin, float* tail_out,
+                               float* full_out, hipStream_t st) {
   const int d = p->d, H = p->n_heads, hd = d / H;
   const int64_t rows = B * n;
+  int rc = gr_embed_ln_launch(p, seqs, rows, n, w.x, w.h, err, st);
+  if (rc) return rc;
+  const float scale = (float)std::sqrt(1.0 / (double)hd);
+  const int nb = p->n_blocks;
+  for (int i = 0; i < nb; ++i) {
+    const bool last = i == nb - 1;
+    if (last && last_only && tail_out) {
+      rc = gr_linear_launch(w.h, rows, d, p->in_proj_w[i] + (int64_t)d * d, 2 * d, p->in_proj_b[i] + d,
+                            nullptr, 0, GR_ACT_NONE, w.qkv, 2 * d, st);
+      if (rc) return rc;
+      rc = gr_sasrec_tail_launch(p, i, w.x, w.qkv, B, n, tail_out, st);
+      if (rc == GR_OK) {
+        fin->done = true;
+        return GR_OK;
+      }
+      if (rc != GR_ERR_UNSUPPORTED) return rc;
+      clear_error();
+    }
+    rc = gr_linear_launch(w.h, rows, d, p->in_proj_w[i], 3 * d, p->in_proj_b[i], nullptr, 0,
+                          GR_ACT_NONE, w.qkv, 3 * d, st);
+    if (rc) return rc;
+    rc = gr_attn_mfma_launch(w.qkv, w.o, B, n, H, hd, scale, 0, st);
+    if (rc) return rc;
+    float* hdst = last && full_out ? full_out : w.h;
+    rc = gr_post_attn_launch(p, i, last ? p->last_ln_w : p->attn_ln_w[i + 1], last ? p->last_ln_b : p->attn_ln_b[i + 1],
+                             w.o, w.x, hdst, rows, st);
+    if (rc) return rc;
+  }
+  if (full_out) {
+    fin->done = true;           // LN_last(X) of every row is in full_out
+    return GR_OK;
+  }
+  // last position of LN_last(X) (a tail-unsupported shape): gather it
+  rc = run_gather_last(w.h, B, n, d, tail_out, st);
+  if (rc) return rc;
+  fin->done = true;
+  return GR_OK;
+}
+
+static bool rowtile_ok(const gr_sasrec_params* p, int32_t n) {
+  const int hd = p->d / p->n_heads;
+  return option("sas_rowtile") == 1 && p->d == 128 && p->n_blocks >= 1 &&
+         (p->mlp == 32 || p->mlp == 64 || p->mlp == 128) && (hd == 32 || hd == 64 || hd == 128) && n >= 1;
+}
+
+static int run_forward(const gr_sasrec_params* p, const int64_t* seqs, int64_t B, int32_t n,
+                       const SasWs& w, int32_t* err, int last_only, SasOut* fin, float* tail_out,
+                       hipStream_t st, float* full_out = nullptr) {
+  const int d = p->d, H = p->n_heads, hd = d / H;
+  const int64_t rows = B * n;
+  *fin = SasOut{w.x, n, n - 1, false};
+  if (rowtile_ok(p, n) && (last_only ? tail_out != nullptr : full_out != nullptr)) {
+    const int rc = run_forward_rowtile(p, seqs, B, n, w, err, last_only, fin, tail_out, full_out, st);
+    if (rc != GR_ERR_UNSUPPORTED) return rc;
+    clear_error();
+    *fin = SasOut{w.x, n, n - 1, false};
+  }
   {
     const int64_t tot = rows * (d / 4);
     hipLaunchKernelGGL(embed_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, seqs,
@@ -307,13 +371,27 @@ static int run_forward(const gr_sasrec_params* p, const int64_t* seqs, int64_t B
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)att_lds) != hipSuccess)
       return fail(GR_ERR_HIP, "sasrec attention: cannot raise the LDS limit");
   }
-  *fin = SasOut{w.x, n, n - 1};
+  *fin = SasOut{w.x, n, n - 1, false};
   // the pruned final block keeps [B, d] x / h and [B, mlp] f in the (then free) FFN buffer
   const bool prune = last_only && n >= 2 && (int64_t)n * p->mlp >= 2LL * d + p->mlp;
   for (int i = 0; i < p->n_blocks; ++i) {
     const bool last_blk = prune && i == p->n_blocks - 1;
     int rc = run_layernorm(w.x, rows, d, 1, 0, p->attn_ln_w[i], p->attn_ln_b[i], p->eps, w.h, st);
     if (rc) return rc;
+    if (last_only && tail_out && i == p->n_blocks - 1) {
+      // final block for position n-1 only: K | V of every token (rows d .. 3d of W_in), then the
+      // one-query tail (sasrec_tail.hip) writes the final hidden states, last LayerNorm included
+      rc = gr_linear_launch(w.h, rows, d, p->in_proj_w[i] + (int64_t)d * d, 2 * d, p->in_proj_b[i] + d,
+                            nullptr, 0, GR_ACT_NONE, w.qkv, 2 * d, st);
+      if (rc) return rc;
+      rc = gr_sasrec_tail_launch(p, i, w.x, w.qkv, B, n, tail_out, st);
+      if (rc == GR_OK) {
+        fin->done = true;
+        return GR_OK;
+      }
+      if (rc != GR_ERR_UNSUPPORTED) return rc;
+      clear_error();   // shape outside the tail kernel: the full final block below
+    }
     rc = gr_linear_launch(w.h, rows, d, p->in_proj_w[i], 3 * d, p->in_proj_b[i], nullptr, 0,
                           GR_ACT_NONE, w.qkv, 3 * d, st);
     if (rc) return rc;
@@ -337,7 +415,7 @@ static int run_forward(const gr_sasrec_params* p, const int64_t* seqs, int64_t B
       if (!rc) rc = gr_linear_launch(hl, B, d, p->ffn1_w[i], p->mlp, p->ffn1_b[i], nullptr, 0, GR_ACT_RELU, fl, p->mlp, st);
       if (!rc) rc = gr_linear_launch(fl, B, p->mlp, p->ffn2_w[i], d, p->ffn2_b[i], xl, d, GR_ACT_NONE, xl, d, st);
       if (rc) return rc;
-      *fin = SasOut{xl, 1, 0};
+      *fin = SasOut{xl, 1, 0, false};
       break;
     }
     rc = gr_linear_launch(w.o, rows, d, p->out_proj_w[i], d, p->out_proj_b[i], w.x, d, GR_ACT_NONE,
@@ -392,10 +470,22 @@ extern "C" int gr_sasrec_forward_f32(const gr_sasrec_params* p, const int64_t* s
     return fail(GR_ERR_UNSUPPORTED, "sasrec: fused path refused a shape fused_ok accepted");
   }
   SasOut fin;
-  rc = run_forward(p, seqs, B, n, w, err_flag, last_only, &fin, st);
+  rc = run_forward(p, seqs, B, n, w, err_flag, last_only, &fin, last_only ? out : nullptr, st,
+                   last_only ? nullptr : out);
   if (rc) return rc;
+  if (fin.done) return GR_OK;
   if (last_only) return run_layernorm(fin.x, B, p->d, fin.stride, fin.off, p->last_ln_w, p->last_ln_b, p->eps, out, st);
   return run_layernorm(w.x, B * n, p->d, 1, 0, p->last_ln_w, p->last_ln_b, p->eps, out, st);
+}
+
+static int score_hidden(const gr_sasrec_params* p, const float* h, int64_t B, float* logits, int64_t ld,
+                        hipStream_t st) {
+  using namespace gr;
+  int rc = gr_score_launch(h, B, p->d, p->item_emb, p->item_rows, logits, ld, st);
+  if (rc != GR_ERR_UNSUPPORTED) return rc;
+  clear_error();
+  return gr_linear_launch(h, B, p->d, p->item_emb, (int32_t)p->item_rows, nullptr, nullptr, 0,
+                          GR_ACT_NONE, logits, ld, st);
 }
 
 extern "C" int gr_sasrec_predict_ld_f32(const gr_sasrec_params* p, const int64_t* seqs, int64_t B,
@@ -417,16 +507,16 @@ extern "C" int gr_sasrec_predict_ld_f32(const gr_sasrec_params* p, const int64_t
       return fail(GR_ERR_UNSUPPORTED, "sasrec: fused path refused a shape fused_ok accepted");
   } else {
     SasOut fin;
-    rc = run_forward(p, seqs, B, n, w, err_flag, 1, &fin, st);
+    float* hout = w.o;   // [B, d] final hidden states (the attention-output buffer is free by then)
+    rc = run_forward(p, seqs, B, n, w, err_flag, 1, &fin, hout, st);
     if (rc) return rc;
-    rc = run_layernorm(fin.x, B, p->d, fin.stride, fin.off, p->last_ln_w, p->last_ln_b, p->eps, w.h, st);
+    if (!fin.done)
+      rc = run_layernorm(fin.x, B, p->d, fin.stride, fin.off, p->last_ln_w, p->last_ln_b, p->eps, hout, st);
+    if (rc) return rc;
+    return score_hidden(p, hout, B, logits, ld, st);
   }
   if (rc) return rc;
-  rc = gr_score_launch(w.h, B, p->d, p->item_emb, p->item_rows, logits, ld, st);
-  if (rc != GR_ERR_UNSUPPORTED) return rc;
-  clear_error();
-  return gr_linear_launch(w.h, B, p->d, p->item_emb, (int32_t)p->item_rows, nullptr, nullptr, 0,
-                          GR_ACT_NONE, logits, ld, st);
+  return score_hidden(p, w.h, B, logits, ld, st);
 }
 
 extern "C" int gr_sasrec_predict_f32(const gr_sasrec_params* p, const int64_t* seqs, int64_t B,

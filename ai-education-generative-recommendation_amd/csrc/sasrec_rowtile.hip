@@ -1,0 +1,262 @@
+// Row-tile fusions of the layer-wise SASRec forward (d = 128, the C5 shape): everything between
+// two attention launches runs as ONE kernel per 64-token tile, so the residual stream makes one
+// round trip through HBM per block instead of five (SASRec/model.py:80-96, functional.py:6600):
+//
+//   post_attn:  X1 = X + O . Wo^T + bo                       (out-proj + residual, model.py:84)
+//               H1 = LN_f(X1)                                 (model.py:92)
+//               F  = relu(H1 . W1^T + b1)                     (FFN, model.py:37-45, 93)
+//               X2 = X1 + F . W2^T + b2                       (model.py:94)
+//               H2 = LN_next(X2)  (the next block's LN_a, or last_layernorm after the last block)
+//   embed_ln:   X = M[s] + P[t];  H = LN_a0(X)                (model.py:58-60, 80)
+//
+// Tile: 64 rows x 128 features per 256-thread workgroup.  The O and X tiles come in through LDS
+// with 16-B coalesced loads; wave w owns output columns 32w..32w+31 of both 32-row MFMA tiles of
+// every 128-wide product (v_mfma_f32_32x32x2_f32, A = activation rows from LDS, B = weight rows
+// from L2 as float4 fragments), so X1 stays in its registers until the second residual.  Row
+// statistics of the LayerNorms (biased variance, two passes, F.layer_norm) are taken from the
+// LDS image by 4 threads per row.  X2 and H2 leave through LDS with 16-B stores.
+#include <cmath>
+
+#include "gr_common.h"
+
+namespace gr {
+
+constexpr int RT_D = 128;            // features (template-free: the C5 width)
+constexpr int RT_BM = 64;            // rows per workgroup
+constexpr int RT_P = RT_D + 4;       // LDS row pitch of a [64 x 128] image (conflict-free b128 reads)
+
+struct RowTileArgs {
+  const float *wo, *bo, *ln_f_w, *ln_f_b, *w1, *b1, *w2, *b2, *ln_n_w, *ln_n_b;
+  int mlp;
+  float eps;
+};
+
+// acc[rt] (rows 32rt.., columns 32w..) += A[64 x K] (LDS, pitch ap) . W[32w.., 0..K)^T
+template <int K>
+__device__ __forceinline__ void rt_gemm(f32x16 (&acc)[2], const float* A, int ap, const float* __restrict__ W,
+                                        int wrow, int r, int h) {
+  const float* wr = W + (int64_t)wrow * K + 4 * h;
+  const float* a0 = A + r * ap + 4 * h;
+#pragma unroll
+  for (int kc = 0; kc < K / 8; ++kc) {
+    const f32x4 b = *reinterpret_cast<const f32x4*>(wr + 8 * kc);
+    const f32x4 x0 = *reinterpret_cast<const f32x4*>(a0 + 8 * kc);
+    const f32x4 x1 = *reinterpret_cast<const f32x4*>(a0 + 32 * ap + 8 * kc);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      acc[0] = mfma32(x0[s], b[s], acc[0]);
+      acc[1] = mfma32(x1[s], b[s], acc[1]);
+    }
+  }
+}
+
+// LayerNorm of the 64 rows of an LDS image (pitch RT_P) in place or into `dst` (global, row
+// stride RT_D): 4 threads per row, 32 features each.
+__device__ __forceinline__ void rt_layernorm(float* img, const float* __restrict__ w, const float* __restrict__ b,
+                                             float eps, float* dst_global, int64_t rows_left) {
+  const int t = threadIdx.x, row = t >> 2, part = t & 3;
+  float* x = img + row * RT_P + 32 * part;
+  f32x4 v[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) v[i] = *reinterpret_cast<const f32x4*>(x + 4 * i);
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) s += (v[i][0] + v[i][1]) + (v[i][2] + v[i][3]);
+  s += __shfl_xor(s, 1);
+  s += __shfl_xor(s, 2);
+  const float mean = s * (1.0f / RT_D);
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float d = v[i][e] - mean;
+      q = fmaf(d, d, q);
+    }
+  q += __shfl_xor(q, 1);
+  q += __shfl_xor(q, 2);
+  const float rstd = 1.0f / sqrtf(q * (1.0f / RT_D) + eps);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int c = 32 * part + 4 * i;
+    const f32x4 ww = *reinterpret_cast<const f32x4*>(w + c);
+    const f32x4 bb = *reinterpret_cast<const f32x4*>(b + c);
+    f32x4 y;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) y[e] = (v[i][e] - mean) * rstd * ww[e] + bb[e];
+    if (dst_global) {
+      if (row < rows_left) *reinterpret_cast<f32x4*>(dst_global + (int64_t)row * RT_D + c) = y;
+    } else {
+      *reinterpret_cast<f32x4*>(x + 4 * i) = y;
+    }
+  }
+}
+
+template <int MT>
+__global__ __launch_bounds__(256, 2) void post_attn_kernel(const RowTileArgs a, const float* __restrict__ O,
+                                                           float* X, float* __restrict__ Hn, int64_t M) {
+  constexpr int MLP = 32 * MT;
+  constexpr int FP = MLP + 4;
+  __shared__ __attribute__((aligned(16))) float bufA[RT_BM * RT_P];   // O, then F
+  __shared__ __attribute__((aligned(16))) float bufB[RT_BM * RT_P];   // X, X1 -> H1, X2
+  const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, h = lane >> 5;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int64_t m0 = (int64_t)xcd_remap(blockIdx.x, gridDim.x) * RT_BM;
+  const int64_t left = M - m0;
+  // ---- O and X tiles -> LDS (rows past M read as zeros and are never stored)
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int f = tid + 256 * i, row = f >> 5, c = (f & 31) * 4;
+    const bool ok = row < left;
+    const f32x4 o = ok ? *reinterpret_cast<const f32x4*>(O + (m0 + row) * RT_D + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+    const f32x4 x = ok ? *reinterpret_cast<const f32x4*>(X + (m0 + row) * RT_D + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+    *reinterpret_cast<f32x4*>(bufA + row * RT_P + c) = o;
+    *reinterpret_cast<f32x4*>(bufB + row * RT_P + c) = x;
+  }
+  __syncthreads();
+  const int col = 32 * w + r;
+  // ---- X1 = X + O . Wo^T + bo  (register v of lane (r, h): row 32rt + (v&3) + 8(v>>2) + 4h)
+  f32x16 x1[2];
+  {
+    f32x16 acc[2];
+    const float bo = a.bo[col];
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+      for (int v = 0; v < 16; ++v) acc[rt][v] = 0.f;
+    rt_gemm<RT_D>(acc, bufA, RT_P, a.wo, col, r, h);
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+      for (int v = 0; v < 16; ++v) {
+        const int row = 32 * rt + (v & 3) + 8 * (v >> 2) + 4 * h;
+        x1[rt][v] = bufB[row * RT_P + col] + (acc[rt][v] + bo);
+      }
+  }
+  __syncthreads();   // every wave has read its X and O values
+#pragma unroll
+  for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+    for (int v = 0; v < 16; ++v) bufB[(32 * rt + (v & 3) + 8 * (v >> 2) + 4 * h) * RT_P + col] = x1[rt][v];
+  __syncthreads();
+  rt_layernorm(bufB, a.ln_f_w, a.ln_f_b, a.eps, nullptr, 0);          // H1 = LN_f(X1), in place
+  __syncthreads();
+  // ---- F = relu(H1 . W1^T + b1) -> bufA  (tiles: 2 row tiles x MT column tiles over the 4 waves)
+  for (int t = w; t < 2 * MT; t += 4) {
+    const int rt = t / MT, ct = t % MT;
+    f32x16 acc = {};
+    const float* wr = a.w1 + (int64_t)(32 * ct + r) * RT_D + 4 * h;
+    const float* ar = bufB + (32 * rt + r) * RT_P + 4 * h;
+#pragma unroll
+    for (int kc = 0; kc < RT_D / 8; ++kc) {
+      const f32x4 b = *reinterpret_cast<const f32x4*>(wr + 8 * kc);
+      const f32x4 x = *reinterpret_cast<const f32x4*>(ar + 8 * kc);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) acc = mfma32(x[s], b[s], acc);
+    }
+    const float b1 = a.b1[32 * ct + r];
+#pragma unroll
+    for (int v = 0; v < 16; ++v) {
+      const float y = acc[v] + b1;
+      bufA[(32 * rt + (v & 3) + 8 * (v >> 2) + 4 * h) * FP + 32 * ct + r] = y < 0.f ? 0.f : y;
+    }
+  }
+  __syncthreads();
+  // ---- X2 = X1 + F . W2^T + b2
+  {
+    f32x16 acc[2];
+    const float b2 = a.b2[col];
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+      for (int v = 0; v < 16; ++v) acc[rt][v] = 0.f;
+    rt_gemm<MLP>(acc, bufA, FP, a.w2, col, r, h);
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+      for (int v = 0; v < 16; ++v)
+        bufB[(32 * rt + (v & 3) + 8 * (v >> 2) + 4 * h) * RT_P + col] = x1[rt][v] + (acc[rt][v] + b2);
+  }
+  __syncthreads();
+  // ---- X2 -> X (in place: the tile was read above), H2 = LN_next(X2) -> Hn
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int f = tid + 256 * i, row = f >> 5, c = (f & 31) * 4;
+    if (row < left) *reinterpret_cast<f32x4*>(X + (m0 + row) * RT_D + c) = *reinterpret_cast<const f32x4*>(bufB + row * RT_P + c);
+  }
+  rt_layernorm(bufB, a.ln_n_w, a.ln_n_b, a.eps, Hn + m0 * RT_D, left);
+}
+
+// X = M[s] + P[t] (model.py:58-60) and H = LN_a0(X) for a 64-row tile; out-of-range ids flag err
+// and read the padding row (torch raises IndexError).
+__global__ __launch_bounds__(256) void embed_ln_kernel(const int64_t* __restrict__ seqs, int64_t M, int n,
+                                                       const float* __restrict__ item, int64_t item_rows,
+                                                       const float* __restrict__ pos, const float* __restrict__ lw,
+                                                       const float* __restrict__ lb, float eps,
+                                                       float* __restrict__ X, float* __restrict__ H, int32_t* err) {
+  __shared__ __attribute__((aligned(16))) float img[RT_BM * RT_P];
+  const int tid = threadIdx.x;
+  const int64_t m0 = (int64_t)blockIdx.x * RT_BM;
+  const int64_t left = M - m0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int f = tid + 256 * i, row = f >> 5, c = (f & 31) * 4;
+    f32x4 x = {0.f, 0.f, 0.f, 0.f};
+    if (row < left) {
+      const int64_t g = m0 + row;
+      int64_t id = seqs[g];
+      if (id < 0 || id >= item_rows) {
+        if (err) *err = 1;
+        id = 0;
+      }
+      const int t = (int)(g % n);
+      x = *reinterpret_cast<const f32x4*>(item + id * RT_D + c) + *reinterpret_cast<const f32x4*>(pos + (int64_t)t * RT_D + c);
+      *reinterpret_cast<f32x4*>(X + g * RT_D + c) = x;
+    }
+    *reinterpret_cast<f32x4*>(img + row * RT_P + c) = x;
+  }
+  __syncthreads();
+  rt_layernorm(img, lw, lb, eps, H + m0 * RT_D, left);
+}
+
+}  // namespace gr
+
+// Shapes: d == 128, mlp in {32, 64, 128}; anything else returns GR_ERR_UNSUPPORTED (the caller
+// keeps the kernel-per-op sequence).  ln_next_* = the next block's attention LayerNorm, or the
+// last LayerNorm after the final block.
+int gr_post_attn_launch(const gr_sasrec_params* p, int blk, const float* ln_next_w, const float* ln_next_b,
+                        const float* O, float* X, float* H, int64_t M, hipStream_t st) {
+  using namespace gr;
+  const int mlp = p->mlp;
+  if (p->d != RT_D || (mlp != 32 && mlp != 64 && mlp != 128)) return GR_ERR_UNSUPPORTED;
+  RowTileArgs a;
+  a.wo = p->out_proj_w[blk]; a.bo = p->out_proj_b[blk];
+  a.ln_f_w = p->ffn_ln_w[blk]; a.ln_f_b = p->ffn_ln_b[blk];
+  a.w1 = p->ffn1_w[blk]; a.b1 = p->ffn1_b[blk];
+  a.w2 = p->ffn2_w[blk]; a.b2 = p->ffn2_b[blk];
+  a.ln_n_w = ln_next_w; a.ln_n_b = ln_next_b;
+  a.mlp = mlp; a.eps = p->eps;
+  const float* ptrs[] = {a.wo, a.w1, a.w2, a.ln_f_w, a.ln_f_b, a.ln_n_w, a.ln_n_b, O, X, H};
+  for (const float* q : ptrs)
+    if (!aligned16(q)) return GR_ERR_UNSUPPORTED;
+  const int64_t tiles = (M + RT_BM - 1) / RT_BM;
+  if (tiles > 0x7fffffffLL) return GR_ERR_UNSUPPORTED;
+  switch (mlp) {
+    case 32: hipLaunchKernelGGL(post_attn_kernel<1>, dim3((unsigned)tiles), dim3(256), 0, st, a, O, X, H, M); break;
+    case 64: hipLaunchKernelGGL(post_attn_kernel<2>, dim3((unsigned)tiles), dim3(256), 0, st, a, O, X, H, M); break;
+    default: hipLaunchKernelGGL(post_attn_kernel<4>, dim3((unsigned)tiles), dim3(256), 0, st, a, O, X, H, M); break;
+  }
+  return check_launch("sasrec post-attention row tile");
+}
+
+int gr_embed_ln_launch(const gr_sasrec_params* p, const int64_t* seqs, int64_t M, int32_t n, float* X, float* H,
+                       int32_t* err, hipStream_t st) {
+  using namespace gr;
+  if (p->d != RT_D || p->n_blocks < 1) return GR_ERR_UNSUPPORTED;
+  if (!aligned16(p->attn_ln_w[0]) || !aligned16(p->attn_ln_b[0])) return GR_ERR_UNSUPPORTED;
+  const int64_t tiles = (M + RT_BM - 1) / RT_BM;
+  if (tiles > 0x7fffffffLL) return GR_ERR_UNSUPPORTED;
+  hipLaunchKernelGGL(embed_ln_kernel, dim3((unsigned)tiles), dim3(256), 0, st, seqs, M, n, p->item_emb, p->item_rows,
+                     p->pos_emb, p->attn_ln_w[0], p->attn_ln_b[0], p->eps, X, H, err);
+  return check_launch("sasrec embed + layernorm");
+}

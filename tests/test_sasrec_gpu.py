@@ -310,3 +310,30 @@ def test_binding_cache_sees_weight_changes(dev):
     m.last_layernorm.weight.data = m.last_layernorm.weight.data / 2.0   # new storage
     c = m.predict(seqs)
     assert torch.equal(a, c)
+
+
+@pytest.mark.parametrize("rowtile", [1, 0], ids=["rowtile", "per_op"])
+@pytest.mark.parametrize("heads,mlp,n,blocks,B", [(1, 64, 200, 2, 6), (2, 32, 77, 3, 5), (4, 128, 33, 1, 4),
+                                                  (1, 64, 1, 2, 3), (1, 128, 65, 2, 70)])
+def test_d128_layerwise_paths_vs_oracle(heads, mlp, n, blocks, B, rowtile, dev):
+    """d = 128 (the C5 width): the row-tile fused forward (embed+LN, post-attention row tiles, the
+    last-position tail) and the one-kernel-per-op forward, against the CPU oracle; forward (all
+    positions), last_hidden and predict."""
+    from gr_amd import _lib, synth
+    from oracle import sasrec_oracle
+    _lib.set_option("sas_rowtile", rowtile)
+    try:
+        items = 700
+        p = synth.sasrec_params(128, n, blocks, heads, mlp, dev)
+        m = synth.sasrec_model(items, p, dev, seed=n + blocks)
+        seqs = synth.sequences(B, n, items, 11 + n, dev)
+        sd = {k: v.detach().cpu() for k, v in m.state_dict().items()}
+        ref_f = sasrec_oracle.forward(seqs.cpu(), sd, blocks, heads, 1e-8)
+        got_f = m.forward(seqs).cpu()
+        assert (got_f - ref_f).abs().max().item() < 5e-5
+        assert (m.last_hidden(seqs).cpu() - ref_f[:, -1, :]).abs().max().item() < 5e-5
+        ref = sasrec_oracle.predict(seqs.cpu(), sd, blocks, heads, 1e-8)
+        got = m.predict(seqs).cpu()
+        assert ((got - ref).abs() / ref.abs().amax(1, keepdim=True)).max().item() <= TOL
+    finally:
+        _lib.set_option("sas_rowtile", 1)
