@@ -43,6 +43,9 @@ static std::atomic<int64_t> g_attn_pair{0};
 // sas_rowtile (1: d = 128 layer-wise forwards fuse everything between attention launches into
 // row-tile kernels, sasrec_rowtile.hip; 0: one kernel per op).  A/B timing and a second path.
 static std::atomic<int64_t> g_sas_rowtile{1};
+// rowtile_persist (1: the post-attention row tiles run as a persistent kernel with register-
+// resident weight fragments, 0 (default; 542 vs 553 us per C5 forward): one workgroup per tile).
+static std::atomic<int64_t> g_rowtile_persist{0};
 
 int64_t option(const char* name) {
   if (!strcmp(name, "rq_fused")) return g_rq_fused.load();
@@ -56,6 +59,7 @@ int64_t option(const char* name) {
   if (!strcmp(name, "topk_wg_per_cu")) return g_topk_wg_per_cu.load();
   if (!strcmp(name, "attn_pair")) return g_attn_pair.load();
   if (!strcmp(name, "sas_rowtile")) return g_sas_rowtile.load();
+  if (!strcmp(name, "rowtile_persist")) return g_rowtile_persist.load();
   return -1;
 }
 }  // namespace gr
@@ -74,6 +78,7 @@ extern "C" int gr_set_option(const char* name, int64_t value) {
   if (!strcmp(name, "topk_wg_per_cu") && value >= 0 && value <= 4) { gr::g_topk_wg_per_cu = value; return GR_OK; }
   if (!strcmp(name, "attn_pair") && (value == 0 || value == 1)) { gr::g_attn_pair = value; return GR_OK; }
   if (!strcmp(name, "sas_rowtile") && (value == 0 || value == 1)) { gr::g_sas_rowtile = value; return GR_OK; }
+  if (!strcmp(name, "rowtile_persist") && (value == 0 || value == 1)) { gr::g_rowtile_persist = value; return GR_OK; }
   return gr::fail(GR_ERR_ARG, std::string("gr_set_option: unknown option or value: ") + name);
 }
 

@@ -50,10 +50,13 @@ __device__ __forceinline__ void rt_gemm(f32x16 (&acc)[2], const float* A, int ap
   }
 }
 
-// LayerNorm of the 64 rows of an LDS image (pitch RT_P) in place or into `dst` (global, row
-// stride RT_D): 4 threads per row, 32 features each.
+// LayerNorm of the 64 rows of an LDS image (pitch RT_P) in place, or into `dst_global` (row
+// stride RT_D; rows < rows_left).  Statistics: 4 threads per row, 32 features each.  The global
+// form then writes with 32 threads per row (16 B each: whole rows per instruction, coalesced);
+// it needs the caller's barrier before the image is reused.
 __device__ __forceinline__ void rt_layernorm(float* img, const float* __restrict__ w, const float* __restrict__ b,
                                              float eps, float* dst_global, int64_t rows_left) {
+  __shared__ float st_mean[RT_BM], st_rstd[RT_BM];
   const int t = threadIdx.x, row = t >> 2, part = t & 3;
   float* x = img + row * RT_P + 32 * part;
   f32x4 v[8];
@@ -76,19 +79,36 @@ __device__ __forceinline__ void rt_layernorm(float* img, const float* __restrict
   q += __shfl_xor(q, 1);
   q += __shfl_xor(q, 2);
   const float rstd = 1.0f / sqrtf(q * (1.0f / RT_D) + eps);
+  if (!dst_global) {
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int c = 32 * part + 4 * i;
-    const f32x4 ww = *reinterpret_cast<const f32x4*>(w + c);
-    const f32x4 bb = *reinterpret_cast<const f32x4*>(b + c);
-    f32x4 y;
+    for (int i = 0; i < 8; ++i) {
+      const int c = 32 * part + 4 * i;
+      const f32x4 ww = *reinterpret_cast<const f32x4*>(w + c);
+      const f32x4 bb = *reinterpret_cast<const f32x4*>(b + c);
+      f32x4 y;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) y[e] = (v[i][e] - mean) * rstd * ww[e] + bb[e];
-    if (dst_global) {
-      if (row < rows_left) *reinterpret_cast<f32x4*>(dst_global + (int64_t)row * RT_D + c) = y;
-    } else {
+      for (int e = 0; e < 4; ++e) y[e] = (v[i][e] - mean) * rstd * ww[e] + bb[e];
       *reinterpret_cast<f32x4*>(x + 4 * i) = y;
     }
+    return;
+  }
+  if (part == 0) {
+    st_mean[row] = mean;
+    st_rstd[row] = rstd;
+  }
+  __syncthreads();
+  const int c = (t & 31) * 4;
+  const f32x4 ww = *reinterpret_cast<const f32x4*>(w + c);
+  const f32x4 bb = *reinterpret_cast<const f32x4*>(b + c);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int rr = (t >> 5) + 8 * i;
+    const f32x4 xv = *reinterpret_cast<const f32x4*>(img + rr * RT_P + c);
+    const float m = st_mean[rr], rs = st_rstd[rr];
+    f32x4 y;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) y[e] = (xv[e] - m) * rs * ww[e] + bb[e];
+    if (rr < rows_left) *reinterpret_cast<f32x4*>(dst_global + (int64_t)rr * RT_D + c) = y;
   }
 }
 
@@ -187,6 +207,150 @@ __global__ __launch_bounds__(256, 2) void post_attn_kernel(const RowTileArgs a, 
   rt_layernorm(bufB, a.ln_n_w, a.ln_n_b, a.eps, Hn + m0 * RT_D, left);
 }
 
+// Persistent form of post_attn_kernel: one workgroup per CU (one wave per SIMD, 512-register
+// budget) walks row tiles; each wave's weight fragments (its 32 rows of Wo, W1 and W2 as MFMA B
+// operands) are loaded ONCE into registers, and the next tile's O / X are prefetched into
+// registers while the current tile computes.  Same arithmetic per element as post_attn_kernel
+// (same fragment order, same LayerNorm helper), so both produce identical bits.
+template <int MT>
+__global__ __launch_bounds__(256, 1) void post_attn_persist_kernel(const RowTileArgs a, const float* __restrict__ O,
+                                                                   float* X, float* __restrict__ Hn, int64_t M) {
+  constexpr int MLP = 32 * MT;
+  constexpr int FP = MLP + 4;
+  constexpr int W1N = MT == 4 ? 2 : 1;          // FFN1 row tiles per wave
+  __shared__ __attribute__((aligned(16))) float bufA[RT_BM * RT_P];   // O, then F
+  __shared__ __attribute__((aligned(16))) float bufB[RT_BM * RT_P];   // X, X1 -> H1, X2
+  const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, h = lane >> 5;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int col = 32 * w + r;
+  // FFN1 tile(s) of this wave: column tile c1, row tiles rt1 (.. rt1 + W1N - 1); MT = 1 uses waves 0, 1
+  const int c1 = MT == 4 ? w : MT == 2 ? (w & 1) : 0;
+  const int rt1 = MT == 4 ? 0 : MT == 2 ? (w >> 1) : w;
+  const bool f1 = MT != 1 || w < 2;
+  f32x4 wo[RT_D / 8], w1[RT_D / 8], w2[MLP / 8];
+#pragma unroll
+  for (int kc = 0; kc < RT_D / 8; ++kc) {
+    wo[kc] = *reinterpret_cast<const f32x4*>(a.wo + (int64_t)col * RT_D + 8 * kc + 4 * h);
+    w1[kc] = *reinterpret_cast<const f32x4*>(a.w1 + (int64_t)(32 * c1 + r) * RT_D + 8 * kc + 4 * h);
+  }
+#pragma unroll
+  for (int kc = 0; kc < MLP / 8; ++kc)
+    w2[kc] = *reinterpret_cast<const f32x4*>(a.w2 + (int64_t)col * MLP + 8 * kc + 4 * h);
+  const float bo = a.bo[col], b2 = a.b2[col], b1 = a.b1[32 * c1 + r];
+  const int64_t tiles = (M + RT_BM - 1) / RT_BM;
+  f32x4 po[8], px[8];
+  auto gload = [&](int64_t t) {
+    const int64_t m0 = t * RT_BM;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int f = tid + 256 * i, row = f >> 5, c = (f & 31) * 4;
+      const bool ok = m0 + row < M;
+      po[i] = ok ? *reinterpret_cast<const f32x4*>(O + (m0 + row) * RT_D + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+      px[i] = ok ? *reinterpret_cast<const f32x4*>(X + (m0 + row) * RT_D + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+  auto swrite = [&]() {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int f = tid + 256 * i, row = f >> 5, c = (f & 31) * 4;
+      *reinterpret_cast<f32x4*>(bufA + row * RT_P + c) = po[i];
+      *reinterpret_cast<f32x4*>(bufB + row * RT_P + c) = px[i];
+    }
+  };
+  int64_t t = blockIdx.x;
+  if (t < tiles) {
+    gload(t);
+    swrite();
+  }
+  __syncthreads();
+  for (; t < tiles; t += gridDim.x) {
+    const int64_t m0 = t * RT_BM, left = M - m0;
+    if (t + gridDim.x < tiles) gload(t + gridDim.x);      // lands while this tile computes
+    // ---- X1 = X + O . Wo^T + bo
+    f32x16 x1[2];
+    {
+      f32x16 acc[2] = {};
+      const float* a0 = bufA + r * RT_P + 4 * h;
+#pragma unroll
+      for (int kc = 0; kc < RT_D / 8; ++kc) {
+        const f32x4 xa = *reinterpret_cast<const f32x4*>(a0 + 8 * kc);
+        const f32x4 xb = *reinterpret_cast<const f32x4*>(a0 + 32 * RT_P + 8 * kc);
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) {
+          acc[0] = mfma32(xa[s4], wo[kc][s4], acc[0]);
+          acc[1] = mfma32(xb[s4], wo[kc][s4], acc[1]);
+        }
+      }
+#pragma unroll
+      for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+        for (int v = 0; v < 16; ++v) {
+          const int row = 32 * rt + (v & 3) + 8 * (v >> 2) + 4 * h;
+          x1[rt][v] = bufB[row * RT_P + col] + (acc[rt][v] + bo);
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+      for (int v = 0; v < 16; ++v) bufB[(32 * rt + (v & 3) + 8 * (v >> 2) + 4 * h) * RT_P + col] = x1[rt][v];
+    __syncthreads();
+    rt_layernorm(bufB, a.ln_f_w, a.ln_f_b, a.eps, nullptr, 0);
+    __syncthreads();
+    // ---- F = relu(H1 . W1^T + b1) -> bufA
+    if (f1) {
+#pragma unroll
+      for (int u = 0; u < W1N; ++u) {
+        const int rt = rt1 + u;
+        f32x16 acc = {};
+        const float* ar = bufB + (32 * rt + r) * RT_P + 4 * h;
+#pragma unroll
+        for (int kc = 0; kc < RT_D / 8; ++kc) {
+          const f32x4 x = *reinterpret_cast<const f32x4*>(ar + 8 * kc);
+#pragma unroll
+          for (int s4 = 0; s4 < 4; ++s4) acc = mfma32(x[s4], w1[kc][s4], acc);
+        }
+#pragma unroll
+        for (int v = 0; v < 16; ++v) {
+          const float y = acc[v] + b1;
+          bufA[(32 * rt + (v & 3) + 8 * (v >> 2) + 4 * h) * FP + 32 * c1 + r] = y < 0.f ? 0.f : y;
+        }
+      }
+    }
+    __syncthreads();
+    // ---- X2 = X1 + F . W2^T + b2 -> bufB
+    {
+      f32x16 acc[2] = {};
+      const float* a0 = bufA + r * FP + 4 * h;
+#pragma unroll
+      for (int kc = 0; kc < MLP / 8; ++kc) {
+        const f32x4 xa = *reinterpret_cast<const f32x4*>(a0 + 8 * kc);
+        const f32x4 xb = *reinterpret_cast<const f32x4*>(a0 + 32 * FP + 8 * kc);
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) {
+          acc[0] = mfma32(xa[s4], w2[kc][s4], acc[0]);
+          acc[1] = mfma32(xb[s4], w2[kc][s4], acc[1]);
+        }
+      }
+#pragma unroll
+      for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+        for (int v = 0; v < 16; ++v)
+          bufB[(32 * rt + (v & 3) + 8 * (v >> 2) + 4 * h) * RT_P + col] = x1[rt][v] + (acc[rt][v] + b2);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int f = tid + 256 * i, row = f >> 5, c = (f & 31) * 4;
+      if (row < left) *reinterpret_cast<f32x4*>(X + (m0 + row) * RT_D + c) = *reinterpret_cast<const f32x4*>(bufB + row * RT_P + c);
+    }
+    rt_layernorm(bufB, a.ln_n_w, a.ln_n_b, a.eps, Hn + m0 * RT_D, left);
+    __syncthreads();                                      // bufA / bufB free for the next tile
+    if (t + gridDim.x < tiles) swrite();
+    __syncthreads();
+  }
+}
+
 // X = M[s] + P[t] (model.py:58-60) and H = LN_a0(X) for a 64-row tile; out-of-range ids flag err
 // and read the padding row (torch raises IndexError).
 __global__ __launch_bounds__(256) void embed_ln_kernel(const int64_t* __restrict__ seqs, int64_t M, int n,
@@ -241,6 +405,21 @@ int gr_post_attn_launch(const gr_sasrec_params* p, int blk, const float* ln_next
     if (!aligned16(q)) return GR_ERR_UNSUPPORTED;
   const int64_t tiles = (M + RT_BM - 1) / RT_BM;
   if (tiles > 0x7fffffffLL) return GR_ERR_UNSUPPORTED;
+  if (option("rowtile_persist") != 0) {
+    static int cus = 0;
+    if (!cus) {
+      int dev = 0;
+      if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+      if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1) cus = 256;
+    }
+    const dim3 g((unsigned)(tiles < cus ? tiles : cus));
+    switch (mlp) {
+      case 32: hipLaunchKernelGGL(post_attn_persist_kernel<1>, g, dim3(256), 0, st, a, O, X, H, M); break;
+      case 64: hipLaunchKernelGGL(post_attn_persist_kernel<2>, g, dim3(256), 0, st, a, O, X, H, M); break;
+      default: hipLaunchKernelGGL(post_attn_persist_kernel<4>, g, dim3(256), 0, st, a, O, X, H, M); break;
+    }
+    return check_launch("sasrec post-attention row tiles (persistent)");
+  }
   switch (mlp) {
     case 32: hipLaunchKernelGGL(post_attn_kernel<1>, dim3((unsigned)tiles), dim3(256), 0, st, a, O, X, H, M); break;
     case 64: hipLaunchKernelGGL(post_attn_kernel<2>, dim3((unsigned)tiles), dim3(256), 0, st, a, O, X, H, M); break;

@@ -25,23 +25,44 @@ struct SasTailArgs {
   float eps, scale;
 };
 
-constexpr int ST_MAX_D = 256, ST_MAX_H = 8, ST_MAX_N = 1024, ST_MAX_MLP = 1024;
+constexpr int ST_MAX_D = 256, ST_MAX_H = 8, ST_MAX_N = 1024, ST_MAX_MLP = 256;
+constexpr int ST_NW = 8;                     // waves per workgroup (one workgroup per sequence)
+constexpr int ST_NT = 64 * ST_NW;
+constexpr int ST_U = 8;                      // rows / keys in flight per lane group
 
-// out[o] = bias[o] + W[o, 0..k) . v for o < rows (v in LDS, k % 4 == 0, rows of W 16-B aligned)
+// Segmented lane groups: a group of L = k/4 consecutive lanes (L a power of two <= 64) covers a
+// k-vector with one float4 per lane; 64/L groups per wave, 4 waves per workgroup.
+__device__ __forceinline__ float seg_sum(float v, int L) {
+  for (int o = L >> 1; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+// out[o] = bias[o] + W[o, 0..k) . v (v in LDS), o < rows: one lane group per output row, 16-B
+// coalesced row reads, ST_U rows in flight per group (the kernel is latency-bound: one sequence
+// per workgroup, every phase a dependent step).
 __device__ __forceinline__ void st_gemv(const float* __restrict__ W, const float* __restrict__ bias,
                                         const float* v, int rows, int k, float* out) {
-  for (int o = threadIdx.x; o < rows; o += 256) {
-    const float* w = W + (int64_t)o * k;
-    float acc = 0.f;
-    for (int c = 0; c < k; c += 4) {
-      const f32x4 a = *reinterpret_cast<const f32x4*>(w + c);
-      const f32x4 x = *reinterpret_cast<const f32x4*>(v + c);
-      acc = fmaf(a[0], x[0], acc);
-      acc = fmaf(a[1], x[1], acc);
-      acc = fmaf(a[2], x[2], acc);
-      acc = fmaf(a[3], x[3], acc);
+  const int L = k >> 2, gpw = 64 / L;
+  const int lane = threadIdx.x & 63, l = lane & (L - 1);
+  const int grp = (threadIdx.x >> 6) * gpw + lane / L, ngrp = ST_NW * gpw;
+  const f32x4 x = *reinterpret_cast<const f32x4*>(v + 4 * l);
+  for (int o0 = grp; o0 < rows; o0 += ST_U * ngrp) {
+    f32x4 a[ST_U];
+#pragma unroll
+    for (int u = 0; u < ST_U; ++u) {
+      const int o = o0 + u * ngrp;
+      a[u] = o < rows ? *reinterpret_cast<const f32x4*>(W + (int64_t)o * k + 4 * l) : f32x4{0.f, 0.f, 0.f, 0.f};
     }
-    out[o] = acc + bias[o];
+#pragma unroll
+    for (int u = 0; u < ST_U; ++u) {
+      const int o = o0 + u * ngrp;
+      float acc = a[u][0] * x[0];
+      acc = fmaf(a[u][1], x[1], acc);
+      acc = fmaf(a[u][2], x[2], acc);
+      acc = fmaf(a[u][3], x[3], acc);
+      acc = seg_sum(acc, L);
+      if (l == 0 && o < rows) out[o] = acc + bias[o];
+    }
   }
 }
 
@@ -67,119 +88,121 @@ __device__ __forceinline__ void st_layernorm(const float* in, const float* __res
   }
   __syncthreads();
   const float mean = stat[0], rstd = stat[1];
-  for (int c = threadIdx.x; c < d; c += 256) out[c] = (in[c] - mean) * rstd * w[c] + b[c];
+  for (int c = threadIdx.x; c < d; c += ST_NT) out[c] = (in[c] - mean) * rstd * w[c] + b[c];
   __syncthreads();
 }
 
-__global__ __launch_bounds__(256) void sas_tail_kernel(const SasTailArgs a, const float* __restrict__ X,
+__global__ __launch_bounds__(ST_NT) void sas_tail_kernel(const SasTailArgs a, const float* __restrict__ X,
                                                        const float* __restrict__ KV, float* __restrict__ out) {
   __shared__ __attribute__((aligned(16))) float xl[ST_MAX_D], hl[ST_MAX_D], q[ST_MAX_D], o[ST_MAX_D],
-      x1[ST_MAX_D], l1[ST_MAX_D], fh[ST_MAX_MLP], P[ST_MAX_H * ST_MAX_N], part[256 * 2], red[2 * ST_MAX_H * 4],
-      stat[2];
+      x1[ST_MAX_D], l1[ST_MAX_D], fh[ST_MAX_MLP], P[ST_MAX_H * ST_MAX_N], part[ST_NT * 4],
+      red[2 * ST_MAX_H * ST_NW], stat[2];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int64_t b = blockIdx.x;
   const int d = a.d, n = a.n, H = a.heads, hd = d / H;
+  const int L = d >> 2, gpw = 64 / L, l = lane & (L - 1);
+  const int grp = wave * gpw + lane / L, ngrp = ST_NW * gpw;
+  const int hl4 = hd >> 2;                  // lanes per head within a group
   const float* xr = X + (b * n + n - 1) * d;
-  const float* kv = KV + b * n * 2 * d;   // row j: K[j] = kv[j*2d .. +d), V[j] = kv[j*2d + d .. +d)
-  for (int c = tid; c < d; c += 256) xl[c] = xr[c];
+  const float* kv = KV + b * n * 2 * d;     // row j: K[j] = kv[j*2d .. +d), V[j] = kv[j*2d + d .. +d)
+  for (int c = tid; c < d; c += ST_NT) xl[c] = xr[c];
   __syncthreads();
   st_layernorm(xl, a.ln_a_w, a.ln_a_b, d, a.eps, hl, stat);
   st_gemv(a.wq, a.bq, hl, d, d, q);
   __syncthreads();
-  for (int c = tid; c < d; c += 256) q[c] *= a.scale;     // q * sqrt(1/hd) after the bias
-  __syncthreads();
-  // scores: thread t takes keys t, t+256, ...; per-head partial dots over 16-B chunks of q
-  float mx[ST_MAX_H];
+  // scores: one lane group per key, lane l holds q[4l .. 4l+3] (scaled after the bias, :6578)
+  const f32x4 q4 = *reinterpret_cast<const f32x4*>(q + 4 * l) * a.scale;
+  const int myh = (4 * l) / hd;
+  float mx = -INFINITY;
+  for (int j0 = grp; j0 < n; j0 += ST_U * ngrp) {
+    f32x4 k4[ST_U];
 #pragma unroll
-  for (int hh = 0; hh < ST_MAX_H; ++hh) mx[hh] = -INFINITY;
-  for (int j = tid; j < n; j += 256) {
-    const float* kr = kv + (int64_t)j * 2 * d;
-    float s[ST_MAX_H];
-#pragma unroll
-    for (int hh = 0; hh < ST_MAX_H; ++hh) s[hh] = 0.f;
-    for (int c = 0; c < d; c += 4) {
-      const f32x4 k4 = *reinterpret_cast<const f32x4*>(kr + c);
-      const f32x4 q4 = *reinterpret_cast<const f32x4*>(q + c);
-      const int hh = c / hd;
-      float t = s[0];
-#pragma unroll
-      for (int u = 1; u < ST_MAX_H; ++u) t = hh == u ? s[u] : t;
-      t = fmaf(k4[0], q4[0], t);
-      t = fmaf(k4[1], q4[1], t);
-      t = fmaf(k4[2], q4[2], t);
-      t = fmaf(k4[3], q4[3], t);
-#pragma unroll
-      for (int u = 0; u < ST_MAX_H; ++u) s[u] = hh == u ? t : s[u];
+    for (int u = 0; u < ST_U; ++u) {
+      const int j = j0 + u * ngrp;
+      k4[u] = j < n ? *reinterpret_cast<const f32x4*>(kv + (int64_t)j * 2 * d + 4 * l) : f32x4{0.f, 0.f, 0.f, 0.f};
     }
 #pragma unroll
-    for (int hh = 0; hh < ST_MAX_H; ++hh)
-      if (hh < H) {
-        P[hh * n + j] = s[hh];
-        mx[hh] = fmaxf(mx[hh], s[hh]);
+    for (int u = 0; u < ST_U; ++u) {
+      const int j = j0 + u * ngrp;
+      float s = k4[u][0] * q4[0];
+      s = fmaf(k4[u][1], q4[1], s);
+      s = fmaf(k4[u][2], q4[2], s);
+      s = fmaf(k4[u][3], q4[3], s);
+      s = seg_sum(s, hl4);                 // per head: the head's hd/4 lanes
+      if (j < n && (l & (hl4 - 1)) == 0) {
+        P[myh * n + j] = s;
+        mx = fmaxf(mx, s);
       }
+    }
   }
-  // softmax over keys per head: block max, exp, block sum (functional.py:6590)
-#pragma unroll
-  for (int hh = 0; hh < ST_MAX_H; ++hh) {
-    float m = mx[hh];
+  __syncthreads();
+  // softmax over keys per head (functional.py:6590): max, exp, sum
+  for (int hh = 0; hh < H; ++hh) {
+    float m = -INFINITY;
+    for (int j = tid; j < n; j += ST_NT) m = fmaxf(m, P[hh * n + j]);
     for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off));
-    if (lane == 0 && hh < H) red[hh * 4 + wave] = m;
+    if (lane == 0) red[hh * ST_NW + wave] = m;
   }
   __syncthreads();
-  float sm[ST_MAX_H];
-#pragma unroll
-  for (int hh = 0; hh < ST_MAX_H; ++hh) {
-    const float m = hh < H ? fmaxf(fmaxf(red[hh * 4], red[hh * 4 + 1]), fmaxf(red[hh * 4 + 2], red[hh * 4 + 3])) : 0.f;
-    sm[hh] = 0.f;
-    if (hh < H)
-      for (int j = tid; j < n; j += 256) {
-        const float e = __expf(P[hh * n + j] - m);
-        P[hh * n + j] = e;
-        sm[hh] += e;
-      }
-  }
-#pragma unroll
-  for (int hh = 0; hh < ST_MAX_H; ++hh) {
-    float s = sm[hh];
-    for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
-    if (lane == 0 && hh < H) red[ST_MAX_H * 4 + hh * 4 + wave] = s;
-  }
-  __syncthreads();
-  // o[f] = sum_j p_head(f)[j] V[j][f]: thread t -> feature t % d, key group t / d
-  {
-    const int G = 256 / d;
-    const int f = tid % d, g = tid / d;
-    if (g < G) {
-      const int hh = f / hd;
-      const float* base = ST_MAX_H * 4 + red + hh * 4;
-      const float inv = 1.0f / (base[0] + base[1] + base[2] + base[3]);
-      float acc = 0.f;
-      for (int j = g; j < n; j += G) acc = fmaf(P[hh * n + j] * inv, kv[(int64_t)j * 2 * d + d + f], acc);
-      part[g * d + f] = acc;
+  for (int hh = 0; hh < H; ++hh) {
+    float m = red[hh * ST_NW];
+    for (int u = 1; u < ST_NW; ++u) m = fmaxf(m, red[hh * ST_NW + u]);
+    float sm = 0.f;
+    for (int j = tid; j < n; j += ST_NT) {
+      const float e = __expf(P[hh * n + j] - m);
+      P[hh * n + j] = e;
+      sm += e;
     }
+    for (int off = 32; off > 0; off >>= 1) sm += __shfl_xor(sm, off);
+    if (lane == 0) red[ST_MAX_H * ST_NW + hh * ST_NW + wave] = sm;
+  }
+  __syncthreads();
+  // o = p . V: lane group g sums keys g, g + ngrp, ...; lane l covers features 4l .. 4l+3
+  {
+    const float* sb = red + ST_MAX_H * ST_NW + myh * ST_NW;
+    float tot = sb[0];
+    for (int u = 1; u < ST_NW; ++u) tot += sb[u];
+    const float inv = 1.0f / tot;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int j0 = grp; j0 < n; j0 += ST_U * ngrp) {
+      f32x4 v4[ST_U];
+#pragma unroll
+      for (int u = 0; u < ST_U; ++u) {
+        const int j = j0 + u * ngrp;
+        v4[u] = j < n ? *reinterpret_cast<const f32x4*>(kv + (int64_t)j * 2 * d + d + 4 * l) : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+      for (int u = 0; u < ST_U; ++u) {
+        const int j = j0 + u * ngrp;
+        const float pj = j < n ? P[myh * n + j] * inv : 0.f;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc[e] = fmaf(pj, v4[u][e], acc[e]);
+      }
+    }
+    *reinterpret_cast<f32x4*>(part + grp * d + 4 * l) = acc;
     __syncthreads();
-    for (int c = tid; c < d; c += 256) {
-      float acc = 0.f;
-      for (int gg = 0; gg < G; ++gg) acc += part[gg * d + c];
-      o[c] = acc;
+    for (int c = tid; c < d; c += ST_NT) {
+      float t = 0.f;
+      for (int g = 0; g < ngrp; ++g) t += part[g * d + c];
+      o[c] = t;
     }
     __syncthreads();
   }
   st_gemv(a.wo, a.bo, o, d, d, x1);                          // out_proj
   __syncthreads();
-  for (int c = tid; c < d; c += 256) x1[c] += xl[c];         // residual (model.py:84)
+  for (int c = tid; c < d; c += ST_NT) x1[c] += xl[c];         // residual (model.py:84)
   __syncthreads();
   st_layernorm(x1, a.ln_f_w, a.ln_f_b, d, a.eps, l1, stat);
   st_gemv(a.w1, a.b1, l1, a.mlp, d, fh);
   __syncthreads();
-  for (int c = tid; c < a.mlp; c += 256) fh[c] = fh[c] < 0.f ? 0.f : fh[c];
+  for (int c = tid; c < a.mlp; c += ST_NT) fh[c] = fh[c] < 0.f ? 0.f : fh[c];
   __syncthreads();
-  st_gemv(a.w2, a.b2, fh, d, a.mlp, o);                      // reuse o for W2 f + b2
+  st_gemv(a.w2, a.b2, fh, d, a.mlp, o);                      // W2 f + b2 (o reused)
   __syncthreads();
-  for (int c = tid; c < d; c += 256) x1[c] += o[c];          // residual (model.py:94)
+  for (int c = tid; c < d; c += ST_NT) x1[c] += o[c];          // residual (model.py:94)
   __syncthreads();
   st_layernorm(x1, a.ln_w, a.ln_b, d, a.eps, l1, stat);      // last_layernorm (model.py:96)
-  for (int c = tid; c < d; c += 256) out[b * d + c] = l1[c];
+  for (int c = tid; c < d; c += ST_NT) out[b * d + c] = l1[c];
 }
 
 }  // namespace gr
@@ -191,8 +214,11 @@ int gr_sasrec_tail_launch(const gr_sasrec_params* p, int blk, const float* X, co
                           int64_t B, int32_t n, float* out, hipStream_t st) {
   using namespace gr;
   const int d = p->d, H = p->n_heads;
-  if (d > ST_MAX_D || d % 4 || H > ST_MAX_H || (d / H) % 4 || n > ST_MAX_N || p->mlp > ST_MAX_MLP ||
-      p->mlp % 4 || B > 0x7fffffffLL)
+  auto pow2 = [](int v) { return v >= 1 && (v & (v - 1)) == 0; };
+  // lane groups of k/4 lanes (k = d for the scores / V / Wq / Wo / W1 reads, k = mlp for W2)
+  if (d > ST_MAX_D || d % 4 || !pow2(d / 4) || H > ST_MAX_H || d % H || (d / H) % 4 || !pow2(d / H / 4) ||
+      n > ST_MAX_N || p->mlp > ST_MAX_MLP || p->mlp % 4 || !pow2(p->mlp / 4) || p->mlp / 4 > 64 ||
+      B > 0x7fffffffLL)
     return GR_ERR_UNSUPPORTED;
   SasTailArgs a;
   a.ln_a_w = p->attn_ln_w[blk]; a.ln_a_b = p->attn_ln_b[blk];
@@ -207,6 +233,6 @@ int gr_sasrec_tail_launch(const gr_sasrec_params* p, int blk, const float* X, co
     if (!aligned16(q)) return GR_ERR_UNSUPPORTED;
   a.d = d; a.n = n; a.heads = H; a.mlp = p->mlp; a.eps = p->eps;
   a.scale = (float)std::sqrt(1.0 / (double)(d / H));
-  hipLaunchKernelGGL(sas_tail_kernel, dim3((unsigned)B), dim3(256), 0, st, a, X, KV, out);
+  hipLaunchKernelGGL(sas_tail_kernel, dim3((unsigned)B), dim3(ST_NT), 0, st, a, X, KV, out);
   return check_launch("sasrec tail");
 }
