@@ -46,6 +46,10 @@ static std::atomic<int64_t> g_sas_rowtile{1};
 // rowtile_persist (1: the post-attention row tiles run as a persistent kernel with register-
 // resident weight fragments, 0 (default; 542 vs 553 us per C5 forward): one workgroup per tile).
 static std::atomic<int64_t> g_rowtile_persist{0};
+// rq_resident (1: the quantize kernel stages every level's codebook into LDS once when they fit
+// together, 0 (default): level by level).  Identical results; measured equal at C2 (83.9 vs
+// 84.8 us standalone, scripts/ab_opt.py), so the per-level staging is not what bounds the kernel.
+static std::atomic<int64_t> g_rq_resident{0};
 
 int64_t option(const char* name) {
   if (!strcmp(name, "rq_fused")) return g_rq_fused.load();
@@ -60,6 +64,7 @@ int64_t option(const char* name) {
   if (!strcmp(name, "attn_pair")) return g_attn_pair.load();
   if (!strcmp(name, "sas_rowtile")) return g_sas_rowtile.load();
   if (!strcmp(name, "rowtile_persist")) return g_rowtile_persist.load();
+  if (!strcmp(name, "rq_resident")) return g_rq_resident.load();
   return -1;
 }
 }  // namespace gr
@@ -79,6 +84,7 @@ extern "C" int gr_set_option(const char* name, int64_t value) {
   if (!strcmp(name, "attn_pair") && (value == 0 || value == 1)) { gr::g_attn_pair = value; return GR_OK; }
   if (!strcmp(name, "sas_rowtile") && (value == 0 || value == 1)) { gr::g_sas_rowtile = value; return GR_OK; }
   if (!strcmp(name, "rowtile_persist") && (value == 0 || value == 1)) { gr::g_rowtile_persist = value; return GR_OK; }
+  if (!strcmp(name, "rq_resident") && (value == 0 || value == 1)) { gr::g_rq_resident = value; return GR_OK; }
   return gr::fail(GR_ERR_ARG, std::string("gr_set_option: unknown option or value: ") + name);
 }
 

@@ -46,6 +46,10 @@ __device__ __forceinline__ int cb_off(int c, int q) {
   return c * E + 4 * (q ^ (c & M));
 }
 
+// kch > 0: codebooks streamed through LDS in chunks of kch codes, level by level (three barriers
+// per chunk).  kch == 0 ("resident"): every level's codebook and norms fit in LDS together, so
+// they are staged once at the start (one load phase, one norm phase, two barriers in all) and the
+// level loop runs with no barrier at all.
 template <int E, bool SECOND>
 __global__ __launch_bounds__(RQ_WAVES * 64) void rq_quantize_kernel(
     const float* __restrict__ z, int64_t n, int L, RQLevels lv, int kch, int64_t* __restrict__ idx_out,
@@ -54,9 +58,44 @@ __global__ __launch_bounds__(RQ_WAVES * 64) void rq_quantize_kernel(
   constexpr int HQ = E / 8;            // float4 per lane half
   constexpr int RQ_MAXT = RQMaxT<E>::value;
   extern __shared__ __attribute__((aligned(16))) float sm[];
-  float* cbs = sm;                     // [kch][E] swizzled
-  float* cns = sm + kch * E;           // [kch]
+  const bool resident = kch == 0;
+  int ktot = 0;                        // resident: codes of all levels, each level padded to 32
+  for (int l = 0; l < L; ++l) ktot += (lv.K[l] + 31) & ~31;
+  float* cbs = sm;                     // [kch][E] swizzled (resident: [ktot][E], levels back to back)
+  float* cns = sm + (resident ? ktot : kch) * E;   // [kch] (resident: [ktot])
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r = lane & 31, h = lane >> 5;
+  if (resident) {
+    int off = 0;
+    for (int l = 0; l < L; ++l) {
+      const int K = lv.K[l];
+      for (int f = tid; f < K * (E / 4); f += RQ_WAVES * 64) {
+        const int c = f / (E / 4), q = f % (E / 4);
+        *reinterpret_cast<f32x4*>(cbs + off * E + cb_off<E>(c, q)) =
+            *reinterpret_cast<const f32x4*>(lv.cb[l] + (int64_t)c * E + 4 * q);
+      }
+      off += (K + 31) & ~31;
+    }
+    __syncthreads();
+    off = 0;
+    for (int l = 0; l < L; ++l) {
+      const int K = lv.K[l], kp = (K + 31) & ~31;
+      for (int c = tid; c < kp; c += RQ_WAVES * 64) {
+        float s = __builtin_inff();    // codes past K can never win
+        if (c < K) {
+          s = 0.f;
+#pragma unroll
+          for (int q = 0; q < E / 4; ++q) {
+            const f32x4 v = *reinterpret_cast<const f32x4*>(cbs + off * E + cb_off<E>(c, q));
+#pragma unroll
+            for (int i = 0; i < 4; ++i) s = fmaf(v[i], v[i], s);
+          }
+        }
+        cns[off + c] = s;
+      }
+      off += kp;
+    }
+    __syncthreads();
+  }
   const int t_begin = (int)((int64_t)blockIdx.x * tiles / gridDim.x);
   const int t_end = (int)((int64_t)(blockIdx.x + 1) * tiles / gridDim.x);
   const int my = (t_end - t_begin - w + RQ_WAVES - 1) / RQ_WAVES;  // tiles of this wave (<= MAXT)
@@ -75,9 +114,13 @@ __global__ __launch_bounds__(RQ_WAVES * 64) void rq_quantize_kernel(
     }
   }
 
+  int loff = 0;                        // resident: first (padded) code of level l in the image
   for (int l = 0; l < L; ++l) {
     const int K = lv.K[l];
     const float* cb = lv.cb[l];
+    float* lcbs = resident ? cbs + loff * E : cbs;
+    float* lcns = resident ? cns + loff : cns;
+    if (resident) loff += (K + 31) & ~31;
     float rn[RQ_MAXT], best[RQ_MAXT], second[RQ_MAXT];
     int bi[RQ_MAXT];
 #pragma unroll
@@ -92,31 +135,34 @@ __global__ __launch_bounds__(RQ_WAVES * 64) void rq_quantize_kernel(
       second[i] = __builtin_inff();
       bi[i] = 0x7fffffff;
     }
-    const int c_last = ((K - 1) / kch) * kch;   // first code of the chunk left in LDS
-    for (int c0 = 0; c0 < K; c0 += kch) {
-      const int cnt = min(kch, K - c0);
-      __syncthreads();   // previous chunk / level fully consumed
-      for (int f = tid; f < cnt * (E / 4); f += RQ_WAVES * 64) {
-        const int c = f / (E / 4), q = f % (E / 4);
-        *reinterpret_cast<f32x4*>(cbs + cb_off<E>(c, q)) =
-            *reinterpret_cast<const f32x4*>(cb + (int64_t)(c0 + c) * E + 4 * q);
-      }
-      __syncthreads();
-      // code norms from the LDS image, same k-ordered fma chain as rq_code_norms_kernel
-      for (int c = tid; c < ((cnt + 31) & ~31); c += RQ_WAVES * 64) {
-        float s = __builtin_inff();    // codes past K can never win
-        if (c < cnt) {
-          s = 0.f;
-#pragma unroll
-          for (int q = 0; q < E / 4; ++q) {
-            const f32x4 v = *reinterpret_cast<const f32x4*>(cbs + cb_off<E>(c, q));
-#pragma unroll
-            for (int i = 0; i < 4; ++i) s = fmaf(v[i], v[i], s);
-          }
+    const int step = resident ? K : kch;
+    const int c_last = resident ? 0 : ((K - 1) / kch) * kch;   // first code of the chunk left in LDS
+    for (int c0 = 0; c0 < K; c0 += step) {
+      const int cnt = min(step, K - c0);
+      if (!resident) {
+        __syncthreads();   // previous chunk / level fully consumed
+        for (int f = tid; f < cnt * (E / 4); f += RQ_WAVES * 64) {
+          const int c = f / (E / 4), q = f % (E / 4);
+          *reinterpret_cast<f32x4*>(cbs + cb_off<E>(c, q)) =
+              *reinterpret_cast<const f32x4*>(cb + (int64_t)(c0 + c) * E + 4 * q);
         }
-        cns[c] = s;
+        __syncthreads();
+        // code norms from the LDS image, same k-ordered fma chain as rq_code_norms_kernel
+        for (int c = tid; c < ((cnt + 31) & ~31); c += RQ_WAVES * 64) {
+          float s = __builtin_inff();    // codes past K can never win
+          if (c < cnt) {
+            s = 0.f;
+#pragma unroll
+            for (int q = 0; q < E / 4; ++q) {
+              const f32x4 v = *reinterpret_cast<const f32x4*>(cbs + cb_off<E>(c, q));
+#pragma unroll
+              for (int i = 0; i < 4; ++i) s = fmaf(v[i], v[i], s);
+            }
+          }
+          cns[c] = s;
+        }
+        __syncthreads();
       }
-      __syncthreads();
       const int ct_n = (cnt + 31) >> 5;
 #pragma unroll 1
       for (int ct = 0; ct < ct_n; ++ct) {
@@ -124,11 +170,11 @@ __global__ __launch_bounds__(RQ_WAVES * 64) void rq_quantize_kernel(
         f32x4 a[HQ];
 #pragma unroll
         for (int j = 0; j < HQ; ++j)
-          a[j] = *reinterpret_cast<const f32x4*>(cbs + cb_off<E>(code, HQ * h + j));
+          a[j] = *reinterpret_cast<const f32x4*>(lcbs + cb_off<E>(code, HQ * h + j));
         float cnv[16];
 #pragma unroll
         for (int g4 = 0; g4 < 4; ++g4) {
-          const f32x4 q = *reinterpret_cast<const f32x4*>(cns + ct * 32 + 8 * g4 + 4 * h);
+          const f32x4 q = *reinterpret_cast<const f32x4*>(lcns + ct * 32 + 8 * g4 + 4 * h);
 #pragma unroll
           for (int i = 0; i < 4; ++i) cnv[4 * g4 + i] = q[i];
         }
@@ -179,7 +225,7 @@ __global__ __launch_bounds__(RQ_WAVES * 64) void rq_quantize_kernel(
         f32x4 c[HQ];
 #pragma unroll
         for (int j = 0; j < HQ; ++j)
-          c[j] = in_lds ? *reinterpret_cast<const f32x4*>(cbs + cb_off<E>(b - c_last, HQ * h + j))
+          c[j] = in_lds ? *reinterpret_cast<const f32x4*>(lcbs + cb_off<E>(b - c_last, HQ * h + j))
                         : *reinterpret_cast<const f32x4*>(cb + (int64_t)b * E + (E / 2) * h + 4 * j);
 #pragma unroll
         for (int j = 0; j < HQ; ++j)
@@ -212,11 +258,16 @@ static int launch_norms(const float* cb, int K, int e, float* cn, hipStream_t st
 template <int E>
 static int launch_quantize_e(const float* z, int64_t n, int L, const RQLevels& lv, int64_t* idx,
                              float* best, float* gap, hipStream_t st) {
-  int kmax = 0;
-  for (int l = 0; l < L; ++l) kmax = lv.K[l] > kmax ? lv.K[l] : kmax;
+  int kmax = 0, ktot = 0;
+  for (int l = 0; l < L; ++l) {
+    kmax = lv.K[l] > kmax ? lv.K[l] : kmax;
+    ktot += (lv.K[l] + 31) & ~31;
+  }
   const int kch_max = 1024 * 32 / E;                         // 128 KiB of codebook per chunk
-  const int kch = ((kmax < kch_max ? kmax : kch_max) + 31) & ~31;
-  const size_t lds = (size_t)kch * E * 4 + (size_t)kch * 4;
+  // every level resident in LDS at once when they fit in 128 KiB (C2: 3 x 256 x 32 -> 99 KiB)
+  const bool resident = option("rq_resident") != 0 && (size_t)ktot * (E + 1) * 4 <= 128 * 1024;
+  const int kch = resident ? 0 : ((kmax < kch_max ? kmax : kch_max) + 31) & ~31;
+  const size_t lds = resident ? (size_t)ktot * (E + 1) * 4 : (size_t)kch * E * 4 + (size_t)kch * 4;
   // persistent: one 8-wave workgroup per CU (2 waves per SIMD at this register budget), each with
   // a contiguous balanced range of tiles; more workgroups only when a range would exceed the
   // register-resident residuals (RQ_WAVES x MT tiles)
