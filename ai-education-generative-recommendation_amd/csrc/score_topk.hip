@@ -80,16 +80,19 @@ __device__ __forceinline__ int64_t phys_chunk(int64_t v, int mode, int s) {
 // so two workgroups share each CU and one wave's list insertions / counts overlap another's MFMAs.
 template <int D> struct TkUT { static constexpr int value = 1; };
 
-template <int D, int KC>
+// MODE 0: the exact pass (every chunk); MODE 1: the sample pass.  A template parameter so the
+// two passes are distinct kernels in a profile (their launch grids can coincide).
+template <int D, int KC, int MODE>
 __global__ __launch_bounds__(256, 2) void score_topk_kernel(
     const float* __restrict__ h, int64_t B, const float* __restrict__ table, int64_t rows,
     const float* __restrict__ thr, int mask_col0, unsigned long long* __restrict__ cnt_out,
-    const float* __restrict__ tinit, int tstride, int64_t vchunks, int mode, int s,
+    const float* __restrict__ tinit, int tstride, int64_t vchunks, int s,
     float* __restrict__ cv, int64_t* __restrict__ ci, int64_t seg_stride, int seg_off, int ublocks,
     int slices, int ablate) {
   constexpr int KG = D / 32;
   constexpr int P = D + 4;
   constexpr int LV = TK_CHUNK * D / 4 / 256;
+  constexpr int mode = MODE;
   __shared__ __attribute__((aligned(16))) float tab[2][TK_CHUNK * P];
   const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, hh = lane >> 5;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -336,11 +339,22 @@ static void launch_pass(int d, dim3 grid, hipStream_t st, const float* h, int64_
                         const float* tinit, int tstride, int64_t vchunks, int mode, int s, float* cv,
                         int64_t* ci, int64_t seg_stride, int seg_off, int ub, int sl, int ablate) {
   const dim3 blk(256);
-  switch (d) {
-    case 32: hipLaunchKernelGGL((score_topk_kernel<32, KC>), grid, blk, 0, st, h, B, table, rows, thr, mask_col0, cnt, tinit, tstride, vchunks, mode, s, cv, ci, seg_stride, seg_off, ub, sl, ablate); break;
-    case 64: hipLaunchKernelGGL((score_topk_kernel<64, KC>), grid, blk, 0, st, h, B, table, rows, thr, mask_col0, cnt, tinit, tstride, vchunks, mode, s, cv, ci, seg_stride, seg_off, ub, sl, ablate); break;
-    default: hipLaunchKernelGGL((score_topk_kernel<128, KC>), grid, blk, 0, st, h, B, table, rows, thr, mask_col0, cnt, tinit, tstride, vchunks, mode, s, cv, ci, seg_stride, seg_off, ub, sl, ablate); break;
+#define GR_TK_PASS(DD, MM) hipLaunchKernelGGL((score_topk_kernel<DD, KC, MM>), grid, blk, 0, st, h, B, table, rows, thr, \
+                                             mask_col0, cnt, tinit, tstride, vchunks, s, cv, ci, seg_stride, seg_off, ub, sl, ablate)
+  if (mode == 1) {
+    switch (d) {
+      case 32: GR_TK_PASS(32, 1); break;
+      case 64: GR_TK_PASS(64, 1); break;
+      default: GR_TK_PASS(128, 1); break;
+    }
+    return;
   }
+  switch (d) {
+    case 32: GR_TK_PASS(32, 0); break;
+    case 64: GR_TK_PASS(64, 0); break;
+    default: GR_TK_PASS(128, 0); break;
+  }
+#undef GR_TK_PASS
 }
 
 template <int KC>
