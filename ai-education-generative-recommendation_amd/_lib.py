@@ -13,6 +13,9 @@ LIB_PATH = os.path.join(_PKG, "lib", "libgr_amd.so")
 
 GR_ACT_NONE = 0
 GR_ACT_RELU = 1
+GR_ACT_SIGMOID = 2
+GR_ACT_TANH = 3
+GR_ACT_LEAKYRELU = 4
 GR_MAX_LEVELS = 8
 GR_MAX_LINEAR = 8
 

@@ -132,6 +132,9 @@ __global__ __launch_bounds__(256, 2) void linear_f32_kernel(
           float o = acc[i][j][v];
           if (bias != nullptr) o = o + bv;
           if (ACT == GR_ACT_RELU) o = (o < 0.f) ? 0.f : o;  // NaN propagates like torch.relu
+          if (ACT == GR_ACT_SIGMOID) o = 1.0f / (1.0f + expf(-o));
+          if (ACT == GR_ACT_TANH) o = tanhf(o);
+          if (ACT == GR_ACT_LEAKYRELU) o = (o < 0.f) ? 0.01f * o : o;   // nn.LeakyReLU() slope
           if (RES) o = rv[v] + o;
           y[row * ldy + col] = o;
         }
@@ -164,6 +167,12 @@ static int launch_tile(const float* x, int64_t m, int k, const float* w, int n, 
   GR_LIN_CASE(GR_ACT_RELU, false, true)
   GR_LIN_CASE(GR_ACT_RELU, true, false)
   GR_LIN_CASE(GR_ACT_RELU, true, true)
+  GR_LIN_CASE(GR_ACT_SIGMOID, false, false)
+  GR_LIN_CASE(GR_ACT_SIGMOID, false, true)
+  GR_LIN_CASE(GR_ACT_TANH, false, false)
+  GR_LIN_CASE(GR_ACT_TANH, false, true)
+  GR_LIN_CASE(GR_ACT_LEAKYRELU, false, false)
+  GR_LIN_CASE(GR_ACT_LEAKYRELU, false, true)
 #undef GR_LIN_CASE
   return fail(GR_ERR_ARG, "gr_linear_f32: bad activation");
 }
@@ -181,7 +190,8 @@ int gr_linear_launch(const float* x, int64_t m, int32_t k, const float* w, int32
   if (!aligned16(x) || !aligned16(w))
     return fail(GR_ERR_ARG, "gr_linear_f32: x and w must be 16-byte aligned");
   if (ldy < n || (residual && ldr < n)) return fail(GR_ERR_ARG, "gr_linear_f32: bad row stride");
-  if (act != GR_ACT_NONE && act != GR_ACT_RELU) return fail(GR_ERR_ARG, "gr_linear_f32: bad act");
+  if (act < GR_ACT_NONE || act > GR_ACT_LEAKYRELU) return fail(GR_ERR_ARG, "gr_linear_f32: bad act");
+  if (act > GR_ACT_RELU && residual) return fail(GR_ERR_UNSUPPORTED, "gr_linear_f32: this act takes no residual");
   if (n >= 128) return launch_tile<128, 128, 2, 2>(x, m, k, w, n, bias, residual, ldr, act, y, ldy, stream);
   if (n > 32) return launch_tile<128, 64, 2, 2>(x, m, k, w, n, bias, residual, ldr, act, y, ldy, stream);
   return launch_tile<128, 32, 4, 1>(x, m, k, w, n, bias, residual, ldr, act, y, ldy, stream);

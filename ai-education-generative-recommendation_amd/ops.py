@@ -46,7 +46,8 @@ def check_errors(device=None):
 
 
 def linear(x, weight, bias=None, act="none", residual=None, out=None):
-    """``act(x @ weight.T + bias) (+ residual)`` — F.linear (+ ReLU) on the matrix cores."""
+    """``act(x @ weight.T + bias) (+ residual)`` — F.linear (+ the activations of
+    RQ-VAE/models/layers.py:45-67: relu, sigmoid, tanh, leakyrelu) on the matrix cores."""
     L.require_gpu(x, weight)
     x2 = L.as_f32(x).reshape(-1, x.shape[-1])
     w = L.as_f32(weight)
@@ -57,7 +58,8 @@ def linear(x, weight, bias=None, act="none", residual=None, out=None):
     b = L.as_f32(bias) if bias is not None else None
     r = L.as_f32(residual).reshape(m, n) if residual is not None else None
     y = out if out is not None else torch.empty((m, n), dtype=torch.float32, device=x.device)
-    a = {"none": L.GR_ACT_NONE, "relu": L.GR_ACT_RELU}[act]
+    a = {"none": L.GR_ACT_NONE, "relu": L.GR_ACT_RELU, "sigmoid": L.GR_ACT_SIGMOID, "tanh": L.GR_ACT_TANH,
+         "leakyrelu": L.GR_ACT_LEAKYRELU}[act]
     with torch.cuda.device(x.device):
         L.check(L.lib().gr_linear_f32(L.ptr(x2), m, k, L.ptr(w), n, L.ptr(b), L.ptr(r),
                                       n if r is not None else 0, a, L.ptr(y), n,

@@ -43,9 +43,33 @@ def near_tie_rows(best, gap, znorm2):
     return (gap <= near_tie_bound(best, gap, znorm2)).any(1)
 
 
+_ACTS = {"sigmoid": nn.Sigmoid, "tanh": nn.Tanh, "relu": nn.ReLU, "leakyrelu": nn.LeakyReLU}
+
+
+def _act_name(activation):
+    """activation_layer of RQ-VAE/models/layers.py:45-67 -> the kernel epilogue name (None: none)."""
+    if activation is None:
+        return None
+    if isinstance(activation, str):
+        a = activation.lower()
+        if a == "none":
+            return None
+        if a in _ACTS:
+            return a
+        raise NotImplementedError(f"activation function {activation} is not implemented")
+    for name, cls in _ACTS.items():
+        if isinstance(activation, type) and issubclass(activation, cls):
+            return name
+    raise NotImplementedError(f"gr_amd kernels implement sigmoid / tanh / relu / leakyrelu, not {activation}")
+
+
 class MLPLayers(nn.Module):
-    """Module tree of RQ-VAE/models/layers.py:9-40 (Dropout, Linear, [BN], ReLU per layer; no
-    activation after the last Linear), xavier_normal_ weights and zero biases."""
+    """Module tree of RQ-VAE/models/layers.py:9-40 (Dropout, Linear, [BatchNorm1d], activation per
+    layer; none after the last Linear), xavier_normal_ weights and zero biases.
+
+    Eval forward on the kernels: a BatchNorm1d (running statistics) folds into the Linear before it
+    (W' = W * s, b' = (b - mean) * s + beta, s = gamma / sqrt(var + eps)); ReLU MLPs run the fused
+    encoder kernel (gr_rq_mlp_f32), other activations the gr_linear_f32 epilogues."""
 
     def __init__(self, layers, dropout=0.0, activation="relu", bn=False):
         super().__init__()
@@ -53,6 +77,7 @@ class MLPLayers(nn.Module):
         self.dropout = dropout
         self.activation = activation
         self.use_bn = bn
+        self.act = _act_name(activation)
         mods = []
         last = len(layers) - 2
         for idx, (i, o) in enumerate(zip(layers[:-1], layers[1:])):
@@ -60,11 +85,8 @@ class MLPLayers(nn.Module):
             mods.append(nn.Linear(i, o))
             if bn and idx != last:
                 mods.append(nn.BatchNorm1d(num_features=o))
-            if activation is not None and str(activation).lower() != "none" and idx != last:
-                if str(activation).lower() != "relu":
-                    raise NotImplementedError("gr_amd encoder kernels implement ReLU only "
-                                              "(the activation RQ-VAE/main.py uses)")
-                mods.append(nn.ReLU())
+            if self.act is not None and idx != last:
+                mods.append(_ACTS[self.act]() if isinstance(activation, str) else activation())
         self.mlp_layers = nn.Sequential(*mods)
         self.apply(self._init_weights)
 
@@ -78,25 +100,43 @@ class MLPLayers(nn.Module):
     def linears(self):
         return [m for m in self.mlp_layers if isinstance(m, nn.Linear)]
 
-    def eval_forward(self, x):
-        """layers.py:42-43 in eval mode on ``gr_linear_f32`` layer by layer (any widths; ReLU after
-        every Linear but the last) — the decoder of the no-grad forward."""
-        if self.use_bn:
-            raise NotImplementedError("gr_amd: BatchNorm MLPs are not supported")
+    def folded(self):
+        """(weights, biases) of the eval-mode layers with each BatchNorm1d folded into its Linear."""
         lin = self.linears()
+        bns = [m for m in self.mlp_layers if isinstance(m, nn.BatchNorm1d)]
+        ws, bs = [], []
         for i, m in enumerate(lin):
-            x = ops.linear(x, m.weight.detach(), m.bias.detach(),
-                           act="relu" if i + 1 < len(lin) else "none")
+            w, b = m.weight.detach(), m.bias.detach()
+            if self.use_bn and i < len(lin) - 1:
+                bn = bns[i]
+                s = torch.rsqrt(bn.running_var + bn.eps)
+                if bn.weight is not None:
+                    s = s * bn.weight.detach()
+                w = w * s[:, None]
+                b = (b - bn.running_mean) * s
+                if bn.bias is not None:
+                    b = b + bn.bias.detach()
+            ws.append(w.contiguous())
+            bs.append(b.contiguous())
+        return ws, bs
+
+    def eval_forward(self, x):
+        """layers.py:42-43 in eval mode on ``gr_linear_f32`` layer by layer (any widths; the
+        activation after every Linear but the last) — the decoder of the no-grad forward."""
+        ws, bs = self.folded() if self.use_bn else ([m.weight.detach() for m in self.linears()],
+                                                   [m.bias.detach() for m in self.linears()])
+        for i, (w, b) in enumerate(zip(ws, bs)):
+            x = ops.linear(x, w, b, act=(self.act or "none") if i + 1 < len(ws) else "none")
         return x
 
     def forward(self, x):
-        if self.use_bn:
-            raise NotImplementedError("gr_amd: BatchNorm encoders are not supported (bn=False in "
-                                      "RQ-VAE/main.py)")
-        if self.training and self.dropout > 0:
-            raise RuntimeError("gr_amd MLPLayers runs the eval-mode encoder: call .eval()")
-        lin = self.linears()
-        return ops.rq_mlp(x, [m.weight.detach() for m in lin], [m.bias.detach() for m in lin])
+        if self.training and (self.dropout > 0 or self.use_bn):
+            raise RuntimeError("gr_amd MLPLayers runs the eval-mode encoder: call .eval() (dropout / "
+                               "BatchNorm batch statistics are train-mode only)")
+        if self.act not in ("relu", None) or self.act is None and len(self.linears()) > 1:
+            return self.eval_forward(x)
+        ws, bs = self.folded()
+        return ops.rq_mlp(x, ws, bs)
 
 
 class VectorQuantizer(nn.Module):
@@ -245,8 +285,9 @@ class RQVAE(nn.Module):
         return loss_recon + self.quant_loss_weight * quant_loss, loss_recon
 
     def _check_encode(self, xs, use_sk):
-        if self.bn:
-            raise NotImplementedError("gr_amd: bn=True encoders are not supported")
+        if self.training and self.bn:
+            raise RuntimeError("gr_amd RQVAE.get_indices runs the eval-mode encoder: call .eval() "
+                               "(BatchNorm uses batch statistics in train mode)")
         if self.training and self.dropout_prob > 0:
             raise RuntimeError("gr_amd RQVAE.get_indices runs the eval-mode encoder: call .eval() "
                                "(dropout is active in train mode)")
@@ -261,13 +302,17 @@ class RQVAE(nn.Module):
         whole batch (vq.py:76-84), as the reference does; the batch is one group."""
         self._check_encode(xs, use_sk)
         if use_sk and any(q.sk_epsilon > 0 for q in self.rq.vq_layers):
-            lin = self.encoder.linears()
-            ws, bs = [m.weight.detach() for m in lin], [m.bias.detach() for m in lin]
+            ws, bs = self.encoder.folded()
             return ops.rq_encode_sk(xs, ws, bs, self.rq.codebooks(), self.sk_eps(), self.rq.sk_iters)
         return ops.rq_encode(xs, binding=self.encode_binding())
 
     def encode_binding(self):
-        """The cached device-pointer view of the encoder and codebooks (ops.rq_binding)."""
+        """The cached device-pointer view of the encoder and codebooks (ops.rq_binding).  With
+        BatchNorm the folded weights are recomputed per call (the running statistics may change
+        in place), so that binding is never cached."""
+        if self.bn:
+            ws, bs = self.encoder.folded()
+            return ops.RqBinding(ws, bs, self.rq.codebooks())
         return ops.rq_binding(self, self._encode_params)
 
     def _encode_params(self):
@@ -282,9 +327,8 @@ class RQVAE(nn.Module):
         """``torch.cat([get_indices(g, use_sk=True) for g in groups])`` for consecutive row groups
         of ``xs`` in one launch — the per-group loop of RQ-VAE/infer.py:116-127."""
         self._check_encode(xs, True)
-        lin = self.encoder.linears()
-        return ops.rq_encode_sk(xs, [m.weight.detach() for m in lin], [m.bias.detach() for m in lin],
-                                self.rq.codebooks(), self.sk_eps(), self.rq.sk_iters, group_sizes)
+        ws, bs = self.encoder.folded()
+        return ops.rq_encode_sk(xs, ws, bs, self.rq.codebooks(), self.sk_eps(), self.rq.sk_iters, group_sizes)
 
     @torch.no_grad()
     def get_indices_certified(self, xs):

@@ -38,6 +38,9 @@ extern "C" {
 
 #define GR_ACT_NONE 0
 #define GR_ACT_RELU 1
+#define GR_ACT_SIGMOID 2         /* the activations of RQ-VAE/models/layers.py:45-67 besides   */
+#define GR_ACT_TANH 3            /* ReLU (nn.Sigmoid / nn.Tanh / nn.LeakyReLU(0.01)); gr_linear */
+#define GR_ACT_LEAKYRELU 4       /* only, without a residual                                     */
 
 /* Library identification ("gr_amd <version> gfx950"). */
 const char* gr_version(void);
@@ -74,7 +77,8 @@ int64_t gr_get_option(const char* name);
  * Replaces nn.Linear -> F.linear -> addmm (+ nn.ReLU): RQ-VAE/models/layers.py:23-30 (encoder),
  * SASRec/model.py:37-45 (FFN), torch functional.py:5785-5830 / :6600 (MHA in/out projections) and
  * SASRec/model.py:107 (scoring: w = item table, bias = NULL).
- * bias, residual may be NULL.  `residual` may alias `y` (in-place residual add).
+ * bias, residual may be NULL.  `residual` may alias `y` (in-place residual add).  act: GR_ACT_*
+ * (SIGMOID / TANH / LEAKYRELU only with residual = NULL).
  * Requires k % 4 == 0 and 16-byte aligned x, w.  ldy / ldr are row strides (elements) of y / residual. */
 int gr_linear_f32(const float* x, int64_t m, int32_t k, const float* w, int32_t n,
                   const float* bias, const float* residual, int64_t ldr, int32_t act,

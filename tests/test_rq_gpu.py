@@ -296,3 +296,58 @@ def test_binding_cache_sees_weight_changes(dev):
     w.data = w.data.flip(0).clone()                           # new storage
     c = m.get_indices(xg)
     assert torch.equal(c, fresh()) and torch.equal(c, a)
+
+
+def test_batchnorm_encoder_matches_reference(dev, rq_path, parity_log):
+    """RQVAE(bn=True) (RQ-VAE/models/layers.py:25-26) in eval mode: the BatchNorm folds into its
+    Linear; IDs equal the reference's except certified near-ties (tests/golden/make_golden_bn.py)."""
+    from gr_amd import RQVAE
+    x, sd, out, meta = gl.rq_inputs("rq_bn_3x256")
+    m = RQVAE(in_dim=768, num_emb_list=[meta["K"]] * meta["L"], e_dim=32, layers=[256, 128], dropout_prob=0.1,
+              bn=True, sk_epsilons=[0.0] * meta["L"])
+    missing, unexpected = m.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()}, strict=False)
+    assert not unexpected and all(k.startswith("decoder.") for k in missing)
+    m = m.to(dev).eval()
+    xg = torch.from_numpy(x).to(dev)
+    idx = m.get_indices(xg).cpu().numpy()
+    diff = (idx != out["idx_full"]).any(1)
+    tie = near_tie_rows(out)
+    _, flags = m.get_indices_certified(xg)
+    flags = flags.cpu().numpy()
+    z = m.encoder(xg).cpu().numpy()
+    zerr = (np.linalg.norm(z.astype(np.float64) - out["z"], axis=1) / np.linalg.norm(out["z"], axis=1)).max()
+    parity_log(kind="rq_ids", fixture="rq_bn_3x256", path="fused" if rq_path else "layerwise", rows=len(diff),
+               rows_differ=int(diff.sum()), rows_ref_neartie=int(tie.sum()), rows_product_flagged=int(flags.sum()),
+               max_row_z_ratio=float(zerr))
+    assert not (diff & ~tie).any() and not (diff & ~flags).any()
+    assert diff.sum() <= 2
+    from gr_amd.rqvae import Z_TAU
+    assert zerr <= Z_TAU
+
+
+@pytest.mark.parametrize("act", ["sigmoid", "tanh", "leakyrelu", "none", "relu"])
+@pytest.mark.parametrize("bn", [False, True])
+def test_mlp_activations_and_batchnorm_vs_torch(act, bn, dev):
+    """MLPLayers with every activation of RQ-VAE/models/layers.py:45-67 and optional BatchNorm, eval
+    mode, against the same module tree run by torch on the CPU (fp32, 1e-5 relative)."""
+    from gr_amd.rqvae import MLPLayers
+    torch.manual_seed(7)
+    m = MLPLayers([96, 64, 48, 16], dropout=0.1, activation=act, bn=bn)
+    with torch.no_grad():
+        for mod in m.mlp_layers:
+            if isinstance(mod, torch.nn.BatchNorm1d):
+                mod.running_mean.normal_(0, 0.3)
+                mod.running_var.uniform_(0.5, 2.0)
+                mod.weight.normal_(1, 0.1)
+                mod.bias.normal_(0, 0.1)
+    m.eval()
+    x = torch.randn(300, 96)
+    with torch.no_grad():
+        ref = m.mlp_layers(x)
+    mg = m.to(dev)
+    with torch.no_grad():
+        got = mg(x.to(dev)).cpu()
+        got2 = mg.eval_forward(x.to(dev)).cpu()
+    scale = ref.abs().max()
+    assert (got - ref).abs().max() <= 1e-5 * scale
+    assert (got2 - ref).abs().max() <= 1e-5 * scale
