@@ -139,6 +139,85 @@ def _sharded_rank_topk_fused(h, table_shard, row_offset, targets, k, group, mask
     return _exchange(cnt, v, i, k, group, world)
 
 
+@torch.no_grad()
+def sharded_rank_topk_batches(hs, table_shard, row_offset, targets, k=10, group=None, mask_row0=True,
+                              scorer=None, counter=None, topk_fn=None):
+    """``[sharded_rank_topk(h, ...) for h in hs]`` with the exchange of each batch overlapped with
+    the scoring of the next: the collectives are issued ``async_op=True`` (RCCL runs
+    them on its own stream after the scoring they depend on; the host never blocks), in the order
+      targets(b+1) -> scoring(b) -> [exchange(b) | scoring(b+1)] -> merge(b) ...
+    so the target-logit all-reduce of batch b+1 runs during batch b's scoring and batch b's count
+    all-reduce + candidate all-gather during batch b+1's.  Results are identical to the sequential
+    calls.  ``targets`` is a list of per-batch target tensors."""
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    if world == 1 or len(hs) <= 1:
+        return [sharded_rank_topk(h, table_shard, row_offset, t, k, group, mask_row0, scorer, counter, topk_fn)
+                for h, t in zip(hs, targets)]
+    rows = table_shard.shape[0]
+    fused = (scorer is None and counter is None and topk_fn is None and hs[0].is_cuda and rows > 0
+             and 1 <= k <= 16 and hs[0].shape[1] in (32, 64, 128))
+    if not fused:
+        s_fn, c_fn, t_fn = _default_ops()
+        scorer, counter, topk_fn = scorer or s_fn, counter or c_fn, topk_fn or t_fn
+    m0 = bool(mask_row0 and row_offset == 0)
+    kk = min(k, rows)
+
+    def targets_start(b):   # the owner's target logits -> all-reduce (async)
+        h, t = hs[b], targets[b].reshape(-1).to(torch.int64)
+        own = (t >= row_offset) & (t < row_offset + rows)
+        local = torch.where(own, t - row_offset, torch.zeros_like(t))
+        logits = None
+        if fused:
+            from . import ops
+            tl = ops.score_pairs(h, table_shard, local, mask_col0=m0)
+        else:
+            logits = scorer(h, table_shard)
+            if m0:
+                logits[:, 0] = -1e9                                  # evaluate.py:27
+            tl = logits.gather(1, local.unsqueeze(1)).squeeze(1)
+        ts = torch.where(own, tl, torch.zeros(t.shape, dtype=tl.dtype, device=tl.device))
+        return ts, logits, dist.all_reduce(ts, op=dist.ReduceOp.SUM, group=group, async_op=True)
+
+    def score_start(b, st):   # local counts + top-k, then their exchange (async)
+        ts, logits, work = st
+        work.wait()
+        if fused:
+            from . import ops
+            v, i, cnt = ops.score_topk(hs[b], table_shard, kk, row_offset, thresholds=ts, mask_col0=m0)
+        else:
+            cnt = counter(logits, ts)
+            v, i = topk_fn(logits, kk, row_offset)
+        if kk < k:
+            v = torch.cat([v, torch.full((v.shape[0], k - kk), float("-inf"), dtype=v.dtype, device=v.device)], 1)
+            i = torch.cat([i, torch.full((i.shape[0], k - kk), -1, dtype=i.dtype, device=i.device)], 1)
+        packed = torch.cat([i, v.contiguous().view(torch.int32).to(torch.int64)], 1)
+        parts = [torch.empty_like(packed) for _ in range(world)]
+        return (cnt, parts, dist.all_reduce(cnt, op=dist.ReduceOp.SUM, group=group, async_op=True),
+                dist.all_gather(parts, packed, group=group, async_op=True))
+
+    def finish(sc):
+        cnt, parts, w1, w2 = sc
+        w1.wait()
+        w2.wait()
+        ids = torch.cat([p_[:, :k] for p_ in parts], 1)
+        vals = torch.cat([p_[:, k:].to(torch.int32).view(torch.float32) for p_ in parts], 1)
+        v, i = merge_topk(vals, ids, k)
+        return cnt + 1, v, i
+
+    out, prev = [], None
+    pend = targets_start(0)
+    for b in range(len(hs)):
+        cur = pend
+        if b + 1 < len(hs):
+            pend = targets_start(b + 1)
+        sc = score_start(b, cur)
+        if prev is not None:
+            out.append(finish(prev))
+        prev = sc
+    out.append(finish(prev))
+    return out
+
+
 def hr_ndcg(ranks, top_k=10):
     """HR@k / NDCG@k of SASRec/evaluate.py:36-47 (per-user float64 terms, then the mean)."""
     import numpy as np

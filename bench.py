@@ -68,6 +68,8 @@ def parse():
     ap.add_argument("--c4-items", type=int, default=10_000_000)
     ap.add_argument("--c5-batch", type=int, default=512)
     ap.add_argument("--c5-items", type=int, default=1_000_000)
+    ap.add_argument("--c5-pipeline", type=int, default=1,
+                    help="C5 at N>1: user sub-batches per step whose exchange overlaps the next one's scoring")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--train-batch", type=int, default=128, help="sas_train leg: users per rank per step")
     ap.add_argument("--legs", default="", help="comma list of legs to run (default all): " + ",".join(LEGS))
@@ -322,10 +324,17 @@ def bench_sas_c5(a, world, rank, dev):
     lo, hi = D.shard_range(items + 1, rank, world)
     shard = model.item_emb.weight.detach()[lo:hi]
 
+    P = max(1, a.c5_pipeline)
+    cuts = [B * j // P for j in range(P + 1)]
+
     def step():
         hl = model.last_hidden(seqs[ulo:uhi])
         h = D.all_gather_rows(hl, sizes=usizes) if world > 1 else hl
-        return D.sharded_rank_topk(h, shard, lo, targets, k=10)
+        if P == 1:
+            return D.sharded_rank_topk(h, shard, lo, targets, k=10)
+        # the exchange of sub-batch j overlapped with the scoring of sub-batch j+1
+        return D.sharded_rank_topk_batches([h[x:y] for x, y in zip(cuts[:-1], cuts[1:])], shard, lo,
+                                           [targets[x:y] for x, y in zip(cuts[:-1], cuts[1:])], k=10)
 
     steps, warm = max(2, min(a.steps, 10)), 2
     wall, dev_ms = timed(step, steps, warm, world)
@@ -338,7 +347,7 @@ def bench_sas_c5(a, world, rank, dev):
             "config": {"workload": "sas_c5: SASRec d 128, n 200, 2 blocks, 1M-item catalog, rank + top-10",
                        "users_per_step": B, "catalog_rows": items + 1, "rows_per_rank": hi - lo,
                        "parallelism": f"catalog-sharded x{world}: RCCL all-gather h + top-k, all-reduce counts"
-                       if world > 1 else "single shard"},
+                       + (f", {P} pipelined sub-batches" if P > 1 else "") if world > 1 else "single shard"},
             "roofline": roofline("score_topk_kernel<128,10>", 2 * d * (hi - lo) * B, topk_ms, launches=2,
                                  note="one gr_score_topk_f32 call: sample pass + exact pass + 2 merge "
                                       "kernels; flop counts the exact pass only"),

@@ -50,7 +50,22 @@ def _worker(rank, world, port, data, out):
     sizes = [D.shard_range(h.shape[0], r, world)[1] - D.shard_range(h.shape[0], r, world)[0]
              for r in range(world)]
     assert torch.equal(D.all_gather_rows(h[ulo:uhi], sizes=sizes), hg)   # known sizes: no exchange
-    out[rank] = (rk, v, i, hg)
+    # the pipelined form over 3 user batches (exchange of batch b overlapped with batch b+1)
+    cuts = [0, 11, 12, B_ := h.shape[0]]
+    hs = [h[a:b] for a, b in zip(cuts[:-1], cuts[1:])]
+    ts = [targets[a:b] for a, b in zip(cuts[:-1], cuts[1:])]
+    res = D.sharded_rank_topk_batches(hs, table[lo:hi], lo, ts, k, scorer=cpu_score, counter=cpu_count,
+                                      topk_fn=cpu_topk)
+    assert len(res) == 3 and B_ == h.shape[0]
+    # identical to the sequential per-batch calls (the CPU stand-in matmul is not batch-invariant,
+    # so the reference for the pipelined form is the same batches run one after another)
+    for (hb, tb), (r1, v1, i1) in zip(zip(hs, ts), res):
+        r0, v0, i0 = D.sharded_rank_topk(hb, table[lo:hi], lo, tb, k, scorer=cpu_score, counter=cpu_count,
+                                         topk_fn=cpu_topk)
+        assert torch.equal(r0, r1) and torch.equal(v0, v1) and torch.equal(i0, i1)
+    pr = torch.cat([r_[0] for r_ in res])
+    pi = torch.cat([r_[2] for r_ in res])
+    out[rank] = (rk, v, i, hg, (pr, pi))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -81,10 +96,11 @@ def test_catalog_sharded_rank_topk_equals_full_catalog(world):
     ts = lg.gather(1, targets.unsqueeze(1))
     ref_rank = (lg > ts).sum(1) + 1
     ref_v, ref_i = cpu_topk(lg, k, 0)
-    for rk, v, i, hg in res:
+    for rk, v, i, hg, (pr, pi) in res:
         assert torch.equal(rk, ref_rank)
         assert torch.equal(i, ref_i) and torch.equal(v, ref_v)
         assert torch.equal(hg, h)
+        assert torch.equal(pr, ref_rank) and torch.equal(pi, ref_i)
 
 
 def test_merge_topk_tie_and_padding_rules():

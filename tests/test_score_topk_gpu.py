@@ -166,7 +166,12 @@ def _gloo_gpu_worker(rank, world, port, data, out):
     h, table, targets, k = (t.cuda() if torch.is_tensor(t) else t for t in data)
     lo, hi = D.shard_range(table.shape[0], rank, world)
     rk, v, i = D.sharded_rank_topk(h, table[lo:hi].contiguous(), lo, targets, k)   # fused HIP path
-    out[rank] = (rk.cpu(), v.cpu(), i.cpu())
+    # pipelined over 3 batches: async exchange of batch b overlapped with batch b+1's kernels
+    cuts = [0, 40, 41, h.shape[0]]
+    res = D.sharded_rank_topk_batches([h[a:b] for a, b in zip(cuts[:-1], cuts[1:])], table[lo:hi].contiguous(),
+                                      lo, [targets[a:b] for a, b in zip(cuts[:-1], cuts[1:])], k)
+    out[rank] = (rk.cpu(), v.cpu(), i.cpu(), torch.cat([r_[0] for r_ in res]).cpu(),
+                 torch.cat([r_[1] for r_ in res]).cpu(), torch.cat([r_[2] for r_ in res]).cpu())
     dist.barrier()
     dist.destroy_process_group()
 
@@ -199,6 +204,7 @@ def test_catalog_sharded_fused_multi_rank(world, dev):
     out = mgr.dict()
     mp.spawn(_gloo_gpu_worker, args=(world, port, (h, table, tg, k), out), nprocs=world, join=True)
     for r in range(world):
-        rk, v, i = out[r]
+        rk, v, i, pr, pv, pi = out[r]
         assert torch.equal(rk, ref_rank)
         assert torch.equal(i, ref_i) and torch.equal(v, ref_v)
+        assert torch.equal(pr, ref_rank) and torch.equal(pi, ref_i) and torch.equal(pv, ref_v)
