@@ -84,7 +84,9 @@ def build_stamps(verbose=False, extra=(), suffix=""):
 
 if __name__ == "__main__":
     import sys
-    if "--stamps" in sys.argv:
+    if "--abl" in sys.argv:   # diagnostic library with one GR_ABL_* macro (never loaded by the product)
+        print(build_stamps(extra=[f"-D{sys.argv[sys.argv.index('--abl') + 1]}"], suffix="_abl"))
+    elif "--stamps" in sys.argv:
         print(build_stamps())
         print(build_stamps(extra=["-DGR_ABL_NOW1"], suffix="_now1"))
         print(build_stamps(extra=["-DGR_ABL_NOX"], suffix="_nox"))

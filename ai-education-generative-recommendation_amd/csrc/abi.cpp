@@ -43,13 +43,16 @@ static std::atomic<int64_t> g_attn_pair{0};
 // sas_rowtile (1: d = 128 layer-wise forwards fuse everything between attention launches into
 // row-tile kernels, sasrec_rowtile.hip; 0: one kernel per op).  A/B timing and a second path.
 static std::atomic<int64_t> g_sas_rowtile{1};
-// rowtile_persist (1: the post-attention row tiles run as a persistent kernel with register-
-// resident weight fragments, 0 (default; 542 vs 553 us per C5 forward): one workgroup per tile).
-static std::atomic<int64_t> g_rowtile_persist{0};
 // rq_resident (1: the quantize kernel stages every level's codebook into LDS once when they fit
 // together, 0 (default): level by level).  Identical results; measured equal at C2 (83.9 vs
 // 84.8 us standalone, scripts/ab_opt.py), so the per-level staging is not what bounds the kernel.
 static std::atomic<int64_t> g_rq_resident{0};
+// score_slice_major (direct-store scoring: 1 = an XCD's workgroups share catalog slices across
+// user blocks (default: 255 vs 261 us at C3, scripts/ab_opt.py), 0 = they share a user block).
+static std::atomic<int64_t> g_score_slice_major{1};
+// attn_occ1 (hd 128 attention: 1 = one workgroup per CU, 512 registers; 0 = two, 256 registers
+// with a few spills).  Identical results; A/B timing.
+static std::atomic<int64_t> g_attn_occ1{0};
 
 int64_t option(const char* name) {
   if (!strcmp(name, "rq_fused")) return g_rq_fused.load();
@@ -63,8 +66,9 @@ int64_t option(const char* name) {
   if (!strcmp(name, "topk_wg_per_cu")) return g_topk_wg_per_cu.load();
   if (!strcmp(name, "attn_pair")) return g_attn_pair.load();
   if (!strcmp(name, "sas_rowtile")) return g_sas_rowtile.load();
-  if (!strcmp(name, "rowtile_persist")) return g_rowtile_persist.load();
   if (!strcmp(name, "rq_resident")) return g_rq_resident.load();
+  if (!strcmp(name, "score_slice_major")) return g_score_slice_major.load();
+  if (!strcmp(name, "attn_occ1")) return g_attn_occ1.load();
   return -1;
 }
 }  // namespace gr
@@ -83,8 +87,9 @@ extern "C" int gr_set_option(const char* name, int64_t value) {
   if (!strcmp(name, "topk_wg_per_cu") && value >= 0 && value <= 4) { gr::g_topk_wg_per_cu = value; return GR_OK; }
   if (!strcmp(name, "attn_pair") && (value == 0 || value == 1)) { gr::g_attn_pair = value; return GR_OK; }
   if (!strcmp(name, "sas_rowtile") && (value == 0 || value == 1)) { gr::g_sas_rowtile = value; return GR_OK; }
-  if (!strcmp(name, "rowtile_persist") && (value == 0 || value == 1)) { gr::g_rowtile_persist = value; return GR_OK; }
   if (!strcmp(name, "rq_resident") && (value == 0 || value == 1)) { gr::g_rq_resident = value; return GR_OK; }
+  if (!strcmp(name, "score_slice_major") && (value == 0 || value == 1)) { gr::g_score_slice_major = value; return GR_OK; }
+  if (!strcmp(name, "attn_occ1") && (value == 0 || value == 1)) { gr::g_attn_occ1 = value; return GR_OK; }
   return gr::fail(GR_ERR_ARG, std::string("gr_set_option: unknown option or value: ") + name);
 }
 

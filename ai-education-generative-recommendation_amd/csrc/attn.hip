@@ -33,10 +33,10 @@ struct AttnTile {                  // one 32-query tile owned by a wave
 // Two workgroups per CU: at hd = 128 that caps the kernel at 256 VGPRs (a few spill), and still
 // measured 85 vs 114 us per C5 call (steady state) — the second workgroup's MFMAs fill the gaps
 // of the first's barriers and softmax.
-template <int HD>
-__global__ __launch_bounds__(256, 2) void attn_mfma_kernel(const float* __restrict__ qkv,
-                                                           float* __restrict__ out, int n, int H,
-                                                           float scale, int qt_lo) {
+template <int HD, int OCC>
+__global__ __launch_bounds__(256, OCC) void attn_mfma_kernel(const float* __restrict__ qkv,
+                                                             float* __restrict__ out, int n, int H,
+                                                             float scale, int qt_lo) {
   constexpr int FT = HD / 32;
   constexpr int KP = HD + 4;   // K row pitch: conflict-free ds_read_b128 of 16 rows
   constexpr int VP = HD + 8;   // V row pitch: the two lane halves (4 rows apart) on disjoint banks
@@ -369,10 +369,15 @@ int gr_attn_mfma_launch(const float* qkv, float* out, int64_t B, int n, int H, i
     }
     return check_launch("sasrec attention (mfma, paired tiles)");
   }
+  // attn_occ1 (hd 128): one workgroup per CU at 512 registers (no spills) instead of two at 256
+  const bool occ1 = option("attn_occ1") != 0;
   switch (hd) {
-    case 32: hipLaunchKernelGGL(attn_mfma_kernel<32>, g, blk, 0, st, qkv, out, n, H, scale, qt_lo); break;
-    case 64: hipLaunchKernelGGL(attn_mfma_kernel<64>, g, blk, 0, st, qkv, out, n, H, scale, qt_lo); break;
-    default: hipLaunchKernelGGL(attn_mfma_kernel<128>, g, blk, 0, st, qkv, out, n, H, scale, qt_lo); break;
+    case 32: hipLaunchKernelGGL((attn_mfma_kernel<32, 2>), g, blk, 0, st, qkv, out, n, H, scale, qt_lo); break;
+    case 64: hipLaunchKernelGGL((attn_mfma_kernel<64, 2>), g, blk, 0, st, qkv, out, n, H, scale, qt_lo); break;
+    default:
+      if (occ1) hipLaunchKernelGGL((attn_mfma_kernel<128, 1>), g, blk, 0, st, qkv, out, n, H, scale, qt_lo);
+      else hipLaunchKernelGGL((attn_mfma_kernel<128, 2>), g, blk, 0, st, qkv, out, n, H, scale, qt_lo);
+      break;
   }
   return check_launch("sasrec attention (mfma)");
 }

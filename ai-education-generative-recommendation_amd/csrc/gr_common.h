@@ -65,9 +65,11 @@ int gr_score_launch(const float* h, int64_t B, int32_t d, const float* table, in
 int gr_sasrec_tail_launch(const gr_sasrec_params* p, int blk, const float* X, const float* KV,
                           int64_t B, int32_t n, float* out, hipStream_t st);
 int gr_post_attn_launch(const gr_sasrec_params* p, int blk, const float* ln_next_w, const float* ln_next_b,
-                        const float* O, float* X, float* H, int64_t M, hipStream_t st);
-int gr_embed_ln_launch(const gr_sasrec_params* p, const int64_t* seqs, int64_t M, int32_t n, float* X, float* H,
-                       int32_t* err, hipStream_t st);
+                        const float* wn, const float* bn, int nout, const float* O, float* X, float* H,
+                        int64_t M, hipStream_t st);
+int gr_embed_ln_launch(const gr_sasrec_params* p, const int64_t* seqs, int64_t M, int32_t n, const float* wn,
+                       const float* bn, int nout, float* X, float* H, int32_t* err, hipStream_t st);
+bool gr_sasrec_tail_ok(const gr_sasrec_params* p, int32_t n);
 int gr_linear_launch(const float* x, int64_t m, int32_t k, const float* w, int32_t n,
                      const float* bias, const float* residual, int64_t ldr, int32_t act, float* y,
                      int64_t ldy, hipStream_t stream);

@@ -300,32 +300,46 @@ static int run_forward_rowtile(const gr_sasrec_params* p, const int64_t* seqs, i
                                float* full_out, hipStream_t st) {
   const int d = p->d, H = p->n_heads, hd = d / H;
   const int64_t rows = B * n;
-  int rc = gr_embed_ln_launch(p, seqs, rows, n, w.x, w.h, err, st);
+  const int nb = p->n_blocks;
+  const bool tail = last_only && tail_out && gr_sasrec_tail_ok(p, n);
+  // block i's in-projection, fused into the kernel that produces its LayerNorm input: Q|K|V, or
+  // K|V only for the final block of a last-position forward (its one query is the tail's)
+  auto proj = [&](int i, const float** wn, const float** bn, int* nout) {
+    const bool kv = tail && i == nb - 1;
+    *wn = p->in_proj_w[i] + (kv ? (int64_t)d * d : 0);
+    *bn = p->in_proj_b[i] + (kv ? d : 0);
+    *nout = kv ? 2 * d : 3 * d;
+  };
+  const float *wn, *bn;
+  int nout;
+  // block 0: embed + LN_a0 -> H, then the in-projection as a plain GEMM (folding it into the
+  // embed kernel measured slower: 218 us vs 37 + 133 at C5, its weight fragments come from L2
+  // with one 16-B piece per row per lane); later blocks fold it into post_attn (198 us vs
+  // 115 + 97 for the final block's K|V)
+  int rc = gr_embed_ln_launch(p, seqs, rows, n, nullptr, nullptr, 0, w.x, w.h, err, st);
+  if (rc) return rc;
+  proj(0, &wn, &bn, &nout);
+  rc = gr_linear_launch(w.h, rows, d, wn, nout, bn, nullptr, 0, GR_ACT_NONE, w.qkv, nout, st);
   if (rc) return rc;
   const float scale = (float)std::sqrt(1.0 / (double)hd);
-  const int nb = p->n_blocks;
   for (int i = 0; i < nb; ++i) {
     const bool last = i == nb - 1;
-    if (last && last_only && tail_out) {
-      rc = gr_linear_launch(w.h, rows, d, p->in_proj_w[i] + (int64_t)d * d, 2 * d, p->in_proj_b[i] + d,
-                            nullptr, 0, GR_ACT_NONE, w.qkv, 2 * d, st);
-      if (rc) return rc;
+    if (last && tail) {
       rc = gr_sasrec_tail_launch(p, i, w.x, w.qkv, B, n, tail_out, st);
-      if (rc == GR_OK) {
-        fin->done = true;
-        return GR_OK;
-      }
-      if (rc != GR_ERR_UNSUPPORTED) return rc;
-      clear_error();
+      if (rc) return rc;
+      fin->done = true;
+      return GR_OK;
     }
-    rc = gr_linear_launch(w.h, rows, d, p->in_proj_w[i], 3 * d, p->in_proj_b[i], nullptr, 0,
-                          GR_ACT_NONE, w.qkv, 3 * d, st);
-    if (rc) return rc;
     rc = gr_attn_mfma_launch(w.qkv, w.o, B, n, H, hd, scale, 0, st);
     if (rc) return rc;
-    float* hdst = last && full_out ? full_out : w.h;
-    rc = gr_post_attn_launch(p, i, last ? p->last_ln_w : p->attn_ln_w[i + 1], last ? p->last_ln_b : p->attn_ln_b[i + 1],
-                             w.o, w.x, hdst, rows, st);
+    if (!last) {
+      proj(i + 1, &wn, &bn, &nout);
+      rc = gr_post_attn_launch(p, i, p->attn_ln_w[i + 1], p->attn_ln_b[i + 1], wn, bn, nout, w.o, w.x, w.qkv,
+                               rows, st);
+    } else {
+      rc = gr_post_attn_launch(p, i, p->last_ln_w, p->last_ln_b, nullptr, nullptr, 0, w.o, w.x,
+                               full_out ? full_out : w.h, rows, st);
+    }
     if (rc) return rc;
   }
   if (full_out) {

@@ -27,19 +27,31 @@ constexpr int RT_P = RT_D + 4;       // LDS row pitch of a [64 x 128] image (con
 
 struct RowTileArgs {
   const float *wo, *bo, *ln_f_w, *ln_f_b, *w1, *b1, *w2, *b2, *ln_n_w, *ln_n_b;
-  int mlp;
+  const float *wn, *bn;   // the next block's in-projection (rows of W_in / b_in), or null
+  int mlp, nout;          // nout: 3d (Q|K|V) or 2d (K|V only, the final block of a tail forward)
   float eps;
 };
 
 // acc[rt] (rows 32rt.., columns 32w..) += A[64 x K] (LDS, pitch ap) . W[32w.., 0..K)^T
+// The weight fragments come from L2 RT_PF 8-deep slices ahead of their MFMAs (the compiler on its
+// own keeps only one load in flight, which leaves most of each L2 round trip exposed).
+constexpr int RT_PF = 4;
 template <int K>
 __device__ __forceinline__ void rt_gemm(f32x16 (&acc)[2], const float* A, int ap, const float* __restrict__ W,
                                         int wrow, int r, int h) {
+  constexpr int NK = K / 8, PF = RT_PF < NK ? RT_PF : NK;
+#ifdef GR_ABL_WROW   // diagnostic build only: every lane of a half reads the tile's first row (wrong data)
+  wrow &= ~31;
+#endif
   const float* wr = W + (int64_t)wrow * K + 4 * h;
   const float* a0 = A + r * ap + 4 * h;
+  f32x4 wb[PF];
 #pragma unroll
-  for (int kc = 0; kc < K / 8; ++kc) {
-    const f32x4 b = *reinterpret_cast<const f32x4*>(wr + 8 * kc);
+  for (int i = 0; i < PF; ++i) wb[i] = *reinterpret_cast<const f32x4*>(wr + 8 * i);
+#pragma unroll
+  for (int kc = 0; kc < NK; ++kc) {
+    const f32x4 b = wb[kc % PF];
+    if (kc + PF < NK) wb[kc % PF] = *reinterpret_cast<const f32x4*>(wr + 8 * (kc + PF));
     const f32x4 x0 = *reinterpret_cast<const f32x4*>(a0 + 8 * kc);
     const f32x4 x1 = *reinterpret_cast<const f32x4*>(a0 + 32 * ap + 8 * kc);
 #pragma unroll
@@ -112,6 +124,33 @@ __device__ __forceinline__ void rt_layernorm(float* img, const float* __restrict
   }
 }
 
+// out[row][c] = bias[c] + img[row, :] . W[c, :] for the 64 rows of an LDS image (pitch RT_P,
+// K = RT_D) and c < nout (nout % 32 == 0; row stride of out = nout): the next block's in-projection
+// (torch functional.py:5823) straight from the LayerNorm image.  Wave w takes column tiles w,
+// w+4, ...; the MFMA chain per element is gr_linear_f32's (k-ordered, bias added last).
+__device__ __forceinline__ void rt_project(const float* img, const float* __restrict__ W, const float* __restrict__ bias,
+                                           int nout, float* out, int64_t rows_left) {
+  const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, h = lane >> 5;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  for (int ct = w; ct < nout / 32; ct += 4) {
+    f32x16 acc[2];
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+      for (int v = 0; v < 16; ++v) acc[rt][v] = 0.f;
+    const int c = 32 * ct + r;
+    rt_gemm<RT_D>(acc, img, RT_P, W, c, r, h);
+    const float bv = bias[c];
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+      for (int v = 0; v < 16; ++v) {
+        const int row = 32 * rt + (v & 3) + 8 * (v >> 2) + 4 * h;
+        if (row < rows_left) out[(int64_t)row * nout + c] = acc[rt][v] + bv;
+      }
+  }
+}
+
 template <int MT>
 __global__ __launch_bounds__(256, 2) void post_attn_kernel(const RowTileArgs a, const float* __restrict__ O,
                                                            float* X, float* __restrict__ Hn, int64_t M) {
@@ -123,15 +162,24 @@ __global__ __launch_bounds__(256, 2) void post_attn_kernel(const RowTileArgs a, 
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int64_t m0 = (int64_t)xcd_remap(blockIdx.x, gridDim.x) * RT_BM;
   const int64_t left = M - m0;
-  // ---- O and X tiles -> LDS (rows past M read as zeros and are never stored)
+  // ---- O and X tiles -> LDS: all 16 loads in flight at once (clamped rows, no branch around a
+  // load); rows past M are zeroed when written and never stored
+  {
+    f32x4 o[8], x[8];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int f = tid + 256 * i, row = f >> 5, c = (f & 31) * 4;
-    const bool ok = row < left;
-    const f32x4 o = ok ? *reinterpret_cast<const f32x4*>(O + (m0 + row) * RT_D + c) : f32x4{0.f, 0.f, 0.f, 0.f};
-    const f32x4 x = ok ? *reinterpret_cast<const f32x4*>(X + (m0 + row) * RT_D + c) : f32x4{0.f, 0.f, 0.f, 0.f};
-    *reinterpret_cast<f32x4*>(bufA + row * RT_P + c) = o;
-    *reinterpret_cast<f32x4*>(bufB + row * RT_P + c) = x;
+    for (int i = 0; i < 8; ++i) {
+      const int f = tid + 256 * i, row = f >> 5, c = (f & 31) * 4;
+      const int64_t g = m0 + (row < left ? row : left - 1);
+      o[i] = *reinterpret_cast<const f32x4*>(O + g * RT_D + c);
+      x[i] = *reinterpret_cast<const f32x4*>(X + g * RT_D + c);
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int f = tid + 256 * i, row = f >> 5, c = (f & 31) * 4;
+      const bool ok = row < left;
+      *reinterpret_cast<f32x4*>(bufA + row * RT_P + c) = ok ? o[i] : f32x4{0.f, 0.f, 0.f, 0.f};
+      *reinterpret_cast<f32x4*>(bufB + row * RT_P + c) = ok ? x[i] : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
   }
   __syncthreads();
   const int col = 32 * w + r;
@@ -198,156 +246,20 @@ __global__ __launch_bounds__(256, 2) void post_attn_kernel(const RowTileArgs a, 
         bufB[(32 * rt + (v & 3) + 8 * (v >> 2) + 4 * h) * RT_P + col] = x1[rt][v] + (acc[rt][v] + b2);
   }
   __syncthreads();
-  // ---- X2 -> X (in place: the tile was read above), H2 = LN_next(X2) -> Hn
+  // ---- X2 -> X (in place: the tile was read above); then either H2 = LN_next(X2) -> Hn, or the
+  // next block's in-projection of LN_next(X2) -> Hn as [rows x nout] (the LN stays in LDS)
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     const int f = tid + 256 * i, row = f >> 5, c = (f & 31) * 4;
     if (row < left) *reinterpret_cast<f32x4*>(X + (m0 + row) * RT_D + c) = *reinterpret_cast<const f32x4*>(bufB + row * RT_P + c);
   }
-  rt_layernorm(bufB, a.ln_n_w, a.ln_n_b, a.eps, Hn + m0 * RT_D, left);
-}
-
-// Persistent form of post_attn_kernel: one workgroup per CU (one wave per SIMD, 512-register
-// budget) walks row tiles; each wave's weight fragments (its 32 rows of Wo, W1 and W2 as MFMA B
-// operands) are loaded ONCE into registers, and the next tile's O / X are prefetched into
-// registers while the current tile computes.  Same arithmetic per element as post_attn_kernel
-// (same fragment order, same LayerNorm helper), so both produce identical bits.
-template <int MT>
-__global__ __launch_bounds__(256, 1) void post_attn_persist_kernel(const RowTileArgs a, const float* __restrict__ O,
-                                                                   float* X, float* __restrict__ Hn, int64_t M) {
-  constexpr int MLP = 32 * MT;
-  constexpr int FP = MLP + 4;
-  constexpr int W1N = MT == 4 ? 2 : 1;          // FFN1 row tiles per wave
-  __shared__ __attribute__((aligned(16))) float bufA[RT_BM * RT_P];   // O, then F
-  __shared__ __attribute__((aligned(16))) float bufB[RT_BM * RT_P];   // X, X1 -> H1, X2
-  const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, h = lane >> 5;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int col = 32 * w + r;
-  // FFN1 tile(s) of this wave: column tile c1, row tiles rt1 (.. rt1 + W1N - 1); MT = 1 uses waves 0, 1
-  const int c1 = MT == 4 ? w : MT == 2 ? (w & 1) : 0;
-  const int rt1 = MT == 4 ? 0 : MT == 2 ? (w >> 1) : w;
-  const bool f1 = MT != 1 || w < 2;
-  f32x4 wo[RT_D / 8], w1[RT_D / 8], w2[MLP / 8];
-#pragma unroll
-  for (int kc = 0; kc < RT_D / 8; ++kc) {
-    wo[kc] = *reinterpret_cast<const f32x4*>(a.wo + (int64_t)col * RT_D + 8 * kc + 4 * h);
-    w1[kc] = *reinterpret_cast<const f32x4*>(a.w1 + (int64_t)(32 * c1 + r) * RT_D + 8 * kc + 4 * h);
-  }
-#pragma unroll
-  for (int kc = 0; kc < MLP / 8; ++kc)
-    w2[kc] = *reinterpret_cast<const f32x4*>(a.w2 + (int64_t)col * MLP + 8 * kc + 4 * h);
-  const float bo = a.bo[col], b2 = a.b2[col], b1 = a.b1[32 * c1 + r];
-  const int64_t tiles = (M + RT_BM - 1) / RT_BM;
-  f32x4 po[8], px[8];
-  auto gload = [&](int64_t t) {
-    const int64_t m0 = t * RT_BM;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int f = tid + 256 * i, row = f >> 5, c = (f & 31) * 4;
-      const bool ok = m0 + row < M;
-      po[i] = ok ? *reinterpret_cast<const f32x4*>(O + (m0 + row) * RT_D + c) : f32x4{0.f, 0.f, 0.f, 0.f};
-      px[i] = ok ? *reinterpret_cast<const f32x4*>(X + (m0 + row) * RT_D + c) : f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-  };
-  auto swrite = [&]() {
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int f = tid + 256 * i, row = f >> 5, c = (f & 31) * 4;
-      *reinterpret_cast<f32x4*>(bufA + row * RT_P + c) = po[i];
-      *reinterpret_cast<f32x4*>(bufB + row * RT_P + c) = px[i];
-    }
-  };
-  int64_t t = blockIdx.x;
-  if (t < tiles) {
-    gload(t);
-    swrite();
-  }
-  __syncthreads();
-  for (; t < tiles; t += gridDim.x) {
-    const int64_t m0 = t * RT_BM, left = M - m0;
-    if (t + gridDim.x < tiles) gload(t + gridDim.x);      // lands while this tile computes
-    // ---- X1 = X + O . Wo^T + bo
-    f32x16 x1[2];
-    {
-      f32x16 acc[2] = {};
-      const float* a0 = bufA + r * RT_P + 4 * h;
-#pragma unroll
-      for (int kc = 0; kc < RT_D / 8; ++kc) {
-        const f32x4 xa = *reinterpret_cast<const f32x4*>(a0 + 8 * kc);
-        const f32x4 xb = *reinterpret_cast<const f32x4*>(a0 + 32 * RT_P + 8 * kc);
-#pragma unroll
-        for (int s4 = 0; s4 < 4; ++s4) {
-          acc[0] = mfma32(xa[s4], wo[kc][s4], acc[0]);
-          acc[1] = mfma32(xb[s4], wo[kc][s4], acc[1]);
-        }
-      }
-#pragma unroll
-      for (int rt = 0; rt < 2; ++rt)
-#pragma unroll
-        for (int v = 0; v < 16; ++v) {
-          const int row = 32 * rt + (v & 3) + 8 * (v >> 2) + 4 * h;
-          x1[rt][v] = bufB[row * RT_P + col] + (acc[rt][v] + bo);
-        }
-    }
+  if (a.wn) {
+    __syncthreads();   // the X2 stores have read the image the LayerNorm rewrites
+    rt_layernorm(bufB, a.ln_n_w, a.ln_n_b, a.eps, nullptr, 0);
     __syncthreads();
-#pragma unroll
-    for (int rt = 0; rt < 2; ++rt)
-#pragma unroll
-      for (int v = 0; v < 16; ++v) bufB[(32 * rt + (v & 3) + 8 * (v >> 2) + 4 * h) * RT_P + col] = x1[rt][v];
-    __syncthreads();
-    rt_layernorm(bufB, a.ln_f_w, a.ln_f_b, a.eps, nullptr, 0);
-    __syncthreads();
-    // ---- F = relu(H1 . W1^T + b1) -> bufA
-    if (f1) {
-#pragma unroll
-      for (int u = 0; u < W1N; ++u) {
-        const int rt = rt1 + u;
-        f32x16 acc = {};
-        const float* ar = bufB + (32 * rt + r) * RT_P + 4 * h;
-#pragma unroll
-        for (int kc = 0; kc < RT_D / 8; ++kc) {
-          const f32x4 x = *reinterpret_cast<const f32x4*>(ar + 8 * kc);
-#pragma unroll
-          for (int s4 = 0; s4 < 4; ++s4) acc = mfma32(x[s4], w1[kc][s4], acc);
-        }
-#pragma unroll
-        for (int v = 0; v < 16; ++v) {
-          const float y = acc[v] + b1;
-          bufA[(32 * rt + (v & 3) + 8 * (v >> 2) + 4 * h) * FP + 32 * c1 + r] = y < 0.f ? 0.f : y;
-        }
-      }
-    }
-    __syncthreads();
-    // ---- X2 = X1 + F . W2^T + b2 -> bufB
-    {
-      f32x16 acc[2] = {};
-      const float* a0 = bufA + r * FP + 4 * h;
-#pragma unroll
-      for (int kc = 0; kc < MLP / 8; ++kc) {
-        const f32x4 xa = *reinterpret_cast<const f32x4*>(a0 + 8 * kc);
-        const f32x4 xb = *reinterpret_cast<const f32x4*>(a0 + 32 * FP + 8 * kc);
-#pragma unroll
-        for (int s4 = 0; s4 < 4; ++s4) {
-          acc[0] = mfma32(xa[s4], w2[kc][s4], acc[0]);
-          acc[1] = mfma32(xb[s4], w2[kc][s4], acc[1]);
-        }
-      }
-#pragma unroll
-      for (int rt = 0; rt < 2; ++rt)
-#pragma unroll
-        for (int v = 0; v < 16; ++v)
-          bufB[(32 * rt + (v & 3) + 8 * (v >> 2) + 4 * h) * RT_P + col] = x1[rt][v] + (acc[rt][v] + b2);
-    }
-    __syncthreads();
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int f = tid + 256 * i, row = f >> 5, c = (f & 31) * 4;
-      if (row < left) *reinterpret_cast<f32x4*>(X + (m0 + row) * RT_D + c) = *reinterpret_cast<const f32x4*>(bufB + row * RT_P + c);
-    }
+    rt_project(bufB, a.wn, a.bn, a.nout, Hn + m0 * a.nout, left);
+  } else {
     rt_layernorm(bufB, a.ln_n_w, a.ln_n_b, a.eps, Hn + m0 * RT_D, left);
-    __syncthreads();                                      // bufA / bufB free for the next tile
-    if (t + gridDim.x < tiles) swrite();
-    __syncthreads();
   }
 }
 
@@ -357,39 +269,61 @@ __global__ __launch_bounds__(256) void embed_ln_kernel(const int64_t* __restrict
                                                        const float* __restrict__ item, int64_t item_rows,
                                                        const float* __restrict__ pos, const float* __restrict__ lw,
                                                        const float* __restrict__ lb, float eps,
-                                                       float* __restrict__ X, float* __restrict__ H, int32_t* err) {
+                                                       const float* __restrict__ wn, const float* __restrict__ bn,
+                                                       int nout, float* __restrict__ X, float* __restrict__ H,
+                                                       int32_t* err) {
   __shared__ __attribute__((aligned(16))) float img[RT_BM * RT_P];
   const int tid = threadIdx.x;
   const int64_t m0 = (int64_t)blockIdx.x * RT_BM;
   const int64_t left = M - m0;
+  // ids first (8 loads in flight), then the 8 embedding rows and 8 position rows together
+  int64_t ids[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int row = (tid + 256 * i) >> 5;
+    ids[i] = seqs[m0 + (row < left ? row : left - 1)];
+  }
+  f32x4 e[8], ps[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     const int f = tid + 256 * i, row = f >> 5, c = (f & 31) * 4;
-    f32x4 x = {0.f, 0.f, 0.f, 0.f};
-    if (row < left) {
-      const int64_t g = m0 + row;
-      int64_t id = seqs[g];
-      if (id < 0 || id >= item_rows) {
-        if (err) *err = 1;
-        id = 0;
-      }
-      const int t = (int)(g % n);
-      x = *reinterpret_cast<const f32x4*>(item + id * RT_D + c) + *reinterpret_cast<const f32x4*>(pos + (int64_t)t * RT_D + c);
-      *reinterpret_cast<f32x4*>(X + g * RT_D + c) = x;
+    const int64_t g = m0 + (row < left ? row : left - 1);
+    int64_t id = ids[i];
+    if (id < 0 || id >= item_rows) {   // flag only real rows (clamped duplicates re-read a real id)
+      if (err && row < left) *err = 1;
+      id = 0;
     }
+    e[i] = *reinterpret_cast<const f32x4*>(item + id * RT_D + c);
+    ps[i] = *reinterpret_cast<const f32x4*>(pos + (int64_t)(g % n) * RT_D + c);
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int f = tid + 256 * i, row = f >> 5, c = (f & 31) * 4;
+    const bool ok = row < left;
+    const f32x4 x = ok ? e[i] + ps[i] : f32x4{0.f, 0.f, 0.f, 0.f};
+    if (ok) *reinterpret_cast<f32x4*>(X + (m0 + row) * RT_D + c) = x;
     *reinterpret_cast<f32x4*>(img + row * RT_P + c) = x;
   }
   __syncthreads();
-  rt_layernorm(img, lw, lb, eps, H + m0 * RT_D, left);
+  if (wn) {   // block 0's in-projection of LN_a0(X) -> H as [rows x nout]
+    rt_layernorm(img, lw, lb, eps, nullptr, 0);
+    __syncthreads();
+    rt_project(img, wn, bn, nout, H + m0 * nout, left);
+  } else {
+    rt_layernorm(img, lw, lb, eps, H + m0 * RT_D, left);
+  }
 }
 
 }  // namespace gr
 
 // Shapes: d == 128, mlp in {32, 64, 128}; anything else returns GR_ERR_UNSUPPORTED (the caller
 // keeps the kernel-per-op sequence).  ln_next_* = the next block's attention LayerNorm, or the
-// last LayerNorm after the final block.
+// last LayerNorm after the final block.  wn / bn (nout = 3d or 2d columns): the next block's
+// in-projection, computed from the LayerNorm image and written to H as [M x nout]; null: H gets
+// the LayerNorm output itself [M x d].
 int gr_post_attn_launch(const gr_sasrec_params* p, int blk, const float* ln_next_w, const float* ln_next_b,
-                        const float* O, float* X, float* H, int64_t M, hipStream_t st) {
+                        const float* wn, const float* bn, int nout, const float* O, float* X, float* H,
+                        int64_t M, hipStream_t st) {
   using namespace gr;
   const int mlp = p->mlp;
   if (p->d != RT_D || (mlp != 32 && mlp != 64 && mlp != 128)) return GR_ERR_UNSUPPORTED;
@@ -399,27 +333,14 @@ int gr_post_attn_launch(const gr_sasrec_params* p, int blk, const float* ln_next
   a.w1 = p->ffn1_w[blk]; a.b1 = p->ffn1_b[blk];
   a.w2 = p->ffn2_w[blk]; a.b2 = p->ffn2_b[blk];
   a.ln_n_w = ln_next_w; a.ln_n_b = ln_next_b;
+  a.wn = wn; a.bn = bn; a.nout = nout;
   a.mlp = mlp; a.eps = p->eps;
   const float* ptrs[] = {a.wo, a.w1, a.w2, a.ln_f_w, a.ln_f_b, a.ln_n_w, a.ln_n_b, O, X, H};
   for (const float* q : ptrs)
     if (!aligned16(q)) return GR_ERR_UNSUPPORTED;
+  if (wn && (!aligned16(wn) || !bn || nout % 32 || nout < 32)) return GR_ERR_UNSUPPORTED;
   const int64_t tiles = (M + RT_BM - 1) / RT_BM;
   if (tiles > 0x7fffffffLL) return GR_ERR_UNSUPPORTED;
-  if (option("rowtile_persist") != 0) {
-    static int cus = 0;
-    if (!cus) {
-      int dev = 0;
-      if (hipGetDevice(&dev) != hipSuccess) dev = 0;
-      if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1) cus = 256;
-    }
-    const dim3 g((unsigned)(tiles < cus ? tiles : cus));
-    switch (mlp) {
-      case 32: hipLaunchKernelGGL(post_attn_persist_kernel<1>, g, dim3(256), 0, st, a, O, X, H, M); break;
-      case 64: hipLaunchKernelGGL(post_attn_persist_kernel<2>, g, dim3(256), 0, st, a, O, X, H, M); break;
-      default: hipLaunchKernelGGL(post_attn_persist_kernel<4>, g, dim3(256), 0, st, a, O, X, H, M); break;
-    }
-    return check_launch("sasrec post-attention row tiles (persistent)");
-  }
   switch (mlp) {
     case 32: hipLaunchKernelGGL(post_attn_kernel<1>, dim3((unsigned)tiles), dim3(256), 0, st, a, O, X, H, M); break;
     case 64: hipLaunchKernelGGL(post_attn_kernel<2>, dim3((unsigned)tiles), dim3(256), 0, st, a, O, X, H, M); break;
@@ -428,14 +349,15 @@ int gr_post_attn_launch(const gr_sasrec_params* p, int blk, const float* ln_next
   return check_launch("sasrec post-attention row tile");
 }
 
-int gr_embed_ln_launch(const gr_sasrec_params* p, const int64_t* seqs, int64_t M, int32_t n, float* X, float* H,
-                       int32_t* err, hipStream_t st) {
+int gr_embed_ln_launch(const gr_sasrec_params* p, const int64_t* seqs, int64_t M, int32_t n, const float* wn,
+                       const float* bn, int nout, float* X, float* H, int32_t* err, hipStream_t st) {
   using namespace gr;
   if (p->d != RT_D || p->n_blocks < 1) return GR_ERR_UNSUPPORTED;
   if (!aligned16(p->attn_ln_w[0]) || !aligned16(p->attn_ln_b[0])) return GR_ERR_UNSUPPORTED;
+  if (wn && (!aligned16(wn) || !bn || nout % 32 || nout < 32)) return GR_ERR_UNSUPPORTED;
   const int64_t tiles = (M + RT_BM - 1) / RT_BM;
   if (tiles > 0x7fffffffLL) return GR_ERR_UNSUPPORTED;
   hipLaunchKernelGGL(embed_ln_kernel, dim3((unsigned)tiles), dim3(256), 0, st, seqs, M, n, p->item_emb, p->item_rows,
-                     p->pos_emb, p->attn_ln_w[0], p->attn_ln_b[0], p->eps, X, H, err);
+                     p->pos_emb, p->attn_ln_w[0], p->attn_ln_b[0], p->eps, wn, bn, nout, X, H, err);
   return check_launch("sasrec embed + layernorm");
 }

@@ -210,16 +210,21 @@ __global__ __launch_bounds__(ST_NT) void sas_tail_kernel(const SasTailArgs a, co
 // Returns GR_ERR_UNSUPPORTED for shapes outside the kernel's limits (the caller keeps the
 // layer-wise final block).  X: [B, n, d] residual stream entering the final block; KV: [B, n, 2d]
 // = LN_a(X) . W_in[d:3d]^T + b_in[d:3d]; out: [B, d] = the final hidden state of position n-1.
+// The shapes sas_tail_kernel covers: lane groups of k/4 lanes (k = d for the scores / V / Wq / Wo /
+// W1 reads, k = mlp for W2), at most 8 heads and 1024 keys.
+bool gr_sasrec_tail_ok(const gr_sasrec_params* p, int32_t n) {
+  using namespace gr;
+  const int d = p->d, H = p->n_heads;
+  auto pow2 = [](int v) { return v >= 1 && (v & (v - 1)) == 0; };
+  return !(d > ST_MAX_D || d % 4 || !pow2(d / 4) || H > ST_MAX_H || d % H || (d / H) % 4 || !pow2(d / H / 4) ||
+           n > ST_MAX_N || p->mlp > ST_MAX_MLP || p->mlp % 4 || !pow2(p->mlp / 4) || p->mlp / 4 > 64);
+}
+
 int gr_sasrec_tail_launch(const gr_sasrec_params* p, int blk, const float* X, const float* KV,
                           int64_t B, int32_t n, float* out, hipStream_t st) {
   using namespace gr;
   const int d = p->d, H = p->n_heads;
-  auto pow2 = [](int v) { return v >= 1 && (v & (v - 1)) == 0; };
-  // lane groups of k/4 lanes (k = d for the scores / V / Wq / Wo / W1 reads, k = mlp for W2)
-  if (d > ST_MAX_D || d % 4 || !pow2(d / 4) || H > ST_MAX_H || d % H || (d / H) % 4 || !pow2(d / H / 4) ||
-      n > ST_MAX_N || p->mlp > ST_MAX_MLP || p->mlp % 4 || !pow2(p->mlp / 4) || p->mlp / 4 > 64 ||
-      B > 0x7fffffffLL)
-    return GR_ERR_UNSUPPORTED;
+  if (!gr_sasrec_tail_ok(p, n) || B > 0x7fffffffLL) return GR_ERR_UNSUPPORTED;
   SasTailArgs a;
   a.ln_a_w = p->attn_ln_w[blk]; a.ln_a_b = p->attn_ln_b[blk];
   a.wq = p->in_proj_w[blk];     a.bq = p->in_proj_b[blk];

@@ -354,7 +354,7 @@ template <int D>
 __global__ __launch_bounds__(256, 2) void score_direct_kernel(const float* __restrict__ h, int64_t B,
                                                             const float* __restrict__ table, int64_t rows,
                                                             float* __restrict__ out, int64_t ld,
-                                                            int ublocks, int slices) {
+                                                            int ublocks, int slices, int slice_major) {
   constexpr int KG = D / 32;
   constexpr int P = D + 4;
   constexpr int LV = SC_CHUNK * D / 4 / 256;
@@ -362,7 +362,10 @@ __global__ __launch_bounds__(256, 2) void score_direct_kernel(const float* __res
   const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, hh = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wgid = xcd_remap(blockIdx.x, gridDim.x);
-  const int ub = wgid / slices, sl = wgid % slices;
+  // user-block major: an XCD's workgroups share users and sweep the catalog; slice major: they
+  // share catalog slices across the user blocks (each table chunk read from HBM once per XCD)
+  const int ub = slice_major ? wgid % ublocks : wgid / slices;
+  const int sl = slice_major ? wgid / ublocks : wgid % slices;
   const int64_t chunks = (rows + SC_CHUNK - 1) / SC_CHUNK;
   const int64_t c_begin = chunks * sl / slices, c_end = chunks * (sl + 1) / slices;
   if (c_begin >= c_end) return;
@@ -498,10 +501,11 @@ int gr_score_launch(const float* h, int64_t B, int32_t d, const float* table, in
     if (sl2 > chunks) sl2 = chunks;
     if (sl2 < 1) sl2 = 1;
     const dim3 g2((unsigned)(ublocks * sl2));
+    const int smaj = option("score_slice_major") != 0 ? 1 : 0;
     switch (d) {
-      case 32: hipLaunchKernelGGL(score_direct_kernel<32>, g2, dim3(256), 0, st, h, B, table, rows, logits, ld, (int)ublocks, (int)sl2); break;
-      case 64: hipLaunchKernelGGL(score_direct_kernel<64>, g2, dim3(256), 0, st, h, B, table, rows, logits, ld, (int)ublocks, (int)sl2); break;
-      default: hipLaunchKernelGGL(score_direct_kernel<128>, g2, dim3(256), 0, st, h, B, table, rows, logits, ld, (int)ublocks, (int)sl2); break;
+      case 32: hipLaunchKernelGGL(score_direct_kernel<32>, g2, dim3(256), 0, st, h, B, table, rows, logits, ld, (int)ublocks, (int)sl2, smaj); break;
+      case 64: hipLaunchKernelGGL(score_direct_kernel<64>, g2, dim3(256), 0, st, h, B, table, rows, logits, ld, (int)ublocks, (int)sl2, smaj); break;
+      default: hipLaunchKernelGGL(score_direct_kernel<128>, g2, dim3(256), 0, st, h, B, table, rows, logits, ld, (int)ublocks, (int)sl2, smaj); break;
     }
     return check_launch("gr_score_f32 (direct)");
   }

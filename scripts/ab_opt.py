@@ -30,18 +30,26 @@ def timeit(fn, reps=50, spin=0.5):
 
 
 ap = argparse.ArgumentParser()
-ap.add_argument("--what", default="rq", choices=["rq", "quant"])
+ap.add_argument("--what", default="rq", choices=["rq", "quant", "score", "predict"])
 ap.add_argument("--opt", default="rq_resident=0,1")
 ap.add_argument("--L", type=int, default=3)
 ap.add_argument("--K", type=int, default=256)
 ap.add_argument("--n", type=int, default=100_000)
 a = ap.parse_args()
 dev = torch.device("cuda:0")
-m = synth.rqvae_model(a.L, a.K, dev)
-x = synth.items(a.n, 1000, dev)
-b = m.encode_binding()
-z = ops.rq_mlp(x, b.ws, b.bs)
-fn = (lambda: m.get_indices(x)) if a.what == "rq" else (lambda: ops.rq_quantize(z, b.cbs))
+if a.what in ("rq", "quant"):
+    m = synth.rqvae_model(a.L, a.K, dev)
+    x = synth.items(a.n, 1000, dev)
+    b = m.encode_binding()
+    z = ops.rq_mlp(x, b.ws, b.bs)
+    fn = (lambda: m.get_indices(x)) if a.what == "rq" else (lambda: ops.rq_quantize(z, b.cbs))
+else:   # C3 shapes: 2048 users, d 64, 100k items (--n = users)
+    sm = synth.sasrec_model(100_000, synth.sasrec_params(64, 50, 2, 1, 64, dev), dev)
+    seqs = synth.sequences(a.n if a.n != 100_000 else 2048, 50, 100_000, 2000, dev)
+    hh = sm.last_hidden(seqs)
+    tab = sm.item_emb.weight.detach()
+    outb = ops.logits_buffer(hh.shape[0], tab.shape[0], dev)
+    fn = (lambda: ops.score(hh, tab, out=outb)) if a.what == "score" else (lambda: sm.predict(seqs))
 name, vals = a.opt.split("=")
 ref = None
 for v in vals.split(","):

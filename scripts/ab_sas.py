@@ -12,6 +12,9 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from gr_amd import _lib, synth  # noqa: E402
 
+if os.environ.get("GR_DIAG_LIB"):   # diagnostic build (build.py --abl MACRO): results may be wrong
+    _lib.LIB_PATH = os.path.join(os.path.dirname(_lib.LIB_PATH), os.environ["GR_DIAG_LIB"])
+
 
 def timeit(fn, reps=30, spin=0.5):
     import time
