@@ -152,22 +152,36 @@ def kernel_ms(fn, reps=50, warmup=2):
     return e0.elapsed_time(e1) / reps
 
 
-def traffic_of(kernel):
-    """HBM bytes per launch of ``kernel`` from the committed PMC summary, or None."""
+TOPK_CALL_KERNELS = ["score_topk_kernel<128,10,", "topk_merge_kernel<10>"]
+
+
+def call_traffic(leg, kernels, anchor):
+    """HBM bytes per call from the committed PMC summary (profiles/traffic.json, written per bench
+    leg and launch shape by scripts/pmc_traffic.py): the bytes of every launch in ``leg`` whose
+    kernel name starts with one of ``kernels``, divided by the number of launches of ``anchor``
+    (one per call).  None when the leg was not profiled."""
     p = os.path.join(ROOT, "profiles", "traffic.json")
     if not os.path.exists(p):
         return None, None
-    t = json.load(open(p)).get(kernel)
-    return (t["bytes_per_launch"], t["source"]) if t else (None, None)
+    t = json.load(open(p))
+    groups = t.get("legs", {}).get(leg)
+    if not groups:
+        return None, None
+    name = lambda key: key.rsplit("@", 1)[0]
+    calls = sum(g["launches"] for k, g in groups.items() if name(k).startswith(anchor))
+    if calls == 0:
+        return None, None
+    tot = sum(g["bytes_per_launch"] * g["launches"] for k, g in groups.items()
+              if any(name(k).startswith(p) for p in kernels))
+    return tot / calls, f"{t.get('source', '')}, leg {leg}"
 
 
-def roofline(kernel, flop, ms, bound="mfma", launches=1, note=None):
-    """``kernel`` names the dominant kernel (the profiles/traffic.json key); ``launches`` = its
-    launches per timed call (traffic is per call, like ``achieved``)."""
+def roofline(kernel, flop, ms, leg, bound="mfma", call_kernels=None, note=None):
+    """``kernel`` names the dominant kernel (prefix of its profiled name); ``call_kernels`` lists
+    the kernel-name prefixes one timed call launches (default: ``kernel`` alone), so ``traffic``
+    is per call, like ``achieved``."""
     ach = flop / (ms * 1e-3) / 1e12
-    tr, src = traffic_of(kernel)
-    if tr is not None:
-        tr *= launches
+    tr, src = call_traffic(leg, call_kernels or [kernel], kernel)
     return {"bound": bound, "achieved": ach, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
             "frac": ach / FP32_PEAK_TFLOPS, "traffic": tr, "traffic_source": src, "kernel": kernel,
             "flop_per_launch": flop, "kernel_ms": ms, **({"note": note} if note else {})}
@@ -245,7 +259,7 @@ def bench_rq_c2(a, world, rank, dev):
                                "e 32, data-derived codebooks, BERT-statistics item embeddings",
                    "items_per_rank_per_step": a.rq_items, "global_batch": a.rq_items * world,
                    "parallelism": f"item-sharded x{world}, no collective"},
-        "roofline": roofline("rq_encoder_kernel<256,128>", ENC_FLOP_PER_ITEM * a.rq_items, enc_ms),
+        "roofline": roofline("rq_encoder_kernel<256,128>", ENC_FLOP_PER_ITEM * a.rq_items, enc_ms, "c2"),
         "call": {"kernels": "rq_encoder_kernel + rq_quantize_kernel", "device_ms": dev_ms,
                  "flop_per_item": rq_flop_per_item(L, K),
                  "frac_of_fp32_peak": rq_flop_per_item(L, K) * a.rq_items / (dev_ms * 1e-3) / 1e12 / FP32_PEAK_TFLOPS,
@@ -297,7 +311,7 @@ def bench_sas_c3(a, world, rank, dev):
            "config": {"workload": "sas_c3: SASRec predict, 2 blocks, d 64, n 50, H 1, mlp 64, "
                                   "100k-item full-catalog logits written", "users_per_rank_per_step": a.sas_batch,
                       "parallelism": f"user-sharded x{world}, no collective"},
-           "roofline": roofline("score_direct_kernel<64>", 2 * d * (items + 1) * a.sas_batch, score_ms),
+           "roofline": roofline("score_direct_kernel<64>", 2 * d * (items + 1) * a.sas_batch, score_ms, "sasrec"),
            "call": {"device_ms": dev_ms, "flop_per_user": fl,
                     "frac_of_fp32_peak": fl * a.sas_batch / (dev_ms * 1e-3) / 1e12 / FP32_PEAK_TFLOPS,
                     "forward_ms": fwd_ms, "score_ms": score_ms,
@@ -309,7 +323,7 @@ def bench_sas_c3(a, world, rank, dev):
     return res, model, (n, items)
 
 
-def bench_sas_c5(a, world, rank, dev):
+def bench_sas_c5(a, world, rank, dev, time_it=True):
     """C5: the catalog sharded over the ranks; every rank runs the transformer for its share of the
     users, hidden states are all-gathered, each rank scores ALL users against its catalog shard,
     then counts are all-reduced and top-10 lists all-gathered (gr_amd.dist)."""
@@ -336,6 +350,8 @@ def bench_sas_c5(a, world, rank, dev):
         return D.sharded_rank_topk_batches([h[x:y] for x, y in zip(cuts[:-1], cuts[1:])], shard, lo,
                                            [targets[x:y] for x, y in zip(cuts[:-1], cuts[1:])], k=10)
 
+    if not time_it:   # setup only (the shard leg alone): no C5 launches in its profile
+        return None, model, model.last_hidden(seqs), targets
     steps, warm = max(2, min(a.steps, 10)), 2
     wall, dev_ms = timed(step, steps, warm, world)
     h = model.last_hidden(seqs)
@@ -348,9 +364,11 @@ def bench_sas_c5(a, world, rank, dev):
                        "users_per_step": B, "catalog_rows": items + 1, "rows_per_rank": hi - lo,
                        "parallelism": f"catalog-sharded x{world}: RCCL all-gather h + top-k, all-reduce counts"
                        + (f", {P} pipelined sub-batches" if P > 1 else "") if world > 1 else "single shard"},
-            "roofline": roofline("score_topk_kernel<128,10>", 2 * d * (hi - lo) * B, topk_ms, launches=2,
-                                 note="one gr_score_topk_f32 call: sample pass + exact pass + 2 merge "
-                                      "kernels; flop counts the exact pass only"),
+            "roofline": roofline("score_topk_kernel<128,10,0>", 2 * d * (hi - lo) * B, topk_ms, "c5",
+                                 call_kernels=TOPK_CALL_KERNELS,
+                                 note="one gr_score_topk_f32 call: exact pass (MODE 0) + sample pass (MODE 1) "
+                                      "+ 2 merge kernels; flop counts the exact pass only; traffic is the "
+                                      "whole call's"),
             "call": {"device_ms_rank0": dev_ms, "flop_per_user": sas_flop_per_user(d, n, items),
                      "forward_ms": fwd_ms, "score_topk_ms": topk_ms,
                      "note": "rank + top-10 fused into the scoring pass (gr_score_topk_f32): the "
@@ -405,6 +423,7 @@ def bench_sas_train(a, world, rank, dev):
     wall, dev_ms = timed(step, a.steps, a.warmup, world)
     dense_ms = kernel_ms(dense_step, reps=10)
     nbytes = sas_train_bytes(B, n, d, items + 1, J)
+    tr, tr_src = call_traffic("train", ["neg_sample_kernel", "bce_"], "neg_sample_kernel")
     res = {"metric": "train_seqs_scored/s", "value": B * world * a.steps / wall, "unit": "seqs/s",
            "ms_per_step": wall / a.steps * 1e3, "scaling": "weak",
            "config": {"workload": f"sas_train: SASRec train.py:131-167 scoring + sampled BCE, forward + "
@@ -412,7 +431,9 @@ def bench_sas_train(a, world, rank, dev):
                       "users_per_rank_per_step": B, "parallelism": f"user-sharded x{world}, no collective"},
            "roofline": {"bound": "hbm", "achieved": nbytes / (dev_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
                         "unit": "GB/s", "frac": nbytes / (dev_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                        "traffic": None, "kernel": "whole step (gr_neg_samples + gr_sampled_bce fwd + bwd: 5 kernels + dM fill)",
+                        "traffic": tr, "traffic_source": tr_src and tr_src + " (the 5 gr:: kernels; the "
+                                                                    "dM fill is a hipMemsetAsync, not counted)",
+                        "kernel": "whole step (gr_neg_samples + gr_sampled_bce fwd + bwd: 5 kernels + dM fill)",
                         "bytes_per_step": nbytes, "step_device_ms": dev_ms},
            "reference_formulation_gpu": {"note": "train.py:134-167 as written ([B, n, N+1] score matrix, "
                                                  "gathers, dense backward) in torch on the same GPU, "
@@ -460,9 +481,10 @@ def bench_c5_shard(a, model, h, targets, dev, shards=8):
             "config": {"workload": f"c5_shard: {B} users x one {hi - lo}-row catalog shard (1/{shards} of "
                                    f"{model.item_emb.weight.shape[0]}), d {d}, target logit + rank + top-{k}",
                        "rows": hi - lo, "users": B},
-            "roofline": roofline("score_topk_kernel<128,10>", flop, topk_ms, launches=2,
+            "roofline": roofline("score_topk_kernel<128,10,0>", flop, topk_ms, "shard",
+                                 call_kernels=TOPK_CALL_KERNELS,
                                  note="one gr_score_topk_f32 call on the shard (all its launches); flop "
-                                      "counts the scoring GEMM once"),
+                                      "counts the scoring GEMM once; traffic is the whole call's"),
             "call": {"device_ms": dev_ms, "score_topk_ms": topk_ms, "score_count_ms": cnt_ms,
                      "frac_of_fp32_peak_step": flop / (dev_ms * 1e-3) / 1e12 / FP32_PEAK_TFLOPS}}
 
@@ -573,7 +595,7 @@ def main():
         del c4_model
         torch.cuda.empty_cache()
     if "c5" in legs or "shard" in legs:
-        c5, c5_model, h5, t5 = bench_sas_c5(a, world, rank, dev)
+        c5, c5_model, h5, t5 = bench_sas_c5(a, world, rank, dev, time_it="c5" in legs)
         if "c5" in legs:
             line["sasrec_c5"] = c5
             if cpu:

@@ -41,13 +41,19 @@ for s in $STEPS; do
         cd "$ROOT"
         python3 scripts/trace_stats.py "$OUT/prof_$leg/run_kernel_trace.csv" --leg $leg > "$OUT/trace_$leg.csv" || true
       done ;;
-    pmc)  # HBM traffic per kernel: FETCH_SIZE and WRITE_SIZE in separate passes
+    pmc)  # HBM traffic per bench leg and kernel: FETCH_SIZE and WRITE_SIZE in separate passes
       export TMPDIR=/tmp
-      cd /tmp
-      step pmcb_FETCH 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmcb_FETCH" -o run -- python3 "$ROOT/bench.py" --steps 3 --warmup 1 --no-cpu-baseline --skip c4,calls --spinup-s 0.2 && \
-      step pmcb_WRITE 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmcb_WRITE" -o run -- python3 "$ROOT/bench.py" --steps 3 --warmup 1 --no-cpu-baseline --skip c4,calls --spinup-s 0.2 && \
-      python3 "$ROOT/scripts/pmc_traffic.py" "$OUT/pmcb_FETCH" "$OUT/pmcb_WRITE" "$TAG" > "$OUT/traffic.json"
-      cd "$ROOT" ;;
+      specs=""
+      for leg in ${GR_PMC_LEGS:-c2 sasrec c5 shard train}; do
+        cd /tmp
+        for c in FETCH_SIZE WRITE_SIZE; do
+          step pmc_${leg}_$c 240 rocprofv3 --pmc $c --output-format csv -d "$OUT/pmc_${leg}_$c" -o run -- \
+              python3 "$ROOT/bench.py" --legs $leg --steps 3 --warmup 1 --no-cpu-baseline --spinup-s 0.1
+        done
+        cd "$ROOT"
+        specs="$specs $leg=$OUT/pmc_${leg}_FETCH_SIZE,$OUT/pmc_${leg}_WRITE_SIZE"
+      done
+      python3 scripts/pmc_traffic.py --tag "$TAG" $specs > "$OUT/traffic.json" ;;
   esac
 done
 echo "== done"
