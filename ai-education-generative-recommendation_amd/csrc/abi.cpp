@@ -53,6 +53,11 @@ static std::atomic<int64_t> g_score_slice_major{1};
 // attn_occ1 (hd 128 attention: 1 = one workgroup per CU, 512 registers; 0 = two, 256 registers
 // with a few spills).  Identical results; A/B timing.
 static std::atomic<int64_t> g_attn_occ1{0};
+// attn_alt (1 (default): the attention kernel's wave -> query-tile order alternates between rounds,
+// balancing the causal work over the waves; 0: ascending in every round)
+static std::atomic<int64_t> g_attn_alt{1};
+// attn_lazy (hd 128 attention: 1 = lazy softmax rescaling + masks on the diagonal / last tile only)
+static std::atomic<int64_t> g_attn_lazy{1};
 
 int64_t option(const char* name) {
   if (!strcmp(name, "rq_fused")) return g_rq_fused.load();
@@ -69,6 +74,8 @@ int64_t option(const char* name) {
   if (!strcmp(name, "rq_resident")) return g_rq_resident.load();
   if (!strcmp(name, "score_slice_major")) return g_score_slice_major.load();
   if (!strcmp(name, "attn_occ1")) return g_attn_occ1.load();
+  if (!strcmp(name, "attn_alt")) return g_attn_alt.load();
+  if (!strcmp(name, "attn_lazy")) return g_attn_lazy.load();
   return -1;
 }
 }  // namespace gr
@@ -90,6 +97,8 @@ extern "C" int gr_set_option(const char* name, int64_t value) {
   if (!strcmp(name, "rq_resident") && (value == 0 || value == 1)) { gr::g_rq_resident = value; return GR_OK; }
   if (!strcmp(name, "score_slice_major") && (value == 0 || value == 1)) { gr::g_score_slice_major = value; return GR_OK; }
   if (!strcmp(name, "attn_occ1") && (value == 0 || value == 1)) { gr::g_attn_occ1 = value; return GR_OK; }
+  if (!strcmp(name, "attn_alt") && (value == 0 || value == 1)) { gr::g_attn_alt = value; return GR_OK; }
+  if (!strcmp(name, "attn_lazy") && (value == 0 || value == 1)) { gr::g_attn_lazy = value; return GR_OK; }
   return gr::fail(GR_ERR_ARG, std::string("gr_set_option: unknown option or value: ") + name);
 }
 

@@ -12,7 +12,11 @@
 // halves.  Keys are walked up to the diagonal with an online softmax (running max / sum per query,
 // O rescaled), and O^T[f][query] += V^T . P^T takes value rows as the A operand (lane = feature,
 // one ds_read_b32 feeding both query tiles) and P^T straight from the S^T registers.  fp32
-// throughout (v_mfma_f32_32x32x2_f32); exp via v_exp_f32.  Each output row sees exactly the same
+// throughout (v_mfma_f32_32x32x2_f32); exp via v_exp_f32.  LAZY (the default): the running max
+// is a reference point that moves only when a tile's max exceeds it by more than AT_LAZY, so the
+// O / l rescale (64 accumulator multiplies per lane at hd 128) runs on a few tiles per row, and
+// only the diagonal and the last key tile build masks (C5: 116 -> 100 us per call; a different
+// fp32 rounding of the same softmax, within the logits tolerance).  Each output row sees exactly the same
 // instruction sequence whichever tiles are launched, so a last-tile-only launch (the final block of
 // a last-position forward) reproduces the full launch's rows bit for bit.
 #include <cmath>
@@ -33,10 +37,12 @@ struct AttnTile {                  // one 32-query tile owned by a wave
 // Two workgroups per CU: at hd = 128 that caps the kernel at 256 VGPRs (a few spill), and still
 // measured 85 vs 114 us per C5 call (steady state) — the second workgroup's MFMAs fill the gaps
 // of the first's barriers and softmax.
-template <int HD, int OCC>
+constexpr float AT_LAZY = 8.f;   // lazy-rescale threshold (natural-log units)
+
+template <int HD, int OCC, bool LAZY>
 __global__ __launch_bounds__(256, OCC) void attn_mfma_kernel(const float* __restrict__ qkv,
                                                              float* __restrict__ out, int n, int H,
-                                                             float scale, int qt_lo) {
+                                                             float scale, int qt_lo, int alt) {
   constexpr int FT = HD / 32;
   constexpr int KP = HD + 4;   // K row pitch: conflict-free ds_read_b128 of 16 rows
   constexpr int VP = HD + 8;   // V row pitch: the two lane halves (4 rows apart) on disjoint banks
@@ -55,11 +61,15 @@ __global__ __launch_bounds__(256, OCC) void attn_mfma_kernel(const float* __rest
   const int T = (n + 31) / 32;
 
   // rounds of 4 query tiles, one per wave, taken from the end (the first round streams every key
-  // tile with all 4 waves busy for most of them; the short causal tail comes last)
-  for (int t1 = T; t1 > qt_lo; t1 -= 4) {
+  // tile with all 4 waves busy for most of them; the short causal tail comes last).  The wave ->
+  // tile order alternates between rounds (descending, then ascending), so a wave that had a long
+  // tile gets a short one next: at n = 200 (T = 7) the waves run 7+1, 6+2, 5+3 and 4 key-tile
+  // steps instead of 4+1, 5+2, 6+3 and 7.
+  for (int t1 = T, round = 0; t1 > qt_lo; t1 -= 4, ++round) {
     const int t0 = t1 - 4 > qt_lo ? t1 - 4 : qt_lo;
     const int nt = t1 - t0;
-    int myq[2] = {w < nt ? t0 + w : -1, -1};
+    const int mine = alt && (round & 1) == 0 ? t1 - 1 - w : t0 + w;
+    int myq[2] = {w < nt ? mine : -1, -1};
     AttnTile<HD> at[1];
 #pragma unroll
     for (int u = 0; u < 1; ++u) {
@@ -123,29 +133,58 @@ __global__ __launch_bounds__(256, OCC) void attn_mfma_kernel(const float* __rest
       for (int u = 0; u < NU; ++u) {
         AttnTile<HD>& A = at[U0 + u];
         const int qi = myq[U0 + u] * 32 + r;
-        // causal / padding mask: register v holds key 32kt + (v&3) + 8(v>>2) + 4h for query qi
+        // causal / padding mask: register v holds key 32kt + (v&3) + 8(v>>2) + 4h for query qi;
+        // only the diagonal tile and the catalog's last tile have masked keys (wave-uniform test)
         float tmax = -INFINITY;
+        if (!LAZY || kt == myq[U0 + u] || kt * 32 + 32 > n) {
 #pragma unroll
-        for (int v = 0; v < 16; ++v) {
-          const int key = kt * 32 + (v & 3) + 8 * (v >> 2) + 4 * h;
-          if (key > qi || key >= n) S[u][v] = -INFINITY;
-          tmax = fmaxf(tmax, S[u][v]);
+          for (int v = 0; v < 16; ++v) {
+            const int key = kt * 32 + (v & 3) + 8 * (v >> 2) + 4 * h;
+            if (key > qi || key >= n) S[u][v] = -INFINITY;
+            tmax = fmaxf(tmax, S[u][v]);
+          }
+        } else {
+#pragma unroll
+          for (int v = 0; v < 16; ++v) tmax = fmaxf(tmax, S[u][v]);
         }
         tmax = fmaxf(tmax, __shfl_xor(tmax, 32));
-        const float mn = fmaxf(A.m, tmax);
-        const float alpha = __expf(A.m - mn);   // 0 on the first tile (m = -inf)
         float ts = 0.f;
+        if (LAZY) {
+          // lazy rescaling: the reference point m moves only when a score exceeds it by more
+          // than AT_LAZY (exp <= e^8 in between, far from fp32 overflow), so O and l are
+          // rescaled on a few tiles per row instead of every tile
+          const bool up = tmax > A.m + AT_LAZY;   // always on the first tile (m = -inf)
+          if (__any(up)) {
+            const float mn = up ? tmax : A.m;
+            const float alpha = __expf(A.m - mn);   // 1 for lanes that keep m, 0 on the first tile
+            A.l *= alpha;
+            A.m = mn;
 #pragma unroll
-        for (int v = 0; v < 16; ++v) {
-          const float e = __expf(S[u][v] - mn);
-          S[u][v] = e;
-          ts += e;
+            for (int ft = 0; ft < FT; ++ft) A.O[ft] *= alpha;
+          }
+#pragma unroll
+          for (int v = 0; v < 16; ++v) {
+            const float e = __expf(S[u][v] - A.m);
+            S[u][v] = e;
+            ts += e;
+          }
+          ts += __shfl_xor(ts, 32);
+          A.l += ts;
+        } else {
+          const float mn = fmaxf(A.m, tmax);
+          const float alpha = __expf(A.m - mn);   // 0 on the first tile (m = -inf)
+#pragma unroll
+          for (int v = 0; v < 16; ++v) {
+            const float e = __expf(S[u][v] - mn);
+            S[u][v] = e;
+            ts += e;
+          }
+          ts += __shfl_xor(ts, 32);
+          A.l = A.l * alpha + ts;
+          A.m = mn;
+#pragma unroll
+          for (int ft = 0; ft < FT; ++ft) A.O[ft] *= alpha;
         }
-        ts += __shfl_xor(ts, 32);
-        A.l = A.l * alpha + ts;
-        A.m = mn;
-#pragma unroll
-        for (int ft = 0; ft < FT; ++ft) A.O[ft] *= alpha;
       }
       // O^T[f][q] += V^T[f][key] P^T[key][q]: A = value rows (lane = feature), B = S^T registers
 #pragma unroll
@@ -153,7 +192,8 @@ __global__ __launch_bounds__(256, OCC) void attn_mfma_kernel(const float* __rest
 #pragma unroll
         for (int s = 0; s < 16; ++s) {
           const int key = (s & 3) + 8 * (s >> 2) + 4 * h;
-          const float vv = kt * 32 + key < n ? vs[bf][key * VP + 32 * ft + r] : 0.f;
+          // keys past n: P = 0 and V holds a clamped (finite) row, so no select is needed
+          const float vv = LAZY ? vs[bf][key * VP + 32 * ft + r] : kt * 32 + key < n ? vs[bf][key * VP + 32 * ft + r] : 0.f;
 #pragma unroll
           for (int u = 0; u < NU; ++u) at[U0 + u].O[ft] = mfma32(vv, S[u][s], at[U0 + u].O[ft]);
         }
@@ -371,12 +411,21 @@ int gr_attn_mfma_launch(const float* qkv, float* out, int64_t B, int n, int H, i
   }
   // attn_occ1 (hd 128): one workgroup per CU at 512 registers (no spills) instead of two at 256
   const bool occ1 = option("attn_occ1") != 0;
+  const int alt = option("attn_alt") != 0 ? 1 : 0;
+  const bool lazy = option("attn_lazy") != 0;   // lazy softmax rescaling, diagonal-only masks
   switch (hd) {
-    case 32: hipLaunchKernelGGL((attn_mfma_kernel<32, 2>), g, blk, 0, st, qkv, out, n, H, scale, qt_lo); break;
-    case 64: hipLaunchKernelGGL((attn_mfma_kernel<64, 2>), g, blk, 0, st, qkv, out, n, H, scale, qt_lo); break;
+    case 32:
+      if (lazy) hipLaunchKernelGGL((attn_mfma_kernel<32, 2, true>), g, blk, 0, st, qkv, out, n, H, scale, qt_lo, alt);
+      else hipLaunchKernelGGL((attn_mfma_kernel<32, 2, false>), g, blk, 0, st, qkv, out, n, H, scale, qt_lo, alt);
+      break;
+    case 64:
+      if (lazy) hipLaunchKernelGGL((attn_mfma_kernel<64, 2, true>), g, blk, 0, st, qkv, out, n, H, scale, qt_lo, alt);
+      else hipLaunchKernelGGL((attn_mfma_kernel<64, 2, false>), g, blk, 0, st, qkv, out, n, H, scale, qt_lo, alt);
+      break;
     default:
-      if (occ1) hipLaunchKernelGGL((attn_mfma_kernel<128, 1>), g, blk, 0, st, qkv, out, n, H, scale, qt_lo);
-      else hipLaunchKernelGGL((attn_mfma_kernel<128, 2>), g, blk, 0, st, qkv, out, n, H, scale, qt_lo);
+      if (occ1) hipLaunchKernelGGL((attn_mfma_kernel<128, 1, false>), g, blk, 0, st, qkv, out, n, H, scale, qt_lo, alt);
+      else if (lazy) hipLaunchKernelGGL((attn_mfma_kernel<128, 2, true>), g, blk, 0, st, qkv, out, n, H, scale, qt_lo, alt);
+      else hipLaunchKernelGGL((attn_mfma_kernel<128, 2, false>), g, blk, 0, st, qkv, out, n, H, scale, qt_lo, alt);
       break;
   }
   return check_launch("sasrec attention (mfma)");
