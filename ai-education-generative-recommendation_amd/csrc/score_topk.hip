@@ -61,7 +61,38 @@ struct LaneList {
       moved = b;
     }
   }
+  // Insert (x, col) into the list ordered by (value desc, column asc), columns in any order.
+  __device__ __forceinline__ void insert_any(float x, int col) {
+    bool moved = false;
+#pragma unroll
+    for (int q = 0; q < KC; ++q) {
+      const bool b = moved || x > v[q] || (x == v[q] && col < c[q] && col >= 0);
+      const float tv = v[q];
+      const int tc = c[q];
+      v[q] = b ? x : tv;
+      c[q] = b ? col : tc;
+      x = b ? tv : x;
+      col = b ? tc : col;
+      moved = b;
+    }
+  }
 };
+
+// The two lane halves of a user (lanes r and r + 32) hold one sorted candidate list each; lane
+// half 0 ends with the top KC of both by (value desc, column asc), so a (user, slice) of the exact
+// pass writes one segment instead of two and the final merge reads half as many candidates.
+template <int KC>
+__device__ __forceinline__ void merge_halves(LaneList<KC>& ll) {
+  float ov[KC];
+  int oc[KC];
+#pragma unroll
+  for (int q = 0; q < KC; ++q) {
+    ov[q] = __shfl_xor(ll.v[q], 32);
+    oc[q] = __shfl_xor(ll.c[q], 32);
+  }
+#pragma unroll
+  for (int q = 0; q < KC; ++q) ll.insert_any(ov[q], oc[q]);
+}
 
 // The largest float below t (t > -inf, not NaN): x > prev_below(t)  <=>  x >= t.
 __device__ __forceinline__ float prev_below(float t) {
@@ -197,6 +228,28 @@ __global__ __launch_bounds__(256, 2) void score_topk_kernel(
           }
         }
     }
+    if (mode == 2) {   // tile pass: strict counts + the max logit of every 32-row tile per user
+#pragma unroll
+      for (int ut = 0; ut < UT; ++ut) {
+        const int64_t u = u0 + ut * 32 + r;
+#pragma unroll
+        for (int it = 0; it < 2; ++it) {
+          float m = -INFINITY;   // fmaxf skips the NaN of rows past the catalog
+#pragma unroll
+          for (int v = 0; v < 16; ++v) {
+            const float x = acc[ut][it][v];
+            cgt[ut] += x > th[ut] ? 1 : 0;
+            m = fmaxf(m, x);
+          }
+          m = fmaxf(m, __shfl_xor(m, 32));
+          if (hh == 0 && u < B) cv[u * seg_stride + 2 * vc + it] = m;
+        }
+      }
+      if (vc + 1 < v_end) swrite(buf ^ 1);
+      __syncthreads();
+      buf ^= 1;
+      continue;
+    }
     if (mode == 1) {   // sample pass: bucket maxima (bucket = position mod KC), nothing else
 #pragma unroll
       for (int ut = 0; ut < UT; ++ut)
@@ -239,25 +292,164 @@ __global__ __launch_bounds__(256, 2) void score_topk_kernel(
     __syncthreads();
     buf ^= 1;
   }
-  // strict counts: the two lane halves of a user, one atomic per (user, slice)
+  // strict counts: the two lane halves of a user, one atomic per (user, slice).  The sample pass
+  // (which counts nothing) clears them instead, from its first slice: the exact pass runs after it.
 #pragma unroll
   for (int ut = 0; ut < UT; ++ut) {
     const int x = cgt[ut] + __shfl_xor(cgt[ut], 32);
     const int64_t u = u0 + ut * 32 + r;
-    if (cnt_out && hh == 0 && u < B && x) atomicAdd(&cnt_out[u], (unsigned long long)x);
+    if (mode == 2) {   // per-(user, slice) partial counts, summed by the select kernel
+      if (hh == 0 && u < B) reinterpret_cast<unsigned*>(ci)[u * slices + sl] = (unsigned)x;
+    } else if (mode == 1) {
+      if (cnt_out && sl == 0 && hh == 0 && u < B) cnt_out[u] = 0ull;
+    } else if (cnt_out && hh == 0 && u < B && x) {
+      atomicAdd(&cnt_out[u], (unsigned long long)x);
+    }
   }
-  // candidate segment (pass, slice, half) of each user: the lane's sorted list
+  if (mode == 2) return;
+  // candidate segments of each user: the exact pass writes one per slice (the merged list of its
+  // two lane halves), the sample pass one per (slice, half) — merging unsorted bucket maxima costs
+  // more than the merge kernel saves on a pass that scores one chunk per workgroup
 #pragma unroll
   for (int ut = 0; ut < UT; ++ut) {
+    if (mode == 0) merge_halves<KC>(ll[ut]);
     const int64_t u = u0 + ut * 32 + r;
-    if (u >= B) continue;
-    const int64_t base = u * seg_stride + (int64_t)(seg_off + 2 * sl + hh) * KC;
+    if (u >= B || (mode == 0 && hh != 0)) continue;
+    const int64_t base = u * seg_stride + (int64_t)(seg_off + (mode == 0 ? sl : 2 * sl + hh)) * KC;
 #pragma unroll
     for (int q = 0; q < KC; ++q) {   // (the sample pass's bucket maxima carry no column)
       cv[base + q] = ll[ut].v[q];
       ci[base + q] = mode == 1 ? (int64_t)q : ll[ut].c[q] < 0 ? INT64_MAX : (int64_t)ll[ut].c[q];
     }
   }
+}
+
+// Tile design (topk_impl 1, the default).  The tile pass (MODE 2) scores every chunk once, counts,
+// and records per user the max logit of every 32-row tile.  Let M_k be the k-th largest tile max:
+// those k tiles hold k distinct items >= M_k, so the user's k-th best logit is >= M_k and every
+// top-k item lies in a tile whose max is >= M_k (about k tiles; more only on exact ties).  This
+// kernel (one workgroup per user) finds M_k, re-scores just those tiles with the tile pass's exact
+// MFMA chain (table rows as the A operand, the user as B: bitwise the same logits), and selects
+// the top k by (value desc, column asc); it also sums the partial counts.
+template <int D, int KC>
+__global__ __launch_bounds__(256) void topk_select_kernel(const float* __restrict__ h, int64_t B,
+                                                          const float* __restrict__ table, int64_t rows,
+                                                          int mask_col0, int k, int64_t id_offset,
+                                                          const float* __restrict__ tmax, int64_t T,
+                                                          const unsigned* __restrict__ cpart, int slices,
+                                                          unsigned long long* __restrict__ cnt_out,
+                                                          float* __restrict__ vals, int64_t* __restrict__ ids) {
+  constexpr int KG = D / 32;
+  __shared__ int list[256];
+  __shared__ int nlist, saturated;
+  __shared__ float mk_s;
+  __shared__ unsigned long long csum;
+  const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, hh = lane >> 5, w = tid >> 6;
+  const int64_t u = blockIdx.x;
+  const float* tm = tmax + u * T;
+  if (tid == 0) {
+    nlist = 0;
+    saturated = 0;
+    csum = 0ull;
+    mk_s = -INFINITY;
+  }
+  __syncthreads();
+  if (cnt_out) {
+    unsigned long long c = 0;
+    for (int i = tid; i < slices; i += 256) c += cpart[u * slices + i];
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
+    if (lane == 0 && c) atomicAdd(&csum, c);
+  }
+  // M_k = the k-th largest tile max; each thread keeps its own KC best tiles (batches of MB loads)
+  TopList<KC> tl;
+  tl.init();
+  {
+    constexpr int MB = 16;
+    for (int64_t q0 = tid; q0 < T; q0 += 256 * MB) {
+      float v[MB];
+#pragma unroll
+      for (int b = 0; b < MB; ++b) {
+        const int64_t q = q0 + 256 * b;
+        v[b] = tm[q < T ? q : q0];
+      }
+#pragma unroll
+      for (int b = 0; b < MB; ++b)
+        if (q0 + 256 * b < T) tl.push(v[b], q0 + 256 * b);
+    }
+    tl.block_select(k, [&](int q, float v, int64_t) {
+      if (q == k - 1) mk_s = v;
+    });
+  }
+  __syncthreads();
+  const float mk = mk_s;
+  if (cnt_out && tid == 0) cnt_out[u] = csum;
+  // The qualifying tiles (max >= M_k) are the threads' list entries >= M_k, unless a thread's list
+  // is all >= M_k (it may hold more: exact ties) or they overflow the list -- then every tile is
+  // re-checked, 256 at a time.
+  int mine = 0;
+#pragma unroll
+  for (int q = 0; q < KC; ++q) mine += (tl.i[q] != INT64_MAX && tl.v[q] >= mk) ? 1 : 0;
+  if (mine == KC) saturated = 1;
+  if (mine) atomicAdd(&nlist, mine);
+  __syncthreads();
+  const bool slow = saturated != 0 || nlist > 256;   // (ties past the list's capacity)
+  __syncthreads();
+  if (tid == 0) nlist = 0;
+  __syncthreads();
+  if (!slow) {
+#pragma unroll
+    for (int q = 0; q < KC; ++q)
+      if (tl.i[q] != INT64_MAX && tl.v[q] >= mk) list[atomicAdd(&nlist, 1)] = (int)tl.i[q];
+  }
+  f32x4 hf[KG][4];   // the user's B operand (the same in every lane column)
+#pragma unroll
+  for (int g = 0; g < KG; ++g)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) hf[g][q] = *reinterpret_cast<const f32x4*>(h + u * D + 32 * g + 8 * q + 4 * hh);
+  TopList<KC> best;
+  best.init();
+  for (int64_t b0 = 0; b0 < (slow ? T : 1); b0 += 256) {
+    if (slow) {
+      __syncthreads();
+      if (tid == 0) nlist = 0;
+      __syncthreads();
+      const int64_t t = b0 + tid;
+      if (t < T && tm[t] >= mk) list[atomicAdd(&nlist, 1)] = (int)t;
+    }
+    __syncthreads();
+    const int n = nlist;
+    for (int e = w; e < n; e += 4) {
+      const int64_t row = (int64_t)list[e] * 32 + r;
+      const int64_t rc = row < rows ? row : rows - 1;
+      f32x4 a[KG][4];
+#pragma unroll
+      for (int g = 0; g < KG; ++g)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) a[g][q] = *reinterpret_cast<const f32x4*>(table + rc * D + 32 * g + 8 * q + 4 * hh);
+      f32x16 acc;
+#pragma unroll
+      for (int v = 0; v < 16; ++v) acc[v] = 0.f;
+#pragma unroll
+      for (int g = 0; g < KG; ++g)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+          for (int s4 = 0; s4 < 4; ++s4) acc = mfma32(a[g][q][s4], hf[g][q][s4], acc);
+      // lane (r, hh) with hh = bit 2 of r holds item r of the tile in register (r&3) + 4(r>>3)
+      float x = 0.f;
+#pragma unroll
+      for (int v = 0; v < 16; ++v)
+        if ((v & 3) + 8 * (v >> 2) + 4 * hh == r) x = acc[v];
+      if (((r >> 2) & 1) == hh && row < rows) {
+        if (mask_col0 && row == 0) x = TK_MASK;
+        if (x == x) best.push(x, row);   // NaN never enters (as in the list passes)
+      }
+    }
+  }
+  best.block_select(k, [&](int q, float v, int64_t i) {
+    vals[u * k + q] = v;
+    ids[u * k + q] = i == INT64_MAX ? -1 : i + id_offset;
+  });
 }
 
 static int cu_count() {
@@ -283,7 +475,7 @@ struct TopkPlan {
   int64_t v1, slices1;         // the sample pass (s > 0)
   int64_t slices2;             // the full pass
   int kc;
-  int64_t seg_per_user() const { return 2 * (slices1 + slices2); }
+  int64_t seg_per_user() const { return 2 * slices1 + slices2; }
 };
 
 static int64_t slices_for(int64_t ublocks, int64_t vchunks, int d) {
@@ -319,6 +511,27 @@ static TopkPlan topk_plan(int64_t B, int64_t rows, int k, int d) {
   return p;
 }
 
+// Tile design (topk_impl 1): one counting pass over every chunk writing per-user tile maxima, then
+// the select kernel.  Workspace: tile maxima [B][2 * chunks] floats + partial counts [B][slices].
+static bool tile_design() { return option("topk_impl") != 0; }
+
+struct TileWs {
+  int64_t T, slices, ublocks, chunks;
+  size_t tmax, cpart, total;
+};
+static TileWs tile_ws(int64_t B, int64_t rows, int d) {
+  TileWs w;
+  const int uw = users_per_wg(d);
+  w.ublocks = (B + uw - 1) / uw;
+  w.chunks = (rows + TK_CHUNK - 1) / TK_CHUNK;
+  w.slices = slices_for(w.ublocks, w.chunks, d);
+  w.T = 2 * w.chunks;
+  w.tmax = align_up((size_t)B * w.T * sizeof(float), 256);
+  w.cpart = align_up((size_t)B * w.slices * sizeof(unsigned), 256);
+  w.total = w.tmax + w.cpart + 256;
+  return w;
+}
+
 struct TopkWs {
   size_t cv, ci, v1, i1, total;
 };
@@ -349,6 +562,14 @@ static void launch_pass(int d, dim3 grid, hipStream_t st, const float* h, int64_
     }
     return;
   }
+  if (mode == 2) {
+    switch (d) {
+      case 32: GR_TK_PASS(32, 2); break;
+      case 64: GR_TK_PASS(64, 2); break;
+      default: GR_TK_PASS(128, 2); break;
+    }
+    return;
+  }
   switch (d) {
     case 32: GR_TK_PASS(32, 0); break;
     case 64: GR_TK_PASS(64, 0); break;
@@ -369,6 +590,7 @@ static void launch_merge(hipStream_t st, int64_t B, int64_t row_stride, int64_t 
 extern "C" size_t gr_score_topk_workspace_bytes(int64_t B, int32_t d, int64_t rows, int32_t k) {
   (void)d;
   if (B < 1 || rows < 1 || k < 1 || k > 16) return 256;
+  if (gr::tile_design()) return gr::tile_ws(B, rows, d).total;
   const gr::TopkPlan p = gr::topk_plan(B, rows, k, d);
   return gr::topk_ws(B, p, k).total;
 }
@@ -392,9 +614,9 @@ extern "C" int gr_score_topk_f32(const float* h, int64_t B, int32_t d, const flo
   if (B > 65535) return fail(GR_ERR_UNSUPPORTED, "gr_score_topk_f32: B > 65535");
   if (!aligned16(h) || !aligned16(table)) return fail(GR_ERR_ARG, "gr_score_topk_f32: h / table not 16-byte aligned");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  if (counts_out && hipMemsetAsync(counts_out, 0, (size_t)B * sizeof(int64_t), st) != hipSuccess)
-    return fail(GR_ERR_HIP, "gr_score_topk_f32: memset failed");
   if (rows == 0) {   // nothing to rank: every entry is padding
+    if (counts_out && hipMemsetAsync(counts_out, 0, (size_t)B * sizeof(int64_t), st) != hipSuccess)
+      return fail(GR_ERR_HIP, "gr_score_topk_f32: memset failed");
     if (hipMemsetAsync(ids_out, 0xff, (size_t)B * k * sizeof(int64_t), st) != hipSuccess)
       return fail(GR_ERR_HIP, "gr_score_topk_f32: memset failed");
     const float ninf = -INFINITY;
@@ -404,8 +626,46 @@ extern "C" int gr_score_topk_f32(const float* h, int64_t B, int32_t d, const flo
       return fail(GR_ERR_HIP, "gr_score_topk_f32: memset failed");
     return GR_OK;
   }
+  if (tile_design()) {
+    const TileWs tw = tile_ws(B, rows, d);
+    if (!workspace || workspace_bytes < tw.total)
+      return fail(GR_ERR_WORKSPACE, "gr_score_topk_f32: workspace too small (need " + std::to_string(tw.total) + " bytes)");
+    if (tw.ublocks * tw.slices > 0x7fffffffLL || tw.T > 0x7fffffffLL)
+      return fail(GR_ERR_UNSUPPORTED, "gr_score_topk_f32: grid too large");
+    char* base = reinterpret_cast<char*>(align_up(reinterpret_cast<uintptr_t>(workspace), 256));
+    auto* tmax = reinterpret_cast<float*>(base);
+    auto* cpart = reinterpret_cast<unsigned*>(base + tw.tmax);
+    auto* cnt = reinterpret_cast<unsigned long long*>(counts_out);
+    auto runt = [&](auto kc_tag) -> int {
+      constexpr int KC = decltype(kc_tag)::value;
+      launch_pass<KC>(d, dim3((unsigned)(tw.ublocks * tw.slices)), st, h, B, table, rows, thresholds, mask_col0,
+                      nullptr, nullptr, 0, tw.chunks, 2, 1, tmax, reinterpret_cast<int64_t*>(cpart), tw.T, 0,
+                      (int)tw.ublocks, (int)tw.slices, 0);
+      int rc = check_launch("gr_score_topk_f32 (tile pass)");
+      if (rc) return rc;
+#define GR_TK_SEL(DD) hipLaunchKernelGGL((topk_select_kernel<DD, KC>), dim3((unsigned)B), dim3(256), 0, st, h, B, \
+                                         table, rows, mask_col0, k, id_offset, tmax, tw.T, cpart, (int)tw.slices, \
+                                         cnt, vals_out, ids_out)
+      switch (d) {
+        case 32: GR_TK_SEL(32); break;
+        case 64: GR_TK_SEL(64); break;
+        default: GR_TK_SEL(128); break;
+      }
+#undef GR_TK_SEL
+      return check_launch("gr_score_topk_f32 (select)");
+    };
+    switch (kc_for(k)) {
+      case 4: return runt(std::integral_constant<int, 4>{});
+      case 10: return runt(std::integral_constant<int, 10>{});
+      default: return runt(std::integral_constant<int, 16>{});
+    }
+  }
   const TopkPlan p = topk_plan(B, rows, k, d);
   const TopkWs wl = topk_ws(B, p, k);
+  // the strict counts start at zero: the sample pass clears them when there is one (no launch of
+  // its own), a memset otherwise
+  if (counts_out && !p.s && hipMemsetAsync(counts_out, 0, (size_t)B * sizeof(int64_t), st) != hipSuccess)
+    return fail(GR_ERR_HIP, "gr_score_topk_f32: memset failed");
   if (!workspace || workspace_bytes < wl.total)
     return fail(GR_ERR_WORKSPACE, "gr_score_topk_f32: workspace too small (need " + std::to_string(wl.total) + " bytes)");
   if (p.ublocks * p.slices2 > 0x7fffffffLL)
@@ -425,7 +685,7 @@ extern "C" int gr_score_topk_f32(const float* h, int64_t B, int32_t d, const flo
     int rc;
     if (p.s) {   // sample pass -> T_S = the k-th largest bucket maximum per user
       launch_pass<KC>(d, dim3((unsigned)(p.ublocks * p.slices1)), st, h, B, table, rows, nullptr, mask_col0,
-                      nullptr, nullptr, 0, p.v1, 1, p.s, cv, ci, seg_stride, 0, ub, (int)p.slices1, ablate);
+                      cnt, nullptr, 0, p.v1, 1, p.s, cv, ci, seg_stride, 0, ub, (int)p.slices1, ablate);
       rc = check_launch("gr_score_topk_f32 (sample pass)");
       if (rc) return rc;
       launch_merge<KC>(st, B, seg_stride, 2 * p.slices1 * KC, k, 0, cv, ci, v1, i1);
@@ -439,7 +699,7 @@ extern "C" int gr_score_topk_f32(const float* h, int64_t B, int32_t d, const flo
     rc = check_launch("gr_score_topk_f32 (pass)");
     if (rc) return rc;
     // final merge over the full pass's segments only (the sample's maxima are not candidates)
-    launch_merge<KC>(st, B, seg_stride, 2 * p.slices2 * KC, k, id_offset, cv + 2 * p.slices1 * KC,
+    launch_merge<KC>(st, B, seg_stride, p.slices2 * KC, k, id_offset, cv + 2 * p.slices1 * KC,
                      ci + 2 * p.slices1 * KC, vals_out, ids_out);
     return check_launch("gr_score_topk_f32 (merge)");
   };

@@ -28,22 +28,24 @@ def _reference(h, t, k, id_offset, thr, mask_col0):
 
 
 def _check(h, t, k, id_offset=0, mask_col0=True, seed=0):
-    """Both plans (sample-thresholded two passes where the catalog is long enough, and one pass)
-    against the materialised reference."""
+    """Every plan against the materialised reference: the tile design (tile maxima + re-scored
+    tiles, the default), and the list design with its sample-thresholded two passes and one pass."""
     from gr_amd import _lib, ops
     g = torch.Generator(device=h.device).manual_seed(seed)
     thr = torch.randn(h.shape[0], generator=g, device=h.device)
     rv, ri, rc = _reference(h, t, k, id_offset, thr, mask_col0)
     try:
-        for sample in (1, 0):
+        for impl, sample in ((1, 1), (0, 1), (0, 0)):
+            _lib.set_option("topk_impl", impl)
             _lib.set_option("topk_sample", sample)
             v, i, c = ops.score_topk(h, t, k, id_offset, thresholds=thr, mask_col0=mask_col0)
-            assert torch.equal(i, ri)
-            assert torch.equal(v, rv)
-            assert torch.equal(c, rc)
+            assert torch.equal(i, ri), (impl, sample)
+            assert torch.equal(v, rv), (impl, sample)
+            assert torch.equal(c, rc), (impl, sample)
             v2, i2 = ops.score_topk(h, t, k, id_offset, mask_col0=mask_col0)   # without counts
-            assert torch.equal(v2, rv) and torch.equal(i2, ri)
+            assert torch.equal(v2, rv) and torch.equal(i2, ri), (impl, sample)
     finally:
+        _lib.set_option("topk_impl", 1)
         _lib.set_option("topk_sample", 1)
 
 
