@@ -66,6 +66,7 @@ SIGNATURES = {
     "gr_sampled_bce_fwd_f32": (ctypes.c_int, [_vp, _i64, _i32, _i32, _vp, _i64, _vp, _vp, _i32, _f32,
                                               _vp, _vp, _vp, _vp, _vp]),
     "gr_neg_samples": (ctypes.c_int, [_vp, _i64, _i32, _i64, _i32, ctypes.c_uint64, _vp, _vp, _vp]),
+    "gr_neg_samples_dseed": (ctypes.c_int, [_vp, _i64, _i32, _i64, _i32, ctypes.c_uint64, _vp, _vp, _vp, _vp]),
     "gr_sampled_bce_bwd_f32": (ctypes.c_int, [_vp, _i64, _i32, _i32, _vp, _i64, _vp, _vp, _i32, _vp,
                                               _vp, _vp, _vp, _vp]),
     "gr_rank_f32": (ctypes.c_int, [_vp, _i64, _i64, _i64, _vp, _i32, _vp, _vp]),

@@ -65,6 +65,8 @@ static std::atomic<int64_t> g_rq_occ2{0};
 // topk_impl (1 (default): gr_score_topk_f32 = tile-max counting pass + select/re-score kernel;
 // 0: sample pass + exact list pass + merges)
 static std::atomic<int64_t> g_topk_impl{1};
+// topk_sel_abl (diagnostic only, wrong results: bit 1 no re-scoring, 2 no k-th tile select, 4 no final select)
+static std::atomic<int64_t> g_topk_sel_abl{0};
 
 int64_t option(const char* name) {
   if (!strcmp(name, "rq_fused")) return g_rq_fused.load();
@@ -86,6 +88,7 @@ int64_t option(const char* name) {
   if (!strcmp(name, "lin_persist")) return g_lin_persist.load();
   if (!strcmp(name, "rq_occ2")) return g_rq_occ2.load();
   if (!strcmp(name, "topk_impl")) return g_topk_impl.load();
+  if (!strcmp(name, "topk_sel_abl")) return g_topk_sel_abl.load();
   return -1;
 }
 }  // namespace gr
@@ -112,6 +115,7 @@ extern "C" int gr_set_option(const char* name, int64_t value) {
   if (!strcmp(name, "lin_persist") && (value == 0 || value == 1)) { gr::g_lin_persist = value; return GR_OK; }
   if (!strcmp(name, "rq_occ2") && (value == 0 || value == 1)) { gr::g_rq_occ2 = value; return GR_OK; }
   if (!strcmp(name, "topk_impl") && (value == 0 || value == 1)) { gr::g_topk_impl = value; return GR_OK; }
+  if (!strcmp(name, "topk_sel_abl") && value >= 0 && value <= 7) { gr::g_topk_sel_abl = value; return GR_OK; }
   return gr::fail(GR_ERR_ARG, std::string("gr_set_option: unknown option or value: ") + name);
 }
 

@@ -24,7 +24,8 @@ constexpr int NS_MAX_ROUNDS = 4096;
 constexpr int NS_MAX_NEG = 1024;
 
 __global__ __launch_bounds__(256) void neg_sample_kernel(const int64_t* __restrict__ seqs, int64_t B,
-                                                        int n, int64_t item_num, int J, uint64_t seed,
+                                                        int n, int64_t item_num, int J, uint64_t seed0,
+                                                        const uint64_t* __restrict__ seed_dev,
                                                         int64_t* __restrict__ out,
                                                         int32_t* __restrict__ err) {
   __shared__ int64_t taken_ids[4][NS_MAX_NEG];   // per wave: the items kept so far, in order
@@ -34,6 +35,7 @@ __global__ __launch_bounds__(256) void neg_sample_kernel(const int64_t* __restri
   const int64_t* hist = seqs + row * n;
   int64_t* tk = taken_ids[w];
   int taken = 0;
+  const uint64_t seed = seed_dev ? seed0 ^ *seed_dev : seed0;   // (read only; advanced by the caller)
   const uint64_t rkey = mix64(seed ^ mix64((uint64_t)row));
   for (int round = 0; round < NS_MAX_ROUNDS && taken < J; ++round) {
     const uint64_t u = mix64(rkey + (uint64_t)round * 64 + lane);
@@ -61,9 +63,8 @@ __global__ __launch_bounds__(256) void neg_sample_kernel(const int64_t* __restri
 
 }  // namespace gr
 
-extern "C" int gr_neg_samples(const int64_t* seqs, int64_t B, int32_t n, int64_t item_num,
-                              int32_t num_neg, uint64_t seed, int64_t* out, int32_t* err_flag,
-                              void* stream) {
+static int launch_neg(const int64_t* seqs, int64_t B, int32_t n, int64_t item_num, int32_t num_neg,
+                      uint64_t seed, const uint64_t* seed_dev, int64_t* out, int32_t* err_flag, void* stream) {
   using namespace gr;
   clear_error();
   if (B < 0 || n < 0 || num_neg < 0 || item_num < 1) return fail(GR_ERR_ARG, "gr_neg_samples: bad shape");
@@ -74,7 +75,20 @@ extern "C" int gr_neg_samples(const int64_t* seqs, int64_t B, int32_t n, int64_t
     return fail(GR_ERR_ARG, "gr_neg_samples: num_neg > item_num (cannot take a larger sample than the population)");
   if ((B + 3) / 4 > 0x7fffffffLL) return fail(GR_ERR_UNSUPPORTED, "gr_neg_samples: B too large");
   hipLaunchKernelGGL(neg_sample_kernel, dim3((unsigned)((B + 3) / 4)), dim3(256), 0,
-                     reinterpret_cast<hipStream_t>(stream), seqs, B, n, item_num, num_neg, seed, out,
+                     reinterpret_cast<hipStream_t>(stream), seqs, B, n, item_num, num_neg, seed, seed_dev, out,
                      err_flag);
   return check_launch("gr_neg_samples");
+}
+
+extern "C" int gr_neg_samples(const int64_t* seqs, int64_t B, int32_t n, int64_t item_num,
+                              int32_t num_neg, uint64_t seed, int64_t* out, int32_t* err_flag,
+                              void* stream) {
+  return launch_neg(seqs, B, n, item_num, num_neg, seed, nullptr, out, err_flag, stream);
+}
+
+extern "C" int gr_neg_samples_dseed(const int64_t* seqs, int64_t B, int32_t n, int64_t item_num,
+                                    int32_t num_neg, uint64_t seed, const uint64_t* seed_dev, int64_t* out,
+                                    int32_t* err_flag, void* stream) {
+  if (!seed_dev) return gr::fail(GR_ERR_ARG, "gr_neg_samples_dseed: null seed");
+  return launch_neg(seqs, B, n, item_num, num_neg, seed, seed_dev, out, err_flag, stream);
 }

@@ -332,13 +332,14 @@ __global__ __launch_bounds__(256, 2) void score_topk_kernel(
 // MFMA chain (table rows as the A operand, the user as B: bitwise the same logits), and selects
 // the top k by (value desc, column asc); it also sums the partial counts.
 template <int D, int KC>
-__global__ __launch_bounds__(256) void topk_select_kernel(const float* __restrict__ h, int64_t B,
+__global__ __launch_bounds__(256, 2) void topk_select_kernel(const float* __restrict__ h, int64_t B,
                                                           const float* __restrict__ table, int64_t rows,
                                                           int mask_col0, int k, int64_t id_offset,
                                                           const float* __restrict__ tmax, int64_t T,
                                                           const unsigned* __restrict__ cpart, int slices,
                                                           unsigned long long* __restrict__ cnt_out,
-                                                          float* __restrict__ vals, int64_t* __restrict__ ids) {
+                                                          float* __restrict__ vals, int64_t* __restrict__ ids,
+                                                          int abl) {
   constexpr int KG = D / 32;
   __shared__ int list[256];
   __shared__ int nlist, saturated;
@@ -376,9 +377,13 @@ __global__ __launch_bounds__(256) void topk_select_kernel(const float* __restric
       for (int b = 0; b < MB; ++b)
         if (q0 + 256 * b < T) tl.push(v[b], q0 + 256 * b);
     }
-    tl.block_select(k, [&](int q, float v, int64_t) {
-      if (q == k - 1) mk_s = v;
-    });
+    if (abl & 2) {   // diagnostic only (topk_sel_abl): the list head instead of a block select
+      if (tid == 0) mk_s = tl.v[0];
+    } else {
+      tl.block_select(k, [&](int q, float v, int64_t) {
+        if (q == k - 1) mk_s = v;
+      });
+    }
   }
   __syncthreads();
   const float mk = mk_s;
@@ -401,13 +406,14 @@ __global__ __launch_bounds__(256) void topk_select_kernel(const float* __restric
     for (int q = 0; q < KC; ++q)
       if (tl.i[q] != INT64_MAX && tl.v[q] >= mk) list[atomicAdd(&nlist, 1)] = (int)tl.i[q];
   }
-  f32x4 hf[KG][4];   // the user's B operand (the same in every lane column)
-#pragma unroll
-  for (int g = 0; g < KG; ++g)
-#pragma unroll
-    for (int q = 0; q < 4; ++q) hf[g][q] = *reinterpret_cast<const f32x4*>(h + u * D + 32 * g + 8 * q + 4 * hh);
+  __shared__ __attribute__((aligned(16))) float hs[D];   // the user's vector (LDS broadcast reads)
+  if (tid < D / 4) *reinterpret_cast<f32x4*>(hs + 4 * tid) = *reinterpret_cast<const f32x4*>(h + u * D + 4 * tid);
   TopList<KC> best;
   best.init();
+  // Re-scoring on the VALU: one lane per row (two tiles per wave pass), each logit as the fmaf chain
+  // the MFMA evaluates (v_mfma_f32_32x32x2_f32 is an exact fp32 fma chain: per step of 32-deep
+  // group g, slice q and element s, the lane-half-0 feature 32g + 8q + s, then the lane-half-1
+  // feature 32g + 8q + 4 + s) -- bitwise the tile pass's logit, at 1/8 of the MFMA tile's work.
   for (int64_t b0 = 0; b0 < (slow ? T : 1); b0 += 256) {
     if (slow) {
       __syncthreads();
@@ -417,34 +423,48 @@ __global__ __launch_bounds__(256) void topk_select_kernel(const float* __restric
       if (t < T && tm[t] >= mk) list[atomicAdd(&nlist, 1)] = (int)t;
     }
     __syncthreads();
-    const int n = nlist;
-    for (int e = w; e < n; e += 4) {
+    const int n = (abl & 1) ? 0 : nlist;   // diagnostic only: no re-scoring
+    for (int e = 2 * w + (lane >> 5); e < n; e += 8) {
       const int64_t row = (int64_t)list[e] * 32 + r;
       const int64_t rc = row < rows ? row : rows - 1;
-      f32x4 a[KG][4];
-#pragma unroll
-      for (int g = 0; g < KG; ++g)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) a[g][q] = *reinterpret_cast<const f32x4*>(table + rc * D + 32 * g + 8 * q + 4 * hh);
-      f32x16 acc;
-#pragma unroll
-      for (int v = 0; v < 16; ++v) acc[v] = 0.f;
-#pragma unroll
-      for (int g = 0; g < KG; ++g)
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-#pragma unroll
-          for (int s4 = 0; s4 < 4; ++s4) acc = mfma32(a[g][q][s4], hf[g][q][s4], acc);
-      // lane (r, hh) with hh = bit 2 of r holds item r of the tile in register (r&3) + 4(r>>3)
+      const float* tr = table + rc * D;
       float x = 0.f;
+      f32x4 cur[8], nxt[8];   // one 32-feature group of the row in flight while the previous is used
 #pragma unroll
-      for (int v = 0; v < 16; ++v)
-        if ((v & 3) + 8 * (v >> 2) + 4 * hh == r) x = acc[v];
-      if (((r >> 2) & 1) == hh && row < rows) {
+      for (int i = 0; i < 8; ++i) cur[i] = *reinterpret_cast<const f32x4*>(tr + 4 * i);
+#pragma unroll 1
+      for (int g = 0; g < KG; ++g) {   // (not unrolled: the compiler would hoist every load and spill)
+        if (g + 1 < KG) {
+#pragma unroll
+          for (int i = 0; i < 8; ++i) nxt[i] = *reinterpret_cast<const f32x4*>(tr + 32 * (g + 1) + 4 * i);
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const f32x4 h0 = *reinterpret_cast<const f32x4*>(hs + 32 * g + 8 * q);
+          const f32x4 h1 = *reinterpret_cast<const f32x4*>(hs + 32 * g + 8 * q + 4);
+#pragma unroll
+          for (int s4 = 0; s4 < 4; ++s4) {
+            x = fmaf(cur[2 * q][s4], h0[s4], x);
+            x = fmaf(cur[2 * q + 1][s4], h1[s4], x);
+          }
+        }
+        if (g + 1 < KG) {
+#pragma unroll
+          for (int i = 0; i < 8; ++i) cur[i] = nxt[i];
+        }
+      }
+      if (row < rows) {
         if (mask_col0 && row == 0) x = TK_MASK;
         if (x == x) best.push(x, row);   // NaN never enters (as in the list passes)
       }
     }
+  }
+  if (abl & 4) {   // diagnostic only: no final block select
+    if (tid < k) {
+      vals[u * k + tid] = best.v[0];
+      ids[u * k + tid] = best.i[0];
+    }
+    return;
   }
   best.block_select(k, [&](int q, float v, int64_t i) {
     vals[u * k + q] = v;
@@ -645,7 +665,7 @@ extern "C" int gr_score_topk_f32(const float* h, int64_t B, int32_t d, const flo
       if (rc) return rc;
 #define GR_TK_SEL(DD) hipLaunchKernelGGL((topk_select_kernel<DD, KC>), dim3((unsigned)B), dim3(256), 0, st, h, B, \
                                          table, rows, mask_col0, k, id_offset, tmax, tw.T, cpart, (int)tw.slices, \
-                                         cnt, vals_out, ids_out)
+                                         cnt, vals_out, ids_out, (int)option("topk_sel_abl"))
       switch (d) {
         case 32: GR_TK_SEL(32); break;
         case 64: GR_TK_SEL(64); break;

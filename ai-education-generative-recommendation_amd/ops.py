@@ -574,7 +574,7 @@ def sampled_bce_loss(seq_features, item_emb_weight, target_o_t, neg_samples, eps
 _NEG_CALLS = itertools.count()
 
 
-def neg_samples(seq, item_num, num_neg=1, seed=None):
+def neg_samples(seq, item_num, num_neg=1, seed=None, seed_tensor=None):
     """train.py:15-30 ``get_neg_samples(seq, item_num, num_neg)`` on the GPU: ``[B, num_neg]`` int64,
     per row distinct items uniform over ``[1, item_num]`` minus the row's non-zero history (the
     reference's distribution; not numpy's random stream).  ``seed`` defaults to a fresh value per
@@ -584,19 +584,75 @@ def neg_samples(seq, item_num, num_neg=1, seed=None):
     raises ValueError, as numpy's ``choice(replace=False)`` does.  That can only happen when
     ``n + num_neg > item_num`` (the history holds at most ``n`` distinct items), and only then does
     this call synchronise to check; otherwise every candidate is accepted with probability
-    >= 1/2 and the kernel's 4096 rounds of 64 draws cannot fall short.  Unfilled rows hold -1."""
+    >= 1/2 and the kernel's 4096 rounds of 64 draws cannot fall short.  Unfilled rows hold -1.
+
+    ``seed_tensor`` (a CUDA int64 tensor of one element): the stream is keyed by ``seed ^
+    seed_tensor`` read on the device, and ``seed_tensor`` is advanced by one on the stream after
+    the draw -- the form a captured graph replays with fresh negatives (``SasTrainStepGraph``)."""
     L.require_gpu(seq)
     s = seq.to(torch.int64).contiguous()
     if s.dim() != 2:
         raise RuntimeError("neg_samples: seq must be [B, n]")
     B, n = s.shape
     if seed is None:
-        seed = int(torch.randint(0, 2 ** 62, (1,)).item()) ^ next(_NEG_CALLS)
+        seed = 0 if seed_tensor is not None else int(torch.randint(0, 2 ** 62, (1,)).item()) ^ next(_NEG_CALLS)
     out = torch.empty((B, num_neg), dtype=torch.int64, device=s.device)
     err = err_flag(s.device)
     with torch.cuda.device(s.device):
-        L.check(L.lib().gr_neg_samples(L.ptr(s), B, n, int(item_num), int(num_neg), int(seed) & (2 ** 64 - 1),
-                                       L.ptr(out), L.ptr(err), L.stream_of(s.device)), "gr_neg_samples")
+        if seed_tensor is not None:
+            if seed_tensor.dtype != torch.int64 or seed_tensor.numel() != 1 or seed_tensor.device != s.device:
+                raise RuntimeError("neg_samples: seed_tensor must be one int64 element on the sequences' device")
+            L.check(L.lib().gr_neg_samples_dseed(L.ptr(s), B, n, int(item_num), int(num_neg),
+                                                 int(seed) & (2 ** 64 - 1), L.ptr(seed_tensor), L.ptr(out),
+                                                 L.ptr(err), L.stream_of(s.device)), "gr_neg_samples_dseed")
+            seed_tensor.add_(1)
+        else:
+            L.check(L.lib().gr_neg_samples(L.ptr(s), B, n, int(item_num), int(num_neg), int(seed) & (2 ** 64 - 1),
+                                           L.ptr(out), L.ptr(err), L.stream_of(s.device)), "gr_neg_samples")
     if CHECK or 2 * (n + num_neg) > item_num:
         check_errors(s.device)
     return out
+
+
+class SasTrainStepGraph:
+    """The training-side scoring step of SASRec/train.py:131-167 -- negatives (train.py:142),
+    scores + sampled BCE (134-158), ``loss = batch_loss / batch_valid_t`` (161-164) and its backward
+    into ``feats.grad`` / ``table.grad`` -- captured once as a graph (hipGraph via
+    ``torch.cuda.graph``) and replayed: one launch per step instead of ~20 host-issued ones.
+
+    ``feats`` [B, n, d] and ``table`` [rows, d] are leaf tensors with ``requires_grad``; ``inputs``
+    (the sequences the negatives avoid) and ``targets`` are the step's static inputs: copy a new
+    batch into them before ``replay()``.  Each replay draws fresh negatives (device-side seed).
+    ``replay()`` returns the static ``(batch_loss, batch_valid_t)`` device scalars and leaves the
+    gradients in ``.grad`` (overwritten, not accumulated, as with ``zero_grad(set_to_none=True)``
+    before each reference step).  A step with no valid position gives loss 0 and zero gradients,
+    as the reference's ``if batch_valid_t > 0`` does."""
+
+    def __init__(self, feats, table, inputs, targets, item_num, num_neg, eps, seed=0, warmup=3):
+        L.require_gpu(feats, table, inputs, targets)
+        if not (feats.is_leaf and table.is_leaf and feats.requires_grad and table.requires_grad):
+            raise RuntimeError("SasTrainStepGraph: feats and table must be leaf tensors requiring grad")
+        self.feats, self.table, self.inputs, self.targets = feats, table, inputs, targets
+        self.item_num, self.num_neg, self.eps = int(item_num), int(num_neg), float(eps)
+        self.seed = torch.tensor([int(seed)], dtype=torch.int64, device=feats.device)
+        side = torch.cuda.Stream(device=feats.device)
+        side.wait_stream(torch.cuda.current_stream(feats.device))
+        with torch.cuda.stream(side):
+            for _ in range(warmup):   # allocator / autograd warm-up outside the capture
+                feats.grad = table.grad = None
+                self._body()
+        torch.cuda.current_stream(feats.device).wait_stream(side)
+        feats.grad = table.grad = None
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self.out = self._body()
+
+    def _body(self):
+        negs = neg_samples(self.inputs, self.item_num, self.num_neg, seed_tensor=self.seed)
+        bl, valid = sampled_bce_loss(self.feats, self.table, self.targets, negs, self.eps)
+        (bl / valid.clamp(min=1.0)).backward()   # batch_loss is 0 when nothing is valid
+        return bl, valid
+
+    def replay(self):
+        self.graph.replay()
+        return self.out

@@ -420,15 +420,24 @@ def bench_sas_train(a, world, rank, dev):
         feats.grad = table.grad = None
         ((pl + nl).sum() / mask.sum()).backward()
 
-    wall, dev_ms = timed(step, a.steps, a.warmup, world)
+    eager_wall, eager_dev_ms = timed(step, a.steps, a.warmup, world)
+    # the same step captured once and replayed (ops.SasTrainStepGraph: one graph launch per step,
+    # fresh device-seeded negatives each replay) -- the leg's value
+    feats.grad = table.grad = None
+    gstep = ops.SasTrainStepGraph(feats, table, inputs, targets, items, J, 1e-24, seed=3000 + rank)
+    wall, dev_ms = timed(gstep.replay, a.steps, a.warmup, world)
     dense_ms = kernel_ms(dense_step, reps=10)
     nbytes = sas_train_bytes(B, n, d, items + 1, J)
     tr, tr_src = call_traffic("train", ["neg_sample_kernel", "bce_"], "neg_sample_kernel")
     res = {"metric": "train_seqs_scored/s", "value": B * world * a.steps / wall, "unit": "seqs/s",
            "ms_per_step": wall / a.steps * 1e3, "scaling": "weak",
            "config": {"workload": f"sas_train: SASRec train.py:131-167 scoring + sampled BCE, forward + "
-                                  f"backward, B {B}, n {n}, d {d}, {items}-item table, {J} negatives",
+                                  f"backward, B {B}, n {n}, d {d}, {items}-item table, {J} negatives; "
+                                  f"the step captured as one graph (ops.SasTrainStepGraph)",
                       "users_per_rank_per_step": B, "parallelism": f"user-sharded x{world}, no collective"},
+           "eager": {"note": "the same step issued op by op from Python (host-launch bound)",
+                     "value": B * world * a.steps / eager_wall, "ms_per_step": eager_wall / a.steps * 1e3,
+                     "step_device_ms": eager_dev_ms},
            "roofline": {"bound": "hbm", "achieved": nbytes / (dev_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
                         "unit": "GB/s", "frac": nbytes / (dev_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
                         "traffic": tr, "traffic_source": tr_src and tr_src + " (the 5 gr:: kernels; the "

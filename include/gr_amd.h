@@ -283,6 +283,13 @@ int gr_sampled_bce_bwd_f32(const float* feats, int64_t B, int32_t n, int32_t d, 
 int gr_neg_samples(const int64_t* seqs, int64_t B, int32_t n, int64_t item_num, int32_t num_neg,
                    uint64_t seed, int64_t* out, int32_t* err_flag, void* stream);
 
+/* gr_neg_samples keyed by seed ^ *seed_dev (a device uint64 the kernel only reads): the form a
+ * captured graph (hipGraph / torch.cuda.graph) replays with fresh negatives, the caller advancing
+ * *seed_dev on the stream between replays (SasTrainStep in the Python package does). */
+int gr_neg_samples_dseed(const int64_t* seqs, int64_t B, int32_t n, int64_t item_num, int32_t num_neg,
+                         uint64_t seed, const uint64_t* seed_dev, int64_t* out, int32_t* err_flag,
+                         void* stream);
+
 #ifdef __cplusplus
 }
 #endif

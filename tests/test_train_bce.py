@@ -248,3 +248,55 @@ def test_full_training_step_matches_reference(name, dev):
     m.eval()
     with torch.no_grad():
         assert _scaled_err(m(seqs), out["feats"]) <= TOL
+
+
+@pytest.mark.gpu
+def test_neg_samples_device_seed(dev):
+    """The device-seeded sampler: keyed by seed ^ *seed_tensor, seed_tensor advanced by one per call;
+    equal keys give equal draws, and the draws keep the contract (distinct, in range, off history)."""
+    from gr_amd import ops
+    g = torch.Generator().manual_seed(11)
+    seqs = torch.randint(0, 5000, (64, 50), generator=g).to(dev)
+    st = torch.tensor([123], dtype=torch.int64, device=dev)
+    a = ops.neg_samples(seqs, 5000, 10, seed_tensor=st)
+    assert int(st.item()) == 124
+    b = ops.neg_samples(seqs, 5000, 10, seed_tensor=torch.tensor([123], dtype=torch.int64, device=dev))
+    c = ops.neg_samples(seqs, 5000, 10, seed_tensor=st)
+    assert torch.equal(a, b) and not torch.equal(a, c)
+    for x in (a, c):
+        assert int(x.min()) >= 1 and int(x.max()) <= 5000
+        for row, hist in zip(x.cpu().tolist(), seqs.cpu().tolist()):
+            assert len(set(row)) == 10 and not (set(row) & set(hist))
+
+
+@pytest.mark.gpu
+def test_train_step_graph_matches_eager(dev):
+    """ops.SasTrainStepGraph replays the step (fresh device-seeded negatives each replay) with the
+    results of the same step issued eagerly on the same negatives: loss and valid exact, gradients
+    within 1e-6 of their largest magnitude (dM accumulates with atomics)."""
+    from gr_amd import ops
+    B, n, d, items, J = 32, 20, 64, 3000, 5
+    g = torch.Generator(device=dev).manual_seed(7)
+    feats = (0.3 * torch.randn(B, n, d, generator=g, device=dev)).requires_grad_(True)
+    table = (0.3 * torch.randn(items + 1, d, generator=g, device=dev)).requires_grad_(True)
+    targets = torch.randint(1, items + 1, (B, n), generator=g, device=dev)
+    targets[:, :5] = 0
+    inputs = torch.roll(targets, 1, dims=1)
+    inputs[:, 0] = 0
+    step = ops.SasTrainStepGraph(feats, table, inputs, targets, items, J, 1e-24, seed=99)
+    seen = []
+    for _ in range(3):
+        key = int(step.seed.item())
+        bl, valid = step.replay()
+        bl, valid = float(bl), float(valid)
+        gf, gt = feats.grad.clone(), table.grad.clone()
+        negs = ops.neg_samples(inputs, items, J, seed_tensor=torch.tensor([key], dtype=torch.int64, device=dev))
+        seen.append(negs)
+        f2 = feats.detach().clone().requires_grad_(True)
+        t2 = table.detach().clone().requires_grad_(True)
+        bl2, valid2 = ops.sampled_bce_loss(f2, t2, targets, negs, 1e-24)
+        (bl2 / valid2).backward()
+        assert bl == float(bl2) and valid == float(valid2)
+        assert (gf - f2.grad).abs().max() <= 1e-6 * f2.grad.abs().max()
+        assert (gt - t2.grad).abs().max() <= 1e-6 * t2.grad.abs().max()
+    assert not torch.equal(seen[0], seen[1])   # fresh negatives per replay
