@@ -58,10 +58,6 @@ static std::atomic<int64_t> g_attn_occ1{0};
 static std::atomic<int64_t> g_attn_alt{1};
 // attn_lazy (hd 128 attention: 1 = lazy softmax rescaling + masks on the diagonal / last tile only)
 static std::atomic<int64_t> g_attn_lazy{1};
-// lin_persist (1: plain projections with more than 4 tiles per CU run the persistent GEMM)
-static std::atomic<int64_t> g_lin_persist{0};
-// rq_occ2 (1: the quantize kernel runs two 8-wave workgroups per CU, <= 2 item tiles per wave)
-static std::atomic<int64_t> g_rq_occ2{0};
 // topk_impl (1 (default): gr_score_topk_f32 = tile-max counting pass + select/re-score kernel;
 // 0: sample pass + exact list pass + merges)
 static std::atomic<int64_t> g_topk_impl{1};
@@ -85,8 +81,6 @@ int64_t option(const char* name) {
   if (!strcmp(name, "attn_occ1")) return g_attn_occ1.load();
   if (!strcmp(name, "attn_alt")) return g_attn_alt.load();
   if (!strcmp(name, "attn_lazy")) return g_attn_lazy.load();
-  if (!strcmp(name, "lin_persist")) return g_lin_persist.load();
-  if (!strcmp(name, "rq_occ2")) return g_rq_occ2.load();
   if (!strcmp(name, "topk_impl")) return g_topk_impl.load();
   if (!strcmp(name, "topk_sel_abl")) return g_topk_sel_abl.load();
   return -1;
@@ -112,8 +106,6 @@ extern "C" int gr_set_option(const char* name, int64_t value) {
   if (!strcmp(name, "attn_occ1") && (value == 0 || value == 1)) { gr::g_attn_occ1 = value; return GR_OK; }
   if (!strcmp(name, "attn_alt") && (value == 0 || value == 1)) { gr::g_attn_alt = value; return GR_OK; }
   if (!strcmp(name, "attn_lazy") && (value == 0 || value == 1)) { gr::g_attn_lazy = value; return GR_OK; }
-  if (!strcmp(name, "lin_persist") && (value == 0 || value == 1)) { gr::g_lin_persist = value; return GR_OK; }
-  if (!strcmp(name, "rq_occ2") && (value == 0 || value == 1)) { gr::g_rq_occ2 = value; return GR_OK; }
   if (!strcmp(name, "topk_impl") && (value == 0 || value == 1)) { gr::g_topk_impl = value; return GR_OK; }
   if (!strcmp(name, "topk_sel_abl") && value >= 0 && value <= 7) { gr::g_topk_sel_abl = value; return GR_OK; }
   return gr::fail(GR_ERR_ARG, std::string("gr_set_option: unknown option or value: ") + name);

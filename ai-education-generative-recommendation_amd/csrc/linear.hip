@@ -143,140 +143,6 @@ __global__ __launch_bounds__(256, 2) void linear_f32_kernel(
   }
 }
 
-// Persistent form (option lin_persist): 2 workgroups per CU walk the tiles (tile = wg + i * grid,
-// logical ids XCD-remapped so a row tile's column tiles share an L2), and the K loop runs on across
-// tile boundaries: the next tile's first 32-deep K slab is loaded while the current tile's last one
-// is consumed, and a tile's epilogue stores go out after the barrier, under the next tile's first
-// MFMAs.  Same per-element fp32 chain as linear_f32_kernel (no residual / activation variants: the
-// plain projections of a forward).
-template <int BM, int BN, int WM, int WN>
-__global__ __launch_bounds__(256, 2) void linear_persist_kernel(
-    const float* __restrict__ x, const float* __restrict__ w, const float* __restrict__ bias,
-    float* __restrict__ y, int64_t M, int N, int K, int64_t ldy, int tiles_m, int tiles_n) {
-  static_assert(WM * WN == 4, "4 waves");
-  constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
-  constexpr int AV = BM * LIN_BK / 4 / 256, BV = BN * LIN_BK / 4 / 256;
-  __shared__ __attribute__((aligned(16))) float lds[2][(BM + BN) * LIN_PITCH];
-
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave / WN, wn = wave % WN, r = lane & 31, h = lane >> 5;
-  const int G = gridDim.x;
-  const int64_t ntiles = (int64_t)tiles_m * tiles_n;
-  int64_t tile = xcd_remap(blockIdx.x, G);
-  if (tile >= ntiles) return;
-  const int nk = (K + LIN_BK - 1) / LIN_BK;
-
-  f32x4 ra[AV], rb[BV];
-  auto gload = [&](int64_t t, int k0) {
-    const int64_t m0 = (t / tiles_n) * BM;
-    const int n0 = (int)(t % tiles_n) * BN;
-#pragma unroll
-    for (int i = 0; i < AV; ++i) {
-      const int f = tid + 256 * i, row = f >> 3, kk = k0 + (f & 7) * 4;
-      const int64_t gr_ = m0 + row;
-      ra[i] = (gr_ < M && kk < K) ? *reinterpret_cast<const f32x4*>(x + gr_ * K + kk)
-                                  : f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-#pragma unroll
-    for (int i = 0; i < BV; ++i) {
-      const int f = tid + 256 * i, row = f >> 3, kk = k0 + (f & 7) * 4;
-      const int gn = n0 + row;
-      rb[i] = (gn < N && kk < K) ? *reinterpret_cast<const f32x4*>(w + (int64_t)gn * K + kk)
-                                 : f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-  };
-  auto swrite = [&](int buf) {
-    float* s = lds[buf];
-#pragma unroll
-    for (int i = 0; i < AV; ++i) {
-      const int f = tid + 256 * i;
-      *reinterpret_cast<f32x4*>(s + (f >> 3) * LIN_PITCH + (f & 7) * 4) = ra[i];
-    }
-#pragma unroll
-    for (int i = 0; i < BV; ++i) {
-      const int f = tid + 256 * i;
-      *reinterpret_cast<f32x4*>(s + (BM + (f >> 3)) * LIN_PITCH + (f & 7) * 4) = rb[i];
-    }
-  };
-
-  f32x16 acc[TM][TN];
-#pragma unroll
-  for (int a = 0; a < TM; ++a)
-#pragma unroll
-    for (int b = 0; b < TN; ++b)
-#pragma unroll
-      for (int v = 0; v < 16; ++v) acc[a][b][v] = 0.f;
-
-  gload(tile, 0);
-  swrite(0);
-  __syncthreads();
-  int kt = 0, cur = 0;
-  for (;;) {
-    int nkt = kt + 1;
-    int64_t ntile = tile;
-    if (nkt == nk) {
-      nkt = 0;
-      ntile += G;
-    }
-    const bool more = ntile < ntiles;
-    if (more) gload(ntile, nkt * LIN_BK);
-    const float* As = lds[cur] + (wm * (BM / WM) + r) * LIN_PITCH + 4 * h;
-    const float* Bs = lds[cur] + (BM + wn * (BN / WN) + r) * LIN_PITCH + 4 * h;
-#pragma unroll
-    for (int kc = 0; kc < LIN_BK / 8; ++kc) {
-      f32x4 a[TM], b[TN];
-#pragma unroll
-      for (int t = 0; t < TM; ++t) a[t] = *reinterpret_cast<const f32x4*>(As + t * 32 * LIN_PITCH + kc * 8);
-#pragma unroll
-      for (int t = 0; t < TN; ++t) b[t] = *reinterpret_cast<const f32x4*>(Bs + t * 32 * LIN_PITCH + kc * 8);
-#pragma unroll
-      for (int s = 0; s < 4; ++s)
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-          for (int j = 0; j < TN; ++j) acc[i][j] = mfma32(a[i][s], b[j][s], acc[i][j]);
-    }
-    if (more) swrite(cur ^ 1);
-    __syncthreads();
-    if (kt == nk - 1) {   // the tile is complete: bias and store, then start the next one at zero
-      const int64_t m0 = (tile / tiles_n) * BM;
-      const int n0 = (int)(tile % tiles_n) * BN;
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int col = n0 + wn * (BN / WN) + j * 32 + r;
-        const bool cok = col < N;
-        const float bv = (bias != nullptr && cok) ? bias[col] : 0.f;
-#pragma unroll
-        for (int i = 0; i < TM; ++i) {
-#pragma unroll
-          for (int v = 0; v < 16; ++v) {
-            const int64_t row = m0 + wm * (BM / WM) + i * 32 + (v & 3) + 8 * (v >> 2) + 4 * h;
-            float o = acc[i][j][v];
-            if (bias != nullptr) o = o + bv;
-            if (cok && row < M) y[row * ldy + col] = o;
-            acc[i][j][v] = 0.f;
-          }
-        }
-      }
-    }
-    if (!more) break;
-    cur ^= 1;
-    tile = ntile;
-    kt = nkt;
-  }
-}
-
-static int lin_cu_count() {
-  static int cus = 0;
-  if (!cus) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) dev = 0;
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
-      cus = 256;
-  }
-  return cus;
-}
-
 template <int BM, int BN, int WM, int WN>
 static int launch_tile(const float* x, int64_t m, int k, const float* w, int n, const float* bias,
                        const float* residual, int64_t ldr, int act, float* y, int64_t ldy,
@@ -287,12 +153,6 @@ static int launch_tile(const float* x, int64_t m, int k, const float* w, int n, 
   const bool nmajor = (int64_t)n > m;  // iterate the smaller operand's tiles fastest
   const dim3 grid((unsigned)(tm * tn)), block(256);
   const bool res = residual != nullptr;
-  if (!res && act == GR_ACT_NONE && !nmajor && option("lin_persist") != 0 && tm * tn > 4LL * lin_cu_count()) {
-    const dim3 pg((unsigned)(2 * lin_cu_count()));
-    hipLaunchKernelGGL((linear_persist_kernel<BM, BN, WM, WN>), pg, block, 0, stream, x, w, bias, y, m, n, k, ldy,
-                       (int)tm, tn);
-    return check_launch("gr_linear_f32 (persistent)");
-  }
 #define GR_LIN_CASE(A, R, NM)                                                                    \
   if (act == A && res == R && nmajor == NM) {                                                     \
     hipLaunchKernelGGL((linear_f32_kernel<BM, BN, WM, WN, A, R, NM>), grid, block, 0, stream, x, \

@@ -25,8 +25,8 @@ struct RQLevels {
 
 constexpr int RQ_WAVES = 8;           // waves per workgroup
 // max item tiles per wave (residuals held in registers): fewer at e = 64 to stay spill-free
-template <int E, int OCC = 1>
-struct RQMaxT { static constexpr int value = OCC == 2 ? 1 : (E >= 64 ? 2 : 4); };
+template <int E>
+struct RQMaxT { static constexpr int value = E >= 64 ? 2 : 4; };
 
 __global__ __launch_bounds__(256) void rq_code_norms_kernel(const float* __restrict__ cb, int K,
                                                             int e, float* __restrict__ cn) {
@@ -50,17 +50,13 @@ __device__ __forceinline__ int cb_off(int c, int q) {
 // per chunk).  kch == 0 ("resident"): every level's codebook and norms fit in LDS together, so
 // they are staged once at the start (one load phase, one norm phase, two barriers in all) and the
 // level loop runs with no barrier at all.
-// OCC = 2 (option rq_occ2): two workgroups per CU (4 waves per SIMD: the second launch bound is
-// waves per SIMD; <= 128 VGPRs, fewer
-// register-resident tiles per wave), so more independent MFMA chains hide each wave's
-// MFMA -> argmin-epilogue dependency.
-template <int E, bool SECOND, int OCC>
-__global__ __launch_bounds__(RQ_WAVES * 64, 2 * OCC) void rq_quantize_kernel(
+template <int E, bool SECOND>
+__global__ __launch_bounds__(RQ_WAVES * 64) void rq_quantize_kernel(
     const float* __restrict__ z, int64_t n, int L, RQLevels lv, int kch, int64_t* __restrict__ idx_out,
     float* __restrict__ best_out, float* __restrict__ gap_out, int tiles) {
   static_assert(E % 8 == 0 && E <= 64, "e");
   constexpr int HQ = E / 8;            // float4 per lane half
-  constexpr int RQ_MAXT = RQMaxT<E, OCC>::value;
+  constexpr int RQ_MAXT = RQMaxT<E>::value;
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const bool resident = kch == 0;
   int ktot = 0;                        // resident: codes of all levels, each level padded to 32
@@ -276,16 +272,13 @@ static int launch_quantize_e(const float* z, int64_t n, int L, const RQLevels& l
   // a contiguous balanced range of tiles; more workgroups only when a range would exceed the
   // register-resident residuals (RQ_WAVES x MT tiles)
   const int64_t tiles = (n + 31) / 32;
-  // (one tile per wave: only while every tile fits in one pass of 2 workgroups per CU)
-  const bool occ2 = option("rq_occ2") != 0 && !resident && tiles <= 2LL * cu_count() * RQ_WAVES;
-  int64_t grid = (int64_t)cu_count() * (occ2 ? 2 : 1);
-  const int MT = occ2 ? RQMaxT<E, 2>::value : RQMaxT<E, 1>::value;
+  int64_t grid = (int64_t)cu_count();
+  constexpr int MT = RQMaxT<E>::value;
   const int64_t min_grid = (tiles + RQ_WAVES * MT - 1) / (RQ_WAVES * MT);
   if (grid < min_grid) grid = min_grid;
   if (grid > tiles) grid = tiles;
   if (grid > 0x7fffffffLL || tiles > 0x7fffffffLL) return fail(GR_ERR_UNSUPPORTED, "rq quantize: n too large");
-  auto k = (best || gap) ? (occ2 ? rq_quantize_kernel<E, true, 2> : rq_quantize_kernel<E, true, 1>)
-                         : (occ2 ? rq_quantize_kernel<E, false, 2> : rq_quantize_kernel<E, false, 1>);
+  auto k = (best || gap) ? rq_quantize_kernel<E, true> : rq_quantize_kernel<E, false>;
   if (lds > 64 * 1024 &&
       hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
                           (int)lds) != hipSuccess)
