@@ -63,6 +63,8 @@ static std::atomic<int64_t> g_attn_lazy{1};
 static std::atomic<int64_t> g_topk_impl{1};
 // topk_sel_abl (diagnostic only, wrong results: bit 1 no re-scoring, 2 no k-th tile select, 4 no final select)
 static std::atomic<int64_t> g_topk_sel_abl{0};
+// rt_w8 (1 (default): the post-attention row tile runs 8 waves per 64-row tile; 0: 4 waves)
+static std::atomic<int64_t> g_rt_w8{1};
 
 int64_t option(const char* name) {
   if (!strcmp(name, "rq_fused")) return g_rq_fused.load();
@@ -83,6 +85,7 @@ int64_t option(const char* name) {
   if (!strcmp(name, "attn_lazy")) return g_attn_lazy.load();
   if (!strcmp(name, "topk_impl")) return g_topk_impl.load();
   if (!strcmp(name, "topk_sel_abl")) return g_topk_sel_abl.load();
+  if (!strcmp(name, "rt_w8")) return g_rt_w8.load();
   return -1;
 }
 }  // namespace gr
@@ -108,6 +111,7 @@ extern "C" int gr_set_option(const char* name, int64_t value) {
   if (!strcmp(name, "attn_lazy") && (value == 0 || value == 1)) { gr::g_attn_lazy = value; return GR_OK; }
   if (!strcmp(name, "topk_impl") && (value == 0 || value == 1)) { gr::g_topk_impl = value; return GR_OK; }
   if (!strcmp(name, "topk_sel_abl") && value >= 0 && value <= 7) { gr::g_topk_sel_abl = value; return GR_OK; }
+  if (!strcmp(name, "rt_w8") && (value == 0 || value == 1)) { gr::g_rt_w8 = value; return GR_OK; }
   return gr::fail(GR_ERR_ARG, std::string("gr_set_option: unknown option or value: ") + name);
 }
 

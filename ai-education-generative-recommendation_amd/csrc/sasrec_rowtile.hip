@@ -263,6 +263,188 @@ __global__ __launch_bounds__(256, 2) void post_attn_kernel(const RowTileArgs a, 
   }
 }
 
+// ---- 8-wave form of the row tile (option rt_w8): 512 threads per 64-row tile, one 32 x 32 output
+// tile per wave per 128-wide product (4 waves per SIMD with two workgroups per CU instead of 2),
+// LayerNorm statistics from 8 threads per row.  Same products and order of operations per element
+// except the LayerNorm sums (8 partial sums per row instead of 4).
+template <int K>
+__device__ __forceinline__ void rt_gemm1(f32x16& acc, const float* A, int ap, const float* __restrict__ W,
+                                         int wrow, int r, int h) {
+  constexpr int NK = K / 8, PF = RT_PF < NK ? RT_PF : NK;
+  const float* wr = W + (int64_t)wrow * K + 4 * h;
+  const float* a0 = A + r * ap + 4 * h;
+  f32x4 wb[PF];
+#pragma unroll
+  for (int i = 0; i < PF; ++i) wb[i] = *reinterpret_cast<const f32x4*>(wr + 8 * i);
+#pragma unroll
+  for (int kc = 0; kc < NK; ++kc) {
+    const f32x4 b = wb[kc % PF];
+    if (kc + PF < NK) wb[kc % PF] = *reinterpret_cast<const f32x4*>(wr + 8 * (kc + PF));
+    const f32x4 x0 = *reinterpret_cast<const f32x4*>(a0 + 8 * kc);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) acc = mfma32(x0[s], b[s], acc);
+  }
+}
+
+__device__ __forceinline__ void rt_layernorm8(float* img, const float* __restrict__ w, const float* __restrict__ b,
+                                              float eps, float* dst_global, int64_t rows_left) {
+  __shared__ float st_mean[RT_BM], st_rstd[RT_BM];
+  const int t = threadIdx.x, row = t >> 3, part = t & 7;
+  float* x = img + row * RT_P + 16 * part;
+  f32x4 v[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) v[i] = *reinterpret_cast<const f32x4*>(x + 4 * i);
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) s += (v[i][0] + v[i][1]) + (v[i][2] + v[i][3]);
+  s += __shfl_xor(s, 1);
+  s += __shfl_xor(s, 2);
+  s += __shfl_xor(s, 4);
+  const float mean = s * (1.0f / RT_D);
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float d = v[i][e] - mean;
+      q = fmaf(d, d, q);
+    }
+  q += __shfl_xor(q, 1);
+  q += __shfl_xor(q, 2);
+  q += __shfl_xor(q, 4);
+  const float rstd = 1.0f / sqrtf(q * (1.0f / RT_D) + eps);
+  if (!dst_global) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int c = 16 * part + 4 * i;
+      const f32x4 ww = *reinterpret_cast<const f32x4*>(w + c);
+      const f32x4 bb = *reinterpret_cast<const f32x4*>(b + c);
+      f32x4 y;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) y[e] = (v[i][e] - mean) * rstd * ww[e] + bb[e];
+      *reinterpret_cast<f32x4*>(x + 4 * i) = y;
+    }
+    return;
+  }
+  if (part == 0) {
+    st_mean[row] = mean;
+    st_rstd[row] = rstd;
+  }
+  __syncthreads();
+  const int c = (t & 31) * 4;
+  const f32x4 ww = *reinterpret_cast<const f32x4*>(w + c);
+  const f32x4 bb = *reinterpret_cast<const f32x4*>(b + c);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int rr = (t >> 5) + 16 * i;
+    const f32x4 xv = *reinterpret_cast<const f32x4*>(img + rr * RT_P + c);
+    const float m = st_mean[rr], rs = st_rstd[rr];
+    f32x4 y;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) y[e] = (xv[e] - m) * rs * ww[e] + bb[e];
+    if (rr < rows_left) *reinterpret_cast<f32x4*>(dst_global + (int64_t)rr * RT_D + c) = y;
+  }
+}
+
+template <int MT>
+__global__ __launch_bounds__(512, 4) void post_attn8_kernel(const RowTileArgs a, const float* __restrict__ O,
+                                                            float* X, float* __restrict__ Hn, int64_t M) {
+  constexpr int MLP = 32 * MT;
+  constexpr int FP = MLP + 4;
+  __shared__ __attribute__((aligned(16))) float bufA[RT_BM * RT_P];   // O, then F
+  __shared__ __attribute__((aligned(16))) float bufB[RT_BM * RT_P];   // X, X1 -> H1, X2
+  const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, h = lane >> 5;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int64_t m0 = (int64_t)xcd_remap(blockIdx.x, gridDim.x) * RT_BM;
+  const int64_t left = M - m0;
+  {
+    f32x4 o[4], x[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int f = tid + 512 * i, row = f >> 5, c = (f & 31) * 4;
+      const int64_t g = m0 + (row < left ? row : left - 1);
+      o[i] = *reinterpret_cast<const f32x4*>(O + g * RT_D + c);
+      x[i] = *reinterpret_cast<const f32x4*>(X + g * RT_D + c);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int f = tid + 512 * i, row = f >> 5, c = (f & 31) * 4;
+      const bool ok = row < left;
+      *reinterpret_cast<f32x4*>(bufA + row * RT_P + c) = ok ? o[i] : f32x4{0.f, 0.f, 0.f, 0.f};
+      *reinterpret_cast<f32x4*>(bufB + row * RT_P + c) = ok ? x[i] : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  }
+  __syncthreads();
+  const int rb = 32 * (w >> 2), col = 32 * (w & 3) + r;   // this wave's 32 x 32 output tile
+  f32x16 x1;
+  {
+    f32x16 acc;
+#pragma unroll
+    for (int v = 0; v < 16; ++v) acc[v] = 0.f;
+    rt_gemm1<RT_D>(acc, bufA + rb * RT_P, RT_P, a.wo, col, r, h);
+    const float bo = a.bo[col];
+#pragma unroll
+    for (int v = 0; v < 16; ++v) x1[v] = bufB[(rb + (v & 3) + 8 * (v >> 2) + 4 * h) * RT_P + col] + (acc[v] + bo);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int v = 0; v < 16; ++v) bufB[(rb + (v & 3) + 8 * (v >> 2) + 4 * h) * RT_P + col] = x1[v];
+  __syncthreads();
+  rt_layernorm8(bufB, a.ln_f_w, a.ln_f_b, a.eps, nullptr, 0);
+  __syncthreads();
+  for (int t = w; t < 2 * MT; t += 8) {   // F = relu(H1 . W1^T + b1)
+    const int frt = t / MT, fct = t % MT;
+    f32x16 acc;
+#pragma unroll
+    for (int v = 0; v < 16; ++v) acc[v] = 0.f;
+    rt_gemm1<RT_D>(acc, bufB + 32 * frt * RT_P, RT_P, a.w1, 32 * fct + r, r, h);
+    const float b1 = a.b1[32 * fct + r];
+#pragma unroll
+    for (int v = 0; v < 16; ++v) {
+      const float y = acc[v] + b1;
+      bufA[(32 * frt + (v & 3) + 8 * (v >> 2) + 4 * h) * FP + 32 * fct + r] = y < 0.f ? 0.f : y;
+    }
+  }
+  __syncthreads();
+  {   // X2 = X1 + F . W2^T + b2
+    f32x16 acc;
+#pragma unroll
+    for (int v = 0; v < 16; ++v) acc[v] = 0.f;
+    rt_gemm1<MLP>(acc, bufA + rb * FP, FP, a.w2, col, r, h);
+    const float b2 = a.b2[col];
+#pragma unroll
+    for (int v = 0; v < 16; ++v)
+      bufB[(rb + (v & 3) + 8 * (v >> 2) + 4 * h) * RT_P + col] = x1[v] + (acc[v] + b2);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int f = tid + 512 * i, row = f >> 5, c = (f & 31) * 4;
+    if (row < left) *reinterpret_cast<f32x4*>(X + (m0 + row) * RT_D + c) = *reinterpret_cast<const f32x4*>(bufB + row * RT_P + c);
+  }
+  if (a.wn) {
+    __syncthreads();
+    rt_layernorm8(bufB, a.ln_n_w, a.ln_n_b, a.eps, nullptr, 0);
+    __syncthreads();
+    float* out = Hn + m0 * a.nout;
+    for (int t = w; t < 2 * (a.nout / 32); t += 8) {   // the next block's in-projection
+      const int prt = t & 1, pc = 32 * (t >> 1) + r;
+      f32x16 acc;
+#pragma unroll
+      for (int v = 0; v < 16; ++v) acc[v] = 0.f;
+      rt_gemm1<RT_D>(acc, bufB + 32 * prt * RT_P, RT_P, a.wn, pc, r, h);
+      const float bv = a.bn[pc];
+#pragma unroll
+      for (int v = 0; v < 16; ++v) {
+        const int row = 32 * prt + (v & 3) + 8 * (v >> 2) + 4 * h;
+        if (row < left) out[(int64_t)row * a.nout + pc] = acc[v] + bv;
+      }
+    }
+  } else {
+    rt_layernorm8(bufB, a.ln_n_w, a.ln_n_b, a.eps, Hn + m0 * RT_D, left);
+  }
+}
+
 // X = M[s] + P[t] (model.py:58-60) and H = LN_a0(X) for a 64-row tile; out-of-range ids flag err
 // and read the padding row (torch raises IndexError).
 __global__ __launch_bounds__(256) void embed_ln_kernel(const int64_t* __restrict__ seqs, int64_t M, int n,
@@ -341,6 +523,14 @@ int gr_post_attn_launch(const gr_sasrec_params* p, int blk, const float* ln_next
   if (wn && (!aligned16(wn) || !bn || nout % 32 || nout < 32)) return GR_ERR_UNSUPPORTED;
   const int64_t tiles = (M + RT_BM - 1) / RT_BM;
   if (tiles > 0x7fffffffLL) return GR_ERR_UNSUPPORTED;
+  if (option("rt_w8") != 0) {
+    switch (mlp) {
+      case 32: hipLaunchKernelGGL(post_attn8_kernel<1>, dim3((unsigned)tiles), dim3(512), 0, st, a, O, X, H, M); break;
+      case 64: hipLaunchKernelGGL(post_attn8_kernel<2>, dim3((unsigned)tiles), dim3(512), 0, st, a, O, X, H, M); break;
+      default: hipLaunchKernelGGL(post_attn8_kernel<4>, dim3((unsigned)tiles), dim3(512), 0, st, a, O, X, H, M); break;
+    }
+    return check_launch("sasrec post-attention row tile (8 waves)");
+  }
   switch (mlp) {
     case 32: hipLaunchKernelGGL(post_attn_kernel<1>, dim3((unsigned)tiles), dim3(256), 0, st, a, O, X, H, M); break;
     case 64: hipLaunchKernelGGL(post_attn_kernel<2>, dim3((unsigned)tiles), dim3(256), 0, st, a, O, X, H, M); break;
