@@ -18,14 +18,16 @@ namespace gr {
 constexpr int LIN_BK = 32;
 constexpr int LIN_PITCH = LIN_BK + 4;
 
-template <int BM, int BN, int WM, int WN, int ACT, bool RES, bool NMAJOR>
-__global__ __launch_bounds__(256, 2) void linear_f32_kernel(
+// NT = threads per workgroup: 256 (4 waves, 2 workgroups = 2 waves per SIMD) or 512 (8 waves,
+// 4 per SIMD at two workgroups per CU; option lin_w8).
+template <int BM, int BN, int WM, int WN, int ACT, bool RES, bool NMAJOR, int NT = 256>
+__global__ __launch_bounds__(NT, NT / 128) void linear_f32_kernel(
     const float* __restrict__ x, const float* __restrict__ w, const float* __restrict__ bias,
     const float* residual, float* y, int64_t M, int N, int K, int64_t ldy, int64_t ldr,
     int tiles_m, int tiles_n) {
-  static_assert(WM * WN == 4, "4 waves");
+  static_assert(WM * WN == NT / 64, "one wave per (WM, WN) position");
   constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
-  constexpr int AV = BM * LIN_BK / 4 / 256, BV = BN * LIN_BK / 4 / 256;
+  constexpr int AV = BM * LIN_BK / 4 / NT, BV = BN * LIN_BK / 4 / NT;
   static_assert(TM >= 1 && TN >= 1 && AV >= 1 && BV >= 1, "tile");
   __shared__ __attribute__((aligned(16))) float lds[2][(BM + BN) * LIN_PITCH];
 
@@ -42,14 +44,14 @@ __global__ __launch_bounds__(256, 2) void linear_f32_kernel(
   auto gload = [&](int k0) {
 #pragma unroll
     for (int i = 0; i < AV; ++i) {
-      const int f = tid + 256 * i, row = f >> 3, kk = k0 + (f & 7) * 4;
+      const int f = tid + NT * i, row = f >> 3, kk = k0 + (f & 7) * 4;
       const int64_t gr_ = m0 + row;
       ra[i] = (gr_ < M && kk < K) ? *reinterpret_cast<const f32x4*>(x + gr_ * K + kk)
                                   : f32x4{0.f, 0.f, 0.f, 0.f};
     }
 #pragma unroll
     for (int i = 0; i < BV; ++i) {
-      const int f = tid + 256 * i, row = f >> 3, kk = k0 + (f & 7) * 4;
+      const int f = tid + NT * i, row = f >> 3, kk = k0 + (f & 7) * 4;
       const int gn = n0 + row;
       rb[i] = (gn < N && kk < K) ? *reinterpret_cast<const f32x4*>(w + (int64_t)gn * K + kk)
                                  : f32x4{0.f, 0.f, 0.f, 0.f};
@@ -59,12 +61,12 @@ __global__ __launch_bounds__(256, 2) void linear_f32_kernel(
     float* s = lds[buf];
 #pragma unroll
     for (int i = 0; i < AV; ++i) {
-      const int f = tid + 256 * i;
+      const int f = tid + NT * i;
       *reinterpret_cast<f32x4*>(s + (f >> 3) * LIN_PITCH + (f & 7) * 4) = ra[i];
     }
 #pragma unroll
     for (int i = 0; i < BV; ++i) {
-      const int f = tid + 256 * i;
+      const int f = tid + NT * i;
       *reinterpret_cast<f32x4*>(s + (BM + (f >> 3)) * LIN_PITCH + (f & 7) * 4) = rb[i];
     }
   };
@@ -143,7 +145,7 @@ __global__ __launch_bounds__(256, 2) void linear_f32_kernel(
   }
 }
 
-template <int BM, int BN, int WM, int WN>
+template <int BM, int BN, int WM, int WN, int NT = 256>
 static int launch_tile(const float* x, int64_t m, int k, const float* w, int n, const float* bias,
                        const float* residual, int64_t ldr, int act, float* y, int64_t ldy,
                        hipStream_t stream) {
@@ -151,11 +153,11 @@ static int launch_tile(const float* x, int64_t m, int k, const float* w, int n, 
   const int tn = (n + BN - 1) / BN;
   if (tm * tn > 0x7fffffffLL) return fail(GR_ERR_UNSUPPORTED, "gr_linear_f32: grid too large");
   const bool nmajor = (int64_t)n > m;  // iterate the smaller operand's tiles fastest
-  const dim3 grid((unsigned)(tm * tn)), block(256);
+  const dim3 grid((unsigned)(tm * tn)), block(NT);
   const bool res = residual != nullptr;
 #define GR_LIN_CASE(A, R, NM)                                                                    \
   if (act == A && res == R && nmajor == NM) {                                                     \
-    hipLaunchKernelGGL((linear_f32_kernel<BM, BN, WM, WN, A, R, NM>), grid, block, 0, stream, x, \
+    hipLaunchKernelGGL((linear_f32_kernel<BM, BN, WM, WN, A, R, NM, NT>), grid, block, 0, stream, x, \
                        w, bias, residual, y, m, n, k, ldy, ldr, (int)tm, tn);                    \
     return check_launch("gr_linear_f32");                                                        \
   }
@@ -192,8 +194,15 @@ int gr_linear_launch(const float* x, int64_t m, int32_t k, const float* w, int32
   if (ldy < n || (residual && ldr < n)) return fail(GR_ERR_ARG, "gr_linear_f32: bad row stride");
   if (act < GR_ACT_NONE || act > GR_ACT_LEAKYRELU) return fail(GR_ERR_ARG, "gr_linear_f32: bad act");
   if (act > GR_ACT_RELU && residual) return fail(GR_ERR_UNSUPPORTED, "gr_linear_f32: this act takes no residual");
-  if (n >= 128) return launch_tile<128, 128, 2, 2>(x, m, k, w, n, bias, residual, ldr, act, y, ldy, stream);
-  if (n > 32) return launch_tile<128, 64, 2, 2>(x, m, k, w, n, bias, residual, ldr, act, y, ldy, stream);
+  // 8 waves per 128-row tile (4 per SIMD at two workgroups per CU; option lin_w8, the default):
+  // C5 block-0 in-projection 137 -> 124 us, bitwise the same chain
+  const bool w8 = option("lin_w8") != 0;
+  if (n >= 128)
+    return w8 ? launch_tile<128, 128, 2, 4, 512>(x, m, k, w, n, bias, residual, ldr, act, y, ldy, stream)
+              : launch_tile<128, 128, 2, 2>(x, m, k, w, n, bias, residual, ldr, act, y, ldy, stream);
+  if (n > 32)
+    return w8 ? launch_tile<128, 64, 4, 2, 512>(x, m, k, w, n, bias, residual, ldr, act, y, ldy, stream)
+              : launch_tile<128, 64, 2, 2>(x, m, k, w, n, bias, residual, ldr, act, y, ldy, stream);
   return launch_tile<128, 32, 4, 1>(x, m, k, w, n, bias, residual, ldr, act, y, ldy, stream);
 }
 
