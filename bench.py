@@ -152,7 +152,9 @@ def kernel_ms(fn, reps=50, warmup=2):
     return e0.elapsed_time(e1) / reps
 
 
-TOPK_CALL_KERNELS = ["score_topk_kernel<128,10,", "topk_merge_kernel<10>"]
+# one gr_score_topk_f32 call (tile design, topk_impl 1): the tile pass (MODE 2) + the select kernel
+TOPK_PASS = "score_topk_kernel<128,10,2>"
+TOPK_CALL_KERNELS = [TOPK_PASS, "topk_select_kernel<128,10>"]
 
 
 def call_traffic(leg, kernels, anchor):
@@ -364,11 +366,12 @@ def bench_sas_c5(a, world, rank, dev, time_it=True):
                        "users_per_step": B, "catalog_rows": items + 1, "rows_per_rank": hi - lo,
                        "parallelism": f"catalog-sharded x{world}: RCCL all-gather h + top-k, all-reduce counts"
                        + (f", {P} pipelined sub-batches" if P > 1 else "") if world > 1 else "single shard"},
-            "roofline": roofline("score_topk_kernel<128,10,0>", 2 * d * (hi - lo) * B, topk_ms, "c5",
+            "roofline": roofline(TOPK_PASS, 2 * d * (hi - lo) * B, topk_ms, "c5",
                                  call_kernels=TOPK_CALL_KERNELS,
-                                 note="one gr_score_topk_f32 call: exact pass (MODE 0) + sample pass (MODE 1) "
-                                      "+ 2 merge kernels; flop counts the exact pass only; traffic is the "
-                                      "whole call's"),
+                                 note="one gr_score_topk_f32 call: the tile pass (scores, strict counts, "
+                                      "per-user 32-row tile maxima) + the select kernel (re-scores the tiles "
+                                      "at or above the k-th tile max); flop counts the scoring GEMM once; "
+                                      "traffic is the whole call's"),
             "call": {"device_ms_rank0": dev_ms, "flop_per_user": sas_flop_per_user(d, n, items),
                      "forward_ms": fwd_ms, "score_topk_ms": topk_ms,
                      "note": "rank + top-10 fused into the scoring pass (gr_score_topk_f32): the "
@@ -490,7 +493,7 @@ def bench_c5_shard(a, model, h, targets, dev, shards=8):
             "config": {"workload": f"c5_shard: {B} users x one {hi - lo}-row catalog shard (1/{shards} of "
                                    f"{model.item_emb.weight.shape[0]}), d {d}, target logit + rank + top-{k}",
                        "rows": hi - lo, "users": B},
-            "roofline": roofline("score_topk_kernel<128,10,0>", flop, topk_ms, "shard",
+            "roofline": roofline(TOPK_PASS, flop, topk_ms, "shard",
                                  call_kernels=TOPK_CALL_KERNELS,
                                  note="one gr_score_topk_f32 call on the shard (all its launches); flop "
                                       "counts the scoring GEMM once; traffic is the whole call's"),
