@@ -645,7 +645,10 @@ class SasTrainStepGraph:
         feats.grad = table.grad = None
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph):
-            self.out = self._body()
+            # detached: the captured autograd graph (and its AccumulateGrad nodes, created on the
+            # capture stream) is released, so later eager backwards into the same leaves stay on
+            # their own stream
+            self.out = tuple(x.detach() for x in self._body())
 
     def _body(self):
         negs = neg_samples(self.inputs, self.item_num, self.num_neg, seed_tensor=self.seed)

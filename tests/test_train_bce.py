@@ -288,7 +288,7 @@ def test_train_step_graph_matches_eager(dev):
     for _ in range(3):
         key = int(step.seed.item())
         bl, valid = step.replay()
-        bl, valid = float(bl), float(valid)
+        bl, valid = float(bl.detach()), float(valid)
         gf, gt = feats.grad.clone(), table.grad.clone()
         negs = ops.neg_samples(inputs, items, J, seed_tensor=torch.tensor([key], dtype=torch.int64, device=dev))
         seen.append(negs)
@@ -296,7 +296,49 @@ def test_train_step_graph_matches_eager(dev):
         t2 = table.detach().clone().requires_grad_(True)
         bl2, valid2 = ops.sampled_bce_loss(f2, t2, targets, negs, 1e-24)
         (bl2 / valid2).backward()
-        assert bl == float(bl2) and valid == float(valid2)
+        assert bl == float(bl2.detach()) and valid == float(valid2)
         assert (gf - f2.grad).abs().max() <= 1e-6 * f2.grad.abs().max()
         assert (gt - t2.grad).abs().max() <= 1e-6 * t2.grad.abs().max()
     assert not torch.equal(seen[0], seen[1])   # fresh negatives per replay
+
+
+@pytest.mark.gpu
+def test_captured_step_inside_training_loop(dev):
+    """INTEGRATION.md's recipe: transformer forward, features copied into the graph's static leaf,
+    SasTrainStepGraph.replay(), then the transformer backward from feats.grad -- every parameter
+    gradient equals the eager step's (on a copy of the model, same negatives) over two consecutive
+    steps, so the graph's static .grad buffers are reused."""
+    import copy
+    from gr_amd import ops, synth
+    B, n, d, items, J = 16, 20, 64, 2000, 5
+    p = synth.sasrec_params(d, n, 2, 1, 64, dev)
+    p["dropout"] = 0.0
+    m = synth.sasrec_model(items, p, dev, seed=3).train()
+    ref_m = copy.deepcopy(m)
+    g = torch.Generator(device=dev).manual_seed(5)
+    seqs = torch.randint(1, items + 1, (B, n), generator=g, device=dev)
+    seqs[:, :4] = 0
+    targets = torch.roll(seqs, -1, dims=1)
+    targets[:, -1] = torch.randint(1, items + 1, (B,), generator=g, device=dev)
+    targets[seqs == 0] = 0
+    feats = torch.zeros(B, n, d, device=dev, requires_grad=True)
+    step = ops.SasTrainStepGraph(feats, m.item_emb.weight, seqs, targets, items, J, 1e-24, seed=11)
+    for _ in range(2):
+        key = int(step.seed.item())
+        for q in m.parameters():            # optimizer.zero_grad(set_to_none=False)
+            if q.grad is not None:
+                q.grad.zero_()
+        h = m.forward(seqs)
+        with torch.no_grad():
+            feats.copy_(h)
+        step.replay()
+        h.backward(feats.grad)
+        negs = ops.neg_samples(seqs, items, J, seed_tensor=torch.tensor([key], dtype=torch.int64, device=dev))
+        ref_m.zero_grad(set_to_none=True)
+        bl, valid = ops.sampled_bce_loss(ref_m.forward(seqs), ref_m.item_emb.weight, targets, negs, 1e-24)
+        (bl / valid).backward()
+        for (name, q), r in zip(m.named_parameters(), ref_m.parameters()):
+            if r.grad is None:
+                assert q.grad is None or float(q.grad.abs().max()) == 0.0, name
+                continue
+            assert (q.grad - r.grad).abs().max() <= 1e-5 * max(float(r.grad.abs().max()), 1e-30), name
