@@ -23,10 +23,9 @@ struct RQLevels {
   int K[GR_MAX_LEVELS];
 };
 
-constexpr int RQ_WAVES = 8;           // waves per workgroup
 // max item tiles per wave (residuals held in registers): fewer at e = 64 to stay spill-free
-template <int E>
-struct RQMaxT { static constexpr int value = E >= 64 ? 2 : 4; };
+template <int E, int W>
+struct RQMaxT { static constexpr int value = W >= 16 ? 1 : (E >= 64 ? 2 : 4); };
 
 __global__ __launch_bounds__(256) void rq_code_norms_kernel(const float* __restrict__ cb, int K,
                                                             int e, float* __restrict__ cn) {
@@ -50,13 +49,13 @@ __device__ __forceinline__ int cb_off(int c, int q) {
 // per chunk).  kch == 0 ("resident"): every level's codebook and norms fit in LDS together, so
 // they are staged once at the start (one load phase, one norm phase, two barriers in all) and the
 // level loop runs with no barrier at all.
-template <int E, bool SECOND>
-__global__ __launch_bounds__(RQ_WAVES * 64) void rq_quantize_kernel(
+template <int E, bool SECOND, int W>
+__global__ __launch_bounds__(W * 64) void rq_quantize_kernel(
     const float* __restrict__ z, int64_t n, int L, RQLevels lv, int kch, int64_t* __restrict__ idx_out,
     float* __restrict__ best_out, float* __restrict__ gap_out, int tiles) {
   static_assert(E % 8 == 0 && E <= 64, "e");
   constexpr int HQ = E / 8;            // float4 per lane half
-  constexpr int RQ_MAXT = RQMaxT<E>::value;
+  constexpr int RQ_MAXT = RQMaxT<E, W>::value;
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const bool resident = kch == 0;
   int ktot = 0;                        // resident: codes of all levels, each level padded to 32
@@ -68,7 +67,7 @@ __global__ __launch_bounds__(RQ_WAVES * 64) void rq_quantize_kernel(
     int off = 0;
     for (int l = 0; l < L; ++l) {
       const int K = lv.K[l];
-      for (int f = tid; f < K * (E / 4); f += RQ_WAVES * 64) {
+      for (int f = tid; f < K * (E / 4); f += W * 64) {
         const int c = f / (E / 4), q = f % (E / 4);
         *reinterpret_cast<f32x4*>(cbs + off * E + cb_off<E>(c, q)) =
             *reinterpret_cast<const f32x4*>(lv.cb[l] + (int64_t)c * E + 4 * q);
@@ -79,7 +78,7 @@ __global__ __launch_bounds__(RQ_WAVES * 64) void rq_quantize_kernel(
     off = 0;
     for (int l = 0; l < L; ++l) {
       const int K = lv.K[l], kp = (K + 31) & ~31;
-      for (int c = tid; c < kp; c += RQ_WAVES * 64) {
+      for (int c = tid; c < kp; c += W * 64) {
         float s = __builtin_inff();    // codes past K can never win
         if (c < K) {
           s = 0.f;
@@ -98,13 +97,13 @@ __global__ __launch_bounds__(RQ_WAVES * 64) void rq_quantize_kernel(
   }
   const int t_begin = (int)((int64_t)blockIdx.x * tiles / gridDim.x);
   const int t_end = (int)((int64_t)(blockIdx.x + 1) * tiles / gridDim.x);
-  const int my = (t_end - t_begin - w + RQ_WAVES - 1) / RQ_WAVES;  // tiles of this wave (<= MAXT)
+  const int my = (t_end - t_begin - w + W - 1) / W;  // tiles of this wave (<= MAXT)
 
   // residual of this lane's item for each of the wave's tiles: lane half h holds k in [hE/2, ...)
   f32x4 res[RQ_MAXT][HQ];
 #pragma unroll
   for (int i = 0; i < RQ_MAXT; ++i) {
-    const int64_t item = (int64_t)(t_begin + w + i * RQ_WAVES) * 32 + r;
+    const int64_t item = (int64_t)(t_begin + w + i * W) * 32 + r;
     const bool ok = i < my && item < n;
     const int64_t ic = ok ? item : 0;
 #pragma unroll
@@ -141,14 +140,14 @@ __global__ __launch_bounds__(RQ_WAVES * 64) void rq_quantize_kernel(
       const int cnt = min(step, K - c0);
       if (!resident) {
         __syncthreads();   // previous chunk / level fully consumed
-        for (int f = tid; f < cnt * (E / 4); f += RQ_WAVES * 64) {
+        for (int f = tid; f < cnt * (E / 4); f += W * 64) {
           const int c = f / (E / 4), q = f % (E / 4);
           *reinterpret_cast<f32x4*>(cbs + cb_off<E>(c, q)) =
               *reinterpret_cast<const f32x4*>(cb + (int64_t)(c0 + c) * E + 4 * q);
         }
         __syncthreads();
         // code norms from the LDS image, same k-ordered fma chain as rq_code_norms_kernel
-        for (int c = tid; c < ((cnt + 31) & ~31); c += RQ_WAVES * 64) {
+        for (int c = tid; c < ((cnt + 31) & ~31); c += W * 64) {
           float s = __builtin_inff();    // codes past K can never win
           if (c < cnt) {
             s = 0.f;
@@ -215,7 +214,7 @@ __global__ __launch_bounds__(RQ_WAVES * 64) void rq_quantize_kernel(
         }
         int b = bi[i];
         if (b >= K) b = 0;  // no finite distance (NaN/inf input): torch.argmin -> 0
-        const int64_t item = (int64_t)(t_begin + w + i * RQ_WAVES) * 32 + r;
+        const int64_t item = (int64_t)(t_begin + w + i * W) * 32 + r;
         if (h == 0 && item < n) {
           idx_out[item * L + l] = (int64_t)b;
           if (best_out) best_out[item * L + l] = best[i];
@@ -270,20 +269,25 @@ static int launch_quantize_e(const float* z, int64_t n, int L, const RQLevels& l
   const size_t lds = resident ? (size_t)ktot * (E + 1) * 4 : (size_t)kch * E * 4 + (size_t)kch * 4;
   // persistent: one 8-wave workgroup per CU (2 waves per SIMD at this register budget), each with
   // a contiguous balanced range of tiles; more workgroups only when a range would exceed the
-  // register-resident residuals (RQ_WAVES x MT tiles)
+  // register-resident residuals (W x MT tiles)
   const int64_t tiles = (n + 31) / 32;
   int64_t grid = (int64_t)cu_count();
-  constexpr int MT = RQMaxT<E>::value;
-  const int64_t min_grid = (tiles + RQ_WAVES * MT - 1) / (RQ_WAVES * MT);
+  // rq_waves 16 (e <= 32): 16-wave workgroups, 4 waves per SIMD, so a SIMD's item tiles run as
+  // concurrent waves (one hides another's argmin epilogue and LDS latency) instead of in sequence
+  const int W = (E <= 32 && option("rq_waves") == 16) ? 16 : 8;
+  const int MT = W == 16 ? RQMaxT<E, 16>::value : RQMaxT<E, 8>::value;
+  const int64_t min_grid = (tiles + W * MT - 1) / (W * MT);
   if (grid < min_grid) grid = min_grid;
   if (grid > tiles) grid = tiles;
   if (grid > 0x7fffffffLL || tiles > 0x7fffffffLL) return fail(GR_ERR_UNSUPPORTED, "rq quantize: n too large");
-  auto k = (best || gap) ? rq_quantize_kernel<E, true> : rq_quantize_kernel<E, false>;
+  auto k = (best || gap) ? rq_quantize_kernel<E, true, 8> : rq_quantize_kernel<E, false, 8>;
+  if constexpr (E <= 32)
+    if (W == 16) k = (best || gap) ? rq_quantize_kernel<E, true, 16> : rq_quantize_kernel<E, false, 16>;
   if (lds > 64 * 1024 &&
       hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
                           (int)lds) != hipSuccess)
     return fail(GR_ERR_HIP, "rq quantize: cannot raise the LDS limit");
-  hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(RQ_WAVES * 64), lds, st, z, n, L, lv, kch, idx,
+  hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(W * 64), lds, st, z, n, L, lv, kch, idx,
                      best, gap, (int)tiles);
   return check_launch("gr_rq_quantize_f32");
 }

@@ -205,18 +205,15 @@ def rq_quantize(z, codebooks, with_gap=False):
         if c.shape[1] != e:
             raise RuntimeError("rq_quantize: codebook width != latent width")
     dev = z.device
-    norms = [torch.empty(k, dtype=torch.float32, device=dev) for k in Ks]
     idx = torch.empty((n, len(cbs)), dtype=torch.int64, device=dev)
     gap = torch.empty((n, len(cbs)), dtype=torch.float32, device=dev) if with_gap else None
     best = torch.empty((n, len(cbs)), dtype=torch.float32, device=dev) if with_gap else None
     lib = L.lib()
     st = L.stream_of(dev)
     with torch.cuda.device(dev):
-        for c, cn in zip(cbs, norms):
-            L.check(lib.gr_rq_codebook_norms_f32(L.ptr(c), c.shape[0], e, L.ptr(cn), st),
-                    "gr_rq_codebook_norms_f32")
+        # code_norms = NULL: the kernel recomputes the norms from its LDS image of each codebook
         L.check(lib.gr_rq_quantize_f32(L.ptr(z), n, e, len(cbs), L.i32_array(Ks), L.ptr_array(cbs),
-                                       L.ptr_array(norms), L.ptr(idx), L.ptr(best), L.ptr(gap), st),
+                                       None, L.ptr(idx), L.ptr(best), L.ptr(gap), st),
                 "gr_rq_quantize_f32")
     return (idx, best, gap) if with_gap else idx
 
@@ -659,3 +656,82 @@ class SasTrainStepGraph:
     def replay(self):
         self.graph.replay()
         return self.out
+
+
+class SasTrainGraph:
+    """The whole SASRec training step of SASRec/train.py:131-173 -- the transformer forward in
+    train mode (dropout on, the drop-in's autograd path), GPU negatives (device-seeded), the fused
+    sampled BCE, ``loss = batch_loss / batch_valid_t``, backward and ``optimizer.step()`` --
+    captured once as a graph (hipGraph via ``torch.cuda.graph``) and replayed: one launch per step
+    instead of ~150 host-issued kernels at the reference's batch of 128.
+
+    ``optimizer`` must be capturable (``torch.optim.Adam(..., capturable=True)``: its step counter
+    lives on the device).  ``inputs`` [B, n] and ``targets`` [B, n] are the static batch tensors:
+    copy each batch into them before ``replay()``, which returns the static ``(batch_loss,
+    batch_valid_t)`` device scalars.  Capture needs a few warm-up steps (allocator, autograd and the
+    optimizer's lazily created state); the parameters and the optimizer state are restored
+    afterwards, so the first replay is the first real training step.  Dropout draws from torch's
+    graph-safe generator (fresh masks each replay)."""
+
+    def __init__(self, model, optimizer, inputs, targets, item_num, num_neg, eps, seed=0, warmup=3):
+        L.require_gpu(inputs, targets)
+        self.model, self.opt = model, optimizer
+        self.inputs, self.targets = inputs, targets
+        self.item_num, self.num_neg, self.eps = int(item_num), int(num_neg), float(eps)
+        dev = inputs.device
+        self.seed = torch.tensor([int(seed)], dtype=torch.int64, device=dev)
+        params = [p for g in optimizer.param_groups for p in g["params"]]
+        saved_p = [p.detach().clone() for p in params]
+        saved_s = {id(p): {k: (v.detach().clone() if torch.is_tensor(v) else v)
+                           for k, v in optimizer.state[p].items()} for p in params if p in optimizer.state}
+        side = torch.cuda.Stream(device=dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):
+            for _ in range(warmup):
+                self._body()
+        torch.cuda.current_stream(dev).wait_stream(side)
+        self.graph = torch.cuda.CUDAGraph()
+        optimizer.zero_grad(set_to_none=True)
+        with torch.cuda.graph(self.graph):
+            self.out = tuple(x.detach() for x in self._body())
+        with torch.no_grad():   # undo the warm-up steps: the first replay is the first step
+            for p, s in zip(params, saved_p):
+                p.copy_(s)
+            for p in params:
+                st = optimizer.state.get(p, {})
+                old = saved_s.get(id(p))
+                for k, v in st.items():
+                    if torch.is_tensor(v):
+                        if old is not None and torch.is_tensor(old.get(k)):
+                            v.copy_(old[k])
+                        else:
+                            v.zero_()
+            self.seed.fill_(int(seed))
+        self._ring = [torch.cuda.Event() for _ in range(self.MAX_INFLIGHT)]
+        self._n = 0
+
+    # Replays allowed in flight before replay() waits for the oldest one.  One replay of the whole
+    # step is ~250 AQL packets; 20 replays queued back to back (bench.py's timed loop) faulted inside
+    # the rocprim unique-by-key of the embedding backward, twice, with ~5000 packets pending, while
+    # 8-deep bursts ran 1500 steps clean (profiles/r02_train_graph_depth.log).  A training loop that
+    # reads ``batch_valid_t.item()`` each step (train.py:163) never has more than one in flight.
+    MAX_INFLIGHT = 4
+
+    def replay(self):
+        """Launch one captured step; returns the static ``(batch_loss, batch_valid_t)``."""
+        ev = self._ring[self._n % len(self._ring)]
+        if self._n >= len(self._ring):
+            ev.synchronize()    # host waits only when it is MAX_INFLIGHT steps ahead of the GPU
+        self.graph.replay()
+        ev.record()
+        self._n += 1
+        return self.out
+
+    def _body(self):
+        self.opt.zero_grad(set_to_none=True)
+        feats = self.model(self.inputs)                                            # train.py:131
+        negs = neg_samples(self.inputs, self.item_num, self.num_neg, seed_tensor=self.seed)   # :142
+        bl, valid = sampled_bce_loss(feats, self.model.item_emb.weight, self.targets, negs, self.eps)
+        (bl / valid.clamp(min=1.0)).backward()   # :161-172 (batch_loss is 0 when nothing is valid)
+        self.opt.step()                                                            # :173
+        return bl, valid

@@ -72,7 +72,7 @@ def parse():
                     help="C5 at N>1: user sub-batches per step whose exchange overlaps the next one's scoring")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--train-batch", type=int, default=128, help="sas_train leg: users per rank per step")
-    ap.add_argument("--legs", default="", help="comma list of legs to run (default all): " + ",".join(LEGS))
+    ap.add_argument("--legs", default="", help="comma list of legs to run (default: " + ",".join(LEGS) + "; also " + ",".join(OPT_LEGS) + ")")
     ap.add_argument("--skip", default="", help="comma list of legs to skip")
     ap.add_argument("--spinup-s", type=float, default=1.0,
                     help="untimed seconds of each leg's workload before its warmup (clock ramp)")
@@ -465,6 +465,82 @@ def bench_sas_train(a, world, rank, dev):
     return res
 
 
+def sas_step_flop_per_user(d, n, mlp=64, blocks=2, J=10):
+    """One training step of SASRec/train.py:131-173 per user at the reference formulation's
+    transformer (sas_flop_per_user without the catalog scoring) x 3 (forward + backward), plus the
+    sampled scoring's 2 * n * (1 + J) * d per pass (forward, and the backward's two products)."""
+    fwd = sas_flop_per_user(d, n, 0, mlp, blocks) - 2 * d
+    return 3 * fwd + 3 * 2 * n * (1 + J) * d
+
+
+def bench_sas_train_step(a, world, rank, dev):
+    """SURVEY §8(f) row 4, the whole SASRec training step (SASRec/train.py:131-173) at the
+    reference's training batch (main.py: batch 128, dropout 0.2, Adam lr 1e-3 betas (0.9, 0.98),
+    10 negatives) on C3 shapes (d 64, n 50, 100k items): the drop-in transformer under autograd
+    (dropout on), GPU negatives, the fused sampled BCE, backward and the Adam step, captured as one
+    graph (ops.SasTrainGraph) -- next to the same step issued eagerly and the reference's own
+    formulation ([B, n, N+1] score matrix) eagerly on the same GPU."""
+    B, n, d, items, J = a.train_batch, 50, 64, 100_000, 10
+    prm = synth.sasrec_params(d, n, 2, 1, 64, dev)
+    g = torch.Generator(device=dev).manual_seed(4000 + rank)
+    lens = torch.randint(3, n + 1, (B,), generator=g, device=dev)
+    targets = torch.randint(1, items + 1, (B, n), generator=g, device=dev)
+    targets[torch.arange(n, device=dev)[None, :] < (n - lens)[:, None]] = 0
+    inputs = torch.roll(targets, 1, dims=1)
+    inputs[:, 0] = 0
+
+    def make(capturable):
+        m = synth.sasrec_model(items, prm, dev, seed=11).train()   # dropout 0.2 (main.py)
+        return m, torch.optim.Adam(m.parameters(), lr=1e-3, betas=(0.9, 0.98), capturable=capturable)
+
+    m1, o1 = make(True)
+    gstep = ops.SasTrainGraph(m1, o1, inputs, targets, items, J, 1e-24, seed=5000 + rank)
+    wall, dev_ms = timed(gstep.replay, a.steps, a.warmup, world)
+    m2, o2 = make(False)
+
+    def eager():   # the same step op by op
+        o2.zero_grad()
+        h = m2(inputs)
+        ng = ops.neg_samples(inputs, items, J)
+        bl, valid = ops.sampled_bce_loss(h, m2.item_emb.weight, targets, ng, 1e-24)
+        (bl / valid.clamp(min=1.0)).backward()
+        o2.step()
+    e_wall, _ = timed(eager, a.steps, a.warmup, world)
+    negs = ops.neg_samples(inputs, items, J)
+
+    def reference():   # train.py:131-173 as written (score matrix), negatives precomputed
+        o2.zero_grad()
+        h = m2(inputs)
+        sm = torch.matmul(h, m2.item_emb.weight.t())
+        mask = (targets != 0).float()
+        ps = torch.gather(sm, 2, targets.unsqueeze(-1)).squeeze(-1)
+        ns = torch.gather(sm, 2, negs.unsqueeze(1).expand(-1, n, -1))
+        pl = -torch.log(torch.sigmoid(ps) + 1e-24) * mask
+        nl = (-torch.log(1 - torch.sigmoid(ns) + 1e-24) * mask.unsqueeze(-1)).sum(-1)
+        ((pl + nl).sum() / mask.sum()).backward()
+        o2.step()
+    r_ms = kernel_ms(reference, reps=10)
+    fl = sas_step_flop_per_user(d, n, 64, 2, J) * B
+    res = {"metric": "train_steps_seqs/s", "value": B * world * a.steps / wall, "unit": "seqs/s",
+           "ms_per_step": wall / a.steps * 1e3, "scaling": "weak",
+           "config": {"workload": f"sas_train_step: SASRec train.py:131-173 whole step (transformer forward "
+                                  f"+ backward with dropout 0.2, {J} GPU negatives, fused sampled BCE, Adam), "
+                                  f"B {B}, n {n}, d {d}, {items}-item table, one captured graph",
+                      "users_per_rank_per_step": B, "parallelism": f"user-sharded x{world} (data parallel "
+                                                                   f"without the gradient all-reduce)"},
+           "roofline": {"bound": "mfma", "achieved": fl / (dev_ms * 1e-3) / 1e12, "peak": FP32_PEAK_TFLOPS,
+                        "unit": "TFLOP/s", "frac": fl / (dev_ms * 1e-3) / 1e12 / FP32_PEAK_TFLOPS,
+                        "traffic": None, "kernel": "whole step (latency-bound: ~150 small kernels in one graph)",
+                        "flop_per_step": fl, "step_device_ms": dev_ms},
+           "eager": {"note": "the same step issued op by op", "value": B * world * a.steps / e_wall,
+                     "ms_per_step": e_wall / a.steps * 1e3},
+           "reference_formulation_gpu": {"note": "train.py:131-173 as written ([B, n, N+1] score matrix) in "
+                                                 "torch on the same GPU, negatives precomputed (the reference "
+                                                 "draws them on the host)",
+                                         "ms_per_step": r_ms, "speedup": r_ms / (wall / a.steps * 1e3)}}
+    return res
+
+
 def bench_c5_shard(a, model, h, targets, dev, shards=8):
     """The per-GPU work of the 8-GPU C5 point, timed on one GPU: 512 users against one catalog
     shard of 125,001 rows (rows [lo, hi) of the 1M-item table; the first shard, which also masks
@@ -555,6 +631,7 @@ def bench_calls(rq_model, sas_model, sas_n, sas_items, dev, cpu=True):
 
 
 LEGS = ["c2", "calls", "sasrec", "c4", "c5", "shard", "train"]
+OPT_LEGS = ["train_step"]   # run only when named in --legs
 
 
 def main():
@@ -616,6 +693,8 @@ def main():
             line["c5_shard"] = bench_c5_shard(a, c5_model, h5, t5, dev)
         del c5_model, h5
         torch.cuda.empty_cache()
+    if "train_step" in legs:
+        line["sasrec_train_step"] = bench_sas_train_step(a, world, rank, dev)
     if "train" in legs:
         line["sasrec_train"] = bench_sas_train(a, world, rank, dev)
     if rank == 0:

@@ -93,7 +93,9 @@ int gr_rq_codebook_norms_f32(const float* codebook, int32_t K, int32_t e, float*
 /* Residual quantization of latents z[n, e] over L levels (RQ-VAE/models/rq.py:39-56 with
  * VectorQuantizer.forward(use_sk=False), vq.py:63-99):
  *   d = (||r||^2 + ||C_l||^2) - 2 r.C_l^T ;  idx = first argmin ;  r <- r - (r + (C_l[idx] - r))
- * K, codebooks, code_norms: host arrays of length L (code_norms from gr_rq_codebook_norms_f32).
+ * K, codebooks: host arrays of length L.  code_norms: accepted for ABI stability and ignored (may be
+ * NULL); the kernel recomputes each code's norm from its LDS copy of the codebook with the same
+ * k-ordered fma chain as gr_rq_codebook_norms_f32.
  * idx_out[n, L] int64 row-major (the stacked `indices` of rq.py:54).
  * best_out[n, L], gap_out[n, L] (optional, may be NULL): the best fp32 distance and the gap to the
  * second best per level — the near-tie certificate (a row whose gap is within fp32 rounding of

@@ -1,38 +1,63 @@
-"""Time gr_rq_quantize_f32 alone (z already encoded) across item counts and levels, HIP events.
+"""Device-time A/B of a gr_set_option switch on gr_rq_quantize_f32 (C2 codebooks 3 x 256, e 32 by
+default): 20 calls captured in one graph and replayed, so the host's per-call cost (~40-80 us of
+Python + ctypes, which bounded scripts/ab_opt.py's quantize numbers) is off the clock.
 
-    python scripts/ab_quant.py
+    python scripts/ab_quant.py --opt rq_waves=8,16 [--L 3 --K 256] [--n 3200,25600,100000]
 """
+import argparse
 import os
 import sys
 
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from gr_amd import ops  # noqa: E402
-
-dev = torch.device("cuda:0")
-g = torch.Generator(device=dev).manual_seed(0)
+from gr_amd import _lib, ops, synth  # noqa: E402
 
 
-def ms(fn, reps=50):
-    import time
-    t0 = time.perf_counter()
-    while time.perf_counter() - t0 < 0.3:   # clock ramp
-        fn()
-        torch.cuda.synchronize()
+def graph_us(fn, calls=20, reps=10):
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for _ in range(3):
+            fn()
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(calls):
+            fn()
+    for _ in range(20):   # clock ramp
+        g.replay()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     for _ in range(reps):
-        fn()
+        g.replay()
     e1.record()
     torch.cuda.synchronize()
-    return e0.elapsed_time(e1) / reps
+    return e0.elapsed_time(e1) / (reps * calls) * 1e3
 
 
-for L, K in [(3, 256), (1, 256), (4, 1024)]:
-    cbs = [torch.randn((K, 32), generator=g, device=dev) * 0.3 for _ in range(L)]
-    for n in (25_000, 50_000, 100_000, 200_000, 400_000):
-        z = torch.randn((n, 32), generator=g, device=dev)
-        t = ms(lambda: ops.rq_quantize(z, cbs))
-        fl = 2.0 * n * L * K * 32
-        print(f"L={L} K={K} n={n:7d}: {t * 1e3:8.1f} us  {fl / t / 1e9:6.1f} TF/s  {n / t / 1e3:8.1f} M items/s", flush=True)
+ap = argparse.ArgumentParser()
+ap.add_argument("--opt", default="rq_waves=8,16")
+ap.add_argument("--L", type=int, default=3)
+ap.add_argument("--K", type=int, default=256)
+ap.add_argument("--n", default="3200,25600,51200,100000,409600")
+ap.add_argument("--second", action="store_true", help="also return best/second (certified path)")
+a = ap.parse_args()
+dev = torch.device("cuda:0")
+m = synth.rqvae_model(a.L, a.K, dev)
+b = m.encode_binding()
+name, vals = a.opt.split("=")
+for n in [int(v) for v in a.n.split(",")]:
+    x = synth.items(n, 1000, dev)
+    z = ops.rq_mlp(x, b.ws, b.bs)
+    ref = None
+    for v in vals.split(","):
+        _lib.set_option(name, int(v))
+        fn = lambda: ops.rq_quantize(z, b.cbs)   # noqa: E731
+        out = fn()
+        torch.cuda.synchronize()
+        ref = out if ref is None else ref
+        t = graph_us(fn)
+        print(f"quant L={a.L} K={a.K} n={n} {name}={v}: {t:8.2f} us/call  same as first: {torch.equal(out, ref)}",
+              flush=True)
+    _lib.set_option(name, int(vals.split(",")[0]))

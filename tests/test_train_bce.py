@@ -342,3 +342,54 @@ def test_captured_step_inside_training_loop(dev):
                 assert q.grad is None or float(q.grad.abs().max()) == 0.0, name
                 continue
             assert (q.grad - r.grad).abs().max() <= 1e-5 * max(float(r.grad.abs().max()), 1e-30), name
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("opt_name", ["sgd", "adam"])
+def test_whole_train_step_graph_matches_eager(opt_name, dev):
+    """ops.SasTrainGraph (forward + negatives + fused loss + backward + optimizer step, one graph)
+    against the same steps issued eagerly on a copy of the model (dropout 0, the same negatives).
+    SGD: every parameter after three steps within 1e-5 of its scale (the dM atomics reorder last
+    bits).  Adam (the reference's optimizer, train.py:107): per-step losses within 1e-5 relative --
+    Adam turns the rounding noise of a mathematically zero gradient (the attention's key bias) into
+    +-lr steps, so parameters are compared only through the loss they produce.  Both: the warm-up
+    leaves no trace (first replay = step 1) and each replay draws fresh negatives."""
+    import copy
+    from gr_amd import ops, synth
+    B, n, d, items, J = 32, 20, 64, 3000, 5
+    p = synth.sasrec_params(d, n, 2, 1, 64, dev)
+    p["dropout"] = 0.0
+    m = synth.sasrec_model(items, p, dev, seed=7).train()
+    ref = copy.deepcopy(m)
+    if opt_name == "sgd":
+        opt = torch.optim.SGD(m.parameters(), lr=0.05)
+        ref_opt = torch.optim.SGD(ref.parameters(), lr=0.05)
+    else:
+        opt = torch.optim.Adam(m.parameters(), lr=1e-3, betas=(0.9, 0.98), capturable=True)
+        ref_opt = torch.optim.Adam(ref.parameters(), lr=1e-3, betas=(0.9, 0.98))
+    g = torch.Generator(device=dev).manual_seed(9)
+    seqs = torch.randint(1, items + 1, (B, n), generator=g, device=dev)
+    seqs[:, :3] = 0
+    targets = torch.roll(seqs, -1, dims=1)
+    targets[:, -1] = torch.randint(1, items + 1, (B,), generator=g, device=dev)
+    targets[seqs == 0] = 0
+    step = ops.SasTrainGraph(m, opt, seqs, targets, items, J, 1e-24, seed=21)
+    for a, b in zip(m.parameters(), ref.parameters()):
+        assert torch.equal(a, b)   # the warm-up steps were undone
+    keys = []
+    for _ in range(3):
+        key = int(step.seed.item())
+        keys.append(key)
+        bl, valid = step.replay()
+        negs = ops.neg_samples(seqs, items, J, seed_tensor=torch.tensor([key], dtype=torch.int64, device=dev))
+        ref_opt.zero_grad()
+        bl2, valid2 = ops.sampled_bce_loss(ref(seqs), ref.item_emb.weight, targets, negs, 1e-24)
+        (bl2 / valid2).backward()
+        ref_opt.step()
+        assert float(valid) == float(valid2)
+        assert abs(float(bl) - float(bl2.detach())) <= 1e-5 * abs(float(bl2.detach()))
+    assert len(set(keys)) == 3
+    if opt_name == "sgd":
+        with torch.no_grad():
+            for (name, a), b in zip(m.named_parameters(), ref.parameters()):
+                assert (a - b).abs().max() <= 1e-5 * max(float(b.abs().max()), 1e-6), name
