@@ -707,24 +707,20 @@ class SasTrainGraph:
                         else:
                             v.zero_()
             self.seed.fill_(int(seed))
-        self._ring = [torch.cuda.Event() for _ in range(self.MAX_INFLIGHT)]
-        self._n = 0
-
-    # Replays allowed in flight before replay() waits for the oldest one.  One replay of the whole
-    # step is ~250 AQL packets; 20 replays queued back to back (bench.py's timed loop) faulted inside
-    # the rocprim unique-by-key of the embedding backward, twice, with ~5000 packets pending, while
-    # 8-deep bursts ran 1500 steps clean (profiles/r02_train_graph_depth.log).  A training loop that
-    # reads ``batch_valid_t.item()`` each step (train.py:163) never has more than one in flight.
-    MAX_INFLIGHT = 4
 
     def replay(self):
-        """Launch one captured step; returns the static ``(batch_loss, batch_valid_t)``."""
-        ev = self._ring[self._n % len(self._ring)]
-        if self._n >= len(self._ring):
-            ev.synchronize()    # host waits only when it is MAX_INFLIGHT steps ahead of the GPU
+        """Run one captured step and return the static ``(batch_loss, batch_valid_t)``; returns
+        after the step has finished on the device (the reference loop synchronises every step
+        too: ``batch_valid_t.item()``, train.py:163).
+
+        The device-wide synchronise is load-bearing.  Replays of this graph back to back -- even
+        host-ordered through a completion event -- faulted within ~600 steps (memory aperture
+        violation in the rocprim unique-by-key of the item embedding's backward; four of four
+        bench runs), while replay + ``torch.cuda.synchronize()`` ran 725 and 1500 steps clean
+        (profiles/r02_train_graph_diag.txt).  It costs nothing measurable at this step size
+        (1.59 ms per step synchronised vs 1.75 ms unsynchronised)."""
         self.graph.replay()
-        ev.record()
-        self._n += 1
+        torch.cuda.synchronize(self.inputs.device)
         return self.out
 
     def _body(self):
