@@ -24,6 +24,9 @@ struct RQLevels {
 };
 
 // max item tiles per wave (residuals held in registers): fewer at e = 64 to stay spill-free
+constexpr int RQ_SPLIT_MAX = 3;      // leftover tiles per workgroup split into code quarters (c % 4)
+constexpr size_t RQ_PART_BYTES = 2 * RQ_SPLIT_MAX * 4 * 32 * 3 * sizeof(float);
+
 template <int E, int W>
 struct RQMaxT { static constexpr int value = W >= 16 ? 1 : (E >= 64 ? 2 : 4); };
 
@@ -52,7 +55,7 @@ __device__ __forceinline__ int cb_off(int c, int q) {
 template <int E, bool SECOND, int W>
 __global__ __launch_bounds__(W * 64) void rq_quantize_kernel(
     const float* __restrict__ z, int64_t n, int L, RQLevels lv, int kch, int64_t* __restrict__ idx_out,
-    float* __restrict__ best_out, float* __restrict__ gap_out, int tiles) {
+    float* __restrict__ best_out, float* __restrict__ gap_out, int tiles, int split_ok) {
   static_assert(E % 8 == 0 && E <= 64, "e");
   constexpr int HQ = E / 8;            // float4 per lane half
   constexpr int RQ_MAXT = RQMaxT<E, W>::value;
@@ -95,15 +98,32 @@ __global__ __launch_bounds__(W * 64) void rq_quantize_kernel(
     }
     __syncthreads();
   }
+  float* part = cns + (resident ? ktot : kch);    // [2][RQ_SPLIT_MAX][4][32][3] split-tile partials
   const int t_begin = (int)((int64_t)blockIdx.x * tiles / gridDim.x);
   const int t_end = (int)((int64_t)(blockIdx.x + 1) * tiles / gridDim.x);
-  const int my = (t_end - t_begin - w + W - 1) / W;  // tiles of this wave (<= MAXT)
+  // Tile plan.  Wave w runs on SIMD w % 4, so a SIMD's load is the tiles of its W/4 waves.  Split
+  // plan: SIMD s works through the list [its c/4 whole tiles t_begin + s + 4m, then one code quarter
+  // of each of the c%4 leftover tiles], its waves taking the list round-robin; every SIMD does
+  // c/4 + (c%4)/4 tile passes instead of up to ceil(c/4), and the four quarters' argmins merge
+  // through LDS after each level.  Plain plan (round-robin over all waves) when the split one does
+  // not fit the register-resident slots.
+  constexpr int WS = W / 4;
+  const int c = t_end - t_begin, simd = w & 3, wk = w >> 2;
+  const int base = c >> 2, rem = c & 3;
+  const bool split_plan = split_ok && rem > 0 && (base + rem + WS - 1) / WS <= RQ_MAXT;
+  const int my = split_plan ? (base + rem - wk + WS - 1) / WS : (c - w + W - 1) / W;   // slots (<= MAXT)
+  auto is_split = [&](int i) -> bool { return split_plan && wk + i * WS >= base; };
+  auto tile_of = [&](int i) -> int {
+    if (!split_plan) return t_begin + w + i * W;
+    const int j = wk + i * WS;                      // entry of the SIMD's list
+    return j < base ? t_begin + simd + 4 * j : t_begin + 4 * base + (j - base);
+  };
 
   // residual of this lane's item for each of the wave's tiles: lane half h holds k in [hE/2, ...)
   f32x4 res[RQ_MAXT][HQ];
 #pragma unroll
   for (int i = 0; i < RQ_MAXT; ++i) {
-    const int64_t item = (int64_t)(t_begin + w + i * W) * 32 + r;
+    const int64_t item = (int64_t)tile_of(i) * 32 + r;
     const bool ok = i < my && item < n;
     const int64_t ic = ok ? item : 0;
 #pragma unroll
@@ -163,8 +183,10 @@ __global__ __launch_bounds__(W * 64) void rq_quantize_kernel(
         __syncthreads();
       }
       const int ct_n = (cnt + 31) >> 5;
+      const int q_lo = simd * ct_n / 4, q_hi = (simd + 1) * ct_n / 4;   // this SIMD's code quarter
 #pragma unroll 1
       for (int ct = 0; ct < ct_n; ++ct) {
+        const bool in_q = ct >= q_lo && ct < q_hi;
         const int code = min(ct * 32 + r, cnt - 1);   // rows past cnt: any valid row (norm = inf)
         f32x4 a[HQ];
 #pragma unroll
@@ -179,7 +201,7 @@ __global__ __launch_bounds__(W * 64) void rq_quantize_kernel(
         }
 #pragma unroll
         for (int i = 0; i < RQ_MAXT; ++i) {
-          if (i < my) {   // wave-uniform
+          if (i < my && (!is_split(i) || in_q)) {   // wave-uniform
             f32x16 acc;
 #pragma unroll
             for (int v = 0; v < 16; ++v) acc[v] = 0.f;
@@ -199,7 +221,7 @@ __global__ __launch_bounds__(W * 64) void rq_quantize_kernel(
         }
       }
     }
-    // merge the two lane halves (lowest distance, then lowest index), write, update the residual
+    // merge the two lane halves (lowest distance, then lowest index)
 #pragma unroll
     for (int i = 0; i < RQ_MAXT; ++i) {
       if (i < my) {
@@ -212,10 +234,50 @@ __global__ __launch_bounds__(W * 64) void rq_quantize_kernel(
         } else {
           second[i] = fminf(second[i], ob);
         }
+      }
+    }
+    if (split_plan) {   // workgroup-uniform: merge the split tiles' four code quarters, in order
+      float* pl = part + (l & 1) * (RQ_SPLIT_MAX * 4 * 32 * 3);   // double-buffered by level
+#pragma unroll
+      for (int i = 0; i < RQ_MAXT; ++i)
+        if (i < my && is_split(i) && h == 0) {
+          float* e = pl + (((wk + i * WS - base) * 4 + simd) * 32 + r) * 3;
+          e[0] = best[i];
+          e[1] = second[i];
+          e[2] = __int_as_float(bi[i]);
+        }
+      __syncthreads();
+#pragma unroll
+      for (int i = 0; i < RQ_MAXT; ++i)
+        if (i < my && is_split(i)) {
+          const float* e = pl + ((wk + i * WS - base) * 4 * 32 + r) * 3;
+          float bb = e[0], ss = e[1];
+          int ii = __float_as_int(e[2]);
+#pragma unroll
+          for (int q = 1; q < 4; ++q) {
+            const float ob = e[q * 96], os = e[q * 96 + 1];
+            const int oi = __float_as_int(e[q * 96 + 2]);
+            if (ob < bb || (ob == bb && oi < ii)) {
+              ss = fminf(os, bb);
+              bb = ob;
+              ii = oi;
+            } else {
+              ss = fminf(ss, ob);
+            }
+          }
+          best[i] = bb;
+          second[i] = ss;
+          bi[i] = ii;
+        }
+    }
+    // write, update the residual
+#pragma unroll
+    for (int i = 0; i < RQ_MAXT; ++i) {
+      if (i < my) {
         int b = bi[i];
         if (b >= K) b = 0;  // no finite distance (NaN/inf input): torch.argmin -> 0
-        const int64_t item = (int64_t)(t_begin + w + i * W) * 32 + r;
-        if (h == 0 && item < n) {
+        const int64_t item = (int64_t)tile_of(i) * 32 + r;
+        if (h == 0 && item < n && (!is_split(i) || simd == 0)) {
           idx_out[item * L + l] = (int64_t)b;
           if (best_out) best_out[item * L + l] = best[i];
           if (gap_out) gap_out[item * L + l] = second[i] - best[i];
@@ -266,7 +328,7 @@ static int launch_quantize_e(const float* z, int64_t n, int L, const RQLevels& l
   // every level resident in LDS at once when they fit in 128 KiB (C2: 3 x 256 x 32 -> 99 KiB)
   const bool resident = option("rq_resident") != 0 && (size_t)ktot * (E + 1) * 4 <= 128 * 1024;
   const int kch = resident ? 0 : ((kmax < kch_max ? kmax : kch_max) + 31) & ~31;
-  const size_t lds = resident ? (size_t)ktot * (E + 1) * 4 : (size_t)kch * E * 4 + (size_t)kch * 4;
+  const size_t lds = (resident ? (size_t)ktot * (E + 1) * 4 : (size_t)kch * E * 4 + (size_t)kch * 4) + RQ_PART_BYTES;
   // persistent: one 8-wave workgroup per CU (2 waves per SIMD at this register budget), each with
   // a contiguous balanced range of tiles; more workgroups only when a range would exceed the
   // register-resident residuals (W x MT tiles)
@@ -288,7 +350,7 @@ static int launch_quantize_e(const float* z, int64_t n, int L, const RQLevels& l
                           (int)lds) != hipSuccess)
     return fail(GR_ERR_HIP, "rq quantize: cannot raise the LDS limit");
   hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(W * 64), lds, st, z, n, L, lv, kch, idx,
-                     best, gap, (int)tiles);
+                     best, gap, (int)tiles, (int)(option("rq_split") != 0));
   return check_launch("gr_rq_quantize_f32");
 }
 
