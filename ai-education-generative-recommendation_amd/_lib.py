@@ -38,6 +38,12 @@ class SasrecParams(ctypes.Structure):
                 ("last_ln_w", _vp), ("last_ln_b", _vp)]
 
 
+class SasrecTrainBufs(ctypes.Structure):
+    """Mirror of ``gr_sasrec_train_bufs`` (include/gr_amd.h)."""
+    _fields_ = [(f, _vp) for f in ("xin", "hs", "qkv", "prob", "os", "x1", "fs", "zs", "us", "xl",
+                                   "g_qkv", "g_out", "g_z", "g_y", "g_vec")]
+
+
 # (name, restype, argtypes) for every entry point of include/gr_amd.h
 SIGNATURES = {
     "gr_version": (ctypes.c_char_p, []),
@@ -62,6 +68,13 @@ SIGNATURES = {
                                              _vp, _sz, _vp, _vp]),
     "gr_sasrec_predict_ld_f32": (ctypes.c_int, [ctypes.POINTER(SasrecParams), _vp, _i64, _i32, _vp,
                                                 _i64, _vp, _sz, _vp, _vp]),
+    "gr_sasrec_train_vec_width": (_i32, [ctypes.POINTER(SasrecParams), _i32]),
+    "gr_sasrec_train_fwd_f32": (ctypes.c_int, [ctypes.POINTER(SasrecParams), _vp, _i64, _i32, _f32,
+                                               ctypes.c_uint64, _vp, ctypes.POINTER(SasrecTrainBufs), _vp,
+                                               _vp, _vp]),
+    "gr_sasrec_train_bwd_f32": (ctypes.c_int, [ctypes.POINTER(SasrecParams), _vp, _i64, _i32, _f32,
+                                               ctypes.c_uint64, _vp, ctypes.POINTER(SasrecTrainBufs), _vp,
+                                               _vp, _vp]),
     "gr_score_f32": (ctypes.c_int, [_vp, _i64, _i32, _vp, _i64, _vp, _i64, _vp]),
     "gr_sampled_bce_fwd_f32": (ctypes.c_int, [_vp, _i64, _i32, _i32, _vp, _i64, _vp, _vp, _i32, _f32,
                                               _vp, _vp, _vp, _vp, _vp]),

@@ -611,6 +611,113 @@ def neg_samples(seq, item_num, num_neg=1, seed=None, seed_tensor=None):
     return out
 
 
+# --------------------------------------------------------------------------------------------
+# Transformer training forward / backward (SASRec/model.py:49-96 under train.py:131 and :161-172)
+
+_DROP_SEED = {}
+
+
+def dropout_seed(device):
+    """The device's dropout seed word: every train-mode forward snapshots it and advances it by one
+    on the stream (a captured step therefore replays with fresh masks).  Initialised from torch's
+    global generator, so ``torch.manual_seed`` makes runs repeatable."""
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    t = _DROP_SEED.get(idx)
+    if t is None:
+        t = torch.randint(0, 2 ** 62, (1,), dtype=torch.int64).to(torch.device("cuda", idx))
+        _DROP_SEED[idx] = t
+    return t
+
+
+def sasrec_train_supported(model, n):
+    return (n <= 64 and n <= model.pos_emb.weight.shape[0] and model.d <= 64
+            and model.d % model.num_heads == 0 and model.mlp_layer <= 128 and 1 <= model.num_blocks <= 8)
+
+
+def _train_params(model):
+    """The parameters the transformer's forward reads, in the order _SasTrain returns gradients."""
+    ps = [model.item_emb.weight, model.pos_emb.weight]
+    for la, at, lf, ff in zip(model.attention_layernorms, model.attention_layers, model.forward_layernorms,
+                              model.forward_layers):
+        ps += [la.weight, la.bias, at.in_proj_weight, at.in_proj_bias, at.out_proj.weight, at.out_proj.bias,
+               lf.weight, lf.bias, ff[0].weight, ff[0].bias, ff[3].weight, ff[3].bias]
+    return ps + [model.last_layernorm.weight, model.last_layernorm.bias]
+
+
+class _SasTrain(torch.autograd.Function):
+    """Train-mode SASRec forward (dropout on) and its backward on the kernels of sasrec_train.hip:
+    one launch each; the weight gradients are dG^T A library GEMMs over the B*n rows."""
+
+    @staticmethod
+    def forward(ctx, seqs, binding, p_drop, seed_snap, *params):
+        B, n = seqs.shape
+        p = binding.p
+        d, m, nb, H = p.d, p.mlp, p.n_blocks, p.n_heads
+        dev = seqs.device
+        R = B * n
+        e = lambda *shape: torch.empty(shape, dtype=torch.float32, device=dev)   # noqa: E731
+        bufs = {"xin": e(nb, R, d), "hs": e(nb, R, d), "qkv": e(nb, R, 3 * d), "prob": e(nb, B, H, n, n),
+                "os": e(nb, R, d), "x1": e(nb, R, d), "fs": e(nb, R, d), "zs": e(nb, R, m), "us": e(nb, R, m),
+                "xl": e(R, d)}
+        out = e(B, n, d)
+        err = err_flag(dev)
+        cb = L.SasrecTrainBufs(**{k: v.data_ptr() for k, v in bufs.items()})
+        with torch.cuda.device(dev):
+            L.check(L.lib().gr_sasrec_train_fwd_f32(ctypes.byref(p), L.ptr(seqs), B, n, float(p_drop), 0,
+                                                    L.ptr(seed_snap), ctypes.byref(cb), L.ptr(out), L.ptr(err),
+                                                    L.stream_of(dev)), "gr_sasrec_train_fwd_f32")
+        _check_err(err)
+        ctx.binding, ctx.p_drop, ctx.bufs, ctx.seqs, ctx.seed = binding, p_drop, bufs, seqs, seed_snap
+        ctx.shapes = (B, n, d, m, nb, params[1].shape[0])
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        B, n, d, m, nb, max_len = ctx.shapes
+        bufs, seqs = ctx.bufs, ctx.seqs
+        dev = seqs.device
+        R = B * n
+        p = ctx.binding.p
+        vw = L.lib().gr_sasrec_train_vec_width(ctypes.byref(p), n)
+        e = lambda *shape: torch.empty(shape, dtype=torch.float32, device=dev)   # noqa: E731
+        g = {"g_qkv": e(nb, R, 3 * d), "g_out": e(nb, R, d), "g_z": e(nb, R, m), "g_y": e(nb, R, d),
+             "g_vec": e(B, vw)}
+        g_item = torch.zeros((p.item_rows, d), dtype=torch.float32, device=dev)
+        cb = L.SasrecTrainBufs(**{k: v.data_ptr() for k, v in {**bufs, **g}.items()})
+        dout = dout.contiguous().float()
+        with torch.cuda.device(dev):
+            L.check(L.lib().gr_sasrec_train_bwd_f32(ctypes.byref(p), L.ptr(seqs), B, n, float(ctx.p_drop), 0,
+                                                    L.ptr(ctx.seed), ctypes.byref(cb), L.ptr(dout), L.ptr(g_item),
+                                                    L.stream_of(dev)), "gr_sasrec_train_bwd_f32")
+        vec = g["g_vec"].sum(0)
+        grads = [g_item]
+        dpos = torch.zeros((max_len, d), dtype=torch.float32, device=dev)
+        off = nb * (9 * d + m)
+        dpos[:n] = vec[off + 2 * d:].view(n, d)
+        grads.append(dpos)
+        for k in range(nb):
+            v = vec[k * (9 * d + m):(k + 1) * (9 * d + m)]
+            grads += [v[:d], v[d:2 * d],
+                      g["g_qkv"][k].t() @ bufs["hs"][k], v[2 * d:5 * d],
+                      g["g_out"][k].t() @ bufs["os"][k], v[5 * d:6 * d],
+                      v[6 * d:7 * d], v[7 * d:8 * d],
+                      g["g_z"][k].t() @ bufs["fs"][k], v[8 * d:8 * d + m],
+                      g["g_y"][k].t() @ bufs["us"][k], v[8 * d + m:9 * d + m]]
+        grads += [vec[off:off + d], vec[off + d:off + 2 * d]]
+        return (None, None, None, None, *grads)
+
+
+def sasrec_train_forward(model, log_seqs):
+    """``model.forward(log_seqs)`` in train mode with grad (SASRec/train.py:131): the transformer
+    forward with dropout on the kernels, differentiable in every parameter it reads."""
+    seqs = log_seqs.to(torch.int64).contiguous()
+    L.require_gpu(seqs)
+    seed = dropout_seed(seqs.device)
+    snap = seed.clone()          # this step's masks (forward and backward read the same word)
+    seed.add_(1)
+    return _SasTrain.apply(seqs, sasrec_binding(model), float(model.dropout), snap, *_train_params(model))
+
+
 class SasTrainStepGraph:
     """The training-side scoring step of SASRec/train.py:131-167 -- negatives (train.py:142),
     scores + sampled BCE (134-158), ``loss = batch_loss / batch_valid_t`` (161-164) and its backward

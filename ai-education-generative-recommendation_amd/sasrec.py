@@ -66,6 +66,11 @@ class SASRec(nn.Module):
         with torch.no_grad():
             return ops.sasrec_forward(self._binding(log_seqs), log_seqs)
 
+    # Train-mode forward on the fused training kernels (ops.sasrec_train_forward: one launch
+    # forward, one backward) whenever the shape fits them (n, d <= 64, mlp_layer <= 128); False
+    # keeps the module-by-module autograd path below (used by the parity tests as the reference).
+    fused_train = True
+
     def _forward_autograd(self, log_seqs):
         """model.py:58-96 as module calls: E[s] + P[0..n), then per block a pre-LN causal
         self-attention residual and a pre-LN FFN residual, then the last LayerNorm.  The reference's
@@ -73,6 +78,8 @@ class SASRec(nn.Module):
         n = log_seqs.shape[1]
         if n > self.pos_emb.weight.shape[0]:
             raise IndexError(f"sequence length {n} exceeds max_len {self.pos_emb.weight.shape[0]}")
+        if self.fused_train and ops.sasrec_train_supported(self, n):
+            return ops.sasrec_train_forward(self, log_seqs)
         pos = torch.arange(n, device=log_seqs.device)
         x = self.item_emb(log_seqs) + self.pos_emb(pos).unsqueeze(0)
         causal = torch.ones((n, n), dtype=torch.bool, device=log_seqs.device).triu(1)

@@ -195,6 +195,52 @@ int gr_sasrec_predict_ld_f32(const gr_sasrec_params* p, const int64_t* seqs, int
                              float* logits, int64_t ld, void* workspace, size_t workspace_bytes,
                              int32_t* err_flag, void* stream);
 
+/* SASRec training, the transformer part of one step (SASRec/train.py:131 `model.forward` in train
+ * mode and the backward that `loss.backward()`, train.py:161-172, runs through model.py:49-96).
+ * One workgroup per sequence; n <= 64, d <= 64 (d % num_heads == 0), mlp_layer <= 128, <= 8 blocks.
+ * Dropout p (params['dropout']) on the attention probabilities, the FFN hidden layer and the FFN
+ * output, as nn.MultiheadAttention / nn.Dropout apply it; masks from a counter-based hash keyed by
+ * seed ^ *seed_dev (seed_dev optional), the same for the forward and the backward of one step.
+ * Buffers (device, caller-allocated, fp32): nb = n_blocks, R = B * n rows (sequence-major). */
+typedef struct gr_sasrec_train_bufs {
+  float* xin;    /* [nb, R, d]    LN_a input of each block       (written by the forward) */
+  float* hs;     /* [nb, R, d]    LN_a output = in-projection input                       */
+  float* qkv;    /* [nb, R, 3d]   in-projection output q | k | v                          */
+  float* prob;   /* [nb, B, H, n, n] softmax probabilities before dropout                 */
+  float* os;     /* [nb, R, d]    attention output = out-projection input                 */
+  float* x1;     /* [nb, R, d]    residual after attention = LN_f input                   */
+  float* fs;     /* [nb, R, d]    LN_f output = FFN1 input                                */
+  float* zs;     /* [nb, R, mlp]  FFN1 output before the ReLU                             */
+  float* us;     /* [nb, R, mlp]  dropout(relu(FFN1)) = FFN2 input                        */
+  float* xl;     /* [R, d]        last LayerNorm input                                    */
+  float* g_qkv;  /* [nb, R, 3d]   dloss / d in-projection output  (written by the backward) */
+  float* g_out;  /* [nb, R, d]    dloss / d out-projection output                         */
+  float* g_z;    /* [nb, R, mlp]  dloss / d FFN1 output                                   */
+  float* g_y;    /* [nb, R, d]    dloss / d FFN2 output                                   */
+  float* g_vec;  /* [B, gr_sasrec_train_vec_width] per-sequence partial sums: per block
+                    [ln_a w, ln_a b, in_proj b (3d), out_proj b, ln_f w, ln_f b, ffn1 b (mlp),
+                    ffn2 b], then [last ln w, last ln b], then pos_emb rows [n, d]            */
+} gr_sasrec_train_bufs;
+
+/* Floats per sequence in gr_sasrec_train_bufs.g_vec: n_blocks * (9d + mlp) + 2d + n*d. */
+int32_t gr_sasrec_train_vec_width(const gr_sasrec_params* p, int32_t n);
+
+/* Train-mode forward: seqs[B, n] -> out[B, n, d] (model.py:49-96 with dropout p), saving the
+ * activations in bufs.  err_flag (optional) gets 1 for an id outside [0, item_rows). */
+int gr_sasrec_train_fwd_f32(const gr_sasrec_params* p, const int64_t* seqs, int64_t B, int32_t n,
+                            float p_drop, uint64_t seed, const uint64_t* seed_dev,
+                            const gr_sasrec_train_bufs* bufs, float* out, int32_t* err_flag, void* stream);
+
+/* Backward of the forward above (same seqs, p_drop, seed, bufs): d_out[B, n, d] -> the per-row
+ * gradients and per-sequence partial sums in bufs; item-embedding rows are added (atomically)
+ * into g_item[item_rows, d] (optional; padding row 0 is left untouched).  The host completes the
+ * weight gradients: dW_in = g_qkv^T hs, dW_o = g_out^T os, dW1 = g_z^T fs, dW2 = g_y^T us per
+ * block, and the vectors = g_vec summed over B. */
+int gr_sasrec_train_bwd_f32(const gr_sasrec_params* p, const int64_t* seqs, int64_t B, int32_t n,
+                            float p_drop, uint64_t seed, const uint64_t* seed_dev,
+                            const gr_sasrec_train_bufs* bufs, const float* d_out, float* g_item,
+                            void* stream);
+
 /* Full-catalog (or catalog-shard) scoring logits[B, rows] = h[B, d] . table[rows, d]^T
  * (SASRec/model.py:107).  ld = row stride of logits. */
 int gr_score_f32(const float* h, int64_t B, int32_t d, const float* table, int64_t rows,
