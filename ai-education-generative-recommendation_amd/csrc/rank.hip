@@ -116,7 +116,7 @@ extern "C" int gr_count_gt_f32(const float* logits, int64_t B, int64_t cols, int
   if (!logits || !thresholds || !counts_out) return fail(GR_ERR_ARG, "gr_count_gt_f32: null pointer");
   if (B > 65535) return fail(GR_ERR_UNSUPPORTED, "gr_count_gt_f32: B > 65535");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  if (hipMemsetAsync(counts_out, 0, (size_t)B * sizeof(int64_t), st) != hipSuccess)
+  if (gr_fill32_launch(counts_out, 0u, B * 2, st) != GR_OK)
     return fail(GR_ERR_HIP, "gr_count_gt_f32: memset failed");
   if (cols == 0) return GR_OK;
   const int segs = row_segments(B, cols);
@@ -148,7 +148,7 @@ extern "C" int gr_topk_f32(const float* logits, int64_t B, int64_t cols, int64_t
   if (!workspace || workspace_bytes < need)
     return fail(GR_ERR_WORKSPACE, "gr_topk_f32: workspace too small (need " + std::to_string(need) + " bytes)");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  if (counts_out && hipMemsetAsync(counts_out, 0, (size_t)B * sizeof(int64_t), st) != hipSuccess)
+  if (counts_out && gr_fill32_launch(counts_out, 0u, B * 2, st) != GR_OK)
     return fail(GR_ERR_HIP, "gr_topk_f32: memset failed");
   const int segs = row_segments(B, cols);
   char* base = reinterpret_cast<char*>(align_up(reinterpret_cast<uintptr_t>(workspace), 256));

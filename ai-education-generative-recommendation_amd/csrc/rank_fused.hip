@@ -241,7 +241,7 @@ extern "C" int gr_score_count_gt_f32(const float* h, int64_t B, int32_t d, const
     return fail(GR_ERR_UNSUPPORTED, "gr_score_count_gt_f32: d must be 32, 64 or 128");
   if (!aligned16(h) || !aligned16(table)) return fail(GR_ERR_ARG, "gr_score_count_gt_f32: h / table not 16-byte aligned");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  if (hipMemsetAsync(counts_out, 0, (size_t)B * sizeof(int64_t), st) != hipSuccess)
+  if (gr_fill32_launch(counts_out, 0u, B * 2, st) != GR_OK)
     return fail(GR_ERR_HIP, "gr_score_count_gt_f32: memset failed");
   if (rows == 0) return GR_OK;
   const int64_t ublocks = (B + 128 * RK_UT - 1) / (128 * RK_UT);

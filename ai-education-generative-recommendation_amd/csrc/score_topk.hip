@@ -635,14 +635,14 @@ extern "C" int gr_score_topk_f32(const float* h, int64_t B, int32_t d, const flo
   if (!aligned16(h) || !aligned16(table)) return fail(GR_ERR_ARG, "gr_score_topk_f32: h / table not 16-byte aligned");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (rows == 0) {   // nothing to rank: every entry is padding
-    if (counts_out && hipMemsetAsync(counts_out, 0, (size_t)B * sizeof(int64_t), st) != hipSuccess)
+    if (counts_out && gr_fill32_launch(counts_out, 0u, B * 2, st) != GR_OK)
       return fail(GR_ERR_HIP, "gr_score_topk_f32: memset failed");
-    if (hipMemsetAsync(ids_out, 0xff, (size_t)B * k * sizeof(int64_t), st) != hipSuccess)
+    if (gr_fill32_launch(ids_out, 0xffffffffu, B * k * 2, st) != GR_OK)
       return fail(GR_ERR_HIP, "gr_score_topk_f32: memset failed");
     const float ninf = -INFINITY;
     uint32_t bits;
     memcpy(&bits, &ninf, 4);
-    if (hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(vals_out), (int)bits, (size_t)B * k, st) != hipSuccess)
+    if (gr_fill32_launch(vals_out, bits, B * k, st) != GR_OK)
       return fail(GR_ERR_HIP, "gr_score_topk_f32: memset failed");
     return GR_OK;
   }
@@ -684,7 +684,7 @@ extern "C" int gr_score_topk_f32(const float* h, int64_t B, int32_t d, const flo
   const TopkWs wl = topk_ws(B, p, k);
   // the strict counts start at zero: the sample pass clears them when there is one (no launch of
   // its own), a memset otherwise
-  if (counts_out && !p.s && hipMemsetAsync(counts_out, 0, (size_t)B * sizeof(int64_t), st) != hipSuccess)
+  if (counts_out && !p.s && gr_fill32_launch(counts_out, 0u, B * 2, st) != GR_OK)
     return fail(GR_ERR_HIP, "gr_score_topk_f32: memset failed");
   if (!workspace || workspace_bytes < wl.total)
     return fail(GR_ERR_WORKSPACE, "gr_score_topk_f32: workspace too small (need " + std::to_string(wl.total) + " bytes)");

@@ -246,8 +246,8 @@ extern "C" int gr_sampled_bce_bwd_f32(const float* feats, int64_t B, int32_t n, 
   if (rc) return rc;
   if (!dtable || !grad_scale) return fail(GR_ERR_ARG, "gr_sampled_bce_bwd_f32: null dtable / grad_scale");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  if (hipMemsetAsync(dtable, 0, (size_t)rows * d * sizeof(float), st) != hipSuccess)
-    return fail(GR_ERR_HIP, "gr_sampled_bce_bwd_f32: memset failed");
+  rc = gr_fill32_launch(dtable, 0u, rows * (int64_t)d, st);   // dM = 0 (a kernel: see fill.hip)
+  if (rc) return rc;
   const int64_t P = B * n;
   if (P == 0) return GR_OK;
   if (!coef || !dfeats) return fail(GR_ERR_ARG, "gr_sampled_bce_bwd_f32: null coef / dfeats");

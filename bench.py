@@ -476,10 +476,12 @@ def sas_step_flop_per_user(d, n, mlp=64, blocks=2, J=10):
 def bench_sas_train_step(a, world, rank, dev):
     """SURVEY §8(f) row 4, the whole SASRec training step (SASRec/train.py:131-173) at the
     reference's training batch (main.py: batch 128, dropout 0.2, Adam lr 1e-3 betas (0.9, 0.98),
-    10 negatives) on C3 shapes (d 64, n 50, 100k items): the drop-in transformer under autograd
-    (dropout on), GPU negatives, the fused sampled BCE, backward and the Adam step, captured as one
-    graph (ops.SasTrainGraph) -- next to the same step issued eagerly and the reference's own
-    formulation ([B, n, N+1] score matrix) eagerly on the same GPU."""
+    10 negatives) on C3 shapes (d 64, n 50, 100k items): the transformer forward + backward on the
+    fused training kernels (dropout on), GPU negatives, the fused sampled BCE, the weight-gradient
+    GEMMs and the Adam step, captured as one graph (ops.SasTrainGraph) -- next to the same step
+    issued eagerly, the same captured step with the transformer under torch autograd
+    (module by module, SASRec.fused_train = False), and the reference's own formulation
+    ([B, n, N+1] score matrix, torch modules) eagerly on the same GPU."""
     B, n, d, items, J = a.train_batch, 50, 64, 100_000, 10
     prm = synth.sasrec_params(d, n, 2, 1, 64, dev)
     g = torch.Generator(device=dev).manual_seed(4000 + rank)
@@ -489,13 +491,15 @@ def bench_sas_train_step(a, world, rank, dev):
     inputs = torch.roll(targets, 1, dims=1)
     inputs[:, 0] = 0
 
-    def make(capturable):
+    def make(capturable, fused=True):
         m = synth.sasrec_model(items, prm, dev, seed=11).train()   # dropout 0.2 (main.py)
+        m.fused_train = fused
         return m, torch.optim.Adam(m.parameters(), lr=1e-3, betas=(0.9, 0.98), capturable=capturable)
 
     m1, o1 = make(True)
     gstep = ops.SasTrainGraph(m1, o1, inputs, targets, items, J, 1e-24, seed=5000 + rank)
     wall, dev_ms = timed(gstep.replay, a.steps, a.warmup, world)
+    del gstep, m1, o1
     m2, o2 = make(False)
 
     def eager():   # the same step op by op
@@ -506,38 +510,48 @@ def bench_sas_train_step(a, world, rank, dev):
         (bl / valid.clamp(min=1.0)).backward()
         o2.step()
     e_wall, _ = timed(eager, a.steps, a.warmup, world)
+    m4, o4 = make(True, fused=False)
+    mstep = ops.SasTrainGraph(m4, o4, inputs, targets, items, J, 1e-24, seed=6000 + rank)
+    ma_ms = kernel_ms(mstep.replay, reps=20)
+    del mstep, m4, o4
+    m3, o3 = make(False, fused=False)
     negs = ops.neg_samples(inputs, items, J)
 
-    def reference():   # train.py:131-173 as written (score matrix), negatives precomputed
-        o2.zero_grad()
-        h = m2(inputs)
-        sm = torch.matmul(h, m2.item_emb.weight.t())
+    def reference():   # train.py:131-173 as written (score matrix, torch modules), negatives precomputed
+        o3.zero_grad()
+        h = m3(inputs)
+        sm = torch.matmul(h, m3.item_emb.weight.t())
         mask = (targets != 0).float()
         ps = torch.gather(sm, 2, targets.unsqueeze(-1)).squeeze(-1)
         ns = torch.gather(sm, 2, negs.unsqueeze(1).expand(-1, n, -1))
         pl = -torch.log(torch.sigmoid(ps) + 1e-24) * mask
         nl = (-torch.log(1 - torch.sigmoid(ns) + 1e-24) * mask.unsqueeze(-1)).sum(-1)
         ((pl + nl).sum() / mask.sum()).backward()
-        o2.step()
+        o3.step()
     r_ms = kernel_ms(reference, reps=10)
     fl = sas_step_flop_per_user(d, n, 64, 2, J) * B
+    step_ms = wall / a.steps * 1e3
     res = {"metric": "train_steps_seqs/s", "value": B * world * a.steps / wall, "unit": "seqs/s",
-           "ms_per_step": wall / a.steps * 1e3, "scaling": "weak",
+           "ms_per_step": step_ms, "scaling": "weak",
            "config": {"workload": f"sas_train_step: SASRec train.py:131-173 whole step (transformer forward "
-                                  f"+ backward with dropout 0.2, {J} GPU negatives, fused sampled BCE, Adam), "
-                                  f"B {B}, n {n}, d {d}, {items}-item table, one captured graph",
+                                  f"+ backward with dropout 0.2 on the fused training kernels, {J} GPU negatives, "
+                                  f"fused sampled BCE, weight-gradient GEMMs, Adam), B {B}, n {n}, d {d}, "
+                                  f"{items}-item table, one captured graph",
                       "users_per_rank_per_step": B, "parallelism": f"user-sharded x{world} (data parallel "
                                                                    f"without the gradient all-reduce)"},
            "roofline": {"bound": "mfma", "achieved": fl / (dev_ms * 1e-3) / 1e12, "peak": FP32_PEAK_TFLOPS,
                         "unit": "TFLOP/s", "frac": fl / (dev_ms * 1e-3) / 1e12 / FP32_PEAK_TFLOPS,
-                        "traffic": None, "kernel": "whole step (latency-bound: ~150 small kernels in one graph)",
+                        "traffic": None, "kernel": "whole step (latency-bound: 128 one-sequence workgroups)",
                         "flop_per_step": fl, "step_device_ms": dev_ms},
            "eager": {"note": "the same step issued op by op", "value": B * world * a.steps / e_wall,
                      "ms_per_step": e_wall / a.steps * 1e3},
-           "reference_formulation_gpu": {"note": "train.py:131-173 as written ([B, n, N+1] score matrix) in "
-                                                 "torch on the same GPU, negatives precomputed (the reference "
+           "captured_module_autograd": {"note": "the same captured step with the transformer under torch "
+                                                "autograd, module by module (SASRec.fused_train = False)",
+                                        "ms_per_step": ma_ms, "speedup": ma_ms / step_ms},
+           "reference_formulation_gpu": {"note": "train.py:131-173 as written ([B, n, N+1] score matrix, torch "
+                                                 "modules) on the same GPU, negatives precomputed (the reference "
                                                  "draws them on the host)",
-                                         "ms_per_step": r_ms, "speedup": r_ms / (wall / a.steps * 1e3)}}
+                                         "ms_per_step": r_ms, "speedup": r_ms / step_ms}}
     return res
 
 
