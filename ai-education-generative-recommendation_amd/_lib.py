@@ -40,8 +40,7 @@ class SasrecParams(ctypes.Structure):
 
 class SasrecTrainBufs(ctypes.Structure):
     """Mirror of ``gr_sasrec_train_bufs`` (include/gr_amd.h)."""
-    _fields_ = [(f, _vp) for f in ("xin", "hs", "qkv", "prob", "os", "x1", "fs", "zs", "us", "xl",
-                                   "g_qkv", "g_out", "g_z", "g_y", "g_vec")]
+    _fields_ = [(f, _vp) for f in ("xin", "hs", "qkv", "prob", "os", "x1", "fs", "zs", "us", "xl", "g_vec")]
 
 
 # (name, restype, argtypes) for every entry point of include/gr_amd.h

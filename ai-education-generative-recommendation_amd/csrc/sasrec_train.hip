@@ -6,14 +6,13 @@
 // (nn.MultiheadAttention, LayerNorm, Linear, ReLU, Dropout, the embedding's sort-based backward).
 // Here the forward is one launch and the backward one launch.  Everything a sequence touches
 // (n <= 64 rows of d <= 64 features, the n x n attention of each head) lives in LDS; products are
-// fp32 fma chains over LDS / L2-resident operands (4 x 4 outputs per thread).  The forward saves
+// fp32 products on the matrix cores over LDS / L2-resident operands.  The forward saves
 // what the backward needs (per block: LN_a input and output, Q|K|V, the softmax probabilities, the
 // attention output, the attention residual, LN_f output, FFN1 pre-activation and its dropped-out
-// ReLU).  Weight gradients are contractions over all B*n rows: the backward writes the per-row
-// output gradients (dQKV, dOut, dZ, dY) next to the saved inputs (H, O, F, U), and the host forms
-// dW = dG^T A with library GEMMs; bias / LayerNorm / positional gradients leave the kernel as
-// per-sequence partial sums (one [B, V] buffer, summed over B by the host); item-embedding rows
-// are scattered with atomics (padding row 0 excluded: nn.Embedding(padding_idx=0)).
+// ReLU).  Every parameter gradient but the item table's leaves the backward as a per-sequence
+// partial (dW = dG^T A over the sequence's n rows, bias / LayerNorm column sums, positional rows),
+// laid out in the parameters' order in one [B, V] buffer that the host sums over B; item-embedding
+// rows are scattered with atomics (padding row 0 excluded: nn.Embedding(padding_idx=0)).
 //
 // Dropout (p = params['dropout']) keeps an element when a counter-based hash of (seed, sequence,
 // site, element) is >= p and scales it by 1 / (1 - p), as torch's dropout does (its random stream
@@ -25,7 +24,7 @@
 namespace gr {
 namespace st {
 
-constexpr int NT = 256;     // threads per workgroup (4 waves)
+constexpr int NT = 512;     // threads per workgroup (8 waves, 2 per SIMD)
 constexpr int MAXB = 8;     // transformer blocks
 constexpr int NMAX = 64, DMAX = 64, MMAX = 128;
 
@@ -75,74 +74,77 @@ __device__ __forceinline__ float wave_max(float v) {
 }
 
 // C[r][c] (r < R, c < Cn) = (ACC ? C : 0) + (sum_k A(r,k) B(k,c) + bias[c]) * post
-// with A(r,k) = A[r*sar + k*sak], B(k,c) = Bm[k*sbk + c*sbc]; operands in LDS or global memory.
-// Each thread owns 4 x 4 outputs; k runs in increasing order (one fma chain per output).
+// with A(r,k) = A[r*sar + k*sak], B(k,c) = Bm[k*sbk + c*sbc]; operands in LDS or global memory,
+// C in LDS or global memory.  32 x 32 output tiles on the matrix cores (v_mfma_f32_32x32x2_f32),
+// the workgroup's 4 waves taking tiles round-robin; k in pairs (lane half h feeds k0 + h), loads
+// for 16 k issued ahead of their 8 MFMAs.
 template <bool ACC>
 __device__ __forceinline__ void mm(float* C, int ldc, const float* A, int sar, int sak, const float* Bm,
                                    int sbk, int sbc, int R, int Cn, int K, const float* bias = nullptr,
                                    float post = 1.f) {
-  const int trn = (R + 3) >> 2, tcn = (Cn + 3) >> 2;
-  for (int t = threadIdx.x; t < trn * tcn; t += NT) {
-    const int r0 = (t / tcn) * 4, c0 = (t % tcn) * 4;
-    int ra[4], cb[4];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, i32 = lane & 31, h = lane >> 5;
+  const int trn = (R + 31) >> 5, tcn = (Cn + 31) >> 5;
+  for (int t = wv; t < trn * tcn; t += NT / 64) {
+    const int tr = t / tcn, tc = t - tr * tcn;
+    const float* ap = A + min(tr * 32 + i32, R - 1) * sar;
+    const float* bp = Bm + min(tc * 32 + i32, Cn - 1) * sbc;
+    f32x16 acc;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      ra[i] = min(r0 + i, R - 1) * sar;
-      cb[i] = min(c0 + i, Cn - 1) * sbc;
+    for (int v = 0; v < 16; ++v) acc[v] = 0.f;
+    int k0 = 0;
+    for (; k0 + 16 <= K; k0 += 16) {
+      float av[8], bv[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int k = k0 + 2 * j + h;
+        av[j] = ap[k * sak];
+        bv[j] = bp[k * sbk];
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc = mfma32(av[j], bv[j], acc);
     }
-    float acc[4][4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = 0.f;
-    for (int k = 0; k < K; ++k) {
-      float av[4], bv[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) av[i] = A[ra[i] + k * sak];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) bv[j] = Bm[k * sbk + cb[j]];
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = fmaf(av[i], bv[j], acc[i][j]);
+    for (; k0 < K; k0 += 2) {
+      const int k = k0 + h, kc = min(k, K - 1);
+      const float av = ap[kc * sak], bv = bp[kc * sbk];
+      acc = mfma32(k < K ? av : 0.f, k < K ? bv : 0.f, acc);
     }
+    const int col = tc * 32 + i32;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      if (r0 + i >= R) continue;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        if (c0 + j >= Cn) continue;
-        float v = acc[i][j];
-        if (bias) v += bias[c0 + j];
-        v *= post;
-        float* o = C + (r0 + i) * ldc + c0 + j;
-        *o = ACC ? *o + v : v;
+    for (int v = 0; v < 16; ++v) {
+      const int row = tr * 32 + (v & 3) + 8 * (v >> 2) + 4 * h;
+      if (row < R && col < Cn) {
+        float x = acc[v];
+        if (bias) x += bias[col];
+        x *= post;
+        float* o = C + row * ldc + col;
+        *o = ACC ? *o + x : x;
       }
     }
   }
 }
 
-// LayerNorm of the n rows of X (row stride d) into Y (one wave per row, lane = feature, d <= 64);
-// torch's formula: biased variance, (x - mean) * rsqrt(var + eps) * w + b.
-__device__ __forceinline__ void ln_rows(const float* X, float* Y, const float* w, const float* bb, int n,
-                                        int d, float eps) {
+// LayerNorm of the n rows of X (row pitch px) into Y (pitch py): one wave per row, lane = feature
+// (d <= 64); torch's formula: biased variance, (x - mean) * rsqrt(var + eps) * w + b.
+__device__ __forceinline__ void ln_rows(const float* X, int px, float* Y, int py, const float* w,
+                                        const float* bb, int n, int d, float eps) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const bool on = lane < d;
   const float inv_d = 1.f / (float)d;
   for (int i = wv; i < n; i += NT / 64) {
-    const float x = on ? X[i * d + lane] : 0.f;
+    const float x = on ? X[i * px + lane] : 0.f;
     const float mean = wave_sum(x) * inv_d;
     const float t = on ? x - mean : 0.f;
     const float rstd = rsqrtf(wave_sum(t * t) * inv_d + eps);
-    if (on) Y[i * d + lane] = (x - mean) * rstd * w[lane] + bb[lane];
+    if (on) Y[i * py + lane] = (x - mean) * rstd * w[lane] + bb[lane];
   }
 }
 
-// LayerNorm backward over the n rows: DX[i] += dLN/dx (dy = DY[i], x = X[i] from global / LDS);
-// the sequence's partial dgamma / dbeta (sums over its rows) go to gw[f] / gb[f].  red: NT floats
-// of LDS scratch for the cross-wave sum.
-__device__ __forceinline__ void ln_back(const float* X, const float* DY, float* DX, const float* w, int n,
-                                        int d, float eps, float* gw, float* gb, float* red) {
+// LayerNorm backward over the n rows: DX[i] += dLN/dx (dy = DY[i] (pitch pdy), x = X[i] from global,
+// row stride d); the sequence's partial dgamma / dbeta (sums over its rows) go to gw[f] / gb[f].
+// red: NT floats of LDS scratch for the cross-wave sums.
+__device__ __forceinline__ void ln_back(const float* X, const float* DY, int pdy, float* DX, int pdx,
+                                        const float* w, int n, int d, float eps, float* gw, float* gb,
+                                        float* red) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const bool on = lane < d;
   const float inv_d = 1.f / (float)d;
@@ -153,28 +155,50 @@ __device__ __forceinline__ void ln_back(const float* X, const float* DY, float* 
     const float t = on ? x - mean : 0.f;
     const float rstd = rsqrtf(wave_sum(t * t) * inv_d + eps);
     const float xh = t * rstd;
-    const float dy = on ? DY[i * d + lane] : 0.f;
+    const float dy = on ? DY[i * pdy + lane] : 0.f;
     const float dxh = on ? dy * w[lane] : 0.f;
     const float s1 = wave_sum(dxh), s2 = wave_sum(dxh * xh);
-    if (on) DX[i * d + lane] += rstd * (dxh - s1 * inv_d - xh * (s2 * inv_d));
+    if (on) DX[i * pdx + lane] += rstd * (dxh - s1 * inv_d - xh * (s2 * inv_d));
     pw = fmaf(dy, xh, pw);
     pb += dy;
   }
   red[threadIdx.x] = pw;
   __syncthreads();
-  if (threadIdx.x < d) gw[threadIdx.x] = red[threadIdx.x] + red[64 + threadIdx.x] + red[128 + threadIdx.x] + red[192 + threadIdx.x];
+  if (threadIdx.x < d) {
+    float sw = 0.f;
+    for (int q = 0; q < NT / 64; ++q) sw += red[q * 64 + threadIdx.x];
+    gw[threadIdx.x] = sw;
+  }
   __syncthreads();
   red[threadIdx.x] = pb;
   __syncthreads();
-  if (threadIdx.x < d) gb[threadIdx.x] = red[threadIdx.x] + red[64 + threadIdx.x] + red[128 + threadIdx.x] + red[192 + threadIdx.x];
+  if (threadIdx.x < d) {
+    float sb = 0.f;
+    for (int q = 0; q < NT / 64; ++q) sb += red[q * 64 + threadIdx.x];
+    gb[threadIdx.x] = sb;
+  }
   __syncthreads();
 }
 
-__device__ __forceinline__ void copy_out(float* dst, const float* src, int count) {
-  for (int i = threadIdx.x; i < count; i += NT) dst[i] = src[i];
+// dst[i*w + c] = src[i*ps + c] (LDS, pitch ps -> global, packed rows of w)
+__device__ __forceinline__ void copy_out(float* dst, const float* src, int ps, int n, int w) {
+  for (int idx = threadIdx.x; idx < n * w; idx += NT) {
+    const int i = idx / w, c = idx - i * w;
+    dst[idx] = src[i * ps + c];
+  }
 }
 
-// column sums of an [n x w] LDS matrix (row stride ld) into dst[w] (the sequence's bias gradient)
+// Wt[k][c] = W[c][k] (W: [N, K] row-major in global memory, an nn.Linear weight; Wt: LDS, row pitch
+// pt): coalesced global reads once per stage, so the forward products read their B operand
+// k-major and conflict-free from LDS instead of 32 strided rows from L2.
+__device__ __forceinline__ void stage_t(float* Wt, int pt, const float* W, int N, int K) {
+  for (int idx = threadIdx.x; idx < N * K; idx += NT) {
+    const int c = idx / K, k = idx - c * K;
+    Wt[k * pt + c] = W[idx];
+  }
+}
+
+// column sums of an [n x w] LDS matrix (pitch ld) into dst[w] (the sequence's bias gradient)
 __device__ __forceinline__ void col_sums(float* dst, const float* M, int ld, int n, int w) {
   for (int c = threadIdx.x; c < w; c += NT) {
     float s = 0.f;
@@ -198,21 +222,42 @@ __device__ __forceinline__ Offs offs(const Args& a, int bk, int64_t b) {
   return o;
 }
 
-// g_vec layout per sequence: for each block [ln_a w, ln_a b, b_in (3d), b_o, ln_f w, ln_f b, b1 (m), b2],
-// then [last ln w, last ln b], then pos (n x d).
-__device__ __forceinline__ int vblk(const Args& a) { return 9 * a.d + a.mlp; }
+// g_vec per sequence, in the order of SASRec's parameters: per block [ln_a w, ln_a b, in_proj w
+// (3d x d), in_proj b (3d), out_proj w (d x d), out_proj b, ln_f w, ln_f b, ffn1 w (mlp x d),
+// ffn1 b (mlp), ffn2 w (d x mlp), ffn2 b], then [last ln w, last ln b], then pos (n x d).
+struct VOff {
+  int law, lab, inw, inb, ow, ob, lfw, lfb, w1, b1, w2, b2, size;
+};
+__host__ __device__ __forceinline__ VOff voff(int d, int m) {
+  VOff v;
+  v.law = 0;
+  v.lab = d;
+  v.inw = 2 * d;
+  v.inb = v.inw + 3 * d * d;
+  v.ow = v.inb + 3 * d;
+  v.ob = v.ow + d * d;
+  v.lfw = v.ob + d;
+  v.lfb = v.lfw + d;
+  v.w1 = v.lfb + d;
+  v.b1 = v.w1 + m * d;
+  v.w2 = v.b1 + m;
+  v.b2 = v.w2 + d * m;
+  v.size = v.b2 + d;
+  return v;
+}
 
 __global__ __launch_bounds__(NT) void sas_train_fwd_kernel(const Args a, const int64_t* __restrict__ seqs,
                                                            float* __restrict__ out, int32_t* err) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int n = a.n, d = a.d, m = a.mlp, H = a.heads, hd = d / H, d3 = 3 * d;
+  const int pd = d + 1, pw = (d3 > m ? d3 : m) + 1, pn = n + 1;   // odd LDS pitches: conflict-free columns
   const int64_t b = blockIdx.x;
   const uint64_t seed = a.seed_dev ? a.seed0 ^ *a.seed_dev : a.seed0;
-  float* X = sm;                       // [n][d] residual stream
-  float* Hb = X + n * d;               // [n][d] LayerNorm output / FFN2 output
-  float* BIG = Hb + n * d;             // [n][max(3d, m)] Q|K|V, then FFN hidden
-  float* S = BIG + n * max(d3, m);     // [n][n] one head's scores / probabilities
-  float* Ob = S + n * n;               // [n][d] attention output
+  float* X = sm;                       // [n][pd] residual stream
+  float* Hb = X + n * pd;              // [n][pd] LN output / attention output / FFN2 output
+  float* BIG = Hb + n * pd;            // [n][pw] Q|K|V, then the FFN hidden layer
+  float* S = BIG + n * pw;             // [n][pn] one head's scores / probabilities
+  float* Wt = S + n * pn;              // the current weight, transposed: [K][N + 1]
   const gr_sasrec_train_bufs& g = a.buf;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
 
@@ -224,66 +269,74 @@ __global__ __launch_bounds__(NT) void sas_train_fwd_kernel(const Args a, const i
       if (err) *err = 1;
       s = 0;
     }
-    X[idx] = a.item[s * d + f] + a.pos[i * d + f];
+    X[i * pd + f] = a.item[s * d + f] + a.pos[i * d + f];
   }
   __syncthreads();
   for (int bk = 0; bk < a.nb; ++bk) {
     const Blk& p = a.blk[bk];
     const Offs o = offs(a, bk, b);
-    copy_out(g.xin + o.rd, X, n * d);
-    ln_rows(X, Hb, p.ln_a_w, p.ln_a_b, n, d, a.eps);                               // model.py:80
+    copy_out(g.xin + o.rd, X, pd, n, d);
+    ln_rows(X, pd, Hb, pd, p.ln_a_w, p.ln_a_b, n, d, a.eps);                        // model.py:80
+    stage_t(Wt, d3 + 1, p.w_in, d3, d);
     __syncthreads();
-    copy_out(g.hs + o.rd, Hb, n * d);
-    mm<false>(BIG, d3, Hb, d, 1, p.w_in, 1, d, n, d3, d, p.b_in);                  // in_proj: q|k|v
+    copy_out(g.hs + o.rd, Hb, pd, n, d);
+    mm<false>(BIG, pw, Hb, pd, 1, Wt, d3 + 1, 1, n, d3, d, p.b_in);                 // in_proj: q|k|v
     __syncthreads();
-    copy_out(g.qkv + o.r3, BIG, n * d3);
+    copy_out(g.qkv + o.r3, BIG, pw, n, d3);
     __syncthreads();
     for (int idx = tid; idx < n * d; idx += NT) {                                  // q * head_dim^-0.5
       const int i = idx / d, f = idx - i * d;
-      BIG[i * d3 + f] *= a.q_scale;
+      BIG[i * pw + f] *= a.q_scale;
     }
+    stage_t(Wt, d + 1, p.w_o, d, d);
     __syncthreads();
     for (int hh = 0; hh < H; ++hh) {
-      mm<false>(S, n, BIG + hh * hd, d3, 1, BIG + d + hh * hd, 1, d3, n, n, hd);   // (q s) k^T
+      mm<false>(S, pn, BIG + hh * hd, pw, 1, BIG + d + hh * hd, 1, pw, n, n, hd);   // (q s) k^T
       __syncthreads();
       for (int i = wv; i < n; i += NT / 64) {                                      // causal softmax
         const bool on = lane <= i && lane < n;
-        const float sv = on ? S[i * n + lane] : -__builtin_inff();
+        const float sv = on ? S[i * pn + lane] : -__builtin_inff();
         const float mx = wave_max(sv);
         const float e = on ? __expf(sv - mx) : 0.f;
         const float pr = e / wave_sum(e);
         if (lane < n) {
           g.prob[o.pp + ((int64_t)hh * n + i) * n + lane] = pr;
-          S[i * n + lane] = pr * keep(a, seed, b, 3 * bk, (uint32_t)((hh * n + i) * n + lane));
+          S[i * pn + lane] = pr * keep(a, seed, b, 3 * bk, (uint32_t)((hh * n + i) * n + lane));
         }
       }
       __syncthreads();
-      mm<false>(Ob + hh * hd, d, S, n, 1, BIG + 2 * d + hh * hd, d3, 1, n, hd, n);  // P' v
+      mm<false>(Hb + hh * hd, pd, S, pn, 1, BIG + 2 * d + hh * hd, pw, 1, n, hd, n);  // O = P' v
       __syncthreads();
     }
-    copy_out(g.os + o.rd, Ob, n * d);
-    mm<true>(X, d, Ob, d, 1, p.w_o, 1, d, n, d, d, p.b_o);                         // x + out_proj (model.py:84)
+    copy_out(g.os + o.rd, Hb, pd, n, d);
+    mm<true>(X, pd, Hb, pd, 1, Wt, d + 1, 1, n, d, d, p.b_o);                      // x + out_proj (model.py:84)
     __syncthreads();
-    copy_out(g.x1 + o.rd, X, n * d);
-    ln_rows(X, Hb, p.ln_f_w, p.ln_f_b, n, d, a.eps);                               // model.py:92
+    copy_out(g.x1 + o.rd, X, pd, n, d);
+    ln_rows(X, pd, Hb, pd, p.ln_f_w, p.ln_f_b, n, d, a.eps);                        // model.py:92
+    stage_t(Wt, m + 1, p.w1, m, d);
     __syncthreads();
-    copy_out(g.fs + o.rd, Hb, n * d);
-    mm<false>(BIG, m, Hb, d, 1, p.w1, 1, d, n, m, d, p.b1);                        // FFN1
+    copy_out(g.fs + o.rd, Hb, pd, n, d);
+    mm<false>(BIG, pw, Hb, pd, 1, Wt, m + 1, 1, n, m, d, p.b1);                     // FFN1
     __syncthreads();
-    copy_out(g.zs + o.rm, BIG, n * m);
+    copy_out(g.zs + o.rm, BIG, pw, n, m);
+    stage_t(Wt, d + 1, p.w2, d, m);
     __syncthreads();
-    for (int idx = tid; idx < n * m; idx += NT)                                    // dropout(relu)
-      BIG[idx] = fmaxf(BIG[idx], 0.f) * keep(a, seed, b, 3 * bk + 1, (uint32_t)idx);
+    for (int idx = tid; idx < n * m; idx += NT) {                                  // dropout(relu)
+      const int i = idx / m, c = idx - i * m;
+      BIG[i * pw + c] = fmaxf(BIG[i * pw + c], 0.f) * keep(a, seed, b, 3 * bk + 1, (uint32_t)idx);
+    }
     __syncthreads();
-    copy_out(g.us + o.rm, BIG, n * m);
-    mm<false>(Hb, d, BIG, m, 1, p.w2, 1, m, n, d, m, p.b2);                        // FFN2
+    copy_out(g.us + o.rm, BIG, pw, n, m);
+    mm<false>(Hb, pd, BIG, pw, 1, Wt, d + 1, 1, n, d, m, p.b2);                     // FFN2
     __syncthreads();
-    for (int idx = tid; idx < n * d; idx += NT)                                    // x + dropout(y) (model.py:94)
-      X[idx] += Hb[idx] * keep(a, seed, b, 3 * bk + 2, (uint32_t)idx);
+    for (int idx = tid; idx < n * d; idx += NT) {                                  // x + dropout(y) (model.py:94)
+      const int i = idx / d, f = idx - i * d;
+      X[i * pd + f] += Hb[i * pd + f] * keep(a, seed, b, 3 * bk + 2, (uint32_t)idx);
+    }
     __syncthreads();
   }
-  copy_out(g.xl + b * n * d, X, n * d);
-  ln_rows(X, out + b * n * d, a.ln_w, a.ln_b, n, d, a.eps);                        // model.py:96
+  copy_out(g.xl + b * n * d, X, pd, n, d);
+  ln_rows(X, pd, out + b * n * d, d, a.ln_w, a.ln_b, n, d, a.eps);                  // model.py:96
 }
 
 __global__ __launch_bounds__(NT) void sas_train_bwd_kernel(const Args a, const int64_t* __restrict__ seqs,
@@ -291,79 +344,93 @@ __global__ __launch_bounds__(NT) void sas_train_bwd_kernel(const Args a, const i
                                                            float* __restrict__ g_item) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int n = a.n, d = a.d, m = a.mlp, H = a.heads, hd = d / H, d3 = 3 * d;
+  const int pd = d + 1, pw = (d3 > m ? d3 : m) + 1, pn = n + 1;
   const int64_t b = blockIdx.x;
   const uint64_t seed = a.seed_dev ? a.seed0 ^ *a.seed_dev : a.seed0;
-  float* DX = sm;                      // [n][d] gradient of the residual stream
-  float* T = DX + n * d;               // [n][d] dY, df, dO, dh
-  float* G1 = T + n * d;               // [n][max(3d, m)] dU / dZ, then dQ|dK|dV
-  float* PS = G1 + n * max(d3, m);     // [n][n] dP', then dP and dS
-  float* DS = PS + n * n;              // [n][n] dropped-out probabilities P'
-  float* red = DS + n * n;             // [NT] reduction scratch
+  float* DX = sm;                      // [n][pd] gradient of the residual stream
+  float* T = DX + n * pd;              // [n][pd] dY, df, dO, dh
+  float* G1 = T + n * pd;              // [n][pw] dU / dZ, then dQ|dK|dV
+  float* PS = G1 + n * pw;             // [n][pn] P', then dP', then dS
+  float* red = PS + n * pn;            // [NT] reduction scratch
   const gr_sasrec_train_bufs& g = a.buf;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const VOff vo = voff(d, m);
   float* gv = g.g_vec + b * a.vwidth;
+  float* glast = gv + a.nb * vo.size;
 
   // last LayerNorm (model.py:96)
-  copy_out(T, dF + b * n * d, n * d);
-  for (int i = tid; i < n * d; i += NT) DX[i] = 0.f;
+  for (int idx = tid; idx < n * d; idx += NT) {
+    const int i = idx / d, f = idx - i * d;
+    T[i * pd + f] = dF[b * n * d + idx];
+    DX[i * pd + f] = 0.f;
+  }
   __syncthreads();
-  ln_back(g.xl + b * n * d, T, DX, a.ln_w, n, d, a.eps, gv + a.nb * vblk(a), gv + a.nb * vblk(a) + d, red);
+  ln_back(g.xl + b * n * d, T, pd, DX, pd, a.ln_w, n, d, a.eps, glast, glast + d, red);
   for (int bk = a.nb - 1; bk >= 0; --bk) {
     const Blk& p = a.blk[bk];
     const Offs o = offs(a, bk, b);
-    float* gvb = gv + bk * vblk(a);   // ln_a w | ln_a b | b_in | b_o | ln_f w | ln_f b | b1 | b2
-    // FFN output: x2 = x1 + dropout(y)
-    for (int idx = tid; idx < n * d; idx += NT) T[idx] = DX[idx] * keep(a, seed, b, 3 * bk + 2, (uint32_t)idx);
+    float* gvb = gv + bk * vo.size;
+    // FFN output: x2 = x1 + dropout(y), y = u W2^T + b2
+    for (int idx = tid; idx < n * d; idx += NT) {
+      const int i = idx / d, f = idx - i * d;
+      T[i * pd + f] = DX[i * pd + f] * keep(a, seed, b, 3 * bk + 2, (uint32_t)idx);
+    }
     __syncthreads();
-    copy_out(g.g_y + o.rd, T, n * d);
-    col_sums(gvb + 8 * d + m, T, d, n, d);                                          // db2
-    mm<false>(G1, m, T, d, 1, p.w2, m, 1, n, m, d);                                 // dU = dY W2
+    col_sums(gvb + vo.b2, T, pd, n, d);                                              // db2
+    mm<false>(gvb + vo.w2, m, T, 1, pd, g.us + o.rm, m, 1, d, m, n);                 // dW2 = dY^T u
+    mm<false>(G1, pw, T, pd, 1, p.w2, m, 1, n, m, d);                                // dU = dY W2
     __syncthreads();
-    for (int idx = tid; idx < n * m; idx += NT)                                     // through dropout and relu
-      G1[idx] = g.zs[o.rm + idx] > 0.f ? G1[idx] * keep(a, seed, b, 3 * bk + 1, (uint32_t)idx) : 0.f;
+    for (int idx = tid; idx < n * m; idx += NT) {                                   // through dropout and relu
+      const int i = idx / m, c = idx - i * m;
+      G1[i * pw + c] = g.zs[o.rm + idx] > 0.f ? G1[i * pw + c] * keep(a, seed, b, 3 * bk + 1, (uint32_t)idx) : 0.f;
+    }
     __syncthreads();
-    copy_out(g.g_z + o.rm, G1, n * m);
-    col_sums(gvb + 8 * d, G1, m, n, m);                                             // db1
-    mm<false>(T, d, G1, m, 1, p.w1, d, 1, n, d, m);                                 // df = dZ W1
+    col_sums(gvb + vo.b1, G1, pw, n, m);                                             // db1
+    mm<false>(gvb + vo.w1, d, G1, 1, pw, g.fs + o.rd, d, 1, m, d, n);                // dW1 = dZ^T f
+    mm<false>(T, pd, G1, pw, 1, p.w1, d, 1, n, d, m);                                // df = dZ W1
     __syncthreads();
-    ln_back(g.x1 + o.rd, T, DX, p.ln_f_w, n, d, a.eps, gvb + 6 * d, gvb + 7 * d, red);   // LN_f
+    ln_back(g.x1 + o.rd, T, pd, DX, pd, p.ln_f_w, n, d, a.eps, gvb + vo.lfw, gvb + vo.lfb, red);   // LN_f
     // attention block output: x1 = x + out_proj(O)
-    copy_out(g.g_out + o.rd, DX, n * d);
-    col_sums(gvb + 5 * d, DX, d, n, d);                                             // db_o
-    mm<false>(T, d, DX, d, 1, p.w_o, d, 1, n, d, d);                                // dO = dOut W_o
+    col_sums(gvb + vo.ob, DX, pd, n, d);                                             // db_o
+    mm<false>(gvb + vo.ow, d, DX, 1, pd, g.os + o.rd, d, 1, d, d, n);                // dW_o = dOut^T O
+    mm<false>(T, pd, DX, pd, 1, p.w_o, d, 1, n, d, d);                               // dO = dOut W_o
     __syncthreads();
     const float* Q = g.qkv + o.r3;
     for (int hh = 0; hh < H; ++hh) {
       const float* P = g.prob + o.pp + (int64_t)hh * n * n;
-      for (int idx = tid; idx < n * n; idx += NT)
-        DS[idx] = P[idx] * keep(a, seed, b, 3 * bk, (uint32_t)(hh * n * n + idx));
-      mm<false>(PS, n, T + hh * hd, d, 1, Q + 2 * d + hh * hd, 1, d3, n, n, hd);   // dP' = dO v^T
+      for (int idx = tid; idx < n * n; idx += NT) {                                 // P' = P * keep
+        const int i = idx / n, j = idx - i * n;
+        PS[i * pn + j] = P[idx] * keep(a, seed, b, 3 * bk, (uint32_t)(hh * n * n + idx));
+      }
       __syncthreads();
-      mm<false>(G1 + 2 * d + hh * hd, d3, DS, 1, n, T + hh * hd, d, 1, n, hd, n);  // dV = P'^T dO
+      mm<false>(G1 + 2 * d + hh * hd, pw, PS, 1, pn, T + hh * hd, pd, 1, n, hd, n); // dV = P'^T dO
+      __syncthreads();
+      mm<false>(PS, pn, T + hh * hd, pd, 1, Q + 2 * d + hh * hd, 1, d3, n, n, hd);  // dP' = dO v^T
+      __syncthreads();
       for (int i = wv; i < n; i += NT / 64) {                                       // softmax backward
         const bool on = lane <= i && lane < n;
         const float pr = on ? P[i * n + lane] : 0.f;
-        const float dp = on ? PS[i * n + lane] * keep(a, seed, b, 3 * bk, (uint32_t)((hh * n + i) * n + lane)) : 0.f;
-        const float s = wave_sum(dp * pr);
-        if (lane < n) PS[i * n + lane] = on ? pr * (dp - s) : 0.f;
+        const float dp = on ? PS[i * pn + lane] * keep(a, seed, b, 3 * bk, (uint32_t)((hh * n + i) * n + lane)) : 0.f;
+        const float sdp = wave_sum(dp * pr);
+        if (lane < n) PS[i * pn + lane] = on ? pr * (dp - sdp) : 0.f;
       }
       __syncthreads();
-      mm<false>(G1 + hh * hd, d3, PS, n, 1, Q + d + hh * hd, d3, 1, n, hd, n, nullptr, a.q_scale);  // dQ
-      mm<false>(G1 + d + hh * hd, d3, PS, 1, n, Q + hh * hd, d3, 1, n, hd, n, nullptr, a.q_scale);  // dK
+      mm<false>(G1 + hh * hd, pw, PS, pn, 1, Q + d + hh * hd, d3, 1, n, hd, n, nullptr, a.q_scale);  // dQ
+      mm<false>(G1 + d + hh * hd, pw, PS, 1, pn, Q + hh * hd, d3, 1, n, hd, n, nullptr, a.q_scale);  // dK
       __syncthreads();
     }
-    copy_out(g.g_qkv + o.r3, G1, n * d3);
-    col_sums(gvb + 2 * d, G1, d3, n, d3);                                           // db_in
-    mm<false>(T, d, G1, d3, 1, p.w_in, d, 1, n, d, d3);                             // dh = dQKV W_in
+    col_sums(gvb + vo.inb, G1, pw, n, d3);                                           // db_in
+    mm<false>(gvb + vo.inw, d, G1, 1, pw, g.hs + o.rd, d, 1, d3, d, n);              // dW_in = dQKV^T h
+    mm<false>(T, pd, G1, pw, 1, p.w_in, d, 1, n, d, d3);                             // dh = dQKV W_in
     __syncthreads();
-    ln_back(g.xin + o.rd, T, DX, p.ln_a_w, n, d, a.eps, gvb, gvb + d, red);         // LN_a
+    ln_back(g.xin + o.rd, T, pd, DX, pd, p.ln_a_w, n, d, a.eps, gvb + vo.law, gvb + vo.lab, red);  // LN_a
   }
   // x0 = item_emb[s] + pos_emb[i]: rows of the item table by atomics (padding row 0 keeps a zero
   // gradient, nn.Embedding(padding_idx=0)); positions as this sequence's partial
-  float* gpos = gv + a.nb * vblk(a) + 2 * d;
+  float* gpos = glast + 2 * d;
   for (int idx = tid; idx < n * d; idx += NT) {
     const int i = idx / d, f = idx - i * d;
-    const float v = DX[idx];
+    const float v = DX[i * pd + f];
     gpos[idx] = v;
     const int64_t s = seqs[b * n + i];
     if (s > 0 && s < a.item_rows && g_item) atomicAdd(g_item + s * d + f, v);
@@ -371,10 +438,15 @@ __global__ __launch_bounds__(NT) void sas_train_bwd_kernel(const Args a, const i
 }
 
 static size_t fwd_lds(int n, int d, int m) {
-  return sizeof(float) * ((size_t)n * d * 3 + (size_t)n * (3 * d > m ? 3 * d : m) + (size_t)n * n);
+  const size_t pd = d + 1, pw = (3 * d > m ? 3 * d : m) + 1, pn = n + 1;
+  size_t wt = (size_t)d * (3 * d + 1);                            // W_in^T
+  if ((size_t)d * (m + 1) > wt) wt = (size_t)d * (m + 1);         // W1^T
+  if ((size_t)m * (d + 1) > wt) wt = (size_t)m * (d + 1);         // W2^T
+  return sizeof(float) * ((size_t)n * (2 * pd + pw + pn) + wt);
 }
 static size_t bwd_lds(int n, int d, int m) {
-  return sizeof(float) * ((size_t)n * d * 2 + (size_t)n * (3 * d > m ? 3 * d : m) + 2 * (size_t)n * n + NT);
+  const size_t pd = d + 1, pw = (3 * d > m ? 3 * d : m) + 1, pn = n + 1;
+  return sizeof(float) * ((size_t)n * (2 * pd + pw + pn) + NT);
 }
 
 static int build_args(const gr_sasrec_params* p, int64_t B, int32_t n, float p_drop, uint64_t seed,
@@ -411,7 +483,7 @@ static int build_args(const gr_sasrec_params* p, int64_t B, int32_t n, float p_d
   a.seed_dev = seed_dev;
   a.buf = *bufs;
   a.B = B;
-  a.vwidth = p->n_blocks * (9 * p->d + p->mlp) + 2 * p->d + n * p->d;
+  a.vwidth = p->n_blocks * voff(p->d, p->mlp).size + 2 * p->d + n * p->d;
   return GR_OK;
 }
 
@@ -420,7 +492,7 @@ static int build_args(const gr_sasrec_params* p, int64_t B, int32_t n, float p_d
 
 extern "C" int32_t gr_sasrec_train_vec_width(const gr_sasrec_params* p, int32_t n) {
   if (!p) return 0;
-  return p->n_blocks * (9 * p->d + p->mlp) + 2 * p->d + n * p->d;
+  return p->n_blocks * gr::st::voff(p->d, p->mlp).size + 2 * p->d + n * p->d;
 }
 
 extern "C" int gr_sasrec_train_fwd_f32(const gr_sasrec_params* p, const int64_t* seqs, int64_t B, int32_t n,
@@ -456,7 +528,8 @@ extern "C" int gr_sasrec_train_bwd_f32(const gr_sasrec_params* p, const int64_t*
   int rc = st::build_args(p, B, n, p_drop, seed, seed_dev, bufs, a);
   if (rc) return rc;
   const gr_sasrec_train_bufs& g = *bufs;
-  if (!seqs || !d_out || !g.g_qkv || !g.g_out || !g.g_z || !g.g_y || !g.g_vec)
+  if (!seqs || !d_out || !g.g_vec || !g.xin || !g.hs || !g.qkv || !g.prob || !g.os || !g.x1 || !g.fs ||
+      !g.zs || !g.us || !g.xl)
     return fail(GR_ERR_ARG, "gr_sasrec_train_bwd_f32: null pointer");
   const size_t lds = st::bwd_lds(n, p->d, p->mlp);
   auto k = st::sas_train_bwd_kernel;

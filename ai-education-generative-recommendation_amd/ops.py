@@ -676,35 +676,30 @@ class _SasTrain(torch.autograd.Function):
         B, n, d, m, nb, max_len = ctx.shapes
         bufs, seqs = ctx.bufs, ctx.seqs
         dev = seqs.device
-        R = B * n
         p = ctx.binding.p
         vw = L.lib().gr_sasrec_train_vec_width(ctypes.byref(p), n)
-        e = lambda *shape: torch.empty(shape, dtype=torch.float32, device=dev)   # noqa: E731
-        g = {"g_qkv": e(nb, R, 3 * d), "g_out": e(nb, R, d), "g_z": e(nb, R, m), "g_y": e(nb, R, d),
-             "g_vec": e(B, vw)}
+        g_vec = torch.empty((B, vw), dtype=torch.float32, device=dev)
         g_item = torch.zeros((p.item_rows, d), dtype=torch.float32, device=dev)
-        cb = L.SasrecTrainBufs(**{k: v.data_ptr() for k, v in {**bufs, **g}.items()})
+        cb = L.SasrecTrainBufs(g_vec=g_vec.data_ptr(), **{k: v.data_ptr() for k, v in bufs.items()})
         dout = dout.contiguous().float()
         with torch.cuda.device(dev):
             L.check(L.lib().gr_sasrec_train_bwd_f32(ctypes.byref(p), L.ptr(seqs), B, n, float(ctx.p_drop), 0,
                                                     L.ptr(ctx.seed), ctypes.byref(cb), L.ptr(dout), L.ptr(g_item),
                                                     L.stream_of(dev)), "gr_sasrec_train_bwd_f32")
-        vec = g["g_vec"].sum(0)
-        grads = [g_item]
-        dpos = torch.zeros((max_len, d), dtype=torch.float32, device=dev)
-        off = nb * (9 * d + m)
-        dpos[:n] = vec[off + 2 * d:].view(n, d)
-        grads.append(dpos)
-        for k in range(nb):
-            v = vec[k * (9 * d + m):(k + 1) * (9 * d + m)]
-            grads += [v[:d], v[d:2 * d],
-                      g["g_qkv"][k].t() @ bufs["hs"][k], v[2 * d:5 * d],
-                      g["g_out"][k].t() @ bufs["os"][k], v[5 * d:6 * d],
-                      v[6 * d:7 * d], v[7 * d:8 * d],
-                      g["g_z"][k].t() @ bufs["fs"][k], v[8 * d:8 * d + m],
-                      g["g_y"][k].t() @ bufs["us"][k], v[8 * d + m:9 * d + m]]
-        grads += [vec[off:off + d], vec[off + d:off + 2 * d]]
-        return (None, None, None, None, *grads)
+        vec = g_vec.sum(0)   # every parameter's gradient but the item table's, in parameter order
+        shapes = [(d,), (d,), (3 * d, d), (3 * d,), (d, d), (d,), (d,), (d,), (m, d), (m,), (d, m), (d,)] * nb
+        shapes += [(d,), (d,)]
+        grads, off = [], 0
+        for shp in shapes:
+            k = 1
+            for x in shp:
+                k *= x
+            grads.append(vec[off:off + k].view(shp))
+            off += k
+        # rows n.. of pos_emb get zeros (a pad kernel rather than a copy into a zeros tensor, which
+        # keeps memset / memcpy nodes out of a captured step's graph)
+        dpos = torch.nn.functional.pad(vec[off:off + n * d].view(n, d), (0, 0, 0, max_len - n))
+        return (None, None, None, None, g_item, dpos, *grads)
 
 
 def sasrec_train_forward(model, log_seqs):
@@ -713,7 +708,7 @@ def sasrec_train_forward(model, log_seqs):
     seqs = log_seqs.to(torch.int64).contiguous()
     L.require_gpu(seqs)
     seed = dropout_seed(seqs.device)
-    snap = seed.clone()          # this step's masks (forward and backward read the same word)
+    snap = seed + 0              # this step's masks (forward and backward read the same word); a kernel, not a copy
     seed.add_(1)
     return _SasTrain.apply(seqs, sasrec_binding(model), float(model.dropout), snap, *_train_params(model))
 
@@ -783,6 +778,7 @@ class SasTrainGraph:
     def __init__(self, model, optimizer, inputs, targets, item_num, num_neg, eps, seed=0, warmup=3):
         L.require_gpu(inputs, targets)
         self.model, self.opt = model, optimizer
+        self._sync = not (getattr(model, "fused_train", False) and sasrec_train_supported(model, inputs.shape[1]))
         self.inputs, self.targets = inputs, targets
         self.item_num, self.num_neg, self.eps = int(item_num), int(num_neg), float(eps)
         dev = inputs.device
@@ -816,18 +812,20 @@ class SasTrainGraph:
             self.seed.fill_(int(seed))
 
     def replay(self):
-        """Run one captured step and return the static ``(batch_loss, batch_valid_t)``; returns
-        after the step has finished on the device (the reference loop synchronises every step
-        too: ``batch_valid_t.item()``, train.py:163).
+        """Run one captured step; returns the static ``(batch_loss, batch_valid_t)``.
 
-        The device-wide synchronise is load-bearing.  Replays of this graph back to back -- even
-        host-ordered through a completion event -- faulted within ~600 steps (memory aperture
-        violation in the rocprim unique-by-key of the item embedding's backward; four of four
-        bench runs), while replay + ``torch.cuda.synchronize()`` ran 725 and 1500 steps clean
-        (profiles/r02_train_graph_diag.txt).  It costs nothing measurable at this step size
-        (1.59 ms per step synchronised vs 1.75 ms unsynchronised)."""
+        With the transformer under torch autograd (``fused_train = False`` or a shape the fused
+        kernels do not take), replay synchronises the device after each step.  That graph holds
+        memset nodes (rocprim's sort / unique-by-key temporaries in the embedding backward), and on
+        this ROCm a captured memset node does not reliably clear its buffer once replays queue
+        back to back: 4 of 4 bench runs faulted in the unique-by-key kernel within ~600 steps,
+        replay + ``torch.cuda.synchronize()`` ran 725 and 1500 steps clean, and the library's own
+        memset (the sampled BCE's dM) measurably kept stale data on the 2nd replay until it became
+        a kernel (profiles/r02_train_graph_diag.txt).  The fused path's graph has no memset node
+        and replays back to back."""
         self.graph.replay()
-        torch.cuda.synchronize(self.inputs.device)
+        if self._sync:
+            torch.cuda.synchronize(self.inputs.device)
         return self.out
 
     def _body(self):

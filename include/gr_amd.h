@@ -213,16 +213,14 @@ typedef struct gr_sasrec_train_bufs {
   float* zs;     /* [nb, R, mlp]  FFN1 output before the ReLU                             */
   float* us;     /* [nb, R, mlp]  dropout(relu(FFN1)) = FFN2 input                        */
   float* xl;     /* [R, d]        last LayerNorm input                                    */
-  float* g_qkv;  /* [nb, R, 3d]   dloss / d in-projection output  (written by the backward) */
-  float* g_out;  /* [nb, R, d]    dloss / d out-projection output                         */
-  float* g_z;    /* [nb, R, mlp]  dloss / d FFN1 output                                   */
-  float* g_y;    /* [nb, R, d]    dloss / d FFN2 output                                   */
-  float* g_vec;  /* [B, gr_sasrec_train_vec_width] per-sequence partial sums: per block
-                    [ln_a w, ln_a b, in_proj b (3d), out_proj b, ln_f w, ln_f b, ffn1 b (mlp),
-                    ffn2 b], then [last ln w, last ln b], then pos_emb rows [n, d]            */
+  float* g_vec;  /* [B, gr_sasrec_train_vec_width] (written by the backward) per-sequence partial
+                    gradients in SASRec's parameter order: per block [ln_a w, ln_a b, in_proj w
+                    (3d x d), in_proj b, out_proj w (d x d), out_proj b, ln_f w, ln_f b, ffn1 w
+                    (mlp x d), ffn1 b, ffn2 w (d x mlp), ffn2 b], then [last ln w, last ln b], then
+                    pos_emb rows [n, d]; the parameter gradients are its sum over B             */
 } gr_sasrec_train_bufs;
 
-/* Floats per sequence in gr_sasrec_train_bufs.g_vec: n_blocks * (9d + mlp) + 2d + n*d. */
+/* Floats per sequence in gr_sasrec_train_bufs.g_vec: n_blocks * (4d^2 + 2 d mlp + 9d + mlp) + 2d + n*d. */
 int32_t gr_sasrec_train_vec_width(const gr_sasrec_params* p, int32_t n);
 
 /* Train-mode forward: seqs[B, n] -> out[B, n, d] (model.py:49-96 with dropout p), saving the
@@ -231,11 +229,10 @@ int gr_sasrec_train_fwd_f32(const gr_sasrec_params* p, const int64_t* seqs, int6
                             float p_drop, uint64_t seed, const uint64_t* seed_dev,
                             const gr_sasrec_train_bufs* bufs, float* out, int32_t* err_flag, void* stream);
 
-/* Backward of the forward above (same seqs, p_drop, seed, bufs): d_out[B, n, d] -> the per-row
- * gradients and per-sequence partial sums in bufs; item-embedding rows are added (atomically)
- * into g_item[item_rows, d] (optional; padding row 0 is left untouched).  The host completes the
- * weight gradients: dW_in = g_qkv^T hs, dW_o = g_out^T os, dW1 = g_z^T fs, dW2 = g_y^T us per
- * block, and the vectors = g_vec summed over B. */
+/* Backward of the forward above (same seqs, p_drop, seed, bufs): d_out[B, n, d] -> the
+ * per-sequence partial gradients in bufs.g_vec (sum over B = every parameter's gradient except
+ * the item table's); item-embedding rows are added (atomically) into g_item[item_rows, d]
+ * (optional; padding row 0 is left untouched). */
 int gr_sasrec_train_bwd_f32(const gr_sasrec_params* p, const int64_t* seqs, int64_t B, int32_t n,
                             float p_drop, uint64_t seed, const uint64_t* seed_dev,
                             const gr_sasrec_train_bufs* bufs, const float* d_out, float* g_item,
