@@ -91,17 +91,33 @@ __device__ __forceinline__ void mm(float* C, int ldc, const float* A, int sar, i
     f32x16 acc;
 #pragma unroll
     for (int v = 0; v < 16; ++v) acc[v] = 0.f;
-    int k0 = 0;
-    for (; k0 + 16 <= K; k0 += 16) {
-      float av[8], bv[8];
+    // 16-deep k chunks, double-buffered: the next chunk's loads are in flight during this
+    // chunk's 8 MFMAs (operands in L2 cost ~1 us per dependent round trip)
+    const int kfull = K & ~15;
+    float av[8], bv[8], an[8], bn[8];
+    if (kfull > 0) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const int k = k0 + 2 * j + h;
-        av[j] = ap[k * sak];
-        bv[j] = bp[k * sbk];
+        av[j] = ap[(2 * j + h) * sak];
+        bv[j] = bp[(2 * j + h) * sbk];
+      }
+    }
+    int k0 = 0;
+    for (; k0 < kfull; k0 += 16) {
+      const bool more = k0 + 16 < kfull;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int k = more ? k0 + 16 + 2 * j + h : 2 * j + h;
+        an[j] = ap[k * sak];
+        bn[j] = bp[k * sbk];
       }
 #pragma unroll
       for (int j = 0; j < 8; ++j) acc = mfma32(av[j], bv[j], acc);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        av[j] = an[j];
+        bv[j] = bn[j];
+      }
     }
     for (; k0 < K; k0 += 2) {
       const int k = k0 + h, kc = min(k, K - 1);
