@@ -56,6 +56,13 @@ def merge_topk(vals, ids, k):
     return vk, torch.where(ik == big, torch.full_like(ik, -1), ik)
 
 
+def _world(group):
+    """World size of ``group`` when a process group is initialised, else 0 (no exchange at all).
+    A one-rank group still runs every collective, so a single-GPU job launched under
+    torch.distributed exercises the same RCCL calls as the 8-GPU one."""
+    return dist.get_world_size(group) if dist.is_initialized() else 0
+
+
 def _default_ops():
     from . import ops
     return ops.score, ops.count_gt, ops.topk
@@ -67,7 +74,7 @@ def sharded_rank_topk(h, table_shard, row_offset, targets, k=10, group=None, mas
     """Catalog-sharded scoring: every rank holds ``table_shard`` = rows [row_offset, ...) of the
     item table and the same ``h`` [B, d] / global ``targets`` [B].  Returns (rank [B] int64,
     top values [B, k], top ids [B, k]) identical on every rank."""
-    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    world = _world(group)
     rows = table_shard.shape[0]
     if (scorer is None and counter is None and topk_fn is None and h.is_cuda and rows > 0
             and 1 <= k <= 16 and h.shape[1] in (32, 64, 128)):
@@ -82,7 +89,7 @@ def sharded_rank_topk(h, table_shard, row_offset, targets, k=10, group=None, mas
     own = (t >= row_offset) & (t < row_offset + rows)
     local = torch.where(own, t - row_offset, torch.zeros_like(t))
     ts = torch.where(own, logits.gather(1, local.unsqueeze(1)).squeeze(1), torch.zeros_like(t, dtype=logits.dtype))
-    if world > 1:
+    if world:
         dist.all_reduce(ts, op=dist.ReduceOp.SUM, group=group)
     kk = min(k, rows) if rows > 0 else 0
     if kk > 0 and topk_fn is t_fn and counter is c_fn:
@@ -104,7 +111,7 @@ def sharded_rank_topk(h, table_shard, row_offset, targets, k=10, group=None, mas
 def _exchange(cnt, v, i, k, group, world):
     """Steps 2-3 of the module docstring: global counts and the merged top-k.  The (value, id)
     candidates travel as ONE int64 all-gather: [ids | value bits] per user."""
-    if world > 1:
+    if world:
         dist.all_reduce(cnt, op=dist.ReduceOp.SUM, group=group)
         kk = v.shape[1]
         packed = torch.cat([i, v.contiguous().view(torch.int32).to(torch.int64)], 1)
@@ -128,7 +135,7 @@ def _sharded_rank_topk_fused(h, table_shard, row_offset, targets, k, group, mask
     local = torch.where(own, t - row_offset, torch.zeros_like(t))
     ts = torch.where(own, ops.score_pairs(h, table_shard, local, mask_col0=m0),
                      torch.zeros(t.shape, dtype=torch.float32, device=h.device))
-    if world > 1:
+    if world:
         dist.all_reduce(ts, op=dist.ReduceOp.SUM, group=group)
     kk = min(k, rows)
     v, i, cnt = ops.score_topk(h, table_shard, kk, row_offset, thresholds=ts, mask_col0=m0)
@@ -149,8 +156,8 @@ def sharded_rank_topk_batches(hs, table_shard, row_offset, targets, k=10, group=
     so the target-logit all-reduce of batch b+1 runs during batch b's scoring and batch b's count
     all-reduce + candidate all-gather during batch b+1's.  Results are identical to the sequential
     calls.  ``targets`` is a list of per-batch target tensors."""
-    world = dist.get_world_size(group) if dist.is_initialized() else 1
-    if world == 1 or len(hs) <= 1:
+    world = _world(group)
+    if not world or len(hs) <= 1:
         return [sharded_rank_topk(h, table_shard, row_offset, t, k, group, mask_row0, scorer, counter, topk_fn)
                 for h, t in zip(hs, targets)]
     rows = table_shard.shape[0]

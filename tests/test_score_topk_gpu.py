@@ -157,13 +157,16 @@ def test_score_kernel_variants_identical(B, d, rows, ld, dev):
     assert (outs[0][:, rows:] == 7.0).all()   # nothing written past the row's columns
 
 
-def _gloo_gpu_worker(rank, world, port, data, out):
+def _gloo_gpu_worker(rank, world, port, data, out, backend="gloo"):
     import os as _os
     import torch.distributed as dist
     _os.environ["MASTER_ADDR"] = "127.0.0.1"
     _os.environ["MASTER_PORT"] = str(port)
     torch.cuda.set_device(0)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    if backend == "nccl":   # RCCL, initialised exactly as bench.py does for one rank per GPU
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", 0))
+    else:
+        dist.init_process_group(backend, rank=rank, world_size=world)
     from gr_amd import dist as D
     h, table, targets, k = (t.cuda() if torch.is_tensor(t) else t for t in data)
     lo, hi = D.shard_range(table.shape[0], rank, world)
@@ -178,10 +181,13 @@ def _gloo_gpu_worker(rank, world, port, data, out):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_catalog_sharded_fused_multi_rank(world, dev):
+@pytest.mark.parametrize("world,backend", [(2, "gloo"), (3, "gloo"), (1, "nccl")])
+def test_catalog_sharded_fused_multi_rank(world, backend, dev):
     """The catalog-sharded exchange over real ranks (gloo, every rank on this GPU) with the fused
-    HIP kernels: every rank returns the full-catalog rank / top-k bit for bit."""
+    HIP kernels: every rank returns the full-catalog rank / top-k bit for bit.  The one-rank RCCL
+    case runs every collective of the exchange (a one-rank group still issues them) through the
+    "nccl" backend and bench.py's ``device_id`` initialisation: RCCL needs one GPU per rank, so
+    this box cannot hold more than one."""
     import socket
     import torch.multiprocessing as mp
     from gr_amd import ops
@@ -204,7 +210,7 @@ def test_catalog_sharded_fused_multi_rank(world, dev):
     s.close()
     mgr = mp.Manager()
     out = mgr.dict()
-    mp.spawn(_gloo_gpu_worker, args=(world, port, (h, table, tg, k), out), nprocs=world, join=True)
+    mp.spawn(_gloo_gpu_worker, args=(world, port, (h, table, tg, k), out, backend), nprocs=world, join=True)
     for r in range(world):
         rk, v, i, pr, pv, pi = out[r]
         assert torch.equal(rk, ref_rank)
