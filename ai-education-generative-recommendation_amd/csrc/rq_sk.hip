@@ -27,6 +27,8 @@ struct RQSkLevels {
 };
 
 constexpr int SK_T = 256;
+constexpr int64_t SK_LDS_BYTES = 128 * 1024;   // + ~12.3 KiB static: within the 160 KiB of a CU
+constexpr int SK_SUMS = 1024;                   // row / column sums staged in LDS up to this size
 
 // workgroup-wide reductions (all threads call; result broadcast)
 template <typename T, typename Op>
@@ -40,33 +42,51 @@ __device__ T wg_reduce(T v, Op op, T* sm) {
   return r;
 }
 
+// largest power of two <= min(64, x), at least 1
+__device__ __forceinline__ int pow2_group(int x) {
+  int g = 1;
+  while (g < 64 && 2 * g <= x) g <<= 1;
+  return g;
+}
+
+// One workgroup per group of rows.  The [B, K] Sinkhorn matrix of a group lives in LDS when it fits
+// (every training batch of main.py: 64 x 8; a 64 x 256 batch: 128 KiB) and in the caller's
+// workspace otherwise; both go through the same generic pointer.  Every row / column sum runs in
+// index order in one lane (the reference's argmax can sit on ties that only its rounding order
+// decides: identical rows of a collision group), and the divisions -- the reference's two per
+// element and half-step, Q /= sum; Q /= B, in float64 -- spread over the whole workgroup.  The
+// final argmax / argmin gives each row a group of lanes (a power of two within one wave) that
+// combine their first extremes with shuffles.
 __global__ __launch_bounds__(SK_T) void rq_sk_kernel(const float* __restrict__ z, int e, int L,
                                                      RQSkLevels lv, int sk_iters,
                                                      const int64_t* __restrict__ gptr, int Kmax,
                                                      int64_t* __restrict__ idx_out,
-                                                     float* __restrict__ res, float* __restrict__ dws,
-                                                     double* __restrict__ qws) {
+                                                     float* __restrict__ res, double* __restrict__ qws,
+                                                     int lds_elems) {
+  extern __shared__ __attribute__((aligned(16))) double qlds[];
   __shared__ double smd[SK_T / 64];
   __shared__ float smf[SK_T / 64];
   __shared__ float cn[1024];    // |c|^2 per code (K <= 1024)
+  __shared__ double sums[SK_SUMS];
   const int64_t r0 = gptr[blockIdx.x], r1 = gptr[blockIdx.x + 1];
   const int B = (int)(r1 - r0);
   if (B <= 0) return;
   const int tid = threadIdx.x;
   float* R = res + r0 * e;                 // this group's residuals [B, e]
-  float* Dm = dws + r0 * Kmax;             // [B, K]
-  double* Q = qws + r0 * Kmax;             // [B, K]
   for (int i = tid; i < B * e; i += SK_T) R[i] = z[r0 * e + i];
   __syncthreads();
   for (int l = 0; l < L; ++l) {
     const float* C = lv.cb[l];
     const int K = lv.K[l];
+    double* Q = (int64_t)B * K <= lds_elems ? qlds : qws + r0 * Kmax;   // [B, K]
     for (int k = tid; k < K; k += SK_T) {
       float s = 0.f;
       for (int j = 0; j < e; ++j) s = fmaf(C[(int64_t)k * e + j], C[(int64_t)k * e + j], s);
       cn[k] = s;
     }
     __syncthreads();
+    // d = (|r|^2 + |c|^2) - 2 r.c in fp32 (vq.py:71-73), held as an exact double
+    float mx = -FLT_MAX, mn = FLT_MAX;
     for (int i = tid; i < B * K; i += SK_T) {
       const int b = i / K, k = i % K;
       const float* rb = R + (int64_t)b * e;
@@ -76,22 +96,22 @@ __global__ __launch_bounds__(SK_T) void rq_sk_kernel(const float* __restrict__ z
         rn = fmaf(rb[j], rb[j], rn);
         dot = fmaf(rb[j], ck[j], dot);
       }
-      Dm[(int64_t)b * K + k] = (rn + cn[k]) - 2.0f * dot;
+      const float d = (rn + cn[k]) - 2.0f * dot;
+      Q[i] = (double)d;
+      mx = fmaxf(mx, d);
+      mn = fminf(mn, d);
     }
-    __syncthreads();
     const double eps = lv.eps[l];
+    const int Gr = pow2_group(SK_T / B);            // lanes per row
+    const int rows_per = SK_T / Gr;
+    const int rg = tid / Gr, rl = tid % Gr;
     if (eps > 0.0) {
-      float mx = -FLT_MAX, mn = FLT_MAX;
-      for (int i = tid; i < B * K; i += SK_T) {
-        mx = fmaxf(mx, Dm[i]);
-        mn = fminf(mn, Dm[i]);
-      }
       mx = wg_reduce(mx, [](float a, float b) { return fmaxf(a, b); }, smf);
       mn = wg_reduce(mn, [](float a, float b) { return fminf(a, b); }, smf);
       const float middle = (mx + mn) / 2.0f;
       const float amplitude = (mx - middle) + 1e-5f;
       for (int i = tid; i < B * K; i += SK_T) {
-        const double dc = (double)((Dm[i] - middle) / amplitude);
+        const double dc = (double)(((float)Q[i] - middle) / amplitude);
         Q[i] = exp(-dc / eps);
       }
       __syncthreads();
@@ -107,51 +127,75 @@ __global__ __launch_bounds__(SK_T) void rq_sk_kernel(const float* __restrict__ z
       tot = wg_reduce(tot, [](double a, double b) { return a + b; }, smd);
       for (int i = tid; i < B * K; i += SK_T) Q[i] /= tot;
       __syncthreads();
-      for (int it = 0; it < sk_iters; ++it) {
-        // rows (dim=1): Q /= sum_k Q[b, k]; Q /= B
-        for (int b = tid; b < B; b += SK_T) {
-          double s = 0.0;
-          for (int k = 0; k < K; ++k) s += Q[(int64_t)b * K + k];
-          for (int k = 0; k < K; ++k) {
-            double q = Q[(int64_t)b * K + k] / s;
-            Q[(int64_t)b * K + k] = q / (double)B;
+      const double dB = (double)B, dK = (double)K;
+      if (B <= SK_SUMS && K <= SK_SUMS) {
+        // Each sum runs in index order in one lane (torch's CPU order for the column sums); the
+        // divisions then spread over the whole workgroup.
+        for (int it = 0; it < sk_iters; ++it) {
+          for (int b = tid; b < B; b += SK_T) {   // rows (dim=1): Q /= sum_k Q[b, k]; Q /= B
+            double s = 0.0;
+            for (int k = 0; k < K; ++k) s += Q[(int64_t)b * K + k];
+            sums[b] = s;
           }
-        }
-        __syncthreads();
-        // columns (dim=0): Q /= sum_b Q[b, k]; Q /= K
-        for (int k = tid; k < K; k += SK_T) {
-          double s = 0.0;
-          for (int b = 0; b < B; ++b) s += Q[(int64_t)b * K + k];
-          for (int b = 0; b < B; ++b) {
-            double q = Q[(int64_t)b * K + k] / s;
-            Q[(int64_t)b * K + k] = q / (double)K;
+          __syncthreads();
+          for (int i = tid; i < B * K; i += SK_T) Q[i] = (Q[i] / sums[i / K]) / dB;
+          __syncthreads();
+          for (int k = tid; k < K; k += SK_T) {   // columns (dim=0): Q /= sum_b Q[b, k]; Q /= K
+            double s = 0.0;
+            for (int b = 0; b < B; ++b) s += Q[(int64_t)b * K + k];
+            sums[k] = s;
           }
-        }
-        __syncthreads();
-      }
-    }
-    // per row: first argmax of Q * B (Sinkhorn levels) or first argmin of d; residual update
-    for (int b = tid; b < B; b += SK_T) {
-      int best = 0;
-      if (eps > 0.0) {
-        double bv = Q[(int64_t)b * K] * (double)B;
-        for (int k = 1; k < K; ++k) {
-          const double v = Q[(int64_t)b * K + k] * (double)B;
-          if (v > bv) { bv = v; best = k; }
+          __syncthreads();
+          for (int i = tid; i < B * K; i += SK_T) Q[i] = (Q[i] / sums[i % K]) / dK;
+          __syncthreads();
         }
       } else {
-        float bv = Dm[(int64_t)b * K];
-        for (int k = 1; k < K; ++k) {
-          const float v = Dm[(int64_t)b * K + k];
-          if (v < bv) { bv = v; best = k; }
+        for (int it = 0; it < sk_iters; ++it) {
+          for (int b = tid; b < B; b += SK_T) {
+            double s = 0.0;
+            for (int k = 0; k < K; ++k) s += Q[(int64_t)b * K + k];
+            for (int k = 0; k < K; ++k) Q[(int64_t)b * K + k] = (Q[(int64_t)b * K + k] / s) / dB;
+          }
+          __syncthreads();
+          for (int k = tid; k < K; k += SK_T) {
+            double s = 0.0;
+            for (int b = 0; b < B; ++b) s += Q[(int64_t)b * K + k];
+            for (int b = 0; b < B; ++b) Q[(int64_t)b * K + k] = (Q[(int64_t)b * K + k] / s) / dK;
+          }
+          __syncthreads();
         }
       }
-      idx_out[(r0 + b) * L + l] = best;
-      float* rb = R + (int64_t)b * e;
-      const float* cb = C + (int64_t)best * e;
-      for (int j = 0; j < e; ++j) {
-        const float x = rb[j];
-        rb[j] = x - (x + (cb[j] - x));
+    } else {
+      __syncthreads();
+    }
+    // per row: first argmax of Q * B (Sinkhorn levels) or first argmin of d; residual update
+    for (int b0 = 0; b0 < B; b0 += rows_per) {
+      const int b = b0 + rg;
+      int best = 0x7fffffff;
+      double bv = 0.0;
+      if (b < B) {
+        for (int k = rl; k < K; k += Gr) {   // this lane's first extreme (increasing k)
+          const double v = eps > 0.0 ? Q[(int64_t)b * K + k] * (double)B : -Q[(int64_t)b * K + k];
+          if (best == 0x7fffffff || v > bv) { bv = v; best = k; }
+        }
+      }
+      for (int o = Gr >> 1; o > 0; o >>= 1) {   // larger value, then the lower index
+        const double ov = __shfl_xor(bv, o);
+        const int oi = __shfl_xor(best, o);
+        if (oi != 0x7fffffff && (best == 0x7fffffff || ov > bv || (ov == bv && oi < best))) {
+          bv = ov;
+          best = oi;
+        }
+      }
+      if (b < B) {
+        if (best == 0x7fffffff || best >= K) best = 0;
+        if (rl == 0) idx_out[(r0 + b) * L + l] = best;
+        float* rb = R + (int64_t)b * e;
+        const float* cb = C + (int64_t)best * e;
+        for (int j = rl; j < e; j += Gr) {
+          const float x = rb[j];
+          rb[j] = x - (x + (cb[j] - x));
+        }
       }
     }
     __syncthreads();
@@ -164,8 +208,7 @@ extern "C" size_t gr_rq_encode_sk_workspace_bytes(int64_t n, int32_t e, int32_t 
   if (n < 0 || e < 1 || L < 1 || L > GR_MAX_LEVELS || !K) return 0;
   int64_t kmax = 1;
   for (int l = 0; l < L; ++l) kmax = K[l] > kmax ? K[l] : kmax;
-  return gr::align_up((size_t)n * e * 4, 256) + gr::align_up((size_t)n * kmax * 4, 256) +
-         gr::align_up((size_t)n * kmax * 8, 256) + 256;
+  return gr::align_up((size_t)n * e * 4, 256) + gr::align_up((size_t)n * kmax * 8, 256) + 256;
 }
 
 extern "C" int gr_rq_encode_sk_f32(const float* z, int64_t n, int32_t e, int32_t L, const int32_t* K,
@@ -197,11 +240,16 @@ extern "C" int gr_rq_encode_sk_f32(const float* z, int64_t n, int32_t e, int32_t
   if (n_groups > 0x7fffffffLL) return fail(GR_ERR_UNSUPPORTED, "gr_rq_encode_sk_f32: too many groups");
   char* base = reinterpret_cast<char*>(align_up(reinterpret_cast<uintptr_t>(workspace), 256));
   float* res = reinterpret_cast<float*>(base);
-  float* dws = reinterpret_cast<float*>(base + align_up((size_t)n * e * 4, 256));
-  double* qws = reinterpret_cast<double*>(base + align_up((size_t)n * e * 4, 256) +
-                                          align_up((size_t)n * kmax * 4, 256));
-  hipLaunchKernelGGL(rq_sk_kernel, dim3((unsigned)n_groups), dim3(SK_T), 0,
+  double* qws = reinterpret_cast<double*>(base + align_up((size_t)n * e * 4, 256));
+  // LDS for the Sinkhorn matrix: enough for the largest possible group (n rows) up to 128 KiB
+  const int64_t lds_elems = std::min<int64_t>((int64_t)n * kmax, SK_LDS_BYTES / 8);
+  const size_t lds = (size_t)lds_elems * 8;
+  if (lds > 64 * 1024 &&
+      hipFuncSetAttribute(reinterpret_cast<const void*>(rq_sk_kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)lds) != hipSuccess)
+    return fail(GR_ERR_HIP, "gr_rq_encode_sk_f32: cannot raise the LDS limit");
+  hipLaunchKernelGGL(rq_sk_kernel, dim3((unsigned)n_groups), dim3(SK_T), lds,
                      reinterpret_cast<hipStream_t>(stream), z, e, L, lv, sk_iters, group_ptr, kmax,
-                     idx_out, res, dws, qws);
+                     idx_out, res, qws, (int)lds_elems);
   return check_launch("gr_rq_encode_sk_f32");
 }

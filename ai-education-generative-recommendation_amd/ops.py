@@ -338,6 +338,23 @@ def rq_encode_sk(x, weights, biases, codebooks, sk_eps, sk_iters, group_sizes=No
     return rq_quantize_sk(rq_mlp(x, weights, biases), codebooks, sk_eps, sk_iters, group_sizes)
 
 
+_GROUP_PTRS = {}
+
+
+def _group_ptr(sizes, dev):
+    """Device copy of the group offsets [0, s0, s0+s1, ...].  The one-group form (a training batch)
+    is cached per (n, device) and never freed, so a captured training step (RqTrainGraph) replays
+    the Sinkhorn launch with no host-to-device copy and a pointer that stays valid."""
+    if len(sizes) != 1:
+        return torch.tensor([0] + list(itertools.accumulate(sizes)), dtype=torch.int64).to(dev)
+    key = (sizes[0], str(dev))
+    t = _GROUP_PTRS.get(key)
+    if t is None:
+        t = torch.tensor([0, sizes[0]], dtype=torch.int64).to(dev)
+        _GROUP_PTRS[key] = t
+    return t
+
+
 def rq_quantize_sk(z, codebooks, sk_eps, sk_iters, group_sizes=None):
     """ResidualVectorQuantizer.forward(z, use_sk=True) indices (rq.py:39-56, vq.py:63-84): per level,
     Sinkhorn over the group's distances where ``sk_eps[l] > 0``, plain argmin otherwise."""
@@ -350,9 +367,8 @@ def rq_quantize_sk(z, codebooks, sk_eps, sk_iters, group_sizes=None):
     sizes = [n] if group_sizes is None else [int(s) for s in group_sizes]
     if sum(sizes) != n or any(s < 1 for s in sizes):
         raise RuntimeError("rq_encode_sk: group sizes must be positive and sum to the batch")
-    ptr = torch.tensor([0] + list(itertools.accumulate(sizes)), dtype=torch.int64)
     dev = z.device
-    ptr = ptr.to(dev)
+    ptr = _group_ptr(sizes, dev)
     lib = L.lib()
     ks_c = L.i32_array(Ks)
     eps_c = (ctypes.c_double * len(cbs))(*[float(v) for v in sk_eps])
@@ -836,3 +852,85 @@ class SasTrainGraph:
         (bl / valid.clamp(min=1.0)).backward()   # :161-172 (batch_loss is 0 when nothing is valid)
         self.opt.step()                                                            # :173
         return bl, valid
+
+
+class RqTrainGraph:
+    """One RQ-VAE training step of RQ-VAE/train.py:108-119 -- ``out, rq_loss, indices =
+    model(data)`` (every level's Sinkhorn / argmin assignment on the kernels, dropout on),
+    ``compute_loss``, ``loss.backward()``, ``clip_grad_norm_(params, 1.0)`` and ``optimizer.step()``
+    -- captured once as a graph (hipGraph via ``torch.cuda.graph``) and replayed: one launch per
+    step instead of ~200 host-issued kernels at the reference's batch of 64 (main.py:26).
+
+    ``optimizer`` must be capturable with a tensor learning rate (``torch.optim.AdamW(params,
+    lr=torch.tensor(1e-3, device=dev), weight_decay=1e-4, capturable=True)``): its step counter
+    and lr live on the device, and a scheduler built on it (``get_linear_schedule_with_warmup``,
+    train.py:81-89) writes the new lr in place, so ``scheduler.step()`` after ``replay()`` reaches
+    the captured step.  ``inputs`` [B, in_dim] is the static batch: copy each batch into it before
+    ``replay()``, which returns the static ``(loss, loss_recon, indices)`` device tensors
+    (train.py:120-121's ``.item()`` becomes a device-side sum the caller reads once per epoch).
+
+    A model with ``kmeans_init`` and codebooks not yet initialised is initialised here on
+    ``inputs`` -- the reference's first training batch does the same (vq.py:66-67) -- before the
+    capture.  Warm-up steps (allocator, autograd, the optimizer's lazily created state) are undone
+    afterwards, so the first replay is the first real training step.  Dropout draws from torch's
+    graph-safe generator (fresh masks each replay).  The encoder / decoder run under torch autograd,
+    whose embedding backward holds memset nodes (rocprim temporaries): replay synchronises the
+    device after each step (SasTrainGraph.replay explains why)."""
+
+    def __init__(self, model, optimizer, inputs, max_norm=1.0, use_sk=True, warmup=3, sync=True):
+        L.require_gpu(inputs)
+        for g in optimizer.param_groups:
+            if not g.get("capturable", False) or not torch.is_tensor(g["lr"]):
+                raise RuntimeError("RqTrainGraph: the optimizer must be capturable with a tensor lr "
+                                   "(e.g. AdamW(params, lr=torch.tensor(1e-3, device=dev), capturable=True))")
+        self.model, self.opt, self.inputs = model, optimizer, inputs
+        self.max_norm, self.use_sk, self._sync = float(max_norm), bool(use_sk), bool(sync)
+        dev = inputs.device
+        if model.training and any(not q.initted for q in model.rq.vq_layers):
+            with torch.no_grad():   # vq.py:66-67: k-means init on the first batch's residuals
+                model(inputs, use_sk=self.use_sk)
+        params = [p for g in optimizer.param_groups for p in g["params"]]
+        saved_p = [p.detach().clone() for p in params]
+        saved_s = {id(p): {k: (v.detach().clone() if torch.is_tensor(v) else v)
+                           for k, v in optimizer.state[p].items()} for p in params if p in optimizer.state}
+        saved_lr = [g["lr"].detach().clone() for g in optimizer.param_groups]
+        side = torch.cuda.Stream(device=dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):
+            for _ in range(warmup):
+                self._body()
+        torch.cuda.current_stream(dev).wait_stream(side)
+        self.graph = torch.cuda.CUDAGraph()
+        optimizer.zero_grad(set_to_none=True)
+        with torch.cuda.graph(self.graph):
+            self.out = tuple(x.detach() for x in self._body())
+        with torch.no_grad():   # undo the warm-up steps: the first replay is the first step
+            for p, s in zip(params, saved_p):
+                p.copy_(s)
+            for p in params:
+                st = optimizer.state.get(p, {})
+                old = saved_s.get(id(p))
+                for k, v in st.items():
+                    if torch.is_tensor(v):
+                        if old is not None and torch.is_tensor(old.get(k)):
+                            v.copy_(old[k])
+                        else:
+                            v.zero_()
+            for g, lr in zip(optimizer.param_groups, saved_lr):
+                g["lr"].copy_(lr)
+
+    def replay(self):
+        """Run one captured step; returns the static ``(loss, loss_recon, indices)``."""
+        self.graph.replay()
+        if self._sync:
+            torch.cuda.synchronize(self.inputs.device)
+        return self.out
+
+    def _body(self):
+        self.opt.zero_grad(set_to_none=True)
+        out, rq_loss, indices = self.model(self.inputs, use_sk=self.use_sk)           # train.py:113
+        loss, loss_recon = self.model.compute_loss(out, rq_loss, xs=self.inputs)     # :114
+        loss.backward()                                                              # :116
+        torch.nn.utils.clip_grad_norm_(self.model.parameters(), self.max_norm)       # :117
+        self.opt.step()                                                              # :118
+        return loss, loss_recon, indices

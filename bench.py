@@ -558,6 +558,132 @@ def bench_sas_train_step(a, world, rank, dev):
     return res
 
 
+def rq_step_flop(B, dims):
+    """Algorithmic flops of one RQ-VAE training step (train.py:113-118): encoder + decoder GEMMs
+    forward (2·B·in·out each) and backward (twice that: input and weight gradients)."""
+    lin = sum(2 * B * i * o for i, o in zip(dims[:-1], dims[1:]))
+    return 3 * 2 * lin
+
+
+def _ref_rq_step(model, opt, x, use_sk=True):
+    """RQ-VAE/train.py:110-118 as the reference writes it, in torch ops on any device: the torch
+    MLPs, vq.py:63-99 per level (the [B, K] distance matrix, center_distance_for_constraint,
+    layers.py:85-108's float64 Sinkhorn, argmax), compute_loss, backward, clip, step."""
+    import torch.nn.functional as F
+    opt.zero_grad()
+    z = model.encoder.mlp_layers(x)
+    res, x_q, losses = z, 0, []
+    for q in model.rq.vq_layers:
+        C = q.embedding.weight
+        d = (res ** 2).sum(1, keepdim=True) + (C ** 2).sum(1, keepdim=True).t() - 2 * res @ C.t()
+        if use_sk and q.sk_epsilon > 0:
+            with torch.no_grad():
+                mx, mn = d.max(), d.min()
+                mid = (mx + mn) / 2
+                amp = mx - mid + 1e-5
+                assert amp > 0
+                Q = torch.exp(-((d - mid) / amp).double() / q.sk_epsilon)
+                Bq, Kq = Q.shape
+                Q /= Q.sum(-1, keepdim=True).sum(-2, keepdim=True)
+                for _ in range(q.sk_iters):
+                    Q /= Q.sum(1, keepdim=True)
+                    Q /= Bq
+                    Q /= Q.sum(0, keepdim=True)
+                    Q /= Kq
+                Q *= Bq
+                idx = Q.argmax(-1)
+        else:
+            idx = d.argmin(-1)
+        xq = q.embedding(idx)
+        losses.append(F.mse_loss(xq, res.detach()) + q.beta * F.mse_loss(xq.detach(), res))
+        xq = res + (xq - res).detach()
+        res = res - xq
+        x_q = x_q + xq
+    out = model.decoder.mlp_layers(x_q)
+    loss = F.mse_loss(out, x) + model.quant_loss_weight * torch.stack(losses).mean()
+    loss.backward()
+    torch.nn.utils.clip_grad_norm_(model.parameters(), 1.0)
+    opt.step()
+    return loss
+
+
+def bench_rq_train_step(a, world, rank, dev, cpu=False):
+    """RQ-VAE/train.py:108-119 at main.py's configuration (batch 64, 768 -> [256, 128] -> 32,
+    3 x 8 codebooks, Sinkhorn eps 0.01 x 50 iterations at every level, dropout 0.1, AdamW 1e-3 /
+    1e-4, linear warm-up schedule): the captured step (ops.RqTrainGraph) against the same step op
+    by op and the reference formulation on the same GPU."""
+    import copy
+    from transformers import get_linear_schedule_with_warmup
+    from gr_amd import RQVAE
+    B, dims = 64, [768, 256, 128, 32]
+    torch.manual_seed(11 + rank)
+
+    def make(capturable):
+        m = RQVAE(in_dim=768, num_emb_list=[8, 8, 8], e_dim=32, layers=[256, 128], dropout_prob=0.1,
+                  bn=False, loss_type="mse", quant_loss_weight=0.1, beta=0.25, kmeans_init=False,
+                  kmeans_iters=50, sk_epsilons=[0.01] * 3, sk_iters=50)
+        for q in m.rq.vq_layers:   # stands in for the k-means init of the first batch
+            q.embedding.weight.data.normal_(0.0, 0.3)
+        m = m.to(dev).train()
+        lr = torch.tensor(1e-3, device=dev) if capturable else 1e-3
+        o = torch.optim.AdamW(m.parameters(), lr=lr, weight_decay=1e-4, capturable=capturable)
+        return m, o, get_linear_schedule_with_warmup(o, 10, 10_000)
+
+    x = synth.items(B, 13 + rank, dev)   # BERT-statistics item embeddings (SURVEY §8d)
+    m, o, sch = make(True)
+    inputs = x.clone()
+    step = ops.RqTrainGraph(m, o, inputs)
+
+    def captured():
+        step.replay()
+        sch.step()
+    wall, dev_ms = timed(captured, a.steps, a.warmup, world)
+    m2, o2, sch2 = make(True)
+
+    def eager():
+        o2.zero_grad(set_to_none=True)
+        out, rq_loss, _ = m2(x)
+        loss, _ = m2.compute_loss(out, rq_loss, xs=x)
+        loss.backward()
+        torch.nn.utils.clip_grad_norm_(m2.parameters(), 1.0)
+        o2.step()
+        sch2.step()
+    e_wall, _ = timed(eager, a.steps, a.warmup, world)
+    m3, o3, sch3 = make(False)
+
+    def reference():
+        _ref_rq_step(m3, o3, x)
+        sch3.step()
+    r_ms = kernel_ms(reference, reps=10)
+    fl = rq_step_flop(B, dims) * 2   # encoder and decoder
+    step_ms = wall / a.steps * 1e3
+    res = {"metric": "train_steps_items/s", "value": B * world * a.steps / wall, "unit": "items/s",
+           "ms_per_step": step_ms, "scaling": "weak",
+           "config": {"workload": "rq_train_step: RQ-VAE train.py:108-119 whole step at main.py's configuration "
+                                  "(batch 64, 768 -> [256,128] -> 32, 3x8 codebooks, Sinkhorn eps 0.01 x 50 "
+                                  "iterations per level on the kernels, dropout 0.1, AdamW, clip 1.0, linear "
+                                  "warm-up schedule), one captured graph",
+                      "items_per_rank_per_step": B, "parallelism": f"item-sharded x{world} (data parallel "
+                                                                  f"without the gradient all-reduce)"},
+           "roofline": {"bound": "mfma", "achieved": fl / (dev_ms * 1e-3) / 1e12, "peak": FP32_PEAK_TFLOPS,
+                        "unit": "TFLOP/s", "frac": fl / (dev_ms * 1e-3) / 1e12 / FP32_PEAK_TFLOPS,
+                        "traffic": None, "kernel": "whole step (latency-bound: batch 64)",
+                        "flop_per_step": fl, "step_device_ms": dev_ms},
+           "eager": {"note": "the same step issued op by op (kernel Sinkhorn, torch MLPs)",
+                     "value": B * world * a.steps / e_wall, "ms_per_step": e_wall / a.steps * 1e3},
+           "reference_formulation_gpu": {"note": "train.py:108-119 as written (torch distance matrix, float64 "
+                                                 "Sinkhorn with its host-synchronising amplitude assert) on "
+                                                 "the same GPU", "ms_per_step": r_ms, "speedup": r_ms / step_ms}}
+    if cpu:
+        mc = copy.deepcopy(m3).cpu()
+        oc = torch.optim.AdamW(mc.parameters(), lr=1e-3, weight_decay=1e-4)
+        xc = x.cpu()
+        res["cpu_baseline"] = cpu_median(lambda: _ref_rq_step(mc, oc, xc), B, "items/s",
+                                         "train.py:108-119 reference formulation, batch 64, main.py config")
+    del step
+    return res
+
+
 def bench_c5_shard(a, model, h, targets, dev, shards=8):
     """The per-GPU work of the 8-GPU C5 point, timed on one GPU: 512 users against one catalog
     shard of 125,001 rows (rows [lo, hi) of the 1M-item table; the first shard, which also masks
@@ -648,7 +774,7 @@ def bench_calls(rq_model, sas_model, sas_n, sas_items, dev, cpu=True):
 
 
 LEGS = ["c2", "calls", "sasrec", "c4", "c5", "shard", "train"]
-OPT_LEGS = ["train_step"]   # run only when named in --legs
+OPT_LEGS = ["train_step", "rq_train_step"]   # run only when named in --legs
 
 
 def main():
@@ -714,6 +840,8 @@ def main():
         torch.cuda.empty_cache()
     if "train_step" in legs:
         line["sasrec_train_step"] = bench_sas_train_step(a, world, rank, dev)
+    if "rq_train_step" in legs:
+        line["rq_train_step"] = bench_rq_train_step(a, world, rank, dev, cpu)
     if "train" in legs:
         line["sasrec_train"] = bench_sas_train(a, world, rank, dev)
     if rank == 0:
