@@ -27,6 +27,9 @@ struct RQSkLevels {
 };
 
 constexpr int SK_T = 256;
+struct DcOut {
+  float* p[GR_MAX_LEVELS];
+};
 constexpr int64_t SK_LDS_BYTES = 128 * 1024;   // + ~12.3 KiB static: within the 160 KiB of a CU
 constexpr int SK_SUMS = 1024;                   // row / column sums staged in LDS up to this size
 
@@ -40,6 +43,22 @@ __device__ T wg_reduce(T v, Op op, T* sm) {
   for (int w = 1; w < SK_T / 64; ++w) r = op(r, sm[w]);
   __syncthreads();
   return r;
+}
+
+// ((0 + p[0]) + p[stride]) + ... in index order, with U loads in flight ahead of the dependent adds
+template <int U>
+__device__ __forceinline__ double seq_sum(const double* p, int n, int stride) {
+  double s = 0.0;
+  int i = 0;
+  for (; i + U <= n; i += U) {
+    double v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = p[(int64_t)(i + u) * stride];
+#pragma unroll
+    for (int u = 0; u < U; ++u) s += v[u];
+  }
+  for (; i < n; ++i) s += p[(int64_t)i * stride];
+  return s;
 }
 
 // largest power of two <= min(64, x), at least 1
@@ -62,7 +81,8 @@ __global__ __launch_bounds__(SK_T) void rq_sk_kernel(const float* __restrict__ z
                                                      const int64_t* __restrict__ gptr, int Kmax,
                                                      int64_t* __restrict__ idx_out,
                                                      float* __restrict__ res, double* __restrict__ qws,
-                                                     int lds_elems) {
+                                                     int lds_elems, float* __restrict__ xq_out,
+                                                     float* __restrict__ sq_out) {
   extern __shared__ __attribute__((aligned(16))) double qlds[];
   __shared__ double smd[SK_T / 64];
   __shared__ float smf[SK_T / 64];
@@ -118,48 +138,46 @@ __global__ __launch_bounds__(SK_T) void rq_sk_kernel(const float* __restrict__ z
       // sum_Q = Q.sum(-1).sum(-2): row sums, then their total
       double tot = 0.0;
       if (tid < 64) {
-        for (int b = tid; b < B; b += 64) {
-          double s = 0.0;
-          for (int k = 0; k < K; ++k) s += Q[(int64_t)b * K + k];
-          tot += s;
-        }
+        for (int b = tid; b < B; b += 64) tot += seq_sum<16>(Q + (int64_t)b * K, K, 1);
       }
       tot = wg_reduce(tot, [](double a, double b) { return a + b; }, smd);
       for (int i = tid; i < B * K; i += SK_T) Q[i] /= tot;
       __syncthreads();
       const double dB = (double)B, dK = (double)K;
+      // x / 2^j and x * 2^-j round the same exact value: bitwise equal, and a multiply is far
+      // cheaper than the float64 division sequence (main.py: B 64, K 8)
+      const bool powB = (B & (B - 1)) == 0, powK = (K & (K - 1)) == 0;
+      const double invB = 1.0 / dB, invK = 1.0 / dK;
       if (B <= SK_SUMS && K <= SK_SUMS) {
         // Each sum runs in index order in one lane (torch's CPU order for the column sums); the
         // divisions then spread over the whole workgroup.
         for (int it = 0; it < sk_iters; ++it) {
-          for (int b = tid; b < B; b += SK_T) {   // rows (dim=1): Q /= sum_k Q[b, k]; Q /= B
-            double s = 0.0;
-            for (int k = 0; k < K; ++k) s += Q[(int64_t)b * K + k];
-            sums[b] = s;
-          }
+          for (int b = tid; b < B; b += SK_T)     // rows (dim=1): Q /= sum_k Q[b, k]; Q /= B
+            sums[b] = seq_sum<16>(Q + (int64_t)b * K, K, 1);
           __syncthreads();
-          for (int i = tid; i < B * K; i += SK_T) Q[i] = (Q[i] / sums[i / K]) / dB;
+          if (powB)
+            for (int i = tid; i < B * K; i += SK_T) Q[i] = (Q[i] / sums[i / K]) * invB;
+          else
+            for (int i = tid; i < B * K; i += SK_T) Q[i] = (Q[i] / sums[i / K]) / dB;
           __syncthreads();
-          for (int k = tid; k < K; k += SK_T) {   // columns (dim=0): Q /= sum_b Q[b, k]; Q /= K
-            double s = 0.0;
-            for (int b = 0; b < B; ++b) s += Q[(int64_t)b * K + k];
-            sums[k] = s;
-          }
+          for (int k = tid; k < K; k += SK_T)     // columns (dim=0): Q /= sum_b Q[b, k]; Q /= K
+            sums[k] = seq_sum<16>(Q + k, B, K);
           __syncthreads();
-          for (int i = tid; i < B * K; i += SK_T) Q[i] = (Q[i] / sums[i % K]) / dK;
+          if (powK)
+            for (int i = tid; i < B * K; i += SK_T) Q[i] = (Q[i] / sums[i % K]) * invK;
+          else
+            for (int i = tid; i < B * K; i += SK_T) Q[i] = (Q[i] / sums[i % K]) / dK;
           __syncthreads();
         }
       } else {
         for (int it = 0; it < sk_iters; ++it) {
           for (int b = tid; b < B; b += SK_T) {
-            double s = 0.0;
-            for (int k = 0; k < K; ++k) s += Q[(int64_t)b * K + k];
+            const double s = seq_sum<16>(Q + (int64_t)b * K, K, 1);
             for (int k = 0; k < K; ++k) Q[(int64_t)b * K + k] = (Q[(int64_t)b * K + k] / s) / dB;
           }
           __syncthreads();
           for (int k = tid; k < K; k += SK_T) {
-            double s = 0.0;
-            for (int b = 0; b < B; ++b) s += Q[(int64_t)b * K + k];
+            const double s = seq_sum<16>(Q + k, B, K);
             for (int b = 0; b < B; ++b) Q[(int64_t)b * K + k] = (Q[(int64_t)b * K + k] / s) / dK;
           }
           __syncthreads();
@@ -192,14 +210,71 @@ __global__ __launch_bounds__(SK_T) void rq_sk_kernel(const float* __restrict__ z
         if (rl == 0) idx_out[(r0 + b) * L + l] = best;
         float* rb = R + (int64_t)b * e;
         const float* cb = C + (int64_t)best * e;
+        float* xo = xq_out ? xq_out + (r0 + b) * e : nullptr;
+        float sq = 0.f;
         for (int j = rl; j < e; j += Gr) {
-          const float x = rb[j];
-          rb[j] = x - (x + (cb[j] - x));
+          const float x = rb[j], c = cb[j];
+          const float xs = x + (c - x);                   // vq.py:95 straight-through value
+          if (xo) xo[j] = l == 0 ? xs : xo[j] + xs;       // rq.py:48 x_q += x_res
+          sq = fmaf(c - x, c - x, sq);                    // (x_q - x)^2 of vq.py:88-89
+          rb[j] = x - xs;                                 // rq.py:47
+        }
+        if (sq_out) {   // the row's share of the level's mse (lanes of one row group)
+          for (int o = Gr >> 1; o > 0; o >>= 1) sq += __shfl_xor(sq, o);
+          if (rl == 0) sq_out[(r0 + b) * L + l] = sq;
         }
       }
     }
     __syncthreads();
   }
+}
+
+// Backward of the quantizer's training forward (rq.py:39-56 with vq.py:86-99 per level), for the
+// losses rq_loss = mean_l (mse(x_q_l, r_l.detach()) + beta * mse(x_q_l.detach(), r_l)):
+//   dz        = g_xq + g * beta * 2 (z - C_0[idx_0]) / (n e L)   (straight-through: x_q's gradient
+//               reaches the level-0 residual z; a later residual r_{l+1} = -(x_q_l - r_l).detach()
+//               carries none)
+//   dC_l[k]   = g * 2 / (n e L) * sum_{b : idx_l[b] = k} (C_l[k] - r_l[b])   (rows in index order)
+// r_l is recomputed from z with the forward's exact residual recurrence.  g = *g_rq (device).
+__global__ __launch_bounds__(256) void rq_sk_bwd_dz_kernel(const float* __restrict__ z, int64_t n, int e,
+                                                           const float* __restrict__ c0,
+                                                           const int64_t* __restrict__ idx, int L,
+                                                           const float* __restrict__ g_xq,
+                                                           const float* __restrict__ g_rq, float beta,
+                                                           float* __restrict__ dz) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n * e) return;
+  const int64_t b = i / e;
+  const int j = (int)(i % e);
+  const float scale = (*g_rq / (float)L) * beta * 2.0f / (float)(n * e);
+  const float cz = c0[idx[b * L] * e + j];
+  const float gx = g_xq ? g_xq[i] : 0.f;
+  dz[i] = gx + scale * (z[i] - cz);
+}
+
+__global__ __launch_bounds__(256) void rq_sk_bwd_dc_kernel(const float* __restrict__ z, int64_t n, int e,
+                                                           RQSkLevels lv, int L,
+                                                           const int64_t* __restrict__ idx,
+                                                           const float* __restrict__ g_rq, DcOut dc) {
+  // one thread per (level, code, feature)
+  int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  int l = 0;
+  while (l < L && t >= (int64_t)lv.K[l] * e) t -= (int64_t)lv.K[l] * e, ++l;
+  if (l >= L) return;
+  const int k = (int)(t / e), j = (int)(t % e);
+  const float scale = (*g_rq / (float)L) * 2.0f / (float)(n * e);
+  const float ck = lv.cb[l][(int64_t)k * e + j];
+  float acc = 0.f;
+  for (int64_t b = 0; b < n; ++b) {
+    if (idx[b * L + l] != k) continue;
+    float r = z[b * e + j];
+    for (int m = 0; m < l; ++m) {
+      const float c = lv.cb[m][idx[b * L + m] * e + j];
+      r = r - (r + (c - r));
+    }
+    acc += ck - r;
+  }
+  dc.p[l][(int64_t)k * e + j] = scale * acc;
 }
 
 }  // namespace gr
@@ -216,6 +291,16 @@ extern "C" int gr_rq_encode_sk_f32(const float* z, int64_t n, int32_t e, int32_t
                                    int32_t sk_iters, const int64_t* group_ptr, int64_t n_groups,
                                    int64_t* idx_out, void* workspace, size_t workspace_bytes,
                                    void* stream) {
+  return gr_rq_quantize_sk_train_f32(z, n, e, L, K, codebooks, sk_eps, sk_iters, group_ptr, n_groups,
+                                     idx_out, nullptr, nullptr, workspace, workspace_bytes, stream);
+}
+
+extern "C" int gr_rq_quantize_sk_train_f32(const float* z, int64_t n, int32_t e, int32_t L,
+                                           const int32_t* K, const float* const* codebooks,
+                                           const double* sk_eps, int32_t sk_iters,
+                                           const int64_t* group_ptr, int64_t n_groups, int64_t* idx_out,
+                                           float* xq_out, float* sq_out, void* workspace,
+                                           size_t workspace_bytes, void* stream) {
   using namespace gr;
   clear_error();
   if (n < 0 || e < 1 || L < 1 || n_groups < 0 || sk_iters < 0)
@@ -250,6 +335,40 @@ extern "C" int gr_rq_encode_sk_f32(const float* z, int64_t n, int32_t e, int32_t
     return fail(GR_ERR_HIP, "gr_rq_encode_sk_f32: cannot raise the LDS limit");
   hipLaunchKernelGGL(rq_sk_kernel, dim3((unsigned)n_groups), dim3(SK_T), lds,
                      reinterpret_cast<hipStream_t>(stream), z, e, L, lv, sk_iters, group_ptr, kmax,
-                     idx_out, res, qws, (int)lds_elems);
+                     idx_out, res, qws, (int)lds_elems, xq_out, sq_out);
   return check_launch("gr_rq_encode_sk_f32");
+}
+
+extern "C" int gr_rq_quantize_sk_train_bwd_f32(const float* z, int64_t n, int32_t e, int32_t L,
+                                               const int32_t* K, const float* const* codebooks,
+                                               const int64_t* idx, const float* g_xq, const float* g_rq,
+                                               float beta, float* dz_out, float* const* dcodebooks_out,
+                                               void* stream) {
+  using namespace gr;
+  clear_error();
+  if (n < 0 || e < 1 || L < 1) return fail(GR_ERR_ARG, "gr_rq_quantize_sk_train_bwd_f32: bad shape");
+  if (L > GR_MAX_LEVELS) return fail(GR_ERR_UNSUPPORTED, "gr_rq_quantize_sk_train_bwd_f32: too many levels");
+  if (!z || !K || !codebooks || !idx || !g_rq || !dz_out || !dcodebooks_out)
+    return fail(GR_ERR_ARG, "gr_rq_quantize_sk_train_bwd_f32: null pointer");
+  RQSkLevels lv{};
+  DcOut dc{};
+  int64_t tot = 0;
+  for (int l = 0; l < L; ++l) {
+    if (K[l] < 1 || !codebooks[l] || !dcodebooks_out[l])
+      return fail(GR_ERR_ARG, "gr_rq_quantize_sk_train_bwd_f32: bad codebook");
+    lv.cb[l] = codebooks[l];
+    lv.K[l] = K[l];
+    dc.p[l] = dcodebooks_out[l];
+    tot += (int64_t)K[l] * e;
+  }
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (n > 0) {
+    hipLaunchKernelGGL(rq_sk_bwd_dz_kernel, dim3((unsigned)((n * e + 255) / 256)), dim3(256), 0, st, z, n, e,
+                       codebooks[0], idx, L, g_xq, g_rq, beta, dz_out);
+    const int rc = check_launch("gr_rq_quantize_sk_train_bwd_f32 (dz)");
+    if (rc) return rc;
+  }
+  hipLaunchKernelGGL(rq_sk_bwd_dc_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, z, n, e, lv, L,
+                     idx, g_rq, dc);
+  return check_launch("gr_rq_quantize_sk_train_bwd_f32 (dC)");
 }

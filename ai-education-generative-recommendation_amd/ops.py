@@ -934,3 +934,65 @@ class RqTrainGraph:
         torch.nn.utils.clip_grad_norm_(self.model.parameters(), self.max_norm)       # :117
         self.opt.step()                                                              # :118
         return loss, loss_recon, indices
+
+
+class _RqQuantTrain(torch.autograd.Function):
+    """ResidualVectorQuantizer.forward under autograd (rq.py:39-56, vq.py:63-99) in one launch
+    forward and two backward: the assignment of every level (Sinkhorn or argmin), x_q and the mse
+    numerators (gr_rq_quantize_sk_train_f32); dz and every codebook's gradient
+    (gr_rq_quantize_sk_train_bwd_f32)."""
+
+    @staticmethod
+    def forward(ctx, z, beta, sk_eps, sk_iters, *codebooks):
+        n, e = z.shape
+        dev = z.device
+        Ks = [c.shape[0] for c in codebooks]
+        lib = L.lib()
+        ks_c = L.i32_array(Ks)
+        eps_c = (ctypes.c_double * len(codebooks))(*[float(v) for v in sk_eps])
+        nbytes = lib.gr_rq_encode_sk_workspace_bytes(n, e, len(codebooks), ks_c)
+        wsp = L.workspace(nbytes, dev)
+        idx = torch.empty((n, len(codebooks)), dtype=torch.int64, device=dev)
+        xq = torch.empty((n, e), dtype=torch.float32, device=dev)
+        sq = torch.empty((n, len(codebooks)), dtype=torch.float32, device=dev)
+        with torch.cuda.device(dev):
+            L.check(lib.gr_rq_quantize_sk_train_f32(L.ptr(z), n, e, len(codebooks), ks_c, L.ptr_array(codebooks),
+                                                    eps_c, int(sk_iters), L.ptr(_group_ptr([n], dev)), 1,
+                                                    L.ptr(idx), L.ptr(xq), L.ptr(sq), L.ptr(wsp), nbytes,
+                                                    L.stream_of(dev)), "gr_rq_quantize_sk_train_f32")
+        m = sq.sum(0) / float(n * e)                       # vq.py:88-89: mse per level
+        rq_loss = (m + beta * m).mean()                    # vq.py:90, rq.py:51
+        ctx.save_for_backward(z, idx, *codebooks)
+        ctx.beta = float(beta)
+        ctx.mark_non_differentiable(idx)
+        return xq, rq_loss, idx
+
+    @staticmethod
+    def backward(ctx, g_xq, g_rq, _g_idx):
+        z, idx, *codebooks = ctx.saved_tensors
+        n, e = z.shape
+        dev = z.device
+        g_rq = (g_rq if g_rq is not None else torch.zeros((), device=dev)).to(torch.float32).contiguous()
+        g_xq = g_xq.contiguous() if g_xq is not None else None
+        dz = torch.empty_like(z)
+        dcs = [torch.empty_like(c) for c in codebooks]
+        with torch.cuda.device(dev):
+            L.check(L.lib().gr_rq_quantize_sk_train_bwd_f32(
+                L.ptr(z), n, e, len(codebooks), L.i32_array([c.shape[0] for c in codebooks]),
+                L.ptr_array(codebooks), L.ptr(idx), L.ptr(g_xq) if g_xq is not None else None, L.ptr(g_rq),
+                ctypes.c_float(ctx.beta), L.ptr(dz), L.ptr_array(dcs), L.stream_of(dev)),
+                "gr_rq_quantize_sk_train_bwd_f32")
+        return (dz, None, None, None, *dcs)
+
+
+def rq_quantize_train(z, codebooks, beta, sk_eps, sk_iters):
+    """``(x_q, rq_loss, indices)`` of ResidualVectorQuantizer.forward(z, use_sk) in training
+    (rq.py:39-56): differentiable in ``z`` and every codebook, the whole batch one Sinkhorn group
+    per level where ``sk_eps[l] > 0`` (vq.py:76-84), the plain argmin elsewhere."""
+    L.require_gpu(z, *codebooks)
+    if z.dtype != torch.float32 or any(c.dtype != torch.float32 for c in codebooks):
+        raise TypeError("rq_quantize_train takes float32 tensors")
+    if any(c.shape[0] > 1024 for c in codebooks):
+        raise RuntimeError("rq_quantize_train: codebooks of at most 1024 codes")
+    return _RqQuantTrain.apply(z.contiguous(), float(beta), [float(v) for v in sk_eps], int(sk_iters),
+                               *[c.contiguous() if not c.is_contiguous() else c for c in codebooks])

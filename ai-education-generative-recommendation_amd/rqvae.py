@@ -203,10 +203,23 @@ class ResidualVectorQuantizer(nn.Module):
     def codebooks(self):
         return [q.embedding.weight.detach() for q in self.vq_layers]
 
+    # every level's assignment, x_q and the losses in one launch (ops.rq_quantize_train), backward
+    # in two; False (or a level still waiting for its k-means init) keeps the level-by-level path
+    fused_train = True
+
     def quantize_forward(self, x, use_sk=True, training=False):
-        """rq.py:39-56 with vq.py:63-99 per level: indices from the kernels (one launch per level:
-        the next level's residual depends on this level's assignment, and a level's k-means init
-        on the residual it sees, vq.py:66-67), values and losses under autograd."""
+        """rq.py:39-56 with vq.py:63-99 per level.  Fused path: one launch assigns every level
+        (Sinkhorn over the batch where ``use_sk`` and ``sk_epsilon > 0``, else the argmin), forms
+        x_q and the mse numerators; a custom backward gives dz and every codebook's gradient.
+        Level-by-level path (k-means init pending: a level's init needs the residual it sees,
+        vq.py:66-67): indices from the kernels, values and losses under autograd."""
+        if (self.fused_train and x.is_cuda and all(q.initted for q in self.vq_layers)
+                and all(q.n_e <= 1024 for q in self.vq_layers)):
+            eps = [float(q.sk_epsilon) if use_sk else 0.0 for q in self.vq_layers]
+            z = x.reshape(-1, self.e_dim)
+            xq, rq_loss, idx = ops.rq_quantize_train(z, [q.embedding.weight for q in self.vq_layers],
+                                                     self.beta, eps, self.sk_iters)
+            return xq.view(x.shape), rq_loss, idx.view(tuple(x.shape[:-1]) + (self.num_quantizers,))
         losses, idxs = [], []
         x_q = 0
         residual = x

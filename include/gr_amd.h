@@ -141,6 +141,27 @@ int gr_rq_encode_sk_f32(const float* z, int64_t n, int32_t e, int32_t L, const i
                         const int64_t* group_ptr, int64_t n_groups, int64_t* idx_out,
                         void* workspace, size_t workspace_bytes, void* stream);
 
+/* The quantizer's training forward (RQ-VAE/models/rq.py:39-56, vq.py:63-99 under
+ * RQ-VAE/train.py:113): gr_rq_encode_sk_f32's assignment (one group per call for a training batch)
+ * plus, when non-null, xq_out[n, e] = x_q = sum_l (r_l + (C_l[idx_l] - r_l)) and
+ * sq_out[n, L] = sum_j (C_l[idx_l] - r_l)^2 per row and level (the mse numerators).  Same
+ * workspace as gr_rq_encode_sk_f32. */
+int gr_rq_quantize_sk_train_f32(const float* z, int64_t n, int32_t e, int32_t L, const int32_t* K,
+                                const float* const* codebooks, const double* sk_eps, int32_t sk_iters,
+                                const int64_t* group_ptr, int64_t n_groups, int64_t* idx_out,
+                                float* xq_out, float* sq_out, void* workspace, size_t workspace_bytes,
+                                void* stream);
+
+/* Its backward for rq_loss = mean_l(mse(x_q_l, r_l.detach()) + beta * mse(x_q_l.detach(), r_l))
+ * (vq.py:88-92) and the straight-through x_q (vq.py:95): dz_out[n, e] = g_xq + g * beta * 2 *
+ * (z - C_0[idx_0]) / (n e L) (g_xq may be null: zero), dcodebooks_out[l][K_l, e] =
+ * g * 2 / (n e L) * sum over the rows assigned to each code of (C_l[k] - r_l), rows in index order
+ * (deterministic).  g_rq: device float scalar, the gradient of rq_loss. */
+int gr_rq_quantize_sk_train_bwd_f32(const float* z, int64_t n, int32_t e, int32_t L, const int32_t* K,
+                                    const float* const* codebooks, const int64_t* idx, const float* g_xq,
+                                    const float* g_rq, float beta, float* dz_out,
+                                    float* const* dcodebooks_out, void* stream);
+
 /* ------------------------------------------------------------------------------------------ */
 /* SASRec.  Parameters of one model, as device pointers to the tensors of SASRec.state_dict()
  * (SASRec/model.py:17-47).  Per-block fields are host arrays of length n_blocks.  The dead

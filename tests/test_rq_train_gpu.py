@@ -97,3 +97,28 @@ def test_graph_step_dropout_kmeans_schedule(dev):
     assert not all(torch.equal(a, p) for a, p in zip(before, m.parameters()))
     assert all(v == v for v in losses)        # finite
     assert losses[-1] < first, (first, losses[-1])
+
+
+@pytest.mark.parametrize("K,use_sk", [(8, True), (256, True), (256, False)])
+def test_fused_quantizer_equals_level_by_level(K, use_sk, dev):
+    """ops.rq_quantize_train (one launch forward, two backward) against the level-by-level path
+    (kernel assignment, torch values / losses / autograd): indices exact, outputs and losses within
+    1e-6, every parameter gradient within 1e-5 of its largest magnitude (torch accumulates the
+    straight-through zero terms, (g + a) - a, with rounding; the fused backward does not)."""
+    m = _model(dev, 0.0, False, K=K)
+    ref = copy.deepcopy(m)
+    ref.rq.fused_train = False
+    x = _batches(dev, 1, B=200)[0]
+    outs = []
+    for mm in (m, ref):
+        mm.zero_grad(set_to_none=True)
+        o, rq_loss, idx = mm(x, use_sk=use_sk)
+        loss, _ = mm.compute_loss(o, rq_loss, xs=x)
+        loss.backward()
+        outs.append((o.detach(), rq_loss.detach(), idx))
+    assert torch.equal(outs[0][2], outs[1][2])
+    assert (outs[0][0] - outs[1][0]).abs().max() <= 1e-6 * outs[1][0].abs().max()
+    assert abs(outs[0][1].item() - outs[1][1].item()) <= 1e-6 * abs(outs[1][1].item())
+    for (k, p), (_, q) in zip(m.named_parameters(), ref.named_parameters()):
+        err = ((p.grad - q.grad).abs().max() / q.grad.abs().max().clamp_min(1e-30)).item()
+        assert err <= 1e-5, (k, err)
