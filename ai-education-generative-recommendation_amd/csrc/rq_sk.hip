@@ -98,7 +98,17 @@ __global__ __launch_bounds__(SK_T) void rq_sk_kernel(const float* __restrict__ z
   for (int l = 0; l < L; ++l) {
     const float* C = lv.cb[l];
     const int K = lv.K[l];
-    double* Q = (int64_t)B * K <= lds_elems ? qlds : qws + r0 * Kmax;   // [B, K]
+    // [B, K] row-major (row pitch P = K; an odd LDS pitch against bank conflicts in the row pass
+    // measured slower at 64 x 8, profiles/r02_ab_sk.txt)
+    const bool in_lds = (int64_t)B * K <= lds_elems;
+    double* Q = in_lds ? qlds : qws + r0 * Kmax;
+    const int P = K;
+    const bool powK = (K & (K - 1)) == 0;
+    const int lgK = powK ? __builtin_ctz((unsigned)K) : 0;
+    auto qi = [&](int i) -> int {   // flat element i = b K + k -> its slot b P + k
+      if (P == K) return i;
+      return powK ? (i >> lgK) * P + (i & (K - 1)) : (i / K) * P + i % K;
+    };
     for (int k = tid; k < K; k += SK_T) {
       float s = 0.f;
       for (int j = 0; j < e; ++j) s = fmaf(C[(int64_t)k * e + j], C[(int64_t)k * e + j], s);
@@ -117,7 +127,7 @@ __global__ __launch_bounds__(SK_T) void rq_sk_kernel(const float* __restrict__ z
         dot = fmaf(rb[j], ck[j], dot);
       }
       const float d = (rn + cn[k]) - 2.0f * dot;
-      Q[i] = (double)d;
+      Q[b * P + k] = (double)d;
       mx = fmaxf(mx, d);
       mn = fminf(mn, d);
     }
@@ -131,54 +141,54 @@ __global__ __launch_bounds__(SK_T) void rq_sk_kernel(const float* __restrict__ z
       const float middle = (mx + mn) / 2.0f;
       const float amplitude = (mx - middle) + 1e-5f;
       for (int i = tid; i < B * K; i += SK_T) {
-        const double dc = (double)(((float)Q[i] - middle) / amplitude);
-        Q[i] = exp(-dc / eps);
+        const double dc = (double)(((float)Q[qi(i)] - middle) / amplitude);
+        Q[qi(i)] = exp(-dc / eps);
       }
       __syncthreads();
       // sum_Q = Q.sum(-1).sum(-2): row sums, then their total
       double tot = 0.0;
       if (tid < 64) {
-        for (int b = tid; b < B; b += 64) tot += seq_sum<16>(Q + (int64_t)b * K, K, 1);
+        for (int b = tid; b < B; b += 64) tot += seq_sum<16>(Q + (int64_t)b * P, K, 1);
       }
       tot = wg_reduce(tot, [](double a, double b) { return a + b; }, smd);
-      for (int i = tid; i < B * K; i += SK_T) Q[i] /= tot;
+      for (int i = tid; i < B * K; i += SK_T) Q[qi(i)] /= tot;
       __syncthreads();
       const double dB = (double)B, dK = (double)K;
       // x / 2^j and x * 2^-j round the same exact value: bitwise equal, and a multiply is far
       // cheaper than the float64 division sequence (main.py: B 64, K 8)
-      const bool powB = (B & (B - 1)) == 0, powK = (K & (K - 1)) == 0;
+      const bool powB = (B & (B - 1)) == 0;
       const double invB = 1.0 / dB, invK = 1.0 / dK;
       if (B <= SK_SUMS && K <= SK_SUMS) {
         // Each sum runs in index order in one lane (torch's CPU order for the column sums); the
         // divisions then spread over the whole workgroup.
         for (int it = 0; it < sk_iters; ++it) {
           for (int b = tid; b < B; b += SK_T)     // rows (dim=1): Q /= sum_k Q[b, k]; Q /= B
-            sums[b] = seq_sum<16>(Q + (int64_t)b * K, K, 1);
+            sums[b] = K <= 8 ? seq_sum<8>(Q + (int64_t)b * P, K, 1) : seq_sum<16>(Q + (int64_t)b * P, K, 1);
           __syncthreads();
-          if (powB)
-            for (int i = tid; i < B * K; i += SK_T) Q[i] = (Q[i] / sums[i / K]) * invB;
+          if (powB && powK)
+            for (int i = tid; i < B * K; i += SK_T) Q[qi(i)] = (Q[qi(i)] / sums[i >> lgK]) * invB;
           else
-            for (int i = tid; i < B * K; i += SK_T) Q[i] = (Q[i] / sums[i / K]) / dB;
+            for (int i = tid; i < B * K; i += SK_T) Q[qi(i)] = (Q[qi(i)] / sums[i / K]) / dB;
           __syncthreads();
           for (int k = tid; k < K; k += SK_T)     // columns (dim=0): Q /= sum_b Q[b, k]; Q /= K
-            sums[k] = seq_sum<16>(Q + k, B, K);
+            sums[k] = seq_sum<16>(Q + k, B, P);
           __syncthreads();
           if (powK)
-            for (int i = tid; i < B * K; i += SK_T) Q[i] = (Q[i] / sums[i % K]) * invK;
+            for (int i = tid; i < B * K; i += SK_T) Q[qi(i)] = (Q[qi(i)] / sums[i & (K - 1)]) * invK;
           else
-            for (int i = tid; i < B * K; i += SK_T) Q[i] = (Q[i] / sums[i % K]) / dK;
+            for (int i = tid; i < B * K; i += SK_T) Q[qi(i)] = (Q[qi(i)] / sums[i % K]) / dK;
           __syncthreads();
         }
       } else {
         for (int it = 0; it < sk_iters; ++it) {
           for (int b = tid; b < B; b += SK_T) {
-            const double s = seq_sum<16>(Q + (int64_t)b * K, K, 1);
-            for (int k = 0; k < K; ++k) Q[(int64_t)b * K + k] = (Q[(int64_t)b * K + k] / s) / dB;
+            const double s = seq_sum<16>(Q + (int64_t)b * P, K, 1);
+            for (int k = 0; k < K; ++k) Q[(int64_t)b * P + k] = (Q[(int64_t)b * P + k] / s) / dB;
           }
           __syncthreads();
           for (int k = tid; k < K; k += SK_T) {
-            const double s = seq_sum<16>(Q + k, B, K);
-            for (int b = 0; b < B; ++b) Q[(int64_t)b * K + k] = (Q[(int64_t)b * K + k] / s) / dK;
+            const double s = seq_sum<16>(Q + k, B, P);
+            for (int b = 0; b < B; ++b) Q[(int64_t)b * P + k] = (Q[(int64_t)b * P + k] / s) / dK;
           }
           __syncthreads();
         }
@@ -193,7 +203,7 @@ __global__ __launch_bounds__(SK_T) void rq_sk_kernel(const float* __restrict__ z
       double bv = 0.0;
       if (b < B) {
         for (int k = rl; k < K; k += Gr) {   // this lane's first extreme (increasing k)
-          const double v = eps > 0.0 ? Q[(int64_t)b * K + k] * (double)B : -Q[(int64_t)b * K + k];
+          const double v = eps > 0.0 ? Q[(int64_t)b * P + k] * (double)B : -Q[(int64_t)b * P + k];
           if (best == 0x7fffffff || v > bv) { bv = v; best = k; }
         }
       }

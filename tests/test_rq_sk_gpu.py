@@ -73,3 +73,25 @@ def test_infer_code_emission_matches_reference(dev, tmp_path, parity_log):
     mp = save_codes(final, f)
     assert np.array_equal(np.load(f), final)
     assert json.load(open(mp))["3"] == final[3].tolist()
+
+
+@pytest.mark.parametrize("B,K", [(64, 8), (64, 256), (2048, 8), (1500, 64)])
+def test_sinkhorn_batch_shapes_vs_oracle(B, K, dev, parity_log):
+    """One group of B rows (a training batch) at every level, against the oracle's restatement of
+    vq.py:63-99 / layers.py:85-108 level by level: the LDS-resident matrix (64 x 8, 64 x 256), the
+    large-group LDS loop (2048 x 8) and the workspace-resident matrix (1500 x 64)."""
+    from gr_amd import ops
+    from oracle import rq_oracle
+    g = torch.Generator().manual_seed(B + K)
+    z = torch.randn(B, 32, generator=g)
+    cbs = [torch.randn(K, 32, generator=g) * 0.8 for _ in range(3)]
+    got = ops.rq_quantize_sk(z.to(dev), [c.to(dev) for c in cbs], [0.01, 0.0, 0.01], 50).cpu()
+    r, ref = z.clone(), []
+    for c, eps in zip(cbs, [0.01, 0.0, 0.01]):
+        xq, ind = rq_oracle.vq_level_sk(r, c, eps, 50)
+        ref.append(ind)
+        r = r - xq
+    ref = torch.stack(ref, -1)
+    bad = int((got != ref).any(1).sum())
+    parity_log(kind="rq_sinkhorn_batch", shape=f"B{B} K{K}", rows=B, rows_differ=bad, cap=0)
+    assert bad == 0
