@@ -662,7 +662,10 @@ def _train_params(model):
 
 class _SasTrain(torch.autograd.Function):
     """Train-mode SASRec forward (dropout on) and its backward on the kernels of sasrec_train.hip:
-    one launch each; the weight gradients are dG^T A library GEMMs over the B*n rows."""
+    one launch each.  The backward leaves every parameter gradient but the item table's as a
+    per-sequence partial row of one [B, V] buffer (dW = dG^T A over the sequence's rows, bias and
+    LayerNorm column sums, positional rows), summed over B here; item-table rows are scattered in
+    the kernel."""
 
     @staticmethod
     def forward(ctx, seqs, binding, p_drop, seed_snap, *params):

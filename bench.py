@@ -773,8 +773,8 @@ def bench_calls(rq_model, sas_model, sas_n, sas_items, dev, cpu=True):
     return out
 
 
-LEGS = ["c2", "calls", "sasrec", "c4", "c5", "shard", "train"]
-OPT_LEGS = ["train_step", "rq_train_step"]   # run only when named in --legs
+LEGS = ["c2", "calls", "sasrec", "c4", "c5", "shard", "train", "train_step", "rq_train_step"]
+OPT_LEGS = []   # run only when named in --legs
 
 
 def main():
