@@ -443,9 +443,9 @@ def bench_sas_train(a, world, rank, dev):
                      "step_device_ms": eager_dev_ms},
            "roofline": {"bound": "hbm", "achieved": nbytes / (dev_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
                         "unit": "GB/s", "frac": nbytes / (dev_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                        "traffic": tr, "traffic_source": tr_src and tr_src + " (the 5 gr:: kernels; the "
-                                                                    "dM fill is a hipMemsetAsync, not counted)",
-                        "kernel": "whole step (gr_neg_samples + gr_sampled_bce fwd + bwd: 5 kernels + dM fill)",
+                        "traffic": tr, "traffic_source": tr_src and tr_src + " (the gr:: kernels of the "
+                                                                    "step as profiled)",
+                        "kernel": "whole step (gr_neg_samples + gr_sampled_bce fwd + bwd + the dM fill kernel)",
                         "bytes_per_step": nbytes, "step_device_ms": dev_ms},
            "reference_formulation_gpu": {"note": "train.py:134-167 as written ([B, n, N+1] score matrix, "
                                                  "gathers, dense backward) in torch on the same GPU, "

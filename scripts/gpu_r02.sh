@@ -40,6 +40,7 @@ for s in $STEPS; do
             python3 "$ROOT/bench.py" --legs $leg --steps 10 --warmup 3 --no-cpu-baseline --spinup-s 0.5
         cd "$ROOT"
         python3 scripts/trace_stats.py "$OUT/prof_$leg/run_kernel_trace.csv" --leg $leg > "$OUT/trace_$leg.csv" || true
+        rm -f "$OUT/prof_$leg/run_kernel_trace.csv"   # raw traces exceed gpurun's 64 MiB copy-back
       done ;;
     pmc)  # HBM traffic per bench leg and kernel: FETCH_SIZE and WRITE_SIZE in separate passes
       export TMPDIR=/tmp
