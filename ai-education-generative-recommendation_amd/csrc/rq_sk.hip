@@ -101,7 +101,6 @@ __global__ __launch_bounds__(SK_T) void rq_sk_kernel(const float* __restrict__ z
     // [B, K] row-major (row pitch P = K; an odd LDS pitch against bank conflicts in the row pass
     // measured slower at 64 x 8, profiles/r02_ab_sk.txt)
     const bool in_lds = (int64_t)B * K <= lds_elems;
-    double* Q = in_lds ? qlds : qws + r0 * Kmax;
     const int P = K;
     const bool powK = (K & (K - 1)) == 0;
     const int lgK = powK ? __builtin_ctz((unsigned)K) : 0;
@@ -109,132 +108,139 @@ __global__ __launch_bounds__(SK_T) void rq_sk_kernel(const float* __restrict__ z
       if (P == K) return i;
       return powK ? (i >> lgK) * P + (i & (K - 1)) : (i / K) * P + i % K;
     };
-    for (int k = tid; k < K; k += SK_T) {
-      float s = 0.f;
-      for (int j = 0; j < e; ++j) s = fmaf(C[(int64_t)k * e + j], C[(int64_t)k * e + j], s);
-      cn[k] = s;
-    }
-    __syncthreads();
-    // d = (|r|^2 + |c|^2) - 2 r.c in fp32 (vq.py:71-73), held as an exact double
-    float mx = -FLT_MAX, mn = FLT_MAX;
-    for (int i = tid; i < B * K; i += SK_T) {
-      const int b = i / K, k = i % K;
-      const float* rb = R + (int64_t)b * e;
-      const float* ck = C + (int64_t)k * e;
-      float rn = 0.f, dot = 0.f;
-      for (int j = 0; j < e; ++j) {
-        rn = fmaf(rb[j], rb[j], rn);
-        dot = fmaf(rb[j], ck[j], dot);
+    // The level body takes the matrix's base pointer as a parameter and is instantiated once per
+    // memory space, so the LDS copy compiles to ds_* accesses (a pointer selected at run time
+    // between LDS and the workspace would make every access a flat one).
+    auto level = [&](double* Q) __attribute__((always_inline)) {
+      for (int k = tid; k < K; k += SK_T) {
+        float s = 0.f;
+        for (int j = 0; j < e; ++j) s = fmaf(C[(int64_t)k * e + j], C[(int64_t)k * e + j], s);
+        cn[k] = s;
       }
-      const float d = (rn + cn[k]) - 2.0f * dot;
-      Q[b * P + k] = (double)d;
-      mx = fmaxf(mx, d);
-      mn = fminf(mn, d);
-    }
-    const double eps = lv.eps[l];
-    const int Gr = pow2_group(SK_T / B);            // lanes per row
-    const int rows_per = SK_T / Gr;
-    const int rg = tid / Gr, rl = tid % Gr;
-    if (eps > 0.0) {
-      mx = wg_reduce(mx, [](float a, float b) { return fmaxf(a, b); }, smf);
-      mn = wg_reduce(mn, [](float a, float b) { return fminf(a, b); }, smf);
-      const float middle = (mx + mn) / 2.0f;
-      const float amplitude = (mx - middle) + 1e-5f;
+      __syncthreads();
+      // d = (|r|^2 + |c|^2) - 2 r.c in fp32 (vq.py:71-73), held as an exact double
+      float mx = -FLT_MAX, mn = FLT_MAX;
       for (int i = tid; i < B * K; i += SK_T) {
-        const double dc = (double)(((float)Q[qi(i)] - middle) / amplitude);
-        Q[qi(i)] = exp(-dc / eps);
+        const int b = i / K, k = i % K;
+        const float* rb = R + (int64_t)b * e;
+        const float* ck = C + (int64_t)k * e;
+        float rn = 0.f, dot = 0.f;
+        for (int j = 0; j < e; ++j) {
+          rn = fmaf(rb[j], rb[j], rn);
+          dot = fmaf(rb[j], ck[j], dot);
+        }
+        const float d = (rn + cn[k]) - 2.0f * dot;
+        Q[b * P + k] = (double)d;
+        mx = fmaxf(mx, d);
+        mn = fminf(mn, d);
       }
-      __syncthreads();
-      // sum_Q = Q.sum(-1).sum(-2): row sums, then their total
-      double tot = 0.0;
-      if (tid < 64) {
-        for (int b = tid; b < B; b += 64) tot += seq_sum<16>(Q + (int64_t)b * P, K, 1);
-      }
-      tot = wg_reduce(tot, [](double a, double b) { return a + b; }, smd);
-      for (int i = tid; i < B * K; i += SK_T) Q[qi(i)] /= tot;
-      __syncthreads();
-      const double dB = (double)B, dK = (double)K;
-      // x / 2^j and x * 2^-j round the same exact value: bitwise equal, and a multiply is far
-      // cheaper than the float64 division sequence (main.py: B 64, K 8)
-      const bool powB = (B & (B - 1)) == 0;
-      const double invB = 1.0 / dB, invK = 1.0 / dK;
-      if (B <= SK_SUMS && K <= SK_SUMS) {
-        // Each sum runs in index order in one lane (torch's CPU order for the column sums); the
-        // divisions then spread over the whole workgroup.
-        for (int it = 0; it < sk_iters; ++it) {
-          for (int b = tid; b < B; b += SK_T)     // rows (dim=1): Q /= sum_k Q[b, k]; Q /= B
-            sums[b] = K <= 8 ? seq_sum<8>(Q + (int64_t)b * P, K, 1) : seq_sum<16>(Q + (int64_t)b * P, K, 1);
-          __syncthreads();
-          if (powB && powK)
-            for (int i = tid; i < B * K; i += SK_T) Q[qi(i)] = (Q[qi(i)] / sums[i >> lgK]) * invB;
-          else
-            for (int i = tid; i < B * K; i += SK_T) Q[qi(i)] = (Q[qi(i)] / sums[i / K]) / dB;
-          __syncthreads();
-          for (int k = tid; k < K; k += SK_T)     // columns (dim=0): Q /= sum_b Q[b, k]; Q /= K
-            sums[k] = seq_sum<16>(Q + k, B, P);
-          __syncthreads();
-          if (powK)
-            for (int i = tid; i < B * K; i += SK_T) Q[qi(i)] = (Q[qi(i)] / sums[i & (K - 1)]) * invK;
-          else
-            for (int i = tid; i < B * K; i += SK_T) Q[qi(i)] = (Q[qi(i)] / sums[i % K]) / dK;
-          __syncthreads();
+      const double eps = lv.eps[l];
+      const int Gr = pow2_group(SK_T / B);            // lanes per row
+      const int rows_per = SK_T / Gr;
+      const int rg = tid / Gr, rl = tid % Gr;
+      if (eps > 0.0) {
+        mx = wg_reduce(mx, [](float a, float b) { return fmaxf(a, b); }, smf);
+        mn = wg_reduce(mn, [](float a, float b) { return fminf(a, b); }, smf);
+        const float middle = (mx + mn) / 2.0f;
+        const float amplitude = (mx - middle) + 1e-5f;
+        for (int i = tid; i < B * K; i += SK_T) {
+          const double dc = (double)(((float)Q[qi(i)] - middle) / amplitude);
+          Q[qi(i)] = exp(-dc / eps);
+        }
+        __syncthreads();
+        // sum_Q = Q.sum(-1).sum(-2): row sums, then their total
+        double tot = 0.0;
+        if (tid < 64) {
+          for (int b = tid; b < B; b += 64) tot += seq_sum<16>(Q + (int64_t)b * P, K, 1);
+        }
+        tot = wg_reduce(tot, [](double a, double b) { return a + b; }, smd);
+        for (int i = tid; i < B * K; i += SK_T) Q[qi(i)] /= tot;
+        __syncthreads();
+        const double dB = (double)B, dK = (double)K;
+        // x / 2^j and x * 2^-j round the same exact value: bitwise equal, and a multiply is far
+        // cheaper than the float64 division sequence (main.py: B 64, K 8)
+        const bool powB = (B & (B - 1)) == 0;
+        const double invB = 1.0 / dB, invK = 1.0 / dK;
+        if (B <= SK_SUMS && K <= SK_SUMS) {
+          // Each sum runs in index order in one lane (torch's CPU order for the column sums); the
+          // divisions then spread over the whole workgroup.
+          for (int it = 0; it < sk_iters; ++it) {
+            for (int b = tid; b < B; b += SK_T)     // rows (dim=1): Q /= sum_k Q[b, k]; Q /= B
+              sums[b] = K <= 8 ? seq_sum<8>(Q + (int64_t)b * P, K, 1) : seq_sum<16>(Q + (int64_t)b * P, K, 1);
+            __syncthreads();
+            if (powB && powK)
+              for (int i = tid; i < B * K; i += SK_T) Q[qi(i)] = (Q[qi(i)] / sums[i >> lgK]) * invB;
+            else
+              for (int i = tid; i < B * K; i += SK_T) Q[qi(i)] = (Q[qi(i)] / sums[i / K]) / dB;
+            __syncthreads();
+            for (int k = tid; k < K; k += SK_T)     // columns (dim=0): Q /= sum_b Q[b, k]; Q /= K
+              sums[k] = seq_sum<16>(Q + k, B, P);
+            __syncthreads();
+            if (powK)
+              for (int i = tid; i < B * K; i += SK_T) Q[qi(i)] = (Q[qi(i)] / sums[i & (K - 1)]) * invK;
+            else
+              for (int i = tid; i < B * K; i += SK_T) Q[qi(i)] = (Q[qi(i)] / sums[i % K]) / dK;
+            __syncthreads();
+          }
+        } else {
+          for (int it = 0; it < sk_iters; ++it) {
+            for (int b = tid; b < B; b += SK_T) {
+              const double s = seq_sum<16>(Q + (int64_t)b * P, K, 1);
+              for (int k = 0; k < K; ++k) Q[(int64_t)b * P + k] = (Q[(int64_t)b * P + k] / s) / dB;
+            }
+            __syncthreads();
+            for (int k = tid; k < K; k += SK_T) {
+              const double s = seq_sum<16>(Q + k, B, P);
+              for (int b = 0; b < B; ++b) Q[(int64_t)b * P + k] = (Q[(int64_t)b * P + k] / s) / dK;
+            }
+            __syncthreads();
+          }
         }
       } else {
-        for (int it = 0; it < sk_iters; ++it) {
-          for (int b = tid; b < B; b += SK_T) {
-            const double s = seq_sum<16>(Q + (int64_t)b * P, K, 1);
-            for (int k = 0; k < K; ++k) Q[(int64_t)b * P + k] = (Q[(int64_t)b * P + k] / s) / dB;
+        __syncthreads();
+      }
+      // per row: first argmax of Q * B (Sinkhorn levels) or first argmin of d; residual update
+      for (int b0 = 0; b0 < B; b0 += rows_per) {
+        const int b = b0 + rg;
+        int best = 0x7fffffff;
+        double bv = 0.0;
+        if (b < B) {
+          for (int k = rl; k < K; k += Gr) {   // this lane's first extreme (increasing k)
+            const double v = eps > 0.0 ? Q[(int64_t)b * P + k] * (double)B : -Q[(int64_t)b * P + k];
+            if (best == 0x7fffffff || v > bv) { bv = v; best = k; }
           }
-          __syncthreads();
-          for (int k = tid; k < K; k += SK_T) {
-            const double s = seq_sum<16>(Q + k, B, P);
-            for (int b = 0; b < B; ++b) Q[(int64_t)b * P + k] = (Q[(int64_t)b * P + k] / s) / dK;
+        }
+        for (int o = Gr >> 1; o > 0; o >>= 1) {   // larger value, then the lower index
+          const double ov = __shfl_xor(bv, o);
+          const int oi = __shfl_xor(best, o);
+          if (oi != 0x7fffffff && (best == 0x7fffffff || ov > bv || (ov == bv && oi < best))) {
+            bv = ov;
+            best = oi;
           }
-          __syncthreads();
+        }
+        if (b < B) {
+          if (best == 0x7fffffff || best >= K) best = 0;
+          if (rl == 0) idx_out[(r0 + b) * L + l] = best;
+          float* rb = R + (int64_t)b * e;
+          const float* cb = C + (int64_t)best * e;
+          float* xo = xq_out ? xq_out + (r0 + b) * e : nullptr;
+          float sq = 0.f;
+          for (int j = rl; j < e; j += Gr) {
+            const float x = rb[j], c = cb[j];
+            const float xs = x + (c - x);                   // vq.py:95 straight-through value
+            if (xo) xo[j] = l == 0 ? xs : xo[j] + xs;       // rq.py:48 x_q += x_res
+            sq = fmaf(c - x, c - x, sq);                    // (x_q - x)^2 of vq.py:88-89
+            rb[j] = x - xs;                                 // rq.py:47
+          }
+          if (sq_out) {   // the row's share of the level's mse (lanes of one row group)
+            for (int o = Gr >> 1; o > 0; o >>= 1) sq += __shfl_xor(sq, o);
+            if (rl == 0) sq_out[(r0 + b) * L + l] = sq;
+          }
         }
       }
-    } else {
-      __syncthreads();
-    }
-    // per row: first argmax of Q * B (Sinkhorn levels) or first argmin of d; residual update
-    for (int b0 = 0; b0 < B; b0 += rows_per) {
-      const int b = b0 + rg;
-      int best = 0x7fffffff;
-      double bv = 0.0;
-      if (b < B) {
-        for (int k = rl; k < K; k += Gr) {   // this lane's first extreme (increasing k)
-          const double v = eps > 0.0 ? Q[(int64_t)b * P + k] * (double)B : -Q[(int64_t)b * P + k];
-          if (best == 0x7fffffff || v > bv) { bv = v; best = k; }
-        }
-      }
-      for (int o = Gr >> 1; o > 0; o >>= 1) {   // larger value, then the lower index
-        const double ov = __shfl_xor(bv, o);
-        const int oi = __shfl_xor(best, o);
-        if (oi != 0x7fffffff && (best == 0x7fffffff || ov > bv || (ov == bv && oi < best))) {
-          bv = ov;
-          best = oi;
-        }
-      }
-      if (b < B) {
-        if (best == 0x7fffffff || best >= K) best = 0;
-        if (rl == 0) idx_out[(r0 + b) * L + l] = best;
-        float* rb = R + (int64_t)b * e;
-        const float* cb = C + (int64_t)best * e;
-        float* xo = xq_out ? xq_out + (r0 + b) * e : nullptr;
-        float sq = 0.f;
-        for (int j = rl; j < e; j += Gr) {
-          const float x = rb[j], c = cb[j];
-          const float xs = x + (c - x);                   // vq.py:95 straight-through value
-          if (xo) xo[j] = l == 0 ? xs : xo[j] + xs;       // rq.py:48 x_q += x_res
-          sq = fmaf(c - x, c - x, sq);                    // (x_q - x)^2 of vq.py:88-89
-          rb[j] = x - xs;                                 // rq.py:47
-        }
-        if (sq_out) {   // the row's share of the level's mse (lanes of one row group)
-          for (int o = Gr >> 1; o > 0; o >>= 1) sq += __shfl_xor(sq, o);
-          if (rl == 0) sq_out[(r0 + b) * L + l] = sq;
-        }
-      }
-    }
+    };
+    if (in_lds) level(qlds);
+    else level(qws + r0 * Kmax);
     __syncthreads();
   }
 }
