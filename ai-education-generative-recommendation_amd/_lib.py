@@ -60,6 +60,9 @@ SIGNATURES = {
     "gr_rq_encode_sk_workspace_bytes": (_sz, [_i64, _i32, _i32, _vp]),
     "gr_rq_encode_sk_f32": (ctypes.c_int, [_vp, _i64, _i32, _i32, _vp, _vp, _vp, _i32, _vp, _i64,
                                            _vp, _vp, _sz, _vp]),
+    "gr_mlp_train_fwd_f32": (ctypes.c_int, [_vp, _i64, _i32, _vp, _vp, _vp, _f32, _vp, _vp, _vp, _vp]),
+    "gr_mlp_train_bwd_layer_f32": (ctypes.c_int, [_vp, _i64, _i32, _vp, _i32, _vp, _i32, _f32, _vp, _i32,
+                                                  _vp, _vp, _vp, _vp]),
     "gr_rq_quantize_sk_train_f32": (ctypes.c_int, [_vp, _i64, _i32, _i32, _vp, _vp, _vp, _i32, _vp, _i64,
                                                    _vp, _vp, _vp, _vp, _sz, _vp]),
     "gr_rq_quantize_sk_train_bwd_f32": (ctypes.c_int, [_vp, _i64, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _f32,

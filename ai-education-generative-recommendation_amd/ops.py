@@ -999,3 +999,77 @@ def rq_quantize_train(z, codebooks, beta, sk_eps, sk_iters):
         raise RuntimeError("rq_quantize_train: codebooks of at most 1024 codes")
     return _RqQuantTrain.apply(z.contiguous(), float(beta), [float(v) for v in sk_eps], int(sk_iters),
                                *[c.contiguous() if not c.is_contiguous() else c for c in codebooks])
+
+
+class _MlpTrain(torch.autograd.Function):
+    """MLPLayers.forward in train mode (RQ-VAE/models/layers.py:18-43) and its backward on the
+    kernels of rq_mlp_train.hip: the input dropout, then one launch per layer forward (bias, ReLU,
+    and the next layer's dropout in the epilogue) and one per layer backward (weight and bias
+    gradients and the input gradient with the ReLU and dropout masks folded in)."""
+
+    @staticmethod
+    def forward(ctx, x, p, snap, *params):
+        ws, bs = params[0::2], params[1::2]
+        n = len(ws)
+        M = x.shape[0]
+        dev = x.device
+        dims = [x.shape[1]] + [w.shape[0] for w in ws]
+        outs = [torch.empty((M, dd), dtype=torch.float32, device=dev) for dd in dims[1:]]
+        xd0 = torch.empty_like(x) if p > 0 else x
+        with torch.cuda.device(dev):
+            L.check(L.lib().gr_mlp_train_fwd_f32(L.ptr(x), M, n, L.i32_array(dims), L.ptr_array(ws),
+                                                 L.ptr_array(bs), float(p), L.ptr(snap),
+                                                 L.ptr(xd0) if p > 0 else None, L.ptr_array(outs),
+                                                 L.stream_of(dev)), "gr_mlp_train_fwd_f32")
+        ctx.save_for_backward(xd0, snap, *outs[:-1], *ws)
+        ctx.p, ctx.n = float(p), n
+        return outs[-1]
+
+    @staticmethod
+    def backward(ctx, dout):
+        xd0, snap, *rest = ctx.saved_tensors
+        n = ctx.n
+        acts, ws = [xd0] + rest[:n - 1], rest[n - 1:]
+        M = xd0.shape[0]
+        dev = xd0.device
+        dz = dout.contiguous().float()
+        gw, gb = [None] * n, [None] * n
+        with torch.cuda.device(dev):
+            for i in reversed(range(n)):
+                K, N = acts[i].shape[1], ws[i].shape[0]
+                dW = torch.empty_like(ws[i])
+                db = torch.empty((N,), dtype=torch.float32, device=dev)
+                dX = (torch.empty((M, K), dtype=torch.float32, device=dev)
+                      if i > 0 or ctx.needs_input_grad[0] else None)
+                L.check(L.lib().gr_mlp_train_bwd_layer_f32(
+                    L.ptr(acts[i]), M, K, L.ptr(ws[i]), N, L.ptr(dz), 1 if i > 0 else 2, ctx.p, L.ptr(snap), 0,
+                    L.ptr(dW), L.ptr(db), L.ptr(dX), L.stream_of(dev)), "gr_mlp_train_bwd_layer_f32")
+                gw[i], gb[i] = dW, db
+                dz = dX
+        grads = [dz if ctx.needs_input_grad[0] else None, None, None]
+        for w, b in zip(gw, gb):
+            grads += [w, b]
+        return tuple(grads)
+
+
+def mlp_train_supported(mlp, x):
+    lin = mlp.linears()
+    return (x.is_cuda and x.dim() == 2 and x.dtype == torch.float32 and not mlp.use_bn
+            and (mlp.act == "relu" or len(lin) == 1) and all(m.bias is not None for m in lin)
+            and x.shape[1] == lin[0].weight.shape[1])
+
+
+def mlp_train(x, mlp):
+    """``mlp.mlp_layers(x)`` under autograd (RQ-VAE/models/layers.py:42-43 as RQVAE.forward calls it
+    in training, RQ-VAE/train.py:113): dropout (train mode), Linear, ReLU on the fused training
+    kernels, differentiable in ``x`` and every Linear's weight and bias.  Dropout masks come from the
+    device's seed word (``dropout_seed``), so a captured step replays with fresh masks."""
+    L.require_gpu(x)
+    p = float(mlp.dropout) if mlp.training else 0.0
+    seed = dropout_seed(x.device)
+    snap = seed + 0              # this call's masks (its backward reads the same word)
+    seed.add_(1)
+    params = []
+    for m in mlp.linears():
+        params += [m.weight, m.bias]
+    return _MlpTrain.apply(x.contiguous(), p, snap, *params)

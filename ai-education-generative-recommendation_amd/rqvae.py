@@ -129,6 +129,17 @@ class MLPLayers(nn.Module):
             x = ops.linear(x, w, b, act=(self.act or "none") if i + 1 < len(ws) else "none")
         return x
 
+    # train-mode forward under autograd on the fused training kernels (ops.mlp_train: one launch per
+    # layer and direction); False keeps the torch modules
+    fused_train = True
+
+    def train_forward(self, x):
+        """layers.py:42-43 under autograd (the RQVAE.forward call of RQ-VAE/train.py:113): ReLU MLPs
+        without BatchNorm on ``ops.mlp_train``, anything else on the torch modules."""
+        if self.fused_train and ops.mlp_train_supported(self, x):
+            return ops.mlp_train(x, self)
+        return self.mlp_layers(x)
+
     def forward(self, x):
         if self.training and (self.dropout > 0 or self.use_bn):
             raise RuntimeError("gr_amd MLPLayers runs the eval-mode encoder: call .eval() (dropout / "
@@ -274,17 +285,20 @@ class RQVAE(nn.Module):
 
     def forward(self, x, use_sk=True):
         """rqvae.py:60-65 -> ``(out, rq_loss, indices)``, differentiable (the RQ-VAE/train.py:113 call;
-        SURVEY §8f row 4).  The codebook assignment of every level — vq.py:69-84: the fp32 distance
-        matrix and its argmin, or the batch-coupled Sinkhorn when ``use_sk`` and ``sk_epsilon > 0``
-        (main.py trains with eps 0.01 at every level) — runs on the gfx950 kernels, on the residual
-        exactly as the reference forms it; the straight-through values, the codebook / commitment
-        losses (vq.py:88-95) and the encoder / decoder MLPs stay under autograd (torch modules,
-        dropout active in train mode).  With grad disabled in eval mode, the encoder and decoder
-        also run on the kernels (``gr_rq_mlp_f32`` / ``gr_linear_f32``)."""
+        SURVEY §8f row 4), on the gfx950 kernels end to end:
+        * encoder and decoder: ``MLPLayers.train_forward`` (dropout in train mode, Linear, ReLU;
+          one launch per layer forward and backward, ``ops.mlp_train``);
+        * the quantizer: every level's assignment -- vq.py:69-84, the fp32 distance matrix and its
+          argmin, or the batch-coupled Sinkhorn when ``use_sk`` and ``sk_epsilon > 0`` (main.py
+          trains with eps 0.01 at every level) -- on the residual exactly as the reference forms
+          it, with x_q and the codebook / commitment losses (vq.py:88-95) in the same launch and a
+          two-launch backward (``ops.rq_quantize_train``).
+        With grad disabled in eval mode the encoder and decoder run the inference kernels
+        (``gr_rq_mlp_f32`` / ``gr_linear_f32``)."""
         fast = not torch.is_grad_enabled() and not self.training
-        z = self.encoder(x) if fast else self.encoder.mlp_layers(x)
+        z = self.encoder(x) if fast else self.encoder.train_forward(x)
         x_q, rq_loss, indices = self.rq.quantize_forward(z, use_sk, self.training)
-        out = self.decoder.eval_forward(x_q) if fast else self.decoder.mlp_layers(x_q)
+        out = self.decoder.eval_forward(x_q) if fast else self.decoder.train_forward(x_q)
         return out, rq_loss, indices
 
     def compute_loss(self, out, quant_loss, xs=None):

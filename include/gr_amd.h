@@ -128,6 +128,27 @@ int gr_rq_mlp_f32(const float* x, int64_t n, int32_t n_linear, const int32_t* di
                   const float* const* weights, const float* const* biases, float* z_out,
                   void* workspace, size_t workspace_bytes, void* stream);
 
+/* MLPLayers.forward in train mode (RQ-VAE/models/layers.py:18-43, [Dropout -> Linear -> ReLU] x
+ * (n_linear - 1), then Dropout -> Linear; RQVAE.forward under RQ-VAE/train.py:113).  Dropout p_drop
+ * on every layer input, masks from a counter-based hash of (*seed_dev, layer, element) -- torch's
+ * distribution, not its random stream (seed_dev and xd0 may be null when p_drop = 0).  Outputs:
+ * xd0[M, dims[0]] = the dropped input (p_drop > 0), outs[i][M, dims[i+1]] = the next layer's dropped
+ * input drop(relu(X_i W_i^T + b_i)) for i < n_linear - 1 and the MLP output for the last layer --
+ * the tensors the backward reads. */
+int gr_mlp_train_fwd_f32(const float* x, int64_t M, int32_t n_linear, const int32_t* dims,
+                         const float* const* weights, const float* const* biases, float p_drop,
+                         const uint64_t* seed_dev, float* xd0, float* const* outs, void* stream);
+
+/* Backward of layer i of such an MLP (the autograd of layers.py's Linear / ReLU / Dropout,
+ * train.py:116), one launch, on the layer's dropped input xd_in (xd0, or outs[i-1] of the forward):
+ * dweight[N, K] = dz^T xd_in, dbias[N] = column sums of dz (rows in order), and (dx_out non-null)
+ * dx_out[M, K] = (dz W) * mask, mask per dx_mode: 1 = (xd_in > 0 ? 1 / (1 - p) : 0) (the input came
+ * through ReLU: ReLU' and dropout), 2 = the dropout hash mask of `site` (the first layer), 0 = none.
+ * dz[M, N] is the gradient of this layer's pre-activation output. */
+int gr_mlp_train_bwd_layer_f32(const float* xd_in, int64_t M, int32_t K, const float* weight, int32_t N,
+                               const float* dz, int32_t dx_mode, float p_drop, const uint64_t* seed_dev,
+                               int32_t site, float* dweight, float* dbias, float* dx_out, void* stream);
+
 /* RQVAE.get_indices(xs, use_sk=True) over independent row groups (the collision re-encode of
  * RQ-VAE/infer.py:108-130; vq.py:52-61, 76-84; layers.py:85-108).  z[n, e]: encoder outputs (as
  * gr_rq_encode_f32's z_out), rows grouped contiguously: group g = rows [group_ptr[g],
