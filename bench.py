@@ -625,8 +625,11 @@ def bench_rq_train_step(a, world, rank, dev, cpu=False):
         for q in m.rq.vq_layers:   # stands in for the k-means init of the first batch
             q.embedding.weight.data.normal_(0.0, 0.3)
         m = m.to(dev).train()
-        lr = torch.tensor(1e-3, device=dev) if capturable else 1e-3
-        o = torch.optim.AdamW(m.parameters(), lr=lr, weight_decay=1e-4, capturable=capturable)
+        if capturable:   # the drop-in's step: the fused AdamW kernel (capturable, tensor lr)
+            o = torch.optim.AdamW(m.parameters(), lr=torch.tensor(1e-3, device=dev), weight_decay=1e-4,
+                                  capturable=True, fused=True)
+        else:            # train.py:56-63 as written (foreach AdamW)
+            o = torch.optim.AdamW(m.parameters(), lr=1e-3, weight_decay=1e-4)
         return m, o, get_linear_schedule_with_warmup(o, 10, 10_000)
 
     x = synth.items(B, 13 + rank, dev)   # BERT-statistics item embeddings
@@ -661,8 +664,8 @@ def bench_rq_train_step(a, world, rank, dev, cpu=False):
            "ms_per_step": step_ms, "scaling": "weak",
            "config": {"workload": "rq_train_step: RQ-VAE train.py:108-119 whole step at main.py's configuration "
                                   "(batch 64, 768 -> [256,128] -> 32, 3x8 codebooks, Sinkhorn eps 0.01 x 50 "
-                                  "iterations per level on the kernels, dropout 0.1, AdamW, clip 1.0, linear "
-                                  "warm-up schedule), one captured graph",
+                                  "iterations per level on the kernels, dropout 0.1, AdamW (fused, capturable), "
+                                  "clip 1.0, linear warm-up schedule), one captured graph",
                       "items_per_rank_per_step": B, "parallelism": f"item-sharded x{world} (data parallel "
                                                                   f"without the gradient all-reduce)"},
            "roofline": {"bound": "mfma", "achieved": fl / (dev_ms * 1e-3) / 1e12, "peak": FP32_PEAK_TFLOPS,
