@@ -15,7 +15,8 @@ m = RQVAE(in_dim=768, num_emb_list=[8, 8, 8], e_dim=32, layers=[256, 128], dropo
 for q in m.rq.vq_layers:
     q.embedding.weight.data.normal_(0.0, 0.3)
 m = m.to(dev).train()
-opt = torch.optim.AdamW(m.parameters(), lr=torch.tensor(1e-3, device=dev), weight_decay=1e-4, capturable=True)
+opt = torch.optim.AdamW(m.parameters(), lr=torch.tensor(1e-3, device=dev), weight_decay=1e-4, capturable=True,
+                        fused=True)
 step = ops.RqTrainGraph(m, opt, synth.items(64, 13, dev), sync=False)
 torch.cuda.synchronize()
 for _ in range(int(os.environ.get("GR_REPLAYS", "20"))):
