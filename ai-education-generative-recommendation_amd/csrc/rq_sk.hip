@@ -26,7 +26,7 @@ struct RQSkLevels {
   double eps[GR_MAX_LEVELS];
 };
 
-constexpr int SK_T = 256;
+constexpr int SK_T = 1024;   // 16 waves: the divisions of a half-step spread over all of them (profiles/r02_ab_sk.txt)
 struct DcOut {
   float* p[GR_MAX_LEVELS];
 };
