@@ -52,6 +52,9 @@ static std::atomic<int64_t> g_rq_waves{8};
 // rq_split (1: a quantize workgroup's c % 4 leftover item tiles are split into code quarters, one
 // per SIMD, so the SIMDs' loads differ by at most a quarter tile; 0: round-robin tiles over waves).
 static std::atomic<int64_t> g_rq_split{1};
+// rq_enc_w8 (1 (default): the fused encoder at 8 waves per workgroup, 2 per SIMD, one 32-feature
+// L1 tile each; 0: 4 waves, two tiles each -- bitwise the same z)
+static std::atomic<int64_t> g_rq_enc_w8{1};
 // score_slice_major (direct-store scoring: 1 = an XCD's workgroups share catalog slices across
 // user blocks (default: 255 vs 261 us at C3, scripts/ab_opt.py), 0 = they share a user block).
 static std::atomic<int64_t> g_score_slice_major{1};
@@ -88,6 +91,7 @@ int64_t option(const char* name) {
   if (!strcmp(name, "rq_resident")) return g_rq_resident.load();
   if (!strcmp(name, "rq_waves")) return g_rq_waves.load();
   if (!strcmp(name, "rq_split")) return g_rq_split.load();
+  if (!strcmp(name, "rq_enc_w8")) return g_rq_enc_w8.load();
   if (!strcmp(name, "score_slice_major")) return g_score_slice_major.load();
   if (!strcmp(name, "attn_occ1")) return g_attn_occ1.load();
   if (!strcmp(name, "attn_alt")) return g_attn_alt.load();
@@ -117,6 +121,7 @@ extern "C" int gr_set_option(const char* name, int64_t value) {
   if (!strcmp(name, "rq_resident") && (value == 0 || value == 1)) { gr::g_rq_resident = value; return GR_OK; }
   if (!strcmp(name, "rq_waves") && (value == 8 || value == 16)) { gr::g_rq_waves = value; return GR_OK; }
   if (!strcmp(name, "rq_split") && (value == 0 || value == 1)) { gr::g_rq_split = value; return GR_OK; }
+  if (!strcmp(name, "rq_enc_w8") && (value == 0 || value == 1)) { gr::g_rq_enc_w8 = value; return GR_OK; }
   if (!strcmp(name, "score_slice_major") && (value == 0 || value == 1)) { gr::g_score_slice_major = value; return GR_OK; }
   if (!strcmp(name, "attn_occ1") && (value == 0 || value == 1)) { gr::g_attn_occ1 = value; return GR_OK; }
   if (!strcmp(name, "attn_alt") && (value == 0 || value == 1)) { gr::g_attn_alt = value; return GR_OK; }

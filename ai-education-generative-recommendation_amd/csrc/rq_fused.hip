@@ -3,7 +3,9 @@
 // the first half of RQVAE.get_indices, rqvae.py:67-71); the residual quantization of z runs in
 // rq_quantize_kernel (rq.hip).
 //
-// Grid = one 4-wave workgroup per CU.  Items are cut into 32-item tiles and every workgroup owns a
+// Grid = one workgroup per CU: 8 waves (default, rq_enc_w8; 2 per SIMD, wave w owns L1 features
+// [32w, 32w+32) and L2 feature tile w % 4 of item tile w / 4) or 4 waves (the description below;
+// 493 -> 483 us per C2 call at 8 waves, profiles/r02_ab_quant_ablation.txt, bitwise the same z).  Items are cut into 32-item tiles and every workgroup owns a
 // contiguous, balanced range of tiles (100k items -> 12 or 13 tiles per CU: the chip-level tail is
 // one tile, ~6 %).  A workgroup walks its range in PASSES of FP tiles (a trailing single tile runs
 // a 1-tile instantiation, so a pass costs in proportion to its tiles).  Per pass:
@@ -44,23 +46,27 @@ constexpr int FP = 2;             // tiles per pass
 constexpr int FXC = 64;           // x k-chunk
 constexpr int FXP = FXC + 4;      // LDS pitch of the x image (== 4 mod 64: conflict-free b128)
 
-template <int H1, int H2>
+template <int H1, int H2, int WV = 4>
 struct FusedCfg {
   static constexpr int E = 32;
-  static constexpr int TW1 = H1 / 128;   // L1 feature tiles per wave
-  static constexpr int TW2 = H2 / 128;   // L2 feature tiles per wave
+  static constexpr int NTH = 64 * WV;     // threads per workgroup
+  static constexpr int TW1 = H1 / (32 * WV);   // L1 feature tiles per wave
+  // L2: 4 waves: every wave H2 / 128 feature tiles for all item tiles of the pass; 8 waves: wave w
+  // feature tile w % 4 of item tile w / 4
+  static constexpr int TW2 = WV == 4 ? H2 / 128 : 1;
   static constexpr int P1 = H1 + 4, P2 = H2 + 4, PZ = E + 4;
   static constexpr int PI = FP * FT;     // items per (full) pass
-  static constexpr int XV = PI * 16 / 256;
+  static constexpr int XV = PI * 16 / NTH;
   static constexpr int LDS = 2 * PI * FXP + PI * P1 + PI * P2;
-  static_assert(TW1 >= 1 && TW2 >= 1 && H1 % 128 == 0 && H2 % 128 == 0, "hidden sizes");
+  static_assert(TW1 >= 1 && TW2 >= 1 && H1 % (32 * WV) == 0 && H2 % 128 == 0, "hidden sizes");
+  static_assert(WV == 4 || (WV == 8 && H2 == 128), "8-wave form: H2 = 128");
   static_assert(4 * PI * PZ <= PI * P1, "z partials must fit in the h1 image");
 };
 
 // Per-workgroup state that lives across passes (x staging registers, W1 prefetch, LDS buffer).
-template <int H1, int H2>
+template <int H1, int H2, int WV = 4>
 struct FusedCtx {
-  using C = FusedCfg<H1, H2>;
+  using C = FusedCfg<H1, H2, WV>;
   const float* x;
   int64_t n;
   int D0, NC, t_end;
@@ -79,7 +85,7 @@ struct FusedCtx {
   __device__ __forceinline__ void gload_x(int tb, int c) {
 #pragma unroll
     for (int i = 0; i < C::XV; ++i) {
-      const int f = tid + 256 * i, it = f >> 4, k4 = (f & 15) * 4;
+      const int f = tid + C::NTH * i, it = f >> 4, k4 = (f & 15) * 4;
       const int64_t item = (int64_t)tb * FT + it;
       xok[i] = item < n && (tb + it / FT) < t_end;
       xr[i] = *reinterpret_cast<const f32x4*>(x + (item < n ? item : n - 1) * D0 +
@@ -89,7 +95,7 @@ struct FusedCtx {
   __device__ __forceinline__ void swrite_x(int b) {
 #pragma unroll
     for (int i = 0; i < C::XV; ++i) {
-      const int f = tid + 256 * i;
+      const int f = tid + C::NTH * i;
       *reinterpret_cast<f32x4*>(xs + b * C::PI * FXP + (f >> 4) * FXP + (f & 15) * 4) =
           xok[i] ? xr[i] : f32x4{0.f, 0.f, 0.f, 0.f};
     }
@@ -98,9 +104,9 @@ struct FusedCtx {
 
 // One pass over NP (compile-time) item tiles starting at tile tb.  No runtime branch depends on
 // the number of tiles, so the accumulators stay in AGPRs across the MFMA loops.
-template <int NP, int H1, int H2>
-__device__ __forceinline__ void rq_fused_pass(FusedCtx<H1, H2>& cx, int tb) {
-  using C = FusedCfg<H1, H2>;
+template <int NP, int H1, int H2, int WV>
+__device__ __forceinline__ void rq_fused_pass(FusedCtx<H1, H2, WV>& cx, int tb) {
+  using C = FusedCfg<H1, H2, WV>;
   constexpr int E = C::E, TW1 = C::TW1, TW2 = C::TW2, P1 = C::P1, P2 = C::P2, PZ = C::PZ,
                 PI = C::PI;
   const int w = cx.w, r = cx.r, h = cx.h;
@@ -138,7 +144,7 @@ __device__ __forceinline__ void rq_fused_pass(FusedCtx<H1, H2>& cx, int tb) {
   bool xok_cur[C::XV], xok_nxt[C::XV];   // rows past n / past this workgroup's range -> zeros
 #pragma unroll
   for (int i = 0; i < C::XV; ++i) {
-    const int f = cx.tid + 256 * i, it = f >> 4, k4 = (f & 15) * 4;
+    const int f = cx.tid + C::NTH * i, it = f >> 4, k4 = (f & 15) * 4;
     const int64_t a = (int64_t)tb * FT + it, b = (int64_t)next_tb * FT + it;
     xsrc[i] = cx.x + (a < cx.n ? a : cx.n - 1) * cx.D0 + k4;
     xnxt[i] = cx.x + (b < cx.n ? b : cx.n - 1) * cx.D0 + k4;
@@ -192,7 +198,7 @@ __device__ __forceinline__ void rq_fused_pass(FusedCtx<H1, H2>& cx, int tb) {
       const bool same = c + 1 < NC;
 #pragma unroll
       for (int i = 0; i < C::XV; ++i) {
-        const int f = cx.tid + 256 * i;
+        const int f = cx.tid + C::NTH * i;
         const bool ok = same ? xok_cur[i] : xok_nxt[i];
         *reinterpret_cast<f32x4*>(cx.xs + (cx.buf ^ 1) * PI * FXP + (f >> 4) * FXP + (f & 15) * 4) =
             ok ? cx.xr[i] : f32x4{0.f, 0.f, 0.f, 0.f};
@@ -212,6 +218,7 @@ __device__ __forceinline__ void rq_fused_pass(FusedCtx<H1, H2>& cx, int tb) {
     constexpr int NW = 4 * TW1;
 #endif
     static_assert(NW + 4 * (NP - 1) + NX + 2 * NDW <= M1, "schedule");
+    {
     __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
 #pragma unroll
     for (int i = 0; i < NW; ++i) {
@@ -235,6 +242,7 @@ __device__ __forceinline__ void rq_fused_pass(FusedCtx<H1, H2>& cx, int tb) {
       __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
     }
     __builtin_amdgcn_sched_group_barrier(0x008, NDW, 0);
+    }
 #pragma unroll
     for (int t = 0; t < TW1; ++t)
 #pragma unroll
@@ -270,20 +278,26 @@ __device__ __forceinline__ void rq_fused_pass(FusedCtx<H1, H2>& cx, int tb) {
   GR_STAMP(s2);
 
   // ------------------------------------------------------------------ L2: W2 . h1^T
-  f32x16 acc2[TW2][NP];
+  // 4 waves: wave w, feature tiles [w TW2, w TW2 + TW2) for all NP item tiles; 8 waves: feature
+  // tile w % 4 of item tile w / 4 (a one-tile pass leaves waves 4-7 idle here)
+  constexpr int NP2 = WV == 4 ? NP : 1;
+  const int ft0 = WV == 4 ? w * TW2 : (w & 3);
+  const int it0 = WV == 4 ? 0 : (w >> 2);
+  const bool l2_on = it0 < NP;   // wave-uniform
+  f32x16 acc2[TW2][NP2];
 #pragma unroll
   for (int t = 0; t < TW2; ++t)
 #pragma unroll
-    for (int it = 0; it < NP; ++it)
+    for (int it = 0; it < NP2; ++it)
 #pragma unroll
       for (int v = 0; v < 16; ++v) acc2[t][it][v] = 0.f;
-  {
-    const float* hb = cx.h1s + r * P1 + 16 * h;
+  if (l2_on) {
+    const float* hb = cx.h1s + (it0 * FT + r) * P1 + 16 * h;
     const float* w2row[TW2];
     f32x4 aw2[TW2][4];
 #pragma unroll
     for (int t = 0; t < TW2; ++t) {
-      w2row[t] = cx.W2 + (int64_t)((w * TW2 + t) * 32 + r) * H1 + 16 * h;
+      w2row[t] = cx.W2 + (int64_t)((ft0 + t) * 32 + r) * H1 + 16 * h;
 #pragma unroll
       for (int j = 0; j < 4; ++j) aw2[t][j] = *reinterpret_cast<const f32x4*>(w2row[t] + 4 * j);
     }
@@ -295,13 +309,13 @@ __device__ __forceinline__ void rq_fused_pass(FusedCtx<H1, H2>& cx, int tb) {
       for (int t = 0; t < TW2; ++t)
 #pragma unroll
         for (int j = 0; j < 4; ++j) awn[t][j] = *reinterpret_cast<const f32x4*>(w2row[t] + gn * 32 + 4 * j);
-      f32x4 bx[NP][4];
+      f32x4 bx[NP2][4];
 #pragma unroll
-      for (int it = 0; it < NP; ++it)
+      for (int it = 0; it < NP2; ++it)
 #pragma unroll
         for (int j = 0; j < 4; ++j) bx[it][j] = *reinterpret_cast<const f32x4*>(hb + it * FT * P1 + g * 32 + 4 * j);
 #pragma unroll
-      for (int it = 0; it < NP; ++it)
+      for (int it = 0; it < NP2; ++it)
 #pragma unroll
         for (int j = 0; j < 4; ++j)
 #pragma unroll
@@ -316,34 +330,34 @@ __device__ __forceinline__ void rq_fused_pass(FusedCtx<H1, H2>& cx, int tb) {
         __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
       }
 #pragma unroll
-      for (int i = 0; i < 4 * (NP - 1); ++i) {
+      for (int i = 0; i < 4 * (NP2 - 1); ++i) {
         __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
         __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
       }
-      __builtin_amdgcn_sched_group_barrier(0x008, 16 * NP * TW2 - 4 * TW2 - 4 * (NP - 1), 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 16 * NP2 * TW2 - 4 * TW2 - 4 * (NP2 - 1), 0);
 #pragma unroll
       for (int t = 0; t < TW2; ++t)
 #pragma unroll
         for (int j = 0; j < 4; ++j) aw2[t][j] = awn[t][j];
     }
-  }
 #pragma unroll
-  for (int t = 0; t < TW2; ++t)
+    for (int t = 0; t < TW2; ++t)
 #pragma unroll
-    for (int g4 = 0; g4 < 4; ++g4) {
-      const int f = (w * TW2 + t) * 32 + 8 * g4 + 4 * h;
-      const f32x4 bb = *reinterpret_cast<const f32x4*>(cx.b2 + f);
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int f = (ft0 + t) * 32 + 8 * g4 + 4 * h;
+        const f32x4 bb = *reinterpret_cast<const f32x4*>(cx.b2 + f);
 #pragma unroll
-      for (int it = 0; it < NP; ++it) {
-        f32x4 o;
+        for (int it = 0; it < NP2; ++it) {
+          f32x4 o;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const float u = acc2[t][it][4 * g4 + i] + bb[i];
-          o[i] = u < 0.f ? 0.f : u;
+          for (int i = 0; i < 4; ++i) {
+            const float u = acc2[t][it][4 * g4 + i] + bb[i];
+            o[i] = u < 0.f ? 0.f : u;
+          }
+          *reinterpret_cast<f32x4*>(cx.h2s + ((it0 + it) * FT + r) * P2 + f) = o;
         }
-        *reinterpret_cast<f32x4*>(cx.h2s + (it * FT + r) * P2 + f) = o;
       }
-    }
+  }
   __syncthreads();
 
   GR_STAMP(s3);
@@ -355,7 +369,7 @@ __device__ __forceinline__ void rq_fused_pass(FusedCtx<H1, H2>& cx, int tb) {
 #pragma unroll
       for (int v = 0; v < 16; ++v) acc3[it][v] = 0.f;
     const float* hb = cx.h2s + r * P2 + 16 * h;
-    for (int g = w; g < H2 / 32; g += 4) {
+    for (int g = w; g < H2 / 32 && w < 4; g += 4) {
       f32x4 aw[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j)
@@ -374,7 +388,7 @@ __device__ __forceinline__ void rq_fused_pass(FusedCtx<H1, H2>& cx, int tb) {
 #pragma unroll
     for (int it = 0; it < NP; ++it)
 #pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4) {
+      for (int g4 = 0; g4 < 4 && w < 4; ++g4) {
         f32x4 o;
 #pragma unroll
         for (int i = 0; i < 4; ++i) o[i] = acc3[it][4 * g4 + i];
@@ -411,13 +425,13 @@ __device__ __forceinline__ void rq_fused_pass(FusedCtx<H1, H2>& cx, int tb) {
   GR_STAMP_ADD(5, 0ull, (unsigned long long)NP);
 }
 
-template <int H1, int H2>
-__global__ __launch_bounds__(256, 1) void rq_encoder_kernel(
+template <int H1, int H2, int WV = 4>
+__global__ __launch_bounds__(64 * WV, 1) void rq_encoder_kernel(
     const float* __restrict__ x, int64_t n, int D0, const float* __restrict__ W1,
     const float* __restrict__ b1, const float* __restrict__ W2, const float* __restrict__ b2,
     const float* __restrict__ W3, const float* __restrict__ b3, float* __restrict__ z_out,
     int tiles) {
-  using C = FusedCfg<H1, H2>;
+  using C = FusedCfg<H1, H2, WV>;
   __shared__ __attribute__((aligned(16))) float sm[C::LDS];
   const int t_begin = (int)((int64_t)blockIdx.x * tiles / gridDim.x);
   const int t_end = (int)((int64_t)(blockIdx.x + 1) * tiles / gridDim.x);
@@ -427,7 +441,7 @@ __global__ __launch_bounds__(256, 1) void rq_encoder_kernel(
   unsigned long long k0, r0;
   asm volatile("s_memtime %0\n\ts_memrealtime %1\n\ts_waitcnt lgkmcnt(0)" : "=s"(k0), "=s"(r0)::"memory");
 #endif
-  FusedCtx<H1, H2> cx;
+  FusedCtx<H1, H2, WV> cx;
   cx.x = x; cx.n = n; cx.D0 = D0; cx.NC = D0 / FXC; cx.t_end = t_end;
   cx.W2 = W2; cx.b1 = b1; cx.b2 = b2; cx.W3 = W3; cx.b3 = b3; cx.z_out = z_out;
   cx.xs = sm;                              // [2][PI][FXP]
@@ -449,8 +463,8 @@ __global__ __launch_bounds__(256, 1) void rq_encoder_kernel(
   cx.swrite_x(0);
   __syncthreads();
   int tb = t_begin;
-  for (; tb + FP <= t_end; tb += FP) rq_fused_pass<FP, H1, H2>(cx, tb);
-  if (tb < t_end) rq_fused_pass<1, H1, H2>(cx, tb);   // FP == 2: at most one tile left
+  for (; tb + FP <= t_end; tb += FP) rq_fused_pass<FP, H1, H2, WV>(cx, tb);
+  if (tb < t_end) rq_fused_pass<1, H1, H2, WV>(cx, tb);   // FP == 2: at most one tile left
 #ifdef GR_STAMPS
   unsigned long long k1, r1;
   asm volatile("s_memtime %0\n\ts_memrealtime %1\n\ts_waitcnt lgkmcnt(0)" : "=s"(k1), "=s"(r1)::"memory");
@@ -487,6 +501,12 @@ int gr_rq_encoder_fused_launch(const float* x, int64_t n, int32_t n_linear, cons
       cus = 256;
   }
   const int64_t grid = tiles < cus ? tiles : cus;
+  if (option("rq_enc_w8") == 1) {   // 8 waves (2 per SIMD), one 32-feature L1 tile each
+    hipLaunchKernelGGL((rq_encoder_kernel<256, 128, 8>), dim3((unsigned)grid), dim3(512), 0, st, x, n,
+                       dims[0], weights[0], biases[0], weights[1], biases[1], weights[2], biases[2],
+                       z_out, (int)tiles);
+    return check_launch("rq fused encoder (8 waves)");
+  }
   hipLaunchKernelGGL((rq_encoder_kernel<256, 128>), dim3((unsigned)grid), dim3(256), 0, st, x, n,
                      dims[0], weights[0], biases[0], weights[1], biases[1], weights[2], biases[2],
                      z_out, (int)tiles);
