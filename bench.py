@@ -261,7 +261,7 @@ def bench_rq_c2(a, world, rank, dev):
                                "e 32, data-derived codebooks, BERT-statistics item embeddings",
                    "items_per_rank_per_step": a.rq_items, "global_batch": a.rq_items * world,
                    "parallelism": f"item-sharded x{world}, no collective"},
-        "roofline": roofline("rq_encoder_kernel<256,128>", ENC_FLOP_PER_ITEM * a.rq_items, enc_ms, "c2"),
+        "roofline": roofline("rq_encoder_kernel<256,128,8>", ENC_FLOP_PER_ITEM * a.rq_items, enc_ms, "c2"),
         "call": {"kernels": "rq_encoder_kernel + rq_quantize_kernel", "device_ms": dev_ms,
                  "flop_per_item": rq_flop_per_item(L, K),
                  "frac_of_fp32_peak": rq_flop_per_item(L, K) * a.rq_items / (dev_ms * 1e-3) / 1e12 / FP32_PEAK_TFLOPS,
