@@ -4,8 +4,8 @@
 // rq_quantize_kernel (rq.hip).
 //
 // Grid = one workgroup per CU: 8 waves (default, rq_enc_w8; 2 per SIMD, wave w owns L1 features
-// [32w, 32w+32) and L2 feature tile w % 4 of item tile w / 4) or 4 waves (the description below;
-// 493 -> 483 us per C2 call at 8 waves, profiles/r02_ab_quant_ablation.txt, bitwise the same z).  Items are cut into 32-item tiles and every workgroup owns a
+// [32w, 32w+32), waves 0-3 run L2 and L3 as below) or 4 waves (the description below; 493 -> 462 us
+// per C2 call at 8 waves, profiles/r02_ab_quant_ablation.txt, bitwise the same z).  Items are cut into 32-item tiles and every workgroup owns a
 // contiguous, balanced range of tiles (100k items -> 12 or 13 tiles per CU: the chip-level tail is
 // one tile, ~6 %).  A workgroup walks its range in PASSES of FP tiles (a trailing single tile runs
 // a 1-tile instantiation, so a pass costs in proportion to its tiles).  Per pass:
@@ -51,9 +51,7 @@ struct FusedCfg {
   static constexpr int E = 32;
   static constexpr int NTH = 64 * WV;     // threads per workgroup
   static constexpr int TW1 = H1 / (32 * WV);   // L1 feature tiles per wave
-  // L2: 4 waves: every wave H2 / 128 feature tiles for all item tiles of the pass; 8 waves: wave w
-  // feature tile w % 4 of item tile w / 4
-  static constexpr int TW2 = WV == 4 ? H2 / 128 : 1;
+  static constexpr int TW2 = H2 / 128;   // L2 feature tiles per wave (waves 0-3)
   static constexpr int P1 = H1 + 4, P2 = H2 + 4, PZ = E + 4;
   static constexpr int PI = FP * FT;     // items per (full) pass
   static constexpr int XV = PI * 16 / NTH;
@@ -278,12 +276,13 @@ __device__ __forceinline__ void rq_fused_pass(FusedCtx<H1, H2, WV>& cx, int tb) 
   GR_STAMP(s2);
 
   // ------------------------------------------------------------------ L2: W2 . h1^T
-  // 4 waves: wave w, feature tiles [w TW2, w TW2 + TW2) for all NP item tiles; 8 waves: feature
-  // tile w % 4 of item tile w / 4 (a one-tile pass leaves waves 4-7 idle here)
-  constexpr int NP2 = WV == 4 ? NP : 1;
-  const int ft0 = WV == 4 ? w * TW2 : (w & 3);
-  const int it0 = WV == 4 ? 0 : (w >> 2);
-  const bool l2_on = it0 < NP;   // wave-uniform
+  // waves 0-3: wave w, feature tiles [w TW2, w TW2 + TW2) for all NP item tiles (NP accumulator
+  // chains per wave); in the 8-wave form waves 4-7 skip L2 (splitting it into one chain per wave
+  // over all 8 measured 483 vs 462 us per C2 call)
+  constexpr int NP2 = NP;
+  const int ft0 = w * TW2;
+  const int it0 = 0;
+  const bool l2_on = w < 4;   // wave-uniform
   f32x16 acc2[TW2][NP2];
 #pragma unroll
   for (int t = 0; t < TW2; ++t)

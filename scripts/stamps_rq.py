@@ -21,6 +21,8 @@ dev = torch.device("cuda:0")
 m = synth.rqvae_model(L, K, dev)
 x = synth.items(100_000, 7, dev)
 lib = _lib.lib()
+if os.environ.get("GR_ENC_W8") is not None:   # 8-wave (1) or 4-wave (0) fused encoder
+    _lib.set_option("rq_enc_w8", int(os.environ["GR_ENC_W8"]))
 lib.gr_debug_rq_stamps.argtypes = [ctypes.c_void_p]
 buf = (ctypes.c_ulonglong * 10)()
 m.get_indices(x)
