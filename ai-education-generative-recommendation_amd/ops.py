@@ -876,17 +876,24 @@ class RqTrainGraph:
     ``inputs`` -- the reference's first training batch does the same (vq.py:66-67) -- before the
     capture.  Warm-up steps (allocator, autograd, the optimizer's lazily created state) are undone
     afterwards, so the first replay is the first real training step.  Dropout draws from torch's
-    graph-safe generator (fresh masks each replay).  The encoder / decoder run under torch autograd,
-    whose embedding backward holds memset nodes (rocprim temporaries): replay synchronises the
-    device after each step (SasTrainGraph.replay explains why)."""
+    graph-safe generator (fresh masks each replay).  On the kernel path (fused MLPs and quantizer)
+    replays run back to back (300 replays bitwise equal to synchronised ones,
+    scripts/diag_rq_graph_sync.py); with the torch modules (``fused_train = False``), whose embedding
+    backward holds memset nodes, replay synchronises the device after each step (SasTrainGraph.replay
+    explains why).  ``sync`` overrides the choice."""
 
-    def __init__(self, model, optimizer, inputs, max_norm=1.0, use_sk=True, warmup=3, sync=True):
+    def __init__(self, model, optimizer, inputs, max_norm=1.0, use_sk=True, warmup=3, sync=None):
         L.require_gpu(inputs)
         for g in optimizer.param_groups:
             if not g.get("capturable", False) or not torch.is_tensor(g["lr"]):
                 raise RuntimeError("RqTrainGraph: the optimizer must be capturable with a tensor lr "
                                    "(e.g. AdamW(params, lr=torch.tensor(1e-3, device=dev), capturable=True))")
         self.model, self.opt, self.inputs = model, optimizer, inputs
+        if sync is None:   # the kernel path's graph replays back to back (tested bitwise); torch
+            kern = (getattr(model.encoder, "fused_train", False) and getattr(model.decoder, "fused_train", False)
+                    and getattr(model.rq, "fused_train", False) and mlp_train_supported(model.encoder, inputs)
+                    and not model.bn)
+            sync = not kern   # autograd's embedding backward holds memset nodes: synchronise
         self.max_norm, self.use_sk, self._sync = float(max_norm), bool(use_sk), bool(sync)
         dev = inputs.device
         if model.training and any(not q.initted for q in model.rq.vq_layers):
