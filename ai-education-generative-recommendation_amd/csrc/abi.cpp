@@ -47,7 +47,7 @@ static std::atomic<int64_t> g_sas_rowtile{1};
 // together, 0 (default): level by level).  Identical results; measured equal at C2 (83.9 vs
 // 84.8 us standalone, scripts/ab_opt.py), so the per-level staging is not what bounds the kernel.
 static std::atomic<int64_t> g_rq_resident{0};
-// rq_waves (8 or 16): waves per quantize workgroup at e <= 32 (see rq.hip launch_quantize_e).
+// rq_waves (8): waves per quantize workgroup at e <= 32 (see rq.hip launch_quantize_e; 16 refused).
 static std::atomic<int64_t> g_rq_waves{8};
 // rq_split (1: a quantize workgroup's c % 4 leftover item tiles are split into code quarters, one
 // per SIMD, so the SIMDs' loads differ by at most a quarter tile; 0: round-robin tiles over waves).
@@ -119,7 +119,9 @@ extern "C" int gr_set_option(const char* name, int64_t value) {
   if (!strcmp(name, "attn_pair") && (value == 0 || value == 1)) { gr::g_attn_pair = value; return GR_OK; }
   if (!strcmp(name, "sas_rowtile") && (value == 0 || value == 1)) { gr::g_sas_rowtile = value; return GR_OK; }
   if (!strcmp(name, "rq_resident") && (value == 0 || value == 1)) { gr::g_rq_resident = value; return GR_OK; }
-  if (!strcmp(name, "rq_waves") && (value == 8 || value == 16)) { gr::g_rq_waves = value; return GR_OK; }
+  // rq_waves 16 is refused: its A/B (profiles/r02_ab_quant_ablation.txt) returned indices different
+  // from the 8-wave kernel's at n >= 409,600; only the checked 8-wave form can be selected
+  if (!strcmp(name, "rq_waves") && value == 8) { gr::g_rq_waves = value; return GR_OK; }
   if (!strcmp(name, "rq_split") && (value == 0 || value == 1)) { gr::g_rq_split = value; return GR_OK; }
   if (!strcmp(name, "rq_enc_w8") && (value == 0 || value == 1)) { gr::g_rq_enc_w8 = value; return GR_OK; }
   if (!strcmp(name, "score_slice_major") && (value == 0 || value == 1)) { gr::g_score_slice_major = value; return GR_OK; }
