@@ -57,6 +57,8 @@ SIGNATURES = {
                                         _vp, _vp, _vp, _sz, _vp]),
     "gr_rq_mlp_workspace_bytes": (_sz, [_i64, _i32, _vp]),
     "gr_rq_mlp_f32": (ctypes.c_int, [_vp, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
+    "gr_mlp_exact_f32": (ctypes.c_int, [_vp, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _f32, _i32,
+                                        _vp, _vp, _sz, _vp]),
     "gr_rq_encode_sk_workspace_bytes": (_sz, [_i64, _i32, _i32, _vp]),
     "gr_rq_encode_sk_f32": (ctypes.c_int, [_vp, _i64, _i32, _i32, _vp, _vp, _vp, _i32, _vp, _i64,
                                            _vp, _vp, _sz, _vp]),

@@ -10,7 +10,8 @@ static thread_local std::string g_last_error;
 void set_error(const std::string& msg) { g_last_error = msg; }
 void clear_error() { g_last_error.clear(); }
 
-// Options: rq_fused (1: fused persistent encode kernel when the shape allows, 0: layer-wise path).
+// Options: rq_fused (1: fused persistent encode kernel when the shape allows, 0: layer-wise path;
+// bitwise the same IDs).
 static std::atomic<int64_t> g_rq_fused{1};
 // sas_fused (1: register-resident fused SASRec forward when n <= 64 and d <= 64, 0: layer-wise).
 static std::atomic<int64_t> g_sas_fused{1};
@@ -43,18 +44,9 @@ static std::atomic<int64_t> g_attn_pair{0};
 // sas_rowtile (1: d = 128 layer-wise forwards fuse everything between attention launches into
 // row-tile kernels, sasrec_rowtile.hip; 0: one kernel per op).  A/B timing and a second path.
 static std::atomic<int64_t> g_sas_rowtile{1};
-// rq_resident (1: the quantize kernel stages every level's codebook into LDS once when they fit
-// together, 0 (default): level by level).  Identical results; measured equal at C2 (83.9 vs
-// 84.8 us standalone, scripts/ab_opt.py), so the per-level staging is not what bounds the kernel.
-static std::atomic<int64_t> g_rq_resident{0};
-// rq_waves (8): waves per quantize workgroup at e <= 32 (see rq.hip launch_quantize_e; 16 refused).
-static std::atomic<int64_t> g_rq_waves{8};
 // rq_split (1: a quantize workgroup's c % 4 leftover item tiles are split into code quarters, one
 // per SIMD, so the SIMDs' loads differ by at most a quarter tile; 0: round-robin tiles over waves).
 static std::atomic<int64_t> g_rq_split{1};
-// rq_enc_w8 (1 (default): the fused encoder at 8 waves per workgroup, 2 per SIMD, one 32-feature
-// L1 tile each; 0: 4 waves, two tiles each -- bitwise the same z)
-static std::atomic<int64_t> g_rq_enc_w8{1};
 // score_slice_major (direct-store scoring: 1 = an XCD's workgroups share catalog slices across
 // user blocks (default: 255 vs 261 us at C3, scripts/ab_opt.py), 0 = they share a user block).
 static std::atomic<int64_t> g_score_slice_major{1};
@@ -88,10 +80,7 @@ int64_t option(const char* name) {
   if (!strcmp(name, "topk_wg_per_cu")) return g_topk_wg_per_cu.load();
   if (!strcmp(name, "attn_pair")) return g_attn_pair.load();
   if (!strcmp(name, "sas_rowtile")) return g_sas_rowtile.load();
-  if (!strcmp(name, "rq_resident")) return g_rq_resident.load();
-  if (!strcmp(name, "rq_waves")) return g_rq_waves.load();
   if (!strcmp(name, "rq_split")) return g_rq_split.load();
-  if (!strcmp(name, "rq_enc_w8")) return g_rq_enc_w8.load();
   if (!strcmp(name, "score_slice_major")) return g_score_slice_major.load();
   if (!strcmp(name, "attn_occ1")) return g_attn_occ1.load();
   if (!strcmp(name, "attn_alt")) return g_attn_alt.load();
@@ -118,12 +107,7 @@ extern "C" int gr_set_option(const char* name, int64_t value) {
   if (!strcmp(name, "topk_wg_per_cu") && value >= 0 && value <= 4) { gr::g_topk_wg_per_cu = value; return GR_OK; }
   if (!strcmp(name, "attn_pair") && (value == 0 || value == 1)) { gr::g_attn_pair = value; return GR_OK; }
   if (!strcmp(name, "sas_rowtile") && (value == 0 || value == 1)) { gr::g_sas_rowtile = value; return GR_OK; }
-  if (!strcmp(name, "rq_resident") && (value == 0 || value == 1)) { gr::g_rq_resident = value; return GR_OK; }
-  // rq_waves 16 is refused: its A/B (profiles/r02_ab_quant_ablation.txt) returned indices different
-  // from the 8-wave kernel's at n >= 409,600; only the checked 8-wave form can be selected
-  if (!strcmp(name, "rq_waves") && value == 8) { gr::g_rq_waves = value; return GR_OK; }
   if (!strcmp(name, "rq_split") && (value == 0 || value == 1)) { gr::g_rq_split = value; return GR_OK; }
-  if (!strcmp(name, "rq_enc_w8") && (value == 0 || value == 1)) { gr::g_rq_enc_w8 = value; return GR_OK; }
   if (!strcmp(name, "score_slice_major") && (value == 0 || value == 1)) { gr::g_score_slice_major = value; return GR_OK; }
   if (!strcmp(name, "attn_occ1") && (value == 0 || value == 1)) { gr::g_attn_occ1 = value; return GR_OK; }
   if (!strcmp(name, "attn_alt") && (value == 0 || value == 1)) { gr::g_attn_alt = value; return GR_OK; }

@@ -11,6 +11,14 @@
 // element s to MFMA step s, so MFMA step s covers k = {8kc+s, 8kc+4+s}.  Every output element
 // therefore sees the same k-ordered fp32 fma chain, independent of its tile position — the property
 // the fused rank epilogue relies on (SURVEY §7 hard part 3).
+//
+// EXACT instantiations (gr_linear_exact_launch: the RQ-VAE encoder off the fused kernel's shape)
+// reproduce the reference's CPU nn.Linear bit for bit (oracle/rq_exact.c): the LDS image holds each
+// 8-deep slice de-interleaved (even features in the lane-half-0 float4, odd ones in the half-1
+// float4), so MFMA step s feeds k = 8kc + 2s then 8kc + 2s + 1 -- one fma chain over k in order;
+// MKL's k blocking (mkl_kblock) restarts the chain at the block boundary, and the epilogue adds
+// y = bias; y += block 0; y += block 1.  Optional eval BatchNorm1d after the Linear in torch's CPU
+// formula (layers.py:25-26): a = w / sqrt(var + eps), y = fma(y, a, fma(-mean, a, b)).
 #include "gr_common.h"
 
 namespace gr {
@@ -18,13 +26,22 @@ namespace gr {
 constexpr int LIN_BK = 32;
 constexpr int LIN_PITCH = LIN_BK + 4;
 
+struct BnEval {   // running statistics and affine of an eval-mode BatchNorm1d (all null: none)
+  const float* mean;
+  const float* var;
+  const float* w;
+  const float* b;
+  float eps;
+};
+
 // NT = threads per workgroup: 256 (4 waves, 2 workgroups = 2 waves per SIMD) or 512 (8 waves,
 // 4 per SIMD at two workgroups per CU; option lin_w8).
-template <int BM, int BN, int WM, int WN, int ACT, bool RES, bool NMAJOR, int NT = 256>
+template <int BM, int BN, int WM, int WN, int ACT, bool RES, bool NMAJOR, int NT = 256, bool EXACT = false>
 __global__ __launch_bounds__(NT, NT / 128) void linear_f32_kernel(
     const float* __restrict__ x, const float* __restrict__ w, const float* __restrict__ bias,
     const float* residual, float* y, int64_t M, int N, int K, int64_t ldy, int64_t ldr,
-    int tiles_m, int tiles_n) {
+    int tiles_m, int tiles_n, int ksplit, BnEval bn) {
+#pragma clang fp contract(off)
   static_assert(WM * WN == NT / 64, "one wave per (WM, WN) position");
   constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
   constexpr int AV = BM * LIN_BK / 4 / NT, BV = BN * LIN_BK / 4 / NT;
@@ -57,17 +74,26 @@ __global__ __launch_bounds__(NT, NT / 128) void linear_f32_kernel(
                                  : f32x4{0.f, 0.f, 0.f, 0.f};
     }
   };
+  auto put = [&](float* row, int q4, const f32x4& v) {
+    if constexpr (EXACT) {   // features 4q4..4q4+3 of an 8-slice: even ones to the half-0 float4
+      const int base = (q4 >> 1) * 8 + 2 * (q4 & 1);
+      *reinterpret_cast<f32x2*>(row + base) = f32x2{v[0], v[2]};
+      *reinterpret_cast<f32x2*>(row + base + 4) = f32x2{v[1], v[3]};
+    } else {
+      *reinterpret_cast<f32x4*>(row + q4 * 4) = v;
+    }
+  };
   auto swrite = [&](int buf) {
     float* s = lds[buf];
 #pragma unroll
     for (int i = 0; i < AV; ++i) {
       const int f = tid + NT * i;
-      *reinterpret_cast<f32x4*>(s + (f >> 3) * LIN_PITCH + (f & 7) * 4) = ra[i];
+      put(s + (f >> 3) * LIN_PITCH, f & 7, ra[i]);
     }
 #pragma unroll
     for (int i = 0; i < BV; ++i) {
       const int f = tid + NT * i;
-      *reinterpret_cast<f32x4*>(s + (BM + (f >> 3)) * LIN_PITCH + (f & 7) * 4) = rb[i];
+      put(s + (BM + (f >> 3)) * LIN_PITCH, f & 7, rb[i]);
     }
   };
 
@@ -78,6 +104,8 @@ __global__ __launch_bounds__(NT, NT / 128) void linear_f32_kernel(
     for (int b = 0; b < TN; ++b)
 #pragma unroll
       for (int v = 0; v < 16; ++v) acc[a][b][v] = 0.f;
+  f32x16 sv[EXACT ? TM : 1][EXACT ? TN : 1];   // EXACT: the first k block's chain
+  bool split = false;
 
   const int nk = (K + LIN_BK - 1) / LIN_BK;
   gload(0);
@@ -90,6 +118,19 @@ __global__ __launch_bounds__(NT, NT / 128) void linear_f32_kernel(
     const float* Bs = lds[cur] + (BM + wn * (BN / WN) + r) * LIN_PITCH + 4 * h;
 #pragma unroll
     for (int kc = 0; kc < LIN_BK / 8; ++kc) {
+      if constexpr (EXACT) {
+        if (kt * LIN_BK + kc * 8 == ksplit) {   // MKL's second k block: a fresh chain
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+              sv[i][j] = acc[i][j];
+#pragma unroll
+              for (int v = 0; v < 16; ++v) acc[i][j][v] = 0.f;
+            }
+          split = true;
+        }
+      }
       f32x4 a[TM], b[TN];
 #pragma unroll
       for (int t = 0; t < TM; ++t)
@@ -132,7 +173,19 @@ __global__ __launch_bounds__(NT, NT / 128) void linear_f32_kernel(
         const int64_t row = m0 + wm * (BM / WM) + i * 32 + (v & 3) + 8 * (v >> 2) + 4 * h;
         if (cok && row < M) {
           float o = acc[i][j][v];
-          if (bias != nullptr) o = o + bv;
+          if constexpr (EXACT) {   // y = bias; y += block 0; y += block 1 (MKL); then BatchNorm
+            o = bias != nullptr ? bv : 0.f;
+            if (split) o = o + sv[i][j][v];
+            o = o + acc[i][j][v];
+            if (bn.var != nullptr) {
+              const float inv = 1.0f / sqrtf(bn.var[col] + bn.eps);
+              const float a = bn.w != nullptr ? inv * bn.w[col] : inv;
+              const float c = fmaf(-bn.mean[col], a, bn.b != nullptr ? bn.b[col] : 0.f);
+              o = fmaf(o, a, c);
+            }
+          } else if (bias != nullptr) {
+            o = o + bv;
+          }
           if (ACT == GR_ACT_RELU) o = (o < 0.f) ? 0.f : o;  // NaN propagates like torch.relu
           if (ACT == GR_ACT_SIGMOID) o = 1.0f / (1.0f + expf(-o));
           if (ACT == GR_ACT_TANH) o = tanhf(o);
@@ -145,10 +198,10 @@ __global__ __launch_bounds__(NT, NT / 128) void linear_f32_kernel(
   }
 }
 
-template <int BM, int BN, int WM, int WN, int NT = 256>
+template <int BM, int BN, int WM, int WN, int NT = 256, bool EXACT = false>
 static int launch_tile(const float* x, int64_t m, int k, const float* w, int n, const float* bias,
                        const float* residual, int64_t ldr, int act, float* y, int64_t ldy,
-                       hipStream_t stream) {
+                       hipStream_t stream, int ksplit = -1, BnEval bn = BnEval{}) {
   const int64_t tm = (m + BM - 1) / BM;
   const int tn = (n + BN - 1) / BN;
   if (tm * tn > 0x7fffffffLL) return fail(GR_ERR_UNSUPPORTED, "gr_linear_f32: grid too large");
@@ -157,24 +210,28 @@ static int launch_tile(const float* x, int64_t m, int k, const float* w, int n, 
   const bool res = residual != nullptr;
 #define GR_LIN_CASE(A, R, NM)                                                                    \
   if (act == A && res == R && nmajor == NM) {                                                     \
-    hipLaunchKernelGGL((linear_f32_kernel<BM, BN, WM, WN, A, R, NM, NT>), grid, block, 0, stream, x, \
-                       w, bias, residual, y, m, n, k, ldy, ldr, (int)tm, tn);                    \
+    hipLaunchKernelGGL((linear_f32_kernel<BM, BN, WM, WN, A, R, NM, NT, EXACT>), grid, block, 0,     \
+                       stream, x, w, bias, residual, y, m, n, k, ldy, ldr, (int)tm, tn, ksplit, bn); \
     return check_launch("gr_linear_f32");                                                        \
   }
   GR_LIN_CASE(GR_ACT_NONE, false, false)
   GR_LIN_CASE(GR_ACT_NONE, false, true)
-  GR_LIN_CASE(GR_ACT_NONE, true, false)
-  GR_LIN_CASE(GR_ACT_NONE, true, true)
   GR_LIN_CASE(GR_ACT_RELU, false, false)
   GR_LIN_CASE(GR_ACT_RELU, false, true)
-  GR_LIN_CASE(GR_ACT_RELU, true, false)
-  GR_LIN_CASE(GR_ACT_RELU, true, true)
-  GR_LIN_CASE(GR_ACT_SIGMOID, false, false)
-  GR_LIN_CASE(GR_ACT_SIGMOID, false, true)
-  GR_LIN_CASE(GR_ACT_TANH, false, false)
-  GR_LIN_CASE(GR_ACT_TANH, false, true)
   GR_LIN_CASE(GR_ACT_LEAKYRELU, false, false)
   GR_LIN_CASE(GR_ACT_LEAKYRELU, false, true)
+  if constexpr (EXACT) {
+    return fail(GR_ERR_UNSUPPORTED, "gr_linear_exact: act must be none / relu / leakyrelu, no residual");
+  } else {
+    GR_LIN_CASE(GR_ACT_NONE, true, false)
+    GR_LIN_CASE(GR_ACT_NONE, true, true)
+    GR_LIN_CASE(GR_ACT_RELU, true, false)
+    GR_LIN_CASE(GR_ACT_RELU, true, true)
+    GR_LIN_CASE(GR_ACT_SIGMOID, false, false)
+    GR_LIN_CASE(GR_ACT_SIGMOID, false, true)
+    GR_LIN_CASE(GR_ACT_TANH, false, false)
+    GR_LIN_CASE(GR_ACT_TANH, false, true)
+  }
 #undef GR_LIN_CASE
   return fail(GR_ERR_ARG, "gr_linear_f32: bad activation");
 }
@@ -204,6 +261,29 @@ int gr_linear_launch(const float* x, int64_t m, int32_t k, const float* w, int32
     return w8 ? launch_tile<128, 64, 4, 2, 512>(x, m, k, w, n, bias, residual, ldr, act, y, ldy, stream)
               : launch_tile<128, 64, 2, 2>(x, m, k, w, n, bias, residual, ldr, act, y, ldy, stream);
   return launch_tile<128, 32, 4, 1>(x, m, k, w, n, bias, residual, ldr, act, y, ldy, stream);
+}
+
+// The reference's CPU nn.Linear (+ optional eval BatchNorm1d, + ReLU / LeakyReLU / none) bit for
+// bit: layer-wise RQ-VAE encoder (RQ-VAE/models/layers.py:18-43) off the fused kernel's shape.
+int gr_linear_exact_launch(const float* x, int64_t m, int32_t k, const float* w, int32_t n,
+                           const float* bias, const float* bn_mean, const float* bn_var, const float* bn_w,
+                           const float* bn_b, float bn_eps, int32_t act, float* y, hipStream_t stream) {
+  using namespace gr;
+  if (m < 0 || k <= 0 || n <= 0) return fail(GR_ERR_ARG, "gr_linear_exact: bad shape");
+  if (m == 0) return GR_OK;
+  if (!x || !w || !y) return fail(GR_ERR_ARG, "gr_linear_exact: null pointer");
+  if (k % 4 != 0 || !aligned16(x) || !aligned16(w))
+    return fail(GR_ERR_UNSUPPORTED, "gr_linear_exact: k % 4 == 0 and 16-byte aligned x, w");
+  const int kb = mkl_kblock(k);
+  if (kb < 0 || (kb < k && kb % 8 != 0))
+    return fail(GR_ERR_UNSUPPORTED, "gr_linear_exact: in_features outside the characterised MKL k blocking");
+  if ((bn_mean == nullptr) != (bn_var == nullptr)) return fail(GR_ERR_ARG, "gr_linear_exact: bn mean / var");
+  const BnEval bn{bn_mean, bn_var, bn_w, bn_b, bn_eps};
+  const int ks = kb < k ? kb : -1;
+  // 4-wave 128 x 64 tiles: the second k block's chain doubles the accumulators (larger tiles spill)
+  if (n > 32)
+    return launch_tile<128, 64, 2, 2, 256, true>(x, m, k, w, n, bias, nullptr, 0, act, y, n, stream, ks, bn);
+  return launch_tile<128, 32, 4, 1, 256, true>(x, m, k, w, n, bias, nullptr, 0, act, y, n, stream, ks, bn);
 }
 
 extern "C" int gr_linear_f32(const float* x, int64_t m, int32_t k, const float* w, int32_t n,

@@ -5,15 +5,30 @@
 //   idx = first index of the minimum            (torch.argmin, vq.py:75)
 //   r  <- r - (r + (C[idx] - r))                (vq.py:95 straight-through value, rq.py:47)
 //
-// Quantize kernel: 8-wave workgroups, each owning a contiguous balanced range of 32-item tiles
-// (spread over its waves; several workgroups per CU when the codebook chunk is small, so the
-// per-CU work is balanced).  Levels are processed in order: the level's codebook is staged into
-// LDS (rows XOR-swizzled by 16-byte slot, norms computed in-kernel with the same fma chain as
-// gr_rq_codebook_norms_f32), then every wave sweeps all code tiles for its item tiles with no
-// further barrier: MFMA distance tile with the CODES on the A side (lane = item, 16 codes per
-// lane), a per-lane running argmin (codes visited in increasing order, strict '<'), one exchange
-// between the lane halves, and the residual update from the LDS row of the winner.  Residuals stay
-// in registers across levels.  Codebooks larger than one LDS chunk are streamed in chunks.
+// Every fp32 rounding follows the reference's CPU run (oracle/rq_exact.c), so the semantic IDs are
+// the reference's bit for bit, exact ties included:
+//   * r . c: MKL's order for K = e < 384, one fma chain from 0 over k = 0..e-1.  The MFMA
+//     v_mfma_f32_32x32x2_f32 is an fma chain over its two k slots (lane half 0 first), so lane half
+//     h holds features 8j + 2s + h of its item (float4 j, element s): step (j, s) feeds features
+//     2(4j + s) and 2(4j + s) + 1 -- the chain runs over k in order.  The LDS codebook image holds
+//     each code row in the same de-interleaved order.
+//   * ||r||^2, ||c||^2: ATen's vectorised row sum (aten_rowsq, gr_common.h); a lane holds half of its
+//     item's features, so the two halves swap their four lane sums (4 shuffles) and both finish the
+//     same sequential sum.
+//   * argmin: strict '<' running minimum per lane over increasing code index, then branch-free
+//     merges (lower distance, then lower index).  The round-2 kernel merged its two lane halves with
+//     an if/else whose compiled form (hipcc, ROCm 7.2) kept the lane's own candidate on exact ties
+//     (profiles/r03_rq_tie_diag.txt); exact ties are common because d is quantised at
+//     ulp(|r|^2 + |c|^2).
+//
+// Quantize kernel: 8-wave workgroups, each owning a contiguous balanced range of 32-item tiles.
+// Levels are processed in order: the level's codebook is staged into LDS (rows XOR-swizzled by
+// 16-byte slot, norms computed in-kernel), then every wave sweeps all code tiles for its item tiles
+// with no further barrier: MFMA distance tile with the CODES on the A side (lane = item, 16 codes
+// per lane), a per-lane running argmin, one exchange between the lane halves, and the residual
+// update from the LDS row of the winner.  Residuals stay in registers across levels.  Codebooks
+// larger than one LDS chunk are streamed in chunks.  e <= 64 (padded with zero features to 16, 32
+// or 64: zero terms at the end of the fma chain change nothing).
 #include "gr_common.h"
 
 namespace gr {
@@ -23,82 +38,133 @@ struct RQLevels {
   int K[GR_MAX_LEVELS];
 };
 
-// max item tiles per wave (residuals held in registers): fewer at e = 64 to stay spill-free
+constexpr int RQ_W = 8;              // waves per quantize workgroup
 constexpr int RQ_SPLIT_MAX = 3;      // leftover tiles per workgroup split into code quarters (c % 4)
 constexpr size_t RQ_PART_BYTES = 2 * RQ_SPLIT_MAX * 4 * 32 * 3 * sizeof(float);
 
-template <int E, int W>
-struct RQMaxT { static constexpr int value = W >= 16 ? 1 : (E >= 64 ? 2 : 4); };
+// item tiles per wave held in registers: fewer at e = 64 to stay spill-free
+template <int EP>
+struct RQMaxT { static constexpr int value = EP >= 64 ? 2 : 4; };
 
-__global__ __launch_bounds__(256) void rq_code_norms_kernel(const float* __restrict__ cb, int K,
-                                                            int e, float* __restrict__ cn) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= K) return;
-  const float* row = cb + (int64_t)c * e;
-  float s = 0.f;
-  for (int k = 0; k < e; ++k) s = fmaf(row[k], row[k], s);
-  cn[c] = s;
-}
-
-// Float offset of 16-byte slot q of row c of an LDS codebook image with E/4 slots per row.
-template <int E>
+// Float offset of 16-byte slot q of row c of an LDS codebook image with EP/4 slots per row.
+template <int EP>
 __device__ __forceinline__ int cb_off(int c, int q) {
-  constexpr int S = E / 4;
+  constexpr int S = EP / 4;
   constexpr int M = S >= 8 ? 7 : S - 1;
-  return c * E + 4 * (q ^ (c & M));
+  return c * EP + 4 * (q ^ (c & M));
 }
 
-// kch > 0: codebooks streamed through LDS in chunks of kch codes, level by level (three barriers
-// per chunk).  kch == 0 ("resident"): every level's codebook and norms fit in LDS together, so
-// they are staged once at the start (one load phase, one norm phase, two barriers in all) and the
-// level loop runs with no barrier at all.
-template <int E, bool SECOND, int W>
-__global__ __launch_bounds__(W * 64) void rq_quantize_kernel(
-    const float* __restrict__ z, int64_t n, int L, RQLevels lv, int kch, int64_t* __restrict__ idx_out,
-    float* __restrict__ best_out, float* __restrict__ gap_out, int tiles, int split_ok) {
-  static_assert(E % 8 == 0 && E <= 64, "e");
-  constexpr int HQ = E / 8;            // float4 per lane half
-  constexpr int RQ_MAXT = RQMaxT<E, W>::value;
-  extern __shared__ __attribute__((aligned(16))) float sm[];
-  const bool resident = kch == 0;
-  int ktot = 0;                        // resident: codes of all levels, each level padded to 32
-  for (int l = 0; l < L; ++l) ktot += (lv.K[l] + 31) & ~31;
-  float* cbs = sm;                     // [kch][E] swizzled (resident: [ktot][E], levels back to back)
-  float* cns = sm + (resident ? ktot : kch) * E;   // [kch] (resident: [ktot])
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r = lane & 31, h = lane >> 5;
-  if (resident) {
-    int off = 0;
-    for (int l = 0; l < L; ++l) {
-      const int K = lv.K[l];
-      for (int f = tid; f < K * (E / 4); f += W * 64) {
-        const int c = f / (E / 4), q = f % (E / 4);
-        *reinterpret_cast<f32x4*>(cbs + off * E + cb_off<E>(c, q)) =
-            *reinterpret_cast<const f32x4*>(lv.cb[l] + (int64_t)c * E + 4 * q);
-      }
-      off += (K + 31) & ~31;
-    }
-    __syncthreads();
-    off = 0;
-    for (int l = 0; l < L; ++l) {
-      const int K = lv.K[l], kp = (K + 31) & ~31;
-      for (int c = tid; c < kp; c += W * 64) {
-        float s = __builtin_inff();    // codes past K can never win
-        if (c < K) {
-          s = 0.f;
+// LDS float offset of feature f of row c: lane half f & 1, float4 f >> 3, element (f >> 1) & 3.
+template <int EP>
+__device__ __forceinline__ int feat_off(int c, int f) {
+  return cb_off<EP>(c, (f & 1) * (EP / 8) + (f >> 3)) + ((f >> 1) & 3);
+}
+
+// ||r||^2 of this lane's item in ATen's order (aten_rowsq) with the features split over the lane
+// halves (half h: features 8j + 2s + h in rr[j][s]); every lane of the pair returns the same value.
+template <int EP>
+__device__ __forceinline__ float rn_exact(const f32x4 (&rr)[EP / 8], int e, int h) {
+#pragma clang fp contract(off)
+  constexpr int HQ = EP / 8;
+  const int nv = e >> 3, full = (nv >> 2) << 2, tail = e & 7;
+  float A[4], T[4];
 #pragma unroll
-          for (int q = 0; q < E / 4; ++q) {
-            const f32x4 v = *reinterpret_cast<const f32x4*>(cbs + off * E + cb_off<E>(c, q));
+  for (int s = 0; s < 4; ++s) {
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+    T[s] = 0.f;
 #pragma unroll
-            for (int i = 0; i < 4; ++i) s = fmaf(v[i], v[i], s);
-          }
-        }
-        cns[off + c] = s;
+    for (int v = 0; v < HQ; ++v) {
+      const float x = rr[v][s];
+      const float q = x * x;
+      if (v < nv) {
+        const int a = v < full ? (v & 3) : 0;
+        if (a == 0) a0 = a0 + q;
+        else if (a == 1) a1 = a1 + q;
+        else if (a == 2) a2 = a2 + q;
+        else a3 = a3 + q;
+      } else if (v == nv) {
+        T[s] = q;                      // tail element 8 nv + 2s + h (zero past e)
       }
-      off += kp;
     }
-    __syncthreads();
+    A[s] = ((a0 + a1) + a2) + a3;
   }
-  float* part = cns + (resident ? ktot : kch);    // [2][RQ_SPLIT_MAX][4][32][3] split-tile partials
+  float PA[4], PT[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    PA[s] = __shfl_xor(A[s], 32);
+    PT[s] = __shfl_xor(T[s], 32);
+  }
+  if (e < 8) {   // ATen's scalar row sum (4 accumulators over rows of 4, leftovers into the first)
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+#pragma unroll
+    for (int i = 0; i < 7; ++i)
+      if (i < e) {
+        const float q = ((i & 1) == h) ? T[i >> 1] : PT[i >> 1];
+        const int k = i < ((e >> 2) << 2) ? (i & 3) : 0;
+        if (k == 0) a0 = a0 + q;
+        else if (k == 1) a1 = a1 + q;
+        else if (k == 2) a2 = a2 + q;
+        else a3 = a3 + q;
+      }
+    return ((a0 + a1) + a2) + a3;
+  }
+  float f = 0.f;
+#pragma unroll
+  for (int jj = 0; jj < 7; ++jj)
+    if (jj < tail) f = f + (((jj & 1) == h) ? T[jj >> 1] : PT[jj >> 1]);
+#pragma unroll
+  for (int jj = 0; jj < 8; ++jj) f = f + (((jj & 1) == h) ? A[jj >> 1] : PA[jj >> 1]);
+  return f;
+}
+
+// (best, second, index) merge: the lower distance, then the lower index (branch-free selects).
+template <bool SECOND>
+__device__ __forceinline__ void merge_min(float& best, float& second, int& bi, float ob, float os, int oi) {
+  const bool take = (ob < best) | ((ob == best) & (oi < bi));
+  if (SECOND) second = take ? fminf(os, best) : fminf(second, ob);
+  best = take ? ob : best;
+  bi = take ? oi : bi;
+}
+
+// Stage codes [c0, c0 + cnt) of a level into the LDS image (de-interleaved rows) and their norms.
+template <int EP, int NT>
+__device__ __forceinline__ void stage_codes(const float* __restrict__ cb, int e, int c0, int cnt,
+                                            float* cbs, float* cns, int tid) {
+  constexpr int HQ = EP / 8;
+  if (e == EP) {   // 16-byte rows: a float4 of features 4u..4u+3 -> two 8-byte halves
+    for (int f = tid; f < cnt * (EP / 4); f += NT) {
+      const int c = f / (EP / 4), u = f % (EP / 4), j = u >> 1, e2 = 2 * (u & 1);
+      const f32x4 v = *reinterpret_cast<const f32x4*>(cb + (int64_t)(c0 + c) * EP + 4 * u);
+      *reinterpret_cast<f32x2*>(cbs + cb_off<EP>(c, j) + e2) = f32x2{v[0], v[2]};
+      *reinterpret_cast<f32x2*>(cbs + cb_off<EP>(c, HQ + j) + e2) = f32x2{v[1], v[3]};
+    }
+  } else {
+    for (int f = tid; f < cnt * EP; f += NT) {
+      const int c = f / EP, k = f % EP;
+      cbs[feat_off<EP>(c, k)] = k < e ? cb[(int64_t)(c0 + c) * e + k] : 0.f;
+    }
+  }
+  __syncthreads();
+  for (int c = tid; c < ((cnt + 31) & ~31); c += NT)
+    cns[c] = c < cnt ? aten_rowsq([&](int f) { return cbs[feat_off<EP>(c, f)]; }, e)
+                     : __builtin_inff();   // codes past K can never win
+  __syncthreads();
+}
+
+template <int EP, bool SECOND>
+__global__ __launch_bounds__(RQ_W * 64) void rq_quantize_kernel(
+    const float* __restrict__ z, int64_t n, int e, int L, RQLevels lv, int kch, int64_t* __restrict__ idx_out,
+    float* __restrict__ best_out, float* __restrict__ gap_out, int tiles, int split_ok) {
+#pragma clang fp contract(off)
+  static_assert(EP % 8 == 0 && EP <= 64, "e");
+  constexpr int W = RQ_W, NT = W * 64;
+  constexpr int HQ = EP / 8;           // float4 per lane half
+  constexpr int RQ_MAXT = RQMaxT<EP>::value;
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  float* cbs = sm;                     // [kch][EP] de-interleaved, swizzled
+  float* cns = sm + kch * EP;          // [kch]
+  float* part = cns + kch;             // [2][RQ_SPLIT_MAX][4][32][3] split-tile partials
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r = lane & 31, h = lane >> 5;
   const int t_begin = (int)((int64_t)blockIdx.x * tiles / gridDim.x);
   const int t_end = (int)((int64_t)(blockIdx.x + 1) * tiles / gridDim.x);
   // Tile plan.  Wave w runs on SIMD w % 4, so a SIMD's load is the tiles of its W/4 waves.  Split
@@ -119,69 +185,49 @@ __global__ __launch_bounds__(W * 64) void rq_quantize_kernel(
     return j < base ? t_begin + simd + 4 * j : t_begin + 4 * base + (j - base);
   };
 
-  // residual of this lane's item for each of the wave's tiles: lane half h holds k in [hE/2, ...)
+  // residual of this lane's item for each of the wave's tiles: half h holds features 8j + 2s + h
   f32x4 res[RQ_MAXT][HQ];
 #pragma unroll
   for (int i = 0; i < RQ_MAXT; ++i) {
     const int64_t item = (int64_t)tile_of(i) * 32 + r;
     const bool ok = i < my && item < n;
     const int64_t ic = ok ? item : 0;
+    if (e == EP) {
 #pragma unroll
-    for (int j = 0; j < HQ; ++j) {
-      const f32x4 v = *reinterpret_cast<const f32x4*>(z + ic * E + (E / 2) * h + 4 * j);
-      res[i][j] = ok ? v : f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int j = 0; j < HQ; ++j) {
+        const f32x4 lo = *reinterpret_cast<const f32x4*>(z + ic * EP + 8 * j);
+        const f32x4 hi = *reinterpret_cast<const f32x4*>(z + ic * EP + 8 * j + 4);
+        const f32x4 v = h ? f32x4{lo[1], lo[3], hi[1], hi[3]} : f32x4{lo[0], lo[2], hi[0], hi[2]};
+        res[i][j] = ok ? v : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < HQ; ++j)
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const int f = 8 * j + 2 * s + h;
+          res[i][j][s] = (ok && f < e) ? z[ic * e + f] : 0.f;
+        }
     }
   }
 
-  int loff = 0;                        // resident: first (padded) code of level l in the image
   for (int l = 0; l < L; ++l) {
     const int K = lv.K[l];
     const float* cb = lv.cb[l];
-    float* lcbs = resident ? cbs + loff * E : cbs;
-    float* lcns = resident ? cns + loff : cns;
-    if (resident) loff += (K + 31) & ~31;
     float rn[RQ_MAXT], best[RQ_MAXT], second[RQ_MAXT];
     int bi[RQ_MAXT];
 #pragma unroll
     for (int i = 0; i < RQ_MAXT; ++i) {
-      float part = 0.f;
-#pragma unroll
-      for (int j = 0; j < HQ; ++j)
-#pragma unroll
-        for (int s = 0; s < 4; ++s) part = fmaf(res[i][j][s], res[i][j][s], part);
-      rn[i] = part + __shfl_xor(part, 32);
+      rn[i] = rn_exact<EP>(res[i], e, h);
       best[i] = __builtin_inff();
       second[i] = __builtin_inff();
       bi[i] = 0x7fffffff;
     }
-    const int step = resident ? K : kch;
-    const int c_last = resident ? 0 : ((K - 1) / kch) * kch;   // first code of the chunk left in LDS
-    for (int c0 = 0; c0 < K; c0 += step) {
-      const int cnt = min(step, K - c0);
-      if (!resident) {
-        __syncthreads();   // previous chunk / level fully consumed
-        for (int f = tid; f < cnt * (E / 4); f += W * 64) {
-          const int c = f / (E / 4), q = f % (E / 4);
-          *reinterpret_cast<f32x4*>(cbs + cb_off<E>(c, q)) =
-              *reinterpret_cast<const f32x4*>(cb + (int64_t)(c0 + c) * E + 4 * q);
-        }
-        __syncthreads();
-        // code norms from the LDS image, same k-ordered fma chain as rq_code_norms_kernel
-        for (int c = tid; c < ((cnt + 31) & ~31); c += W * 64) {
-          float s = __builtin_inff();    // codes past K can never win
-          if (c < cnt) {
-            s = 0.f;
-#pragma unroll
-            for (int q = 0; q < E / 4; ++q) {
-              const f32x4 v = *reinterpret_cast<const f32x4*>(cbs + cb_off<E>(c, q));
-#pragma unroll
-              for (int i = 0; i < 4; ++i) s = fmaf(v[i], v[i], s);
-            }
-          }
-          cns[c] = s;
-        }
-        __syncthreads();
-      }
+    const int c_last = ((K - 1) / kch) * kch;   // first code of the chunk left in LDS
+    for (int c0 = 0; c0 < K; c0 += kch) {
+      const int cnt = min(kch, K - c0);
+      __syncthreads();   // previous chunk / level fully consumed
+      stage_codes<EP, NT>(cb, e, c0, cnt, cbs, cns, tid);
       const int ct_n = (cnt + 31) >> 5;
       const int q_lo = simd * ct_n / 4, q_hi = (simd + 1) * ct_n / 4;   // this SIMD's code quarter
 #pragma unroll 1
@@ -191,11 +237,11 @@ __global__ __launch_bounds__(W * 64) void rq_quantize_kernel(
         f32x4 a[HQ];
 #pragma unroll
         for (int j = 0; j < HQ; ++j)
-          a[j] = *reinterpret_cast<const f32x4*>(lcbs + cb_off<E>(code, HQ * h + j));
+          a[j] = *reinterpret_cast<const f32x4*>(cbs + cb_off<EP>(code, HQ * h + j));
         float cnv[16];
 #pragma unroll
         for (int g4 = 0; g4 < 4; ++g4) {
-          const f32x4 q = *reinterpret_cast<const f32x4*>(lcns + ct * 32 + 8 * g4 + 4 * h);
+          const f32x4 q = *reinterpret_cast<const f32x4*>(cns + ct * 32 + 8 * g4 + 4 * h);
 #pragma unroll
           for (int i = 0; i < 4; ++i) cnv[4 * g4 + i] = q[i];
         }
@@ -212,10 +258,13 @@ __global__ __launch_bounds__(W * 64) void rq_quantize_kernel(
 #pragma unroll
             for (int v = 0; v < 16; ++v) {
               const int cd = c0 + ct * 32 + (v & 3) + 8 * (v >> 2) + 4 * h;
-              const float dd = (rn[i] + cnv[v]) - 2.f * acc[v];
-              if (SECOND) second[i] = fminf(second[i], fmaxf(best[i], dd));
-              bi[i] = dd < best[i] ? cd : bi[i];
-              best[i] = fminf(best[i], dd);
+              const float sn = rn[i] + cnv[v];
+              const float tw = 2.f * acc[v];
+              const float dd = sn - tw;
+              const bool lt = dd < best[i];
+              if (SECOND) second[i] = lt ? best[i] : fminf(second[i], dd);
+              bi[i] = lt ? cd : bi[i];
+              best[i] = lt ? dd : best[i];
             }
           }
         }
@@ -227,13 +276,7 @@ __global__ __launch_bounds__(W * 64) void rq_quantize_kernel(
       if (i < my) {
         const float ob = __shfl_xor(best[i], 32), os = __shfl_xor(second[i], 32);
         const int oi = __shfl_xor(bi[i], 32);
-        if (ob < best[i] || (ob == best[i] && oi < bi[i])) {
-          second[i] = fminf(os, best[i]);
-          best[i] = ob;
-          bi[i] = oi;
-        } else {
-          second[i] = fminf(second[i], ob);
-        }
+        merge_min<SECOND>(best[i], second[i], bi[i], ob, os, oi);
       }
     }
     if (split_plan) {   // workgroup-uniform: merge the split tiles' four code quarters, in order
@@ -241,30 +284,21 @@ __global__ __launch_bounds__(W * 64) void rq_quantize_kernel(
 #pragma unroll
       for (int i = 0; i < RQ_MAXT; ++i)
         if (i < my && is_split(i) && h == 0) {
-          float* e = pl + (((wk + i * WS - base) * 4 + simd) * 32 + r) * 3;
-          e[0] = best[i];
-          e[1] = second[i];
-          e[2] = __int_as_float(bi[i]);
+          float* ep = pl + (((wk + i * WS - base) * 4 + simd) * 32 + r) * 3;
+          ep[0] = best[i];
+          ep[1] = second[i];
+          ep[2] = __int_as_float(bi[i]);
         }
       __syncthreads();
 #pragma unroll
       for (int i = 0; i < RQ_MAXT; ++i)
         if (i < my && is_split(i)) {
-          const float* e = pl + ((wk + i * WS - base) * 4 * 32 + r) * 3;
-          float bb = e[0], ss = e[1];
-          int ii = __float_as_int(e[2]);
+          const float* ep = pl + ((wk + i * WS - base) * 4 * 32 + r) * 3;
+          float bb = ep[0], ss = ep[1];
+          int ii = __float_as_int(ep[2]);
 #pragma unroll
-          for (int q = 1; q < 4; ++q) {
-            const float ob = e[q * 96], os = e[q * 96 + 1];
-            const int oi = __float_as_int(e[q * 96 + 2]);
-            if (ob < bb || (ob == bb && oi < ii)) {
-              ss = fminf(os, bb);
-              bb = ob;
-              ii = oi;
-            } else {
-              ss = fminf(ss, ob);
-            }
-          }
+          for (int q = 1; q < 4; ++q)
+            merge_min<SECOND>(bb, ss, ii, ep[q * 96], ep[q * 96 + 1], __float_as_int(ep[q * 96 + 2]));
           best[i] = bb;
           second[i] = ss;
           bi[i] = ii;
@@ -282,22 +316,38 @@ __global__ __launch_bounds__(W * 64) void rq_quantize_kernel(
           if (best_out) best_out[item * L + l] = best[i];
           if (gap_out) gap_out[item * L + l] = second[i] - best[i];
         }
-        const bool in_lds = b >= c_last;   // the winner's row is still in the LDS image
-        f32x4 c[HQ];
+        f32x4 cw[HQ];
+        if (b >= c_last) {   // the winner's row is still in the LDS image
 #pragma unroll
-        for (int j = 0; j < HQ; ++j)
-          c[j] = in_lds ? *reinterpret_cast<const f32x4*>(lcbs + cb_off<E>(b - c_last, HQ * h + j))
-                        : *reinterpret_cast<const f32x4*>(cb + (int64_t)b * E + (E / 2) * h + 4 * j);
+          for (int j = 0; j < HQ; ++j)
+            cw[j] = *reinterpret_cast<const f32x4*>(cbs + cb_off<EP>(b - c_last, HQ * h + j));
+        } else {
+#pragma unroll
+          for (int j = 0; j < HQ; ++j)
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+              const int f = 8 * j + 2 * s + h;
+              cw[j][s] = f < e ? cb[(int64_t)b * e + f] : 0.f;
+            }
+        }
 #pragma unroll
         for (int j = 0; j < HQ; ++j)
 #pragma unroll
           for (int s = 0; s < 4; ++s) {
-            const float xq = res[i][j][s] + (c[j][s] - res[i][j][s]);   // vq.py:95
-            res[i][j][s] = res[i][j][s] - xq;                           // rq.py:47
+            const float xq = res[i][j][s] + (cw[j][s] - res[i][j][s]);   // vq.py:95
+            res[i][j][s] = res[i][j][s] - xq;                            // rq.py:47
           }
       }
     }
   }
+}
+
+__global__ __launch_bounds__(256) void rq_code_norms_kernel(const float* __restrict__ cb, int K,
+                                                            int e, float* __restrict__ cn) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= K) return;
+  const float* row = cb + (int64_t)c * e;
+  cn[c] = aten_rowsq([&](int f) { return row[f]; }, e);
 }
 
 static int cu_count() {
@@ -316,40 +366,29 @@ static int launch_norms(const float* cb, int K, int e, float* cn, hipStream_t st
   return check_launch("gr_rq_codebook_norms_f32");
 }
 
-template <int E>
-static int launch_quantize_e(const float* z, int64_t n, int L, const RQLevels& lv, int64_t* idx,
+template <int EP>
+static int launch_quantize_e(const float* z, int64_t n, int e, int L, const RQLevels& lv, int64_t* idx,
                              float* best, float* gap, hipStream_t st) {
-  int kmax = 0, ktot = 0;
-  for (int l = 0; l < L; ++l) {
-    kmax = lv.K[l] > kmax ? lv.K[l] : kmax;
-    ktot += (lv.K[l] + 31) & ~31;
-  }
-  const int kch_max = 1024 * 32 / E;                         // 128 KiB of codebook per chunk
-  // every level resident in LDS at once when they fit in 128 KiB (C2: 3 x 256 x 32 -> 99 KiB)
-  const bool resident = option("rq_resident") != 0 && (size_t)ktot * (E + 1) * 4 <= 128 * 1024;
-  const int kch = resident ? 0 : ((kmax < kch_max ? kmax : kch_max) + 31) & ~31;
-  const size_t lds = (resident ? (size_t)ktot * (E + 1) * 4 : (size_t)kch * E * 4 + (size_t)kch * 4) + RQ_PART_BYTES;
+  int kmax = 0;
+  for (int l = 0; l < L; ++l) kmax = lv.K[l] > kmax ? lv.K[l] : kmax;
+  const int kch_max = 1024 * 32 / EP;                        // 128 KiB of codebook per chunk
+  const int kch = ((kmax < kch_max ? kmax : kch_max) + 31) & ~31;
+  const size_t lds = (size_t)kch * EP * 4 + (size_t)kch * 4 + RQ_PART_BYTES;
   // persistent: one 8-wave workgroup per CU (2 waves per SIMD at this register budget), each with
   // a contiguous balanced range of tiles; more workgroups only when a range would exceed the
   // register-resident residuals (W x MT tiles)
   const int64_t tiles = (n + 31) / 32;
   int64_t grid = (int64_t)cu_count();
-  // rq_waves 16 (e <= 32): 16-wave workgroups, 4 waves per SIMD, so a SIMD's item tiles run as
-  // concurrent waves (one hides another's argmin epilogue and LDS latency) instead of in sequence
-  const int W = (E <= 32 && option("rq_waves") == 16) ? 16 : 8;
-  const int MT = W == 16 ? RQMaxT<E, 16>::value : RQMaxT<E, 8>::value;
-  const int64_t min_grid = (tiles + W * MT - 1) / (W * MT);
+  const int64_t min_grid = (tiles + RQ_W * RQMaxT<EP>::value - 1) / (RQ_W * RQMaxT<EP>::value);
   if (grid < min_grid) grid = min_grid;
   if (grid > tiles) grid = tiles;
   if (grid > 0x7fffffffLL || tiles > 0x7fffffffLL) return fail(GR_ERR_UNSUPPORTED, "rq quantize: n too large");
-  auto k = (best || gap) ? rq_quantize_kernel<E, true, 8> : rq_quantize_kernel<E, false, 8>;
-  if constexpr (E <= 32)
-    if (W == 16) k = (best || gap) ? rq_quantize_kernel<E, true, 16> : rq_quantize_kernel<E, false, 16>;
+  auto k = (best || gap) ? rq_quantize_kernel<EP, true> : rq_quantize_kernel<EP, false>;
   if (lds > 64 * 1024 &&
       hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
                           (int)lds) != hipSuccess)
     return fail(GR_ERR_HIP, "rq quantize: cannot raise the LDS limit");
-  hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(W * 64), lds, st, z, n, L, lv, kch, idx,
+  hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(RQ_W * 64), lds, st, z, n, e, L, lv, kch, idx,
                      best, gap, (int)tiles, (int)(option("rq_split") != 0));
   return check_launch("gr_rq_quantize_f32");
 }
@@ -357,21 +396,19 @@ static int launch_quantize_e(const float* z, int64_t n, int L, const RQLevels& l
 static int launch_quantize(const float* z, int64_t n, int e, int L, const RQLevels& lv,
                            int64_t* idx, float* best, float* gap, hipStream_t st) {
   if (n == 0) return GR_OK;
-  switch (e) {
-    case 16: return launch_quantize_e<16>(z, n, L, lv, idx, best, gap, st);
-    case 32: return launch_quantize_e<32>(z, n, L, lv, idx, best, gap, st);
-    case 64: return launch_quantize_e<64>(z, n, L, lv, idx, best, gap, st);
-    default: return fail(GR_ERR_UNSUPPORTED, "gr_rq_quantize_f32: e_dim must be 16, 32 or 64");
-  }
+  if (e <= 16) return launch_quantize_e<16>(z, n, e, L, lv, idx, best, gap, st);
+  if (e <= 32) return launch_quantize_e<32>(z, n, e, L, lv, idx, best, gap, st);
+  if (e <= 64) return launch_quantize_e<64>(z, n, e, L, lv, idx, best, gap, st);
+  return fail(GR_ERR_UNSUPPORTED, "gr_rq_quantize_f32: e_dim must be <= 64");
 }
 
 static int check_levels(int32_t e, int32_t L, const int32_t* K, const float* const* cbs) {
-  if (e != 16 && e != 32 && e != 64) return fail(GR_ERR_UNSUPPORTED, "rq: e_dim must be 16, 32 or 64");
+  if (e < 1 || e > 64) return fail(GR_ERR_UNSUPPORTED, "rq: 1 <= e_dim <= 64");
   if (L < 1 || L > GR_MAX_LEVELS) return fail(GR_ERR_UNSUPPORTED, "rq: 1 <= L <= 8 levels");
   if (!K || !cbs) return fail(GR_ERR_ARG, "rq: null K / codebooks");
   for (int l = 0; l < L; ++l) {
     if (K[l] < 1) return fail(GR_ERR_ARG, "rq: codebook size must be >= 1");
-    if (!cbs[l] || !aligned16(cbs[l])) return fail(GR_ERR_ARG, "rq: codebooks must be 16-byte aligned");
+    if (!cbs[l] || ((e == 16 || e == 32 || e == 64) && !aligned16(cbs[l]))) return fail(GR_ERR_ARG, "rq: codebooks must be 16-byte aligned");
   }
   return GR_OK;
 }
@@ -396,7 +433,7 @@ extern "C" int gr_rq_quantize_f32(const float* z, int64_t n, int32_t e, int32_t 
   if (rc) return rc;
   if (n < 0) return fail(GR_ERR_ARG, "gr_rq_quantize_f32: n < 0");
   if (n == 0) return GR_OK;
-  if (!z || !idx_out || !aligned16(z)) return fail(GR_ERR_ARG, "gr_rq_quantize_f32: bad pointer");
+  if (!z || !idx_out || ((e == 16 || e == 32 || e == 64) && !aligned16(z))) return fail(GR_ERR_ARG, "gr_rq_quantize_f32: bad pointer");
   RQLevels lv{};
   for (int l = 0; l < L; ++l) {
     lv.cb[l] = codebooks[l];
@@ -406,14 +443,53 @@ extern "C" int gr_rq_quantize_f32(const float* z, int64_t n, int32_t e, int32_t 
 }
 
 // Workspace layout: two ping-pong activation buffers of the widest layer (the fused path uses the
-// first one for the encoder output z).
+// first one for the encoder output z), then the fused kernel's packed weights.
+static size_t act_bytes(int64_t n, int32_t n_linear, const int32_t* dims) {
+  int widest = 0;
+  for (int i = 1; i <= n_linear; ++i) widest = dims[i] > widest ? dims[i] : widest;
+  return gr::align_up((size_t)n * widest * 4, 256);
+}
+
+static size_t mlp_ws_bytes(int64_t n, int32_t n_linear, const int32_t* dims) {
+  return 2 * act_bytes(n, n_linear, dims) + gr::align_up(gr_rq_fused_pack_floats(n_linear, dims) * 4, 256) + 256;
+}
+
+// The encoder MLP in the reference's CPU order: the fused kernel when the shape is in -> 256 -> 128
+// -> 32 (ReLU, no BatchNorm), else one exact gr_linear launch per layer (any activation of
+// layers.py:45-67 that torch evaluates exactly: ReLU, LeakyReLU, none; optional eval BatchNorm1d).
+static int mlp_exact(const float* x, int64_t n, int32_t n_linear, const int32_t* dims, const float* const* weights,
+                     const float* const* biases, const float* const* bn_mean, const float* const* bn_var,
+                     const float* const* bn_w, const float* const* bn_b, float bn_eps, int32_t act, float* z_out,
+                     void* workspace, hipStream_t st) {
+  using namespace gr;
+  char* ws = reinterpret_cast<char*>(align_up(reinterpret_cast<uintptr_t>(workspace), 256));
+  const size_t ab = act_bytes(n, n_linear, dims);
+  float* buf[2] = {reinterpret_cast<float*>(ws), reinterpret_cast<float*>(ws + ab)};
+  if (!bn_mean && act == GR_ACT_RELU && option("rq_fused") == 1) {
+    const int rc = gr_rq_encoder_fused_launch(x, n, n_linear, dims, weights, biases, z_out,
+                                              reinterpret_cast<float*>(ws + 2 * ab), st);
+    if (rc != GR_ERR_UNSUPPORTED) return rc;
+    clear_error();
+  }
+  const float* cur = x;
+  for (int i = 0; i < n_linear; ++i) {
+    const bool last = i == n_linear - 1;
+    float* out = last ? z_out : buf[i & 1];
+    const bool bn = bn_mean && !last;
+    const int rc = gr_linear_exact_launch(cur, n, dims[i], weights[i], dims[i + 1], biases ? biases[i] : nullptr,
+                                          bn ? bn_mean[i] : nullptr, bn ? bn_var[i] : nullptr,
+                                          bn && bn_w ? bn_w[i] : nullptr, bn && bn_b ? bn_b[i] : nullptr, bn_eps,
+                                          last ? GR_ACT_NONE : act, out, st);
+    if (rc) return rc;
+    cur = out;
+  }
+  return GR_OK;
+}
+
 extern "C" size_t gr_rq_encode_workspace_bytes(int64_t n, int32_t n_linear, const int32_t* dims,
                                                int32_t L, const int32_t* K) {
   if (n < 0 || n_linear < 1 || !dims || L < 1 || !K) return 0;
-  int widest = 0;
-  for (int i = 1; i <= n_linear; ++i) widest = dims[i] > widest ? dims[i] : widest;
-  const size_t act = gr::align_up((size_t)n * widest * 4, 256);
-  return 2 * act + 256;
+  return mlp_ws_bytes(n, n_linear, dims) + gr::align_up((size_t)n * dims[n_linear] * 4, 256);
 }
 
 extern "C" int gr_rq_encode_f32(const float* x, int64_t n, int32_t n_linear, const int32_t* dims,
@@ -435,80 +511,55 @@ extern "C" int gr_rq_encode_f32(const float* x, int64_t n, int32_t n_linear, con
     return fail(GR_ERR_WORKSPACE, "gr_rq_encode_f32: workspace too small (need " + std::to_string(need) + " bytes)");
   if (n == 0) return GR_OK;
   if (!x || !idx_out) return fail(GR_ERR_ARG, "gr_rq_encode_f32: null x / idx_out");
-  char* ws = reinterpret_cast<char*>(align_up(reinterpret_cast<uintptr_t>(workspace), 256));
-  int widest = 0;
-  for (int i = 1; i <= n_linear; ++i) widest = dims[i] > widest ? dims[i] : widest;
-  float* buf[2] = {reinterpret_cast<float*>(ws),
-                   reinterpret_cast<float*>(ws + align_up((size_t)n * widest * 4, 256))};
+  float* zb = z_out;
+  if (!zb) {   // z in the workspace, after the MLP's part
+    char* ws = reinterpret_cast<char*>(align_up(reinterpret_cast<uintptr_t>(workspace), 256));
+    zb = reinterpret_cast<float*>(ws + mlp_ws_bytes(n, n_linear, dims) - 256);
+  }
   RQLevels lv{};
   for (int l = 0; l < L; ++l) {
     lv.cb[l] = codebooks[l];
     lv.K[l] = K[l];
   }
-  const float* z = nullptr;
-  if (option("rq_fused") == 1) {
-    float* zb = z_out ? z_out : buf[0];
-    rc = gr_rq_encoder_fused_launch(x, n, n_linear, dims, weights, biases, zb, st);
-    if (rc == GR_OK) z = zb;
-    else if (rc != GR_ERR_UNSUPPORTED) return rc;
-    else clear_error();
-  }
-  if (!z) {  // layer-wise path
-    const float* cur = x;
-    for (int i = 0; i < n_linear; ++i) {
-      const bool last = i == n_linear - 1;
-      float* out = (last && z_out) ? z_out : buf[i & 1];
-      rc = gr_linear_launch(cur, n, dims[i], weights[i], dims[i + 1], biases ? biases[i] : nullptr,
-                            nullptr, 0, last ? GR_ACT_NONE : GR_ACT_RELU, out, dims[i + 1], st);
-      if (rc) return rc;
-      cur = out;
-    }
-    z = cur;
-  }
-  return launch_quantize(z, n, e, L, lv, idx_out, best_out, gap_out, st);
+  rc = mlp_exact(x, n, n_linear, dims, weights, biases, nullptr, nullptr, nullptr, nullptr, 0.f, GR_ACT_RELU,
+                 zb, workspace, st);
+  if (rc) return rc;
+  return launch_quantize(zb, n, e, L, lv, idx_out, best_out, gap_out, st);
 }
 
 // MLPLayers.forward (RQ-VAE/models/layers.py:42-43, eval): z[n, dims[n_linear]] = the encoder
-// output alone — the fused persistent kernel when the shape is in -> 256 -> 128 -> 32, the
-// layer-wise path otherwise.  Workspace: gr_rq_mlp_workspace_bytes.
+// output alone, in the reference's CPU order.  Workspace: gr_rq_mlp_workspace_bytes.
 extern "C" size_t gr_rq_mlp_workspace_bytes(int64_t n, int32_t n_linear, const int32_t* dims) {
   if (n < 0 || n_linear < 1 || !dims) return 0;
-  int widest = 0;
-  for (int i = 1; i <= n_linear; ++i) widest = dims[i] > widest ? dims[i] : widest;
-  return 2 * gr::align_up((size_t)n * widest * 4, 256) + 256;
+  return mlp_ws_bytes(n, n_linear, dims);
 }
 
 extern "C" int gr_rq_mlp_f32(const float* x, int64_t n, int32_t n_linear, const int32_t* dims,
                              const float* const* weights, const float* const* biases, float* z_out,
                              void* workspace, size_t workspace_bytes, void* stream) {
+  return gr_mlp_exact_f32(x, n, n_linear, dims, weights, biases, nullptr, nullptr, nullptr, nullptr, 0.f,
+                          GR_ACT_RELU, z_out, workspace, workspace_bytes, stream);
+}
+
+extern "C" int gr_mlp_exact_f32(const float* x, int64_t n, int32_t n_linear, const int32_t* dims,
+                                const float* const* weights, const float* const* biases,
+                                const float* const* bn_mean, const float* const* bn_var,
+                                const float* const* bn_w, const float* const* bn_b, float bn_eps,
+                                int32_t act, float* z_out, void* workspace, size_t workspace_bytes,
+                                void* stream) {
   using namespace gr;
   clear_error();
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (n_linear < 1 || n_linear > GR_MAX_LINEAR || !dims || !weights || n < 0)
-    return fail(GR_ERR_ARG, "gr_rq_mlp_f32: bad encoder description");
-  const size_t need = gr_rq_mlp_workspace_bytes(n, n_linear, dims);
+    return fail(GR_ERR_ARG, "gr_mlp_exact_f32: bad encoder description");
+  if (act != GR_ACT_RELU && act != GR_ACT_NONE && act != GR_ACT_LEAKYRELU)
+    return fail(GR_ERR_UNSUPPORTED, "gr_mlp_exact_f32: act must be relu / leakyrelu / none");
+  if ((bn_mean == nullptr) != (bn_var == nullptr)) return fail(GR_ERR_ARG, "gr_mlp_exact_f32: bn mean / var");
+  const size_t need = mlp_ws_bytes(n, n_linear, dims);
   if (!workspace || workspace_bytes < need)
-    return fail(GR_ERR_WORKSPACE, "gr_rq_mlp_f32: workspace too small (need " + std::to_string(need) + " bytes)");
+    return fail(GR_ERR_WORKSPACE, "gr_mlp_exact_f32: workspace too small (need " + std::to_string(need) + " bytes)");
   if (n == 0) return GR_OK;
-  if (!x || !z_out) return fail(GR_ERR_ARG, "gr_rq_mlp_f32: null x / z_out");
-  if (option("rq_fused") == 1) {
-    const int rc = gr_rq_encoder_fused_launch(x, n, n_linear, dims, weights, biases, z_out, st);
-    if (rc != GR_ERR_UNSUPPORTED) return rc;
-    clear_error();
-  }
-  char* ws = reinterpret_cast<char*>(align_up(reinterpret_cast<uintptr_t>(workspace), 256));
-  int widest = 0;
-  for (int i = 1; i <= n_linear; ++i) widest = dims[i] > widest ? dims[i] : widest;
-  float* buf[2] = {reinterpret_cast<float*>(ws),
-                   reinterpret_cast<float*>(ws + align_up((size_t)n * widest * 4, 256))};
-  const float* cur = x;
-  for (int i = 0; i < n_linear; ++i) {
-    const bool last = i == n_linear - 1;
-    float* out = last ? z_out : buf[i & 1];
-    const int rc = gr_linear_launch(cur, n, dims[i], weights[i], dims[i + 1], biases ? biases[i] : nullptr,
-                                    nullptr, 0, last ? GR_ACT_NONE : GR_ACT_RELU, out, dims[i + 1], st);
-    if (rc) return rc;
-    cur = out;
-  }
-  return GR_OK;
+  if (!x || !z_out) return fail(GR_ERR_ARG, "gr_mlp_exact_f32: null x / z_out");
+  return mlp_exact(x, n, n_linear, dims, weights, biases, bn_mean, bn_var, bn_w, bn_b, bn_eps, act, z_out,
+                   workspace, st);
 }

@@ -112,11 +112,8 @@ __global__ __launch_bounds__(SK_T) void rq_sk_kernel(const float* __restrict__ z
     // memory space, so the LDS copy compiles to ds_* accesses (a pointer selected at run time
     // between LDS and the workspace would make every access a flat one).
     auto level = [&](double* Q) __attribute__((always_inline)) {
-      for (int k = tid; k < K; k += SK_T) {
-        float s = 0.f;
-        for (int j = 0; j < e; ++j) s = fmaf(C[(int64_t)k * e + j], C[(int64_t)k * e + j], s);
-        cn[k] = s;
-      }
+      for (int k = tid; k < K; k += SK_T)   // |c|^2 in ATen's row-sum order (vq.py:72)
+        cn[k] = aten_rowsq([&](int f) { return C[(int64_t)k * e + f]; }, e);
       __syncthreads();
       // d = (|r|^2 + |c|^2) - 2 r.c in fp32 (vq.py:71-73), held as an exact double
       float mx = -FLT_MAX, mn = FLT_MAX;
@@ -124,11 +121,10 @@ __global__ __launch_bounds__(SK_T) void rq_sk_kernel(const float* __restrict__ z
         const int b = i / K, k = i % K;
         const float* rb = R + (int64_t)b * e;
         const float* ck = C + (int64_t)k * e;
-        float rn = 0.f, dot = 0.f;
-        for (int j = 0; j < e; ++j) {
-          rn = fmaf(rb[j], rb[j], rn);
-          dot = fmaf(rb[j], ck[j], dot);
-        }
+        // |r|^2 in ATen's row-sum order, r.c as MKL's one fma chain over k (oracle/rq_exact.c)
+        const float rn = aten_rowsq([&](int f) { return rb[f]; }, e);
+        float dot = 0.f;
+        for (int j = 0; j < e; ++j) dot = fmaf(rb[j], ck[j], dot);
         const float d = (rn + cn[k]) - 2.0f * dot;
         Q[b * P + k] = (double)d;
         mx = fmaxf(mx, d);

@@ -307,26 +307,48 @@ def rq_encode(x, weights=None, biases=None, codebooks=None, with_gap=False, with
     return out[0] if len(out) == 1 else tuple(out)
 
 
-def rq_mlp(x, weights, biases):
-    """MLPLayers.forward (RQ-VAE/models/layers.py:42-43, eval): the encoder output ``z`` alone."""
+_EXACT_ACTS = {"relu": 1, "none": 0, None: 0, "leakyrelu": 4}
+
+
+def rq_mlp(x, weights, biases, bn=None, act="relu"):
+    """MLPLayers.forward (RQ-VAE/models/layers.py:18-43, eval): the encoder output ``z`` alone, in
+    the reference's CPU order bit for bit (``gr_mlp_exact_f32``: the fused kernel for in -> 256 ->
+    128 -> 32 ReLU MLPs, exact layer-wise launches otherwise).  ``bn``: None, or (means, vars,
+    weights, biases, eps) of the eval BatchNorm1d after every Linear but the last (weights /
+    biases entries may be None: affine off); ``act``: relu / leakyrelu / none."""
     L.require_gpu(x, *weights)
     x2 = L.as_f32(x)
     n = x2.shape[0]
     ws = [L.as_f32(w) for w in weights]
-    bs = [L.as_f32(b) for b in biases]
+    bs = [L.as_f32(b) for b in biases] if biases is not None else None
     dims = [x2.shape[1]] + [w.shape[0] for w in ws]
     for i, w in enumerate(ws):
         if w.shape[1] != dims[i]:
             raise RuntimeError(f"rq_mlp: Linear {i} expects {w.shape[1]} inputs, got {dims[i]}")
+    if act not in _EXACT_ACTS:
+        raise RuntimeError(f"rq_mlp: activation {act} has no exact kernel (relu / leakyrelu / none)")
     dev = x.device
     lib = L.lib()
     dims_c = L.i32_array(dims)
     nbytes = lib.gr_rq_mlp_workspace_bytes(n, len(ws), dims_c)
     wsp = L.workspace(nbytes, dev)
     z = torch.empty((n, dims[-1]), dtype=torch.float32, device=dev)
+    bn_arrs = [None] * 4
+    eps = 0.0
+    keep = []
+    if bn is not None:
+        means, vars_, bws, bbs, eps = bn
+        for j, group in enumerate((means, vars_, bws, bbs)):
+            if group is None or all(t is None for t in group):
+                continue
+            ts = [L.as_f32(t) for t in group]
+            keep.append(ts)
+            bn_arrs[j] = L.ptr_array(ts)
     with torch.cuda.device(dev):
-        L.check(lib.gr_rq_mlp_f32(L.ptr(x2), n, len(ws), dims_c, L.ptr_array(ws), L.ptr_array(bs),
-                                  L.ptr(z), L.ptr(wsp), nbytes, L.stream_of(dev)), "gr_rq_mlp_f32")
+        L.check(lib.gr_mlp_exact_f32(L.ptr(x2), n, len(ws), dims_c, L.ptr_array(ws),
+                                     L.ptr_array(bs) if bs is not None else None, *bn_arrs, float(eps),
+                                     _EXACT_ACTS[act], L.ptr(z), L.ptr(wsp), nbytes, L.stream_of(dev)),
+                "gr_mlp_exact_f32")
     return z
 
 
@@ -336,6 +358,11 @@ def rq_encode_sk(x, weights, biases, codebooks, sk_eps, sk_iters, group_sizes=No
     consecutive groups, each one reference call (default: the whole batch is one group)."""
     L.require_gpu(x, *weights, *codebooks)
     return rq_quantize_sk(rq_mlp(x, weights, biases), codebooks, sk_eps, sk_iters, group_sizes)
+
+
+def rq_encode_z(z, codebooks, with_gap=False):
+    """``get_indices`` from encoder outputs computed elsewhere (e.g. a BatchNorm encoder)."""
+    return rq_quantize(z, codebooks, with_gap=with_gap)
 
 
 _GROUP_PTRS = {}

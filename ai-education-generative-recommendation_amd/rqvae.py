@@ -67,9 +67,10 @@ class MLPLayers(nn.Module):
     """Module tree of RQ-VAE/models/layers.py:9-40 (Dropout, Linear, [BatchNorm1d], activation per
     layer; none after the last Linear), xavier_normal_ weights and zero biases.
 
-    Eval forward on the kernels: a BatchNorm1d (running statistics) folds into the Linear before it
-    (W' = W * s, b' = (b - mean) * s + beta, s = gamma / sqrt(var + eps)); ReLU MLPs run the fused
-    encoder kernel (gr_rq_mlp_f32), other activations the gr_linear_f32 epilogues."""
+    Eval forward on the kernels in the reference's CPU order, bit for bit (gr_mlp_exact_f32): ReLU,
+    LeakyReLU and activation-free MLPs, with or without the eval BatchNorm1d (torch's CPU formula,
+    not folded); in -> 256 -> 128 -> 32 ReLU MLPs on the fused encoder kernel.  Sigmoid / Tanh run
+    the gr_linear_f32 epilogues (fp32-close, not bitwise: torch's CPU exp / tanh are its own)."""
 
     def __init__(self, layers, dropout=0.0, activation="relu", bn=False):
         super().__init__()
@@ -140,14 +141,25 @@ class MLPLayers(nn.Module):
             return ops.mlp_train(x, self)
         return self.mlp_layers(x)
 
+    def bn_params(self):
+        """(means, vars, weights, biases, eps) of the BatchNorm1d layers (``bn=True``), else None."""
+        bns = [m for m in self.mlp_layers if isinstance(m, nn.BatchNorm1d)]
+        if not bns:
+            return None
+        d = lambda t: None if t is None else t.detach()   # noqa: E731
+        return ([b.running_mean for b in bns], [b.running_var for b in bns], [d(b.weight) for b in bns],
+                [d(b.bias) for b in bns], float(bns[0].eps))
+
     def forward(self, x):
         if self.training and (self.dropout > 0 or self.use_bn):
             raise RuntimeError("gr_amd MLPLayers runs the eval-mode encoder: call .eval() (dropout / "
                                "BatchNorm batch statistics are train-mode only)")
-        if self.act not in ("relu", None) or self.act is None and len(self.linears()) > 1:
+        if self.act not in ("relu", "leakyrelu", None):
             return self.eval_forward(x)
-        ws, bs = self.folded()
-        return ops.rq_mlp(x, ws, bs)
+        lin = self.linears()
+        return ops.rq_mlp(x, [m.weight.detach() for m in lin],
+                          [m.bias.detach() if m.bias is not None else torch.zeros(m.out_features, device=x.device)
+                           for m in lin], bn=self.bn_params(), act=self.act or "none")
 
 
 class VectorQuantizer(nn.Module):
@@ -329,8 +341,9 @@ class RQVAE(nn.Module):
         whole batch (vq.py:76-84), as the reference does; the batch is one group."""
         self._check_encode(xs, use_sk)
         if use_sk and any(q.sk_epsilon > 0 for q in self.rq.vq_layers):
-            ws, bs = self.encoder.folded()
-            return ops.rq_encode_sk(xs, ws, bs, self.rq.codebooks(), self.sk_eps(), self.rq.sk_iters)
+            return ops.rq_quantize_sk(self.encoder(xs), self.rq.codebooks(), self.sk_eps(), self.rq.sk_iters)
+        if self.bn:   # the eval BatchNorm in torch's CPU formula, then the quantizer
+            return ops.rq_quantize(self.encoder(xs), self.rq.codebooks())
         return ops.rq_encode(xs, binding=self.encode_binding())
 
     def encode_binding(self):
@@ -354,8 +367,8 @@ class RQVAE(nn.Module):
         """``torch.cat([get_indices(g, use_sk=True) for g in groups])`` for consecutive row groups
         of ``xs`` in one launch — the per-group loop of RQ-VAE/infer.py:116-127."""
         self._check_encode(xs, True)
-        ws, bs = self.encoder.folded()
-        return ops.rq_encode_sk(xs, ws, bs, self.rq.codebooks(), self.sk_eps(), self.rq.sk_iters, group_sizes)
+        return ops.rq_quantize_sk(self.encoder(xs), self.rq.codebooks(), self.sk_eps(), self.rq.sk_iters,
+                                  group_sizes)
 
     @torch.no_grad()
     def get_indices_certified(self, xs):
@@ -365,5 +378,9 @@ class RQVAE(nn.Module):
         certificate (``near_tie_bound``): it may legitimately differ from a CPU run of the reference.
         Every unflagged row is the reference's answer."""
         self._check_encode(xs, False)
-        idx, best, gap, z = ops.rq_encode(xs, binding=self.encode_binding(), with_gap=True, with_z=True)
+        if self.bn:
+            z = self.encoder(xs)
+            idx, best, gap = ops.rq_quantize(z, self.rq.codebooks(), with_gap=True)
+        else:
+            idx, best, gap, z = ops.rq_encode(xs, binding=self.encode_binding(), with_gap=True, with_z=True)
         return idx, near_tie_rows(best, gap, (z * z).sum(1))

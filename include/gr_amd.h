@@ -48,7 +48,10 @@ const char* gr_version(void);
 const char* gr_last_error(void);
 /* Process-wide path / tuning options (no reference counterpart; used for A/B measurement):
  *   "rq_fused"      1 (default): gr_rq_encode_f32 runs the fused persistent kernel when the encoder
- *                   shape is in -> 256 -> 128 -> 32; 0: the layer-wise path (gr_linear + quantize)
+ *                   shape is in -> 256 -> 128 -> 32; 0: the layer-wise path (exact gr_linear +
+ *                   quantize).  Bitwise identical results.
+ *   "rq_split"      1 (default): a quantize workgroup's leftover item tiles are split into code
+ *                   quarters, one per SIMD; 0: round-robin.  Bitwise identical results.
  *   "sas_fused"     1 (default): gr_sasrec_forward_f32 / gr_sasrec_predict_f32 run the fused
  *                   register-resident forward kernel when n <= 64, d <= 64 (d and the head width
  *                   multiples of 8), mlp <= 128, num_blocks <= 8; 0: the layer-wise pipeline
@@ -93,14 +96,16 @@ int gr_rq_codebook_norms_f32(const float* codebook, int32_t K, int32_t e, float*
 /* Residual quantization of latents z[n, e] over L levels (RQ-VAE/models/rq.py:39-56 with
  * VectorQuantizer.forward(use_sk=False), vq.py:63-99):
  *   d = (||r||^2 + ||C_l||^2) - 2 r.C_l^T ;  idx = first argmin ;  r <- r - (r + (C_l[idx] - r))
+ * Every fp32 rounding is the reference's CPU one (r.C: one fma chain over k in order, as MKL's
+ * sgemm at K = e; the squared norms in ATen's vectorised row-sum order; oracle/rq_exact.c), so
+ * idx_out equals the reference's, exact ties included.
  * K, codebooks: host arrays of length L.  code_norms: accepted for ABI stability and ignored (may be
- * NULL); the kernel recomputes each code's norm from its LDS copy of the codebook with the same
- * k-ordered fma chain as gr_rq_codebook_norms_f32.
+ * NULL); the kernel recomputes each code's norm from its LDS copy of the codebook.
  * idx_out[n, L] int64 row-major (the stacked `indices` of rq.py:54).
  * best_out[n, L], gap_out[n, L] (optional, may be NULL): the best fp32 distance and the gap to the
- * second best per level — the near-tie certificate (a row whose gap is within fp32 rounding of
- * the distances may legitimately differ from a CPU run of the reference).
- * Supports e in {16, 32, 64}, 1 <= L <= GR_MAX_LEVELS, any K >= 1. */
+ * second best per level.
+ * Supports 1 <= e <= 64, 1 <= L <= GR_MAX_LEVELS, any K >= 1; z and the codebooks must be 16-byte
+ * aligned when e is 16, 32 or 64. */
 int gr_rq_quantize_f32(const float* z, int64_t n, int32_t e, int32_t L, const int32_t* K,
                        const float* const* codebooks, const float* const* code_norms,
                        int64_t* idx_out, float* best_out, float* gap_out, void* stream);
@@ -112,6 +117,10 @@ size_t gr_rq_encode_workspace_bytes(int64_t n, int32_t n_linear, const int32_t* 
 
 /* RQVAE.get_indices(xs, use_sk=False) (RQ-VAE/models/rqvae.py:67-71): encoder MLP
  * (layers.py:42-43; ReLU after every Linear but the last) followed by gr_rq_quantize_f32.
+ * The encoder reproduces the reference's CPU nn.Linear bit for bit (MKL's k blocking: one fma chain
+ * per block, y = bias; y += block 0; y += block 1) for every in_features <= 768 (multiples of 4; a
+ * two-block layer needs its block edge on a multiple of 8); other widths are refused
+ * (GR_ERR_UNSUPPORTED). 
  * weights/biases: host arrays (n_linear) of device pointers; codebooks, K: host arrays (L).
  * best_out, gap_out: as gr_rq_quantize_f32 (optional).
  * z_out (optional, may be NULL): the encoder output [n, e]. */
@@ -127,6 +136,19 @@ size_t gr_rq_mlp_workspace_bytes(int64_t n, int32_t n_linear, const int32_t* dim
 int gr_rq_mlp_f32(const float* x, int64_t n, int32_t n_linear, const int32_t* dims,
                   const float* const* weights, const float* const* biases, float* z_out,
                   void* workspace, size_t workspace_bytes, void* stream);
+
+/* MLPLayers.forward in eval mode with the general layer options of RQ-VAE/models/layers.py:18-43,
+ * in the reference's exact CPU order: per layer Linear, then (all but the last) an eval
+ * BatchNorm1d when bn_mean / bn_var are given (host arrays of n_linear - 1 device pointers; bn_w /
+ * bn_b may be NULL arrays = affine off; torch's CPU formula a = w / sqrt(var + eps),
+ * y = fma(y, a, fma(-mean, a, b))) and act (GR_ACT_RELU / GR_ACT_LEAKYRELU / GR_ACT_NONE).
+ * Workspace: gr_rq_mlp_workspace_bytes. */
+int gr_mlp_exact_f32(const float* x, int64_t n, int32_t n_linear, const int32_t* dims,
+                     const float* const* weights, const float* const* biases,
+                     const float* const* bn_mean, const float* const* bn_var,
+                     const float* const* bn_w, const float* const* bn_b, float bn_eps,
+                     int32_t act, float* z_out, void* workspace, size_t workspace_bytes,
+                     void* stream);
 
 /* MLPLayers.forward in train mode (RQ-VAE/models/layers.py:18-43, [Dropout -> Linear -> ReLU] x
  * (n_linear - 1), then Dropout -> Linear; RQVAE.forward under RQ-VAE/train.py:113).  Dropout p_drop
