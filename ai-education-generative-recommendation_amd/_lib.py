@@ -55,6 +55,10 @@ SIGNATURES = {
     "gr_rq_encode_workspace_bytes": (_sz, [_i64, _i32, _vp, _i32, _vp]),
     "gr_rq_encode_f32": (ctypes.c_int, [_vp, _i64, _i32, _vp, _vp, _vp, _i32, _vp, _vp, _vp, _vp,
                                         _vp, _vp, _vp, _sz, _vp]),
+    "gr_rq_encoder_pack_floats": (_sz, [_i32, _vp]),
+    "gr_rq_encoder_pack_f32": (ctypes.c_int, [_i32, _vp, _vp, _vp, _vp]),
+    "gr_rq_encode_packed_f32": (ctypes.c_int, [_vp, _i64, _i32, _vp, _vp, _vp, _vp, _i32, _vp, _vp, _vp,
+                                               _vp, _vp, _vp, _vp, _sz, _vp]),
     "gr_rq_mlp_workspace_bytes": (_sz, [_i64, _i32, _vp]),
     "gr_rq_mlp_f32": (ctypes.c_int, [_vp, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
     "gr_mlp_exact_f32": (ctypes.c_int, [_vp, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _f32, _i32,

@@ -78,6 +78,7 @@ __device__ __forceinline__ float aten_rowsq(At at, int e) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[a][j] = 0.f;
   const int nv = e >> 3, full = (nv >> 2) << 2;
+#pragma unroll
   for (int v = 0; v < nv; ++v) {
     const int a = v < full ? (v & 3) : 0;
 #pragma unroll
@@ -113,12 +114,21 @@ __host__ __device__ inline int mkl_kblock(int K) {
   return (((K + 1) / 2) + 3) & ~3;
 }
 
+// f32-input MFMA 16x16x4: an fma chain over its four k slots in ascending order (lane group
+// l >> 4 = k; profiles/r03_mfma_order.txt).  Lane l supplies A[i = l&15][k = l>>4] and
+// B[k = l>>4][j = l&15]; D register v of lane l holds row 4 (l>>4) + v, column l&15.
+__device__ __forceinline__ f32x4 mfma16(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
 }  // namespace gr
 
 // Internal launchers shared between translation units (all enqueue on `stream`, no sync).
 int gr_rq_encoder_fused_launch(const float* x, int64_t n, int32_t n_linear, const int32_t* dims,
                                const float* const* weights, const float* const* biases,
-                               float* z_out, float* pack, hipStream_t st);
+                               float* z_out, float* pack, hipStream_t st, bool pack_is_ready);
+int gr_rq_encoder_pack_launch(int32_t n_linear, const int32_t* dims, const float* const* weights, float* pack,
+                              hipStream_t st);
 size_t gr_rq_fused_pack_floats(int32_t n_linear, const int32_t* dims);
 int gr_sasrec_fused_launch(const gr_sasrec_params* p, const int64_t* seqs, int64_t B, int32_t n,
                            float* out, int32_t last_only, int32_t* err, hipStream_t st);

@@ -127,11 +127,11 @@ __device__ __forceinline__ void merge_min(float& best, float& second, int& bi, f
 }
 
 // Stage codes [c0, c0 + cnt) of a level into the LDS image (de-interleaved rows) and their norms.
-template <int EP, int NT>
+template <int EP, int NT, bool FULL>
 __device__ __forceinline__ void stage_codes(const float* __restrict__ cb, int e, int c0, int cnt,
                                             float* cbs, float* cns, int tid) {
   constexpr int HQ = EP / 8;
-  if (e == EP) {   // 16-byte rows: a float4 of features 4u..4u+3 -> two 8-byte halves
+  if (FULL) {   // 16-byte rows: a float4 of features 4u..4u+3 -> two 8-byte halves
     for (int f = tid; f < cnt * (EP / 4); f += NT) {
       const int c = f / (EP / 4), u = f % (EP / 4), j = u >> 1, e2 = 2 * (u & 1);
       const f32x4 v = *reinterpret_cast<const f32x4*>(cb + (int64_t)(c0 + c) * EP + 4 * u);
@@ -145,17 +145,34 @@ __device__ __forceinline__ void stage_codes(const float* __restrict__ cb, int e,
     }
   }
   __syncthreads();
-  for (int c = tid; c < ((cnt + 31) & ~31); c += NT)
-    cns[c] = c < cnt ? aten_rowsq([&](int f) { return cbs[feat_off<EP>(c, f)]; }, e)
-                     : __builtin_inff();   // codes past K can never win
+  for (int c = tid; c < ((cnt + 31) & ~31); c += NT) {
+    float s = __builtin_inff();   // codes past K can never win
+    if (c < cnt) {
+      if (FULL) {   // the row's 2 HQ slots as float4 reads, features back in natural order
+        float v[EP];
+#pragma unroll
+        for (int q = 0; q < 2 * HQ; ++q) {
+          const f32x4 t = *reinterpret_cast<const f32x4*>(cbs + cb_off<EP>(c, q));
+#pragma unroll
+          for (int i = 0; i < 4; ++i) v[8 * (q % HQ) + 2 * i + q / HQ] = t[i];
+        }
+        s = aten_rowsq([&](int f) { return v[f]; }, EP);
+      } else {
+        s = aten_rowsq([&](int f) { return cbs[feat_off<EP>(c, f)]; }, e);
+      }
+    }
+    cns[c] = s;
+  }
   __syncthreads();
 }
 
-template <int EP, bool SECOND>
+// FULL: e == EP (16, 32, 64): every loop bound compile-time, 16-byte rows.
+template <int EP, bool SECOND, bool FULL>
 __global__ __launch_bounds__(RQ_W * 64) void rq_quantize_kernel(
-    const float* __restrict__ z, int64_t n, int e, int L, RQLevels lv, int kch, int64_t* __restrict__ idx_out,
+    const float* __restrict__ z, int64_t n, int e_in, int L, RQLevels lv, int kch, int64_t* __restrict__ idx_out,
     float* __restrict__ best_out, float* __restrict__ gap_out, int tiles, int split_ok) {
 #pragma clang fp contract(off)
+  const int e = FULL ? EP : e_in;
   static_assert(EP % 8 == 0 && EP <= 64, "e");
   constexpr int W = RQ_W, NT = W * 64;
   constexpr int HQ = EP / 8;           // float4 per lane half
@@ -192,7 +209,7 @@ __global__ __launch_bounds__(RQ_W * 64) void rq_quantize_kernel(
     const int64_t item = (int64_t)tile_of(i) * 32 + r;
     const bool ok = i < my && item < n;
     const int64_t ic = ok ? item : 0;
-    if (e == EP) {
+    if (FULL) {
 #pragma unroll
       for (int j = 0; j < HQ; ++j) {
         const f32x4 lo = *reinterpret_cast<const f32x4*>(z + ic * EP + 8 * j);
@@ -227,7 +244,7 @@ __global__ __launch_bounds__(RQ_W * 64) void rq_quantize_kernel(
     for (int c0 = 0; c0 < K; c0 += kch) {
       const int cnt = min(kch, K - c0);
       __syncthreads();   // previous chunk / level fully consumed
-      stage_codes<EP, NT>(cb, e, c0, cnt, cbs, cns, tid);
+      stage_codes<EP, NT, FULL>(cb, e, c0, cnt, cbs, cns, tid);
       const int ct_n = (cnt + 31) >> 5;
       const int q_lo = simd * ct_n / 4, q_hi = (simd + 1) * ct_n / 4;   // this SIMD's code quarter
 #pragma unroll 1
@@ -258,9 +275,8 @@ __global__ __launch_bounds__(RQ_W * 64) void rq_quantize_kernel(
 #pragma unroll
             for (int v = 0; v < 16; ++v) {
               const int cd = c0 + ct * 32 + (v & 3) + 8 * (v >> 2) + 4 * h;
-              const float sn = rn[i] + cnv[v];
-              const float tw = 2.f * acc[v];
-              const float dd = sn - tw;
+              // (|r|^2 + |c|^2) - 2 r.c: 2 r.c is exact, so one fma rounds the same value
+              const float dd = fmaf(-2.f, acc[v], rn[i] + cnv[v]);
               const bool lt = dd < best[i];
               if (SECOND) second[i] = lt ? best[i] : fminf(second[i], dd);
               bi[i] = lt ? cd : bi[i];
@@ -383,7 +399,9 @@ static int launch_quantize_e(const float* z, int64_t n, int e, int L, const RQLe
   if (grid < min_grid) grid = min_grid;
   if (grid > tiles) grid = tiles;
   if (grid > 0x7fffffffLL || tiles > 0x7fffffffLL) return fail(GR_ERR_UNSUPPORTED, "rq quantize: n too large");
-  auto k = (best || gap) ? rq_quantize_kernel<EP, true> : rq_quantize_kernel<EP, false>;
+  const bool full = e == EP;
+  auto k = (best || gap) ? (full ? rq_quantize_kernel<EP, true, true> : rq_quantize_kernel<EP, true, false>)
+                         : (full ? rq_quantize_kernel<EP, false, true> : rq_quantize_kernel<EP, false, false>);
   if (lds > 64 * 1024 &&
       hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
                           (int)lds) != hipSuccess)
@@ -460,14 +478,15 @@ static size_t mlp_ws_bytes(int64_t n, int32_t n_linear, const int32_t* dims) {
 static int mlp_exact(const float* x, int64_t n, int32_t n_linear, const int32_t* dims, const float* const* weights,
                      const float* const* biases, const float* const* bn_mean, const float* const* bn_var,
                      const float* const* bn_w, const float* const* bn_b, float bn_eps, int32_t act, float* z_out,
-                     void* workspace, hipStream_t st) {
+                     void* workspace, hipStream_t st, const float* packed = nullptr) {
   using namespace gr;
   char* ws = reinterpret_cast<char*>(align_up(reinterpret_cast<uintptr_t>(workspace), 256));
   const size_t ab = act_bytes(n, n_linear, dims);
   float* buf[2] = {reinterpret_cast<float*>(ws), reinterpret_cast<float*>(ws + ab)};
   if (!bn_mean && act == GR_ACT_RELU && option("rq_fused") == 1) {
     const int rc = gr_rq_encoder_fused_launch(x, n, n_linear, dims, weights, biases, z_out,
-                                              reinterpret_cast<float*>(ws + 2 * ab), st);
+                                              packed ? const_cast<float*>(packed) : reinterpret_cast<float*>(ws + 2 * ab),
+                                              st, packed != nullptr);
     if (rc != GR_ERR_UNSUPPORTED) return rc;
     clear_error();
   }
@@ -492,16 +511,33 @@ extern "C" size_t gr_rq_encode_workspace_bytes(int64_t n, int32_t n_linear, cons
   return mlp_ws_bytes(n, n_linear, dims) + gr::align_up((size_t)n * dims[n_linear] * 4, 256);
 }
 
-extern "C" int gr_rq_encode_f32(const float* x, int64_t n, int32_t n_linear, const int32_t* dims,
-                                const float* const* weights, const float* const* biases, int32_t L,
-                                const int32_t* K, const float* const* codebooks, int64_t* idx_out,
-                                float* best_out, float* gap_out, float* z_out, void* workspace,
-                                size_t workspace_bytes, void* stream) {
+extern "C" size_t gr_rq_encoder_pack_floats(int32_t n_linear, const int32_t* dims) {
+  return (n_linear < 1 || !dims) ? 0 : gr_rq_fused_pack_floats(n_linear, dims);
+}
+
+extern "C" int gr_rq_encoder_pack_f32(int32_t n_linear, const int32_t* dims, const float* const* weights,
+                                      float* packed, void* stream) {
+  using namespace gr;
+  clear_error();
+  if (n_linear < 1 || !dims || !weights || !packed || !aligned16(packed))
+    return fail(GR_ERR_ARG, "gr_rq_encoder_pack_f32: bad arguments");
+  const int rc = gr_rq_encoder_pack_launch(n_linear, dims, weights, packed, reinterpret_cast<hipStream_t>(stream));
+  if (rc == GR_ERR_UNSUPPORTED) return fail(rc, "gr_rq_encoder_pack_f32: not the fused encoder shape");
+  return rc;
+}
+
+extern "C" int gr_rq_encode_packed_f32(const float* x, int64_t n, int32_t n_linear, const int32_t* dims,
+                                       const float* const* weights, const float* const* biases,
+                                       const float* packed, int32_t L, const int32_t* K,
+                                       const float* const* codebooks, int64_t* idx_out, float* best_out,
+                                       float* gap_out, float* z_out, void* workspace, size_t workspace_bytes,
+                                       void* stream) {
   using namespace gr;
   clear_error();
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (n_linear < 1 || n_linear > GR_MAX_LINEAR || !dims || !weights)
     return fail(GR_ERR_ARG, "gr_rq_encode_f32: bad encoder description");
+  if (packed && !aligned16(packed)) return fail(GR_ERR_ARG, "gr_rq_encode_packed_f32: packed not 16-byte aligned");
   const int e = dims[n_linear];
   int rc = check_levels(e, L, K, codebooks);
   if (rc) return rc;
@@ -522,9 +558,18 @@ extern "C" int gr_rq_encode_f32(const float* x, int64_t n, int32_t n_linear, con
     lv.K[l] = K[l];
   }
   rc = mlp_exact(x, n, n_linear, dims, weights, biases, nullptr, nullptr, nullptr, nullptr, 0.f, GR_ACT_RELU,
-                 zb, workspace, st);
+                 zb, workspace, st, packed);
   if (rc) return rc;
   return launch_quantize(zb, n, e, L, lv, idx_out, best_out, gap_out, st);
+}
+
+extern "C" int gr_rq_encode_f32(const float* x, int64_t n, int32_t n_linear, const int32_t* dims,
+                                const float* const* weights, const float* const* biases, int32_t L,
+                                const int32_t* K, const float* const* codebooks, int64_t* idx_out,
+                                float* best_out, float* gap_out, float* z_out, void* workspace,
+                                size_t workspace_bytes, void* stream) {
+  return gr_rq_encode_packed_f32(x, n, n_linear, dims, weights, biases, nullptr, L, K, codebooks, idx_out,
+                                 best_out, gap_out, z_out, workspace, workspace_bytes, stream);
 }
 
 // MLPLayers.forward (RQ-VAE/models/layers.py:42-43, eval): z[n, dims[n_linear]] = the encoder

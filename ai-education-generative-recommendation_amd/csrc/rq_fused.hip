@@ -18,9 +18,10 @@
 //       W1 fragments go straight from L2 to registers, software-pipelined one 32-deep group ahead;
 //       the x chunk ([32FP x 64]) is shared through a double-buffered LDS image staged one chunk
 //       ahead (across pass boundaries too).  At the MKL block boundary the first block's sum plus
-//       the bias is parked in the h1 image and the chain restarts from zero.
+//       the bias moves to registers and the chain restarts from zero.
 //   L2  h2^T[128 x 32FP] = W2 . relu(h1)^T   waves 0-3, wave w owns features [32w, 32w+32)
-//   L3  z^T[32 x 32FP] = W3 . relu(h2)^T     wave it < FP: item tile it, the whole k = 128 chain
+//   L3  z^T[32 x 32FP] = W3 . relu(h2)^T     16x16x4 MFMA tiles (also an fma chain in k order),
+//       one per wave, each the whole k = 128 chain
 #include <type_traits>
 
 #include "gr_common.h"
@@ -52,6 +53,12 @@ __device__ __forceinline__ void put_packed(float* row, int k0, const f32x4& v) {
   *reinterpret_cast<f32x2*>(row + g + 16 + 4 * j + e2) = f32x2{v[1], v[3]};
 }
 
+// x staging: thread f of the workgroup moves 16 bytes (features 4u..4u+3, u = f & 15) of item row
+// xrow(f) of a chunk.  The 16 lanes of a row are contiguous (256-byte global segments); the two rows
+// of a half-wave are 4 apart, 4 x FXP = 16 floats mod 64 banks, so their packed 8-byte LDS writes
+// ([0, 16) + [32, 48) and [16, 32) + [48, 64) of a row's window) never share a bank.
+__device__ __forceinline__ int xrow(int f) { return ((f >> 7) << 3) + ((f >> 5) & 3) + 4 * ((f >> 4) & 1); }
+
 // Per-workgroup state that lives across passes (x staging registers, W1 prefetch, LDS buffer).
 template <int H1, int H2>
 struct FusedCtx {
@@ -74,7 +81,7 @@ struct FusedCtx {
   __device__ __forceinline__ void gload_x(int tb, int c) {
 #pragma unroll
     for (int i = 0; i < C::XV; ++i) {
-      const int f = tid + C::NTH * i, it = f >> 4, k4 = (f & 15) * 4;
+      const int f = tid + C::NTH * i, it = xrow(f), k4 = (f & 15) * 4;
       const int64_t item = (int64_t)tb * FT + it;
       xok[i] = item < n && (tb + it / FT) < t_end;
       xr[i] = *reinterpret_cast<const f32x4*>(x + (item < n ? item : n - 1) * D0 +
@@ -85,7 +92,7 @@ struct FusedCtx {
 #pragma unroll
     for (int i = 0; i < C::XV; ++i) {
       const int f = tid + C::NTH * i;
-      put_packed(xs + b * C::PI * FXP + (f >> 4) * FXP, (f & 15) * 4,
+      put_packed(xs + b * C::PI * FXP + xrow(f) * FXP, (f & 15) * 4,
                  xok[i] ? xr[i] : f32x4{0.f, 0.f, 0.f, 0.f});
     }
   }
@@ -96,11 +103,6 @@ struct FusedCtx {
 __device__ __forceinline__ void store_h_packed(float* row, int g4, int h, const f32x4& o) {
   *reinterpret_cast<f32x2*>(row + 4 * g4 + 2 * h) = f32x2{o[0], o[2]};
   *reinterpret_cast<f32x2*>(row + 16 + 4 * g4 + 2 * h) = f32x2{o[1], o[3]};
-}
-__device__ __forceinline__ f32x4 load_h_packed(const float* row, int g4, int h) {
-  const f32x2 a = *reinterpret_cast<const f32x2*>(row + 4 * g4 + 2 * h);
-  const f32x2 b = *reinterpret_cast<const f32x2*>(row + 16 + 4 * g4 + 2 * h);
-  return f32x4{a[0], b[0], a[1], b[1]};
 }
 
 // One pass over NP (compile-time) item tiles starting at tile tb.  No runtime branch depends on
@@ -137,7 +139,7 @@ __device__ __forceinline__ void rq_fused_pass(FusedCtx<H1, H2>& cx, int tb) {
   bool xok_cur[C::XV], xok_nxt[C::XV];   // rows past n / past this workgroup's range -> zeros
 #pragma unroll
   for (int i = 0; i < C::XV; ++i) {
-    const int f = cx.tid + C::NTH * i, it = f >> 4, k4 = (f & 15) * 4;
+    const int f = cx.tid + C::NTH * i, it = xrow(f), k4 = (f & 15) * 4;
     const int64_t a = (int64_t)tb * FT + it, b = (int64_t)next_tb * FT + it;
     xsrc[i] = cx.x + (a < cx.n ? a : cx.n - 1) * cx.D0 + k4;
     xnxt[i] = cx.x + (b < cx.n ? b : cx.n - 1) * cx.D0 + k4;
@@ -176,7 +178,7 @@ __device__ __forceinline__ void rq_fused_pass(FusedCtx<H1, H2>& cx, int tb) {
       for (int i = 0; i < C::XV; ++i) {
         const int f = cx.tid + C::NTH * i;
         const bool ok = same ? xok_cur[i] : xok_nxt[i];
-        put_packed(cx.xs + (cx.buf ^ 1) * PI * FXP + (f >> 4) * FXP, (f & 15) * 4,
+        put_packed(cx.xs + (cx.buf ^ 1) * PI * FXP + xrow(f) * FXP, (f & 15) * 4,
                    ok ? cx.xr[i] : f32x4{0.f, 0.f, 0.f, 0.f});
       }
     }
@@ -214,48 +216,44 @@ __device__ __forceinline__ void rq_fused_pass(FusedCtx<H1, H2>& cx, int tb) {
     for (int j = 0; j < 4; ++j) cx.awc[j] = awn[j];
   };
   const int f0 = w * 32;   // this wave's first L1 feature
-#pragma unroll 1
-  for (int c = 0; c < NC; ++c) {
-    if (c == cx.csplit) {   // MKL's second k block: park b1 + block 0 in the h1 image, restart
-#pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4) {
-        const f32x4 bb = *reinterpret_cast<const f32x4*>(cx.b1 + f0 + 8 * g4 + 4 * h);
-#pragma unroll
-        for (int it = 0; it < NP; ++it) {
-          f32x4 o;
-#pragma unroll
-          for (int i = 0; i < 4; ++i) o[i] = bb[i] + acc1[it][4 * g4 + i];
-          store_h_packed(cx.h1s + (it * FT + r) * P1 + f0, g4, h, o);
-        }
-      }
-#pragma unroll
-      for (int it = 0; it < NP; ++it)
-#pragma unroll
-        for (int v = 0; v < 16; ++v) acc1[it][v] = 0.f;
-    }
+  auto chunk = [&](int c) {
     group(std::integral_constant<int, 0>{}, c);
     group(std::integral_constant<int, 1>{}, c);
     __syncthreads();
     cx.buf ^= 1;
-  }
-  // y = (b1 + block 0) + block 1 (or b1 + the single block), ReLU, h1 -> LDS packed
+  };
+  int c = 0;
+#pragma unroll 1
+  for (; c < cx.csplit; ++c) chunk(c);
+  // MKL's second k block (in = 768: k >= 384): keep b1 + block 0, restart the chain from zero
   const bool split = cx.csplit < NC;
+  f32x16 part[NP];
 #pragma unroll
   for (int g4 = 0; g4 < 4; ++g4) {
     const f32x4 bb = *reinterpret_cast<const f32x4*>(cx.b1 + f0 + 8 * g4 + 4 * h);
 #pragma unroll
+    for (int it = 0; it < NP; ++it)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        part[it][4 * g4 + i] = split ? bb[i] + acc1[it][4 * g4 + i] : bb[i];
+        if (split) acc1[it][4 * g4 + i] = 0.f;
+      }
+  }
+#pragma unroll 1
+  for (; c < NC; ++c) chunk(c);
+  // y = (b1 + block 0) + block 1 (or b1 + the single block), ReLU, h1 -> LDS packed
+#pragma unroll
+  for (int g4 = 0; g4 < 4; ++g4)
+#pragma unroll
     for (int it = 0; it < NP; ++it) {
-      float* row = cx.h1s + (it * FT + r) * P1 + f0;
-      const f32x4 t = split ? load_h_packed(row, g4, h) : bb;
       f32x4 o;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const float u = t[i] + acc1[it][4 * g4 + i];
+        const float u = part[it][4 * g4 + i] + acc1[it][4 * g4 + i];
         o[i] = u < 0.f ? 0.f : u;
       }
-      store_h_packed(row, g4, h, o);
+      store_h_packed(cx.h1s + (it * FT + r) * P1 + f0, g4, h, o);
     }
-  }
   __syncthreads();
 
   // ------------------------------------------------------------------ L2: W2 . h1^T
@@ -317,44 +315,41 @@ __device__ __forceinline__ void rq_fused_pass(FusedCtx<H1, H2>& cx, int tb) {
           const float u = bb[i] + acc2[it][4 * g4 + i];
           o[i] = u < 0.f ? 0.f : u;
         }
-        store_h_packed(cx.h2s + (it * FT + r) * P2 + w * 32, g4, h, o);
+        // L3 layout: within each 16-feature block, feature 4t + g at 4g + t (a lane of k group g
+        // reads four consecutive 16x16x4 steps as one float4)
+        float* row = cx.h2s + (it * FT + r) * P2 + w * 32 + 16 * (g4 >> 1);
+        const int t = (2 * g4 + h) & 3;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) row[4 * i + t] = o[i];
       }
     }
   }
   __syncthreads();
 
   // ------------------------------------------------------------------ L3: W3 . h2^T
-  // one k-ordered chain per item tile (wave it), z = b3 + chain, straight to HBM
-  if (w < NP) {
-    const int it = w;
-    f32x16 acc3;
+  // 16x16x4 tiles (16 outputs x 16 items), one per wave: item tile w >> 2, item half (w >> 1) & 1,
+  // output half w & 1; one k-ordered chain over k = 0..127 (32 MFMAs), z = b3 + chain, to HBM.
+  // W3 arrives packed for this form: feature 16b + 4t + g of a row at 16b + 4g + t.
+  if (w < 4 * NP) {
+    const int it = w >> 2, ih = (w >> 1) & 1, oh = w & 1;
+    const int lane = cx.tid & 63, j = lane & 15, g = lane >> 4;
+    f32x4 acc3 = {0.f, 0.f, 0.f, 0.f};
+    const float* hb = cx.h2s + (it * FT + 16 * ih + j) * P2 + 4 * g;
+    const float* w3row = cx.W3 + (int64_t)(16 * oh + j) * H2 + 4 * g;
 #pragma unroll
-    for (int v = 0; v < 16; ++v) acc3[v] = 0.f;
-    const float* hb = cx.h2s + (it * FT + r) * P2 + 16 * h;
-    const float* w3row = cx.W3 + (int64_t)r * H2 + 16 * h;
+    for (int b = 0; b < H2 / 16; ++b) {
+      const f32x4 aw = *reinterpret_cast<const f32x4*>(w3row + 16 * b);
+      const f32x4 bx = *reinterpret_cast<const f32x4*>(hb + 16 * b);
 #pragma unroll
-    for (int g = 0; g < H2 / 32; ++g) {
-      f32x4 aw[4], bx[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        aw[j] = *reinterpret_cast<const f32x4*>(w3row + g * 32 + 4 * j);
-        bx[j] = *reinterpret_cast<const f32x4*>(hb + g * 32 + 4 * j);
-      }
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int s = 0; s < 4; ++s) acc3 = mfma32(aw[j][s], bx[j][s], acc3);
+      for (int t = 0; t < 4; ++t) acc3 = mfma16(aw[t], bx[t], acc3);
     }
-    const int64_t item = (int64_t)(tb + it) * FT + r;
+    const int64_t item = (int64_t)(tb + it) * FT + 16 * ih + j;
     if (item < cx.n) {
+      const f32x4 bb = *reinterpret_cast<const f32x4*>(cx.b3 + 16 * oh + 4 * g);
+      f32x4 o;
 #pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4) {
-        const f32x4 bb = *reinterpret_cast<const f32x4*>(cx.b3 + 8 * g4 + 4 * h);
-        f32x4 o;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) o[i] = bb[i] + acc3[4 * g4 + i];
-        *reinterpret_cast<f32x4*>(cx.z_out + item * E + 8 * g4 + 4 * h) = o;
-      }
+      for (int i = 0; i < 4; ++i) o[i] = bb[i] + acc3[i];
+      *reinterpret_cast<f32x4*>(cx.z_out + item * E + 16 * oh + 4 * g) = o;
     }
   }
   // no barrier: h2 is next written after the next pass's L1 barriers
@@ -391,8 +386,9 @@ __global__ __launch_bounds__(64 * FWV, 1) void rq_encoder_kernel(
   if (tb < t_end) rq_fused_pass<1, H1, H2>(cx, tb);   // FP == 2: at most one tile left
 }
 
-// Packed weight images of the three layers (one launch): within every 32-deep k group, feature
-// 8j + 2s + h at 16h + 4j + s.  The layers' images lie back to back in `out`.
+// Packed weight images of the three layers (one launch): W1 and W2 for the 32x32x2 chains (within
+// every 32-deep k group, feature 8j + 2s + h at 16h + 4j + s), W3 for the 16x16x4 chain (within
+// every 16-deep block, feature 4t + g at 4g + t).  The layers' images lie back to back in `out`.
 struct PackArgs {
   const float* w[3];
   int64_t end[3];   // cumulative element counts
@@ -405,7 +401,13 @@ __global__ __launch_bounds__(256) void rq_pack_kernel(PackArgs a, float* __restr
   const int64_t o = i - (l ? a.end[l - 1] : 0);
   const int K = a.K[l];
   const int64_t row = o / K;
-  const int p = (int)(o % K), g = p & ~31, q = p & 31, h = q >> 4, j = (q >> 2) & 3, s = q & 3;
+  const int p = (int)(o % K);
+  if (l == 2) {   // W3 for the 16x16x4 chain: feature 16b + 4t + g at 16b + 4g + t
+    const int b = p & ~15, g = (p >> 2) & 3, t = p & 3;
+    out[i] = a.w[l][row * K + b + 4 * t + g];
+    return;
+  }
+  const int g = p & ~31, q = p & 31, h = q >> 4, j = (q >> 2) & 3, s = q & 3;
   out[i] = a.w[l][row * K + g + 8 * j + 2 * s + h];
 }
 
@@ -420,9 +422,26 @@ size_t gr_rq_fused_pack_floats(int32_t n_linear, const int32_t* dims) {
 // Returns GR_ERR_UNSUPPORTED (without touching the error message) when the encoder shape is not
 // the one this kernel is built for; the caller then runs the layer-wise path.  `pack` = workspace
 // of gr_rq_fused_pack_floats floats (16-byte aligned) for the packed weights.
+int gr_rq_encoder_pack_launch(int32_t n_linear, const int32_t* dims, const float* const* weights, float* pack,
+                              hipStream_t st) {
+  using namespace gr;
+  if (gr_rq_fused_pack_floats(n_linear, dims) == 0) return GR_ERR_UNSUPPORTED;
+  PackArgs pa{};
+  int64_t tot = 0;
+  for (int i = 0; i < 3; ++i) {
+    pa.w[i] = weights[i];
+    pa.K[i] = dims[i];
+    tot += (int64_t)dims[i + 1] * dims[i];
+    pa.end[i] = tot;
+  }
+  hipLaunchKernelGGL(rq_pack_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, pa, pack);
+  return check_launch("rq encoder pack");
+}
+
+// packed: the image gr_rq_encoder_pack_launch wrote (`pack_is_ready`), or workspace for it.
 int gr_rq_encoder_fused_launch(const float* x, int64_t n, int32_t n_linear, const int32_t* dims,
                                const float* const* weights, const float* const* biases,
-                               float* z_out, float* pack, hipStream_t st) {
+                               float* z_out, float* pack, hipStream_t st, bool pack_is_ready) {
   using namespace gr;
   if (n_linear != 3 || dims[3] != 32 || dims[0] % FXC != 0 || !biases) return GR_ERR_UNSUPPORTED;
   if (!(dims[1] == 256 && dims[2] == 128)) return GR_ERR_UNSUPPORTED;
@@ -435,15 +454,10 @@ int gr_rq_encoder_fused_launch(const float* x, int64_t n, int32_t n_linear, cons
   const int64_t tiles = (n + FT - 1) / FT;
   if (tiles > 0x7fffffffLL) return fail(GR_ERR_UNSUPPORTED, "rq encoder: n too large");
   float* wp[3] = {pack, pack + (size_t)dims[0] * 256, pack + (size_t)dims[0] * 256 + 256 * 128};
-  PackArgs pa{};
-  int64_t tot = 0;
-  for (int i = 0; i < 3; ++i) {
-    pa.w[i] = weights[i];
-    pa.K[i] = dims[i];
-    tot += (int64_t)dims[i + 1] * dims[i];
-    pa.end[i] = tot;
+  if (!pack_is_ready) {
+    const int rc = gr_rq_encoder_pack_launch(n_linear, dims, weights, pack, st);
+    if (rc) return rc;
   }
-  hipLaunchKernelGGL(rq_pack_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, pa, pack);
   static int cus = 0;
   if (!cus) {
     int dev = 0;

@@ -242,6 +242,23 @@ class RqBinding:
         self.w_arr, self.b_arr, self.c_arr = L.ptr_array(self.ws), L.ptr_array(self.bs), L.ptr_array(self.cbs)
         self.device = self.ws[0].device
         self._ws_bytes = {}
+        # the fused encoder's packed weight image, re-packed only when a weight changed (in-place
+        # updates bump the shared version counter of the detached views)
+        nf = L.lib().gr_rq_encoder_pack_floats(len(self.ws), self.dims_c)
+        self.packed = torch.empty(nf, dtype=torch.float32, device=self.device) if nf else None
+        self._pack_key = None
+
+    def packed_ptr(self):
+        """Device pointer of the up-to-date packed encoder image (None: not the fused shape)."""
+        if self.packed is None:
+            return None
+        key = tuple(w._version for w in self.ws)
+        if key != self._pack_key:
+            with torch.cuda.device(self.device):
+                L.check(L.lib().gr_rq_encoder_pack_f32(len(self.ws), self.dims_c, self.w_arr, L.ptr(self.packed),
+                                                       L.stream_of(self.device)), "gr_rq_encoder_pack_f32")
+            self._pack_key = key
+        return L.ptr(self.packed)
 
     def workspace_bytes(self, n):
         nb = self._ws_bytes.get(n)
@@ -295,10 +312,10 @@ def rq_encode(x, weights=None, biases=None, codebooks=None, with_gap=False, with
     best = torch.empty((n, nl), dtype=torch.float32, device=dev) if with_gap else None
     z = torch.empty((n, b.dims[-1]), dtype=torch.float32, device=dev) if with_z else None
     with torch.cuda.device(dev):
-        L.check(L.lib().gr_rq_encode_f32(L.ptr(x2), n, len(b.ws), b.dims_c, b.w_arr, b.b_arr,
-                                         nl, b.ks_c, b.c_arr, L.ptr(idx), L.ptr(best), L.ptr(gap),
-                                         L.ptr(z), L.ptr(wsp), nbytes, L.stream_of(dev)),
-                "gr_rq_encode_f32")
+        L.check(L.lib().gr_rq_encode_packed_f32(L.ptr(x2), n, len(b.ws), b.dims_c, b.w_arr, b.b_arr,
+                                                b.packed_ptr(), nl, b.ks_c, b.c_arr, L.ptr(idx), L.ptr(best),
+                                                L.ptr(gap), L.ptr(z), L.ptr(wsp), nbytes, L.stream_of(dev)),
+                "gr_rq_encode_packed_f32")
     out = [idx]
     if with_gap:
         out += [best, gap]

@@ -130,6 +130,23 @@ int gr_rq_encode_f32(const float* x, int64_t n, int32_t n_linear, const int32_t*
                      float* best_out, float* gap_out, float* z_out, void* workspace,
                      size_t workspace_bytes, void* stream);
 
+/* The fused encoder's packed weight image (in -> 256 -> 128 -> 32 encoders; 0 floats otherwise):
+ * W1 / W2 with every 32-deep k group in the order the 32x32x2 MFMA chains consume (feature
+ * 8j + 2s + h at 16h + 4j + s), W3 in the 16x16x4 chain's (feature 4t + g of a 16-block at 4g + t).
+ * gr_rq_encode_f32 writes it into its workspace on every call; a caller that keeps the weights
+ * fixed between calls packs once (gr_rq_encoder_pack_f32, `packed` 16-byte aligned) and passes it
+ * to gr_rq_encode_packed_f32 (same arguments as gr_rq_encode_f32 otherwise; packed = NULL: pack
+ * per call), which saves a launch per call. */
+size_t gr_rq_encoder_pack_floats(int32_t n_linear, const int32_t* dims);
+int gr_rq_encoder_pack_f32(int32_t n_linear, const int32_t* dims, const float* const* weights,
+                           float* packed, void* stream);
+int gr_rq_encode_packed_f32(const float* x, int64_t n, int32_t n_linear, const int32_t* dims,
+                            const float* const* weights, const float* const* biases,
+                            const float* packed, int32_t L, const int32_t* K,
+                            const float* const* codebooks, int64_t* idx_out, float* best_out,
+                            float* gap_out, float* z_out, void* workspace, size_t workspace_bytes,
+                            void* stream);
+
 /* MLPLayers.forward in eval mode (RQ-VAE/models/layers.py:42-43): z_out[n, dims[n_linear]] = the
  * encoder output alone (ReLU after every Linear but the last).  Same kernels as gr_rq_encode_f32. */
 size_t gr_rq_mlp_workspace_bytes(int64_t n, int32_t n_linear, const int32_t* dims);
