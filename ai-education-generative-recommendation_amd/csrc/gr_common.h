@@ -44,6 +44,13 @@ __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
   return start + (orig >> 3);
 }
 
+// The sticky per-device error word (ops.err_flag): the first cause a kernel reports stays (vector
+// global compare-and-swap from 0), so an unfillable negative-sample row (2) is not overwritten by
+// the out-of-range -1 ids a later kernel then sees (1).
+__device__ __forceinline__ void set_err(int32_t* err, int32_t code) {
+  if (err) atomicCAS(err, 0, code);
+}
+
 // f32-input MFMA 32x32x2 (exact k-ordered fp32 fma chain; cdna_hip_programming.md §3).
 // Lane l supplies A[i = l&31][k = l>>5] and B[k = l>>5][j = l&31];
 // D register v of lane l holds row (v&3) + 8*(v>>2) + 4*(l>>5), column l&31.

@@ -57,7 +57,7 @@ __global__ __launch_bounds__(256) void neg_sample_kernel(const int64_t* __restri
   // (ops.check_errors -> ValueError, numpy's choice(replace=False) error); the fused BCE op flags
   // a -1 id as out of range, so it never reads row 0 in its place unnoticed.
   const bool full = taken >= J;
-  if (!full && lane == 0 && err) *err = 2;
+  if (!full && lane == 0) set_err(err, 2);
   for (int q = lane; q < J; q += 64) out[row * J + q] = full ? tk[q] : -1;
 }
 

@@ -35,7 +35,7 @@ __global__ __launch_bounds__(64) void score_pairs_kernel(const float* __restrict
   const int64_t uc = u < B ? u : B - 1;
   int64_t t = ids[uc];
   if (t < 0 || t >= rows) {
-    if (u < B && err) *err = 1;
+    if (u < B) set_err(err, 1);
     t = 0;
   }
   f32x16 acc;

@@ -30,7 +30,7 @@ __global__ __launch_bounds__(256) void embed_kernel(const int64_t* __restrict__ 
   const int t = (int)(row % n);
   int64_t id = seqs[row];
   if (id < 0 || id >= item_rows) {  // torch raises IndexError here; flag it and read the pad row
-    if (err) *err = 1;
+    set_err(err, 1);
     id = 0;
   }
   const f32x4 a = *reinterpret_cast<const f32x4*>(item + id * d + c);

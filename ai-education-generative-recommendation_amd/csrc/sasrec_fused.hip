@@ -228,7 +228,7 @@ __global__ __launch_bounds__(256) void sasrec_fused_kernel(const SasFusedArgs a,
     if (p < n) {
       id = seqs[b * n + p];
       if (id < 0 || id >= a.item_rows) {   // torch raises IndexError; flag and read the pad row
-        if (err) *err = 1;
+        set_err(err, 1);
         id = 0;
       }
     }

@@ -472,7 +472,7 @@ __global__ __launch_bounds__(256) void embed_ln_kernel(const int64_t* __restrict
     const int64_t g = m0 + (row < left ? row : left - 1);
     int64_t id = ids[i];
     if (id < 0 || id >= item_rows) {   // flag only real rows (clamped duplicates re-read a real id)
-      if (err && row < left) *err = 1;
+      if (row < left) set_err(err, 1);
       id = 0;
     }
     e[i] = *reinterpret_cast<const f32x4*>(item + id * RT_D + c);

@@ -282,7 +282,7 @@ __global__ __launch_bounds__(NT) void sas_train_fwd_kernel(const Args a, const i
     const int i = idx / d, f = idx - i * d;
     int64_t s = seqs[b * n + i];
     if (s < 0 || s >= a.item_rows) {
-      if (err) *err = 1;
+      set_err(err, 1);
       s = 0;
     }
     X[i * pd + f] = a.item[s * d + f] + a.pos[i * d + f];

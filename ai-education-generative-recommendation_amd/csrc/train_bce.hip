@@ -17,7 +17,7 @@ namespace gr {
 
 __device__ __forceinline__ int64_t checked_row(int64_t r, int64_t rows, int32_t* err) {
   if (r < 0 || r >= rows) {
-    if (err) *err = 1;
+    set_err(err, 1);
     return 0;
   }
   return r;

@@ -88,7 +88,8 @@ def sharded_rank_topk(h, table_shard, row_offset, targets, k=10, group=None, mas
     t = targets.reshape(-1).to(torch.int64)
     own = (t >= row_offset) & (t < row_offset + rows)
     local = torch.where(own, t - row_offset, torch.zeros_like(t))
-    ts = torch.where(own, logits.gather(1, local.unsqueeze(1)).squeeze(1), torch.zeros_like(t, dtype=logits.dtype))
+    zero = torch.zeros_like(t, dtype=logits.dtype)
+    ts = torch.where(own, logits.gather(1, local.unsqueeze(1)).squeeze(1), zero) if rows > 0 else zero
     if world:
         dist.all_reduce(ts, op=dist.ReduceOp.SUM, group=group)
     kk = min(k, rows) if rows > 0 else 0
@@ -179,9 +180,10 @@ def sharded_rank_topk_batches(hs, table_shard, row_offset, targets, k=10, group=
             tl = ops.score_pairs(h, table_shard, local, mask_col0=m0)
         else:
             logits = scorer(h, table_shard)
-            if m0:
+            if m0 and rows > 0:
                 logits[:, 0] = -1e9                                  # evaluate.py:27
-            tl = logits.gather(1, local.unsqueeze(1)).squeeze(1)
+            tl = (logits.gather(1, local.unsqueeze(1)).squeeze(1) if rows > 0   # an empty shard owns
+                  else torch.zeros(t.shape, dtype=logits.dtype, device=logits.device))   # no target
         ts = torch.where(own, tl, torch.zeros(t.shape, dtype=tl.dtype, device=tl.device))
         return ts, logits, dist.all_reduce(ts, op=dist.ReduceOp.SUM, group=group, async_op=True)
 
@@ -191,9 +193,13 @@ def sharded_rank_topk_batches(hs, table_shard, row_offset, targets, k=10, group=
         if fused:
             from . import ops
             v, i, cnt = ops.score_topk(hs[b], table_shard, kk, row_offset, thresholds=ts, mask_col0=m0)
-        else:
+        elif kk > 0:
             cnt = counter(logits, ts)
             v, i = topk_fn(logits, kk, row_offset)
+        else:   # empty shard (a catalog smaller than the world): no count, no candidate
+            cnt = torch.zeros(logits.shape[0], dtype=torch.int64, device=logits.device)
+            v = torch.empty((logits.shape[0], 0), dtype=logits.dtype, device=logits.device)
+            i = torch.empty((logits.shape[0], 0), dtype=torch.int64, device=logits.device)
         if kk < k:
             v = torch.cat([v, torch.full((v.shape[0], k - kk), float("-inf"), dtype=v.dtype, device=v.device)], 1)
             i = torch.cat([i, torch.full((i.shape[0], k - kk), -1, dtype=i.dtype, device=i.device)], 1)

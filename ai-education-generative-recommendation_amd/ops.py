@@ -666,7 +666,9 @@ def neg_samples(seq, item_num, num_neg=1, seed=None, seed_tensor=None):
         else:
             L.check(L.lib().gr_neg_samples(L.ptr(s), B, n, int(item_num), int(num_neg), int(seed) & (2 ** 64 - 1),
                                            L.ptr(out), L.ptr(err), L.stream_of(s.device)), "gr_neg_samples")
-    if CHECK or 2 * (n + num_neg) > item_num:
+    # a short population is possible only when 2 (n + num_neg) > item_num; never synchronise inside a
+    # graph capture (the captured step classes check once per replay instead)
+    if (CHECK or 2 * (n + num_neg) > item_num) and not torch.cuda.is_current_stream_capturing():
         check_errors(s.device)
     return out
 
@@ -796,6 +798,7 @@ class SasTrainStepGraph:
             raise RuntimeError("SasTrainStepGraph: feats and table must be leaf tensors requiring grad")
         self.feats, self.table, self.inputs, self.targets = feats, table, inputs, targets
         self.item_num, self.num_neg, self.eps = int(item_num), int(num_neg), float(eps)
+        self._check = CHECK or 2 * (inputs.shape[1] + self.num_neg) > self.item_num
         self.seed = torch.tensor([int(seed)], dtype=torch.int64, device=feats.device)
         side = torch.cuda.Stream(device=feats.device)
         side.wait_stream(torch.cuda.current_stream(feats.device))
@@ -820,6 +823,8 @@ class SasTrainStepGraph:
 
     def replay(self):
         self.graph.replay()
+        if self._check:   # a row whose negative population may be short: the reference raises
+            check_errors(self.feats.device)
         return self.out
 
 
@@ -948,6 +953,10 @@ class RqTrainGraph:
         saved_s = {id(p): {k: (v.detach().clone() if torch.is_tensor(v) else v)
                            for k, v in optimizer.state[p].items()} for p in params if p in optimizer.state}
         saved_lr = [g["lr"].detach().clone() for g in optimizer.param_groups]
+        # module buffers too: with bn=True every warm-up / capture forward is a train-mode BatchNorm
+        # step that moves running_mean / running_var / num_batches_tracked
+        bufs = list(model.buffers())
+        saved_b = [b.detach().clone() for b in bufs]
         side = torch.cuda.Stream(device=dev)
         side.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(side):
@@ -972,6 +981,8 @@ class RqTrainGraph:
                             v.zero_()
             for g, lr in zip(optimizer.param_groups, saved_lr):
                 g["lr"].copy_(lr)
+            for b, sb in zip(bufs, saved_b):
+                b.copy_(sb)
 
     def replay(self):
         """Run one captured step; returns the static ``(loss, loss_recon, indices)``."""

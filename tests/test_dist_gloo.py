@@ -129,3 +129,25 @@ def test_hr_ndcg_matches_reference_tail():
     from oracle import metrics_oracle
     ranks = np.array([1, 2, 10, 11, 500, 3, 1])
     assert hr_ndcg(torch.from_numpy(ranks)) == metrics_oracle.hr_ndcg(ranks, 10)
+
+
+def test_catalog_smaller_than_world_leaves_an_empty_shard():
+    """rows = 2 over 3 ranks: one rank holds no catalog rows (the pipelined form indexed
+    column 0 of an empty shard).  Ranks and the padded top-k must equal the full-catalog answer."""
+    g = torch.Generator().manual_seed(11)
+    B, d, rows, k = 23, 8, 2, 4
+    table = torch.randn(rows, d, generator=g)
+    table[0] = 0
+    h = torch.randn(B, d, generator=g)
+    targets = torch.randint(0, rows, (B,), generator=g)
+    res = _run(3, (h, table, targets, k))
+    lg = cpu_score(h, table)
+    lg[:, 0] = -1e9
+    ref_rank = (lg > lg.gather(1, targets.unsqueeze(1))).sum(1) + 1
+    ref_v, ref_i = cpu_topk(lg, rows, 0)
+    for rk, v, i, hg, (pr, pi) in res:
+        assert torch.equal(rk, ref_rank) and torch.equal(pr, ref_rank)
+        assert torch.equal(i[:, :rows], ref_i) and (i[:, rows:] == -1).all()
+        # the CPU stand-in matmul is not shape-invariant in its last bits: values to fp32 rounding
+        assert torch.allclose(v[:, :rows], ref_v, rtol=1e-6, atol=0) and torch.isinf(v[:, rows:]).all()
+        assert torch.equal(pi[:, :rows], ref_i)

@@ -148,3 +148,20 @@ def test_graph_replays_back_to_back_equal_synchronised(dev):
     assert all(torch.equal(a, b) for a, b in zip(*res))
     m = copy.deepcopy(base)
     assert not ops.RqTrainGraph(m, _opt(m, dev, fused=True)[0], x.clone())._sync   # kernel path default
+
+
+def test_capture_restores_module_buffers(dev):
+    """bn=True: the warm-up and capture forwards are train-mode BatchNorm steps; the graph's
+    constructor must leave running_mean / running_var / num_batches_tracked as it found them
+    (ADVICE r2), as it does the parameters and the optimizer state."""
+    from gr_amd import RQVAE, ops
+    torch.manual_seed(0)
+    m = RQVAE(in_dim=768, num_emb_list=[8] * 3, e_dim=32, layers=[256, 128], dropout_prob=0.0, bn=True,
+              sk_epsilons=[0.01] * 3, sk_iters=50).to(dev).train()
+    for q in m.rq.vq_layers:
+        q.embedding.weight.data.normal_(0.0, 0.3)
+    before = [b.detach().clone() for b in m.buffers()]
+    assert len(before) > 0
+    opt, _ = _opt(m, dev)
+    ops.RqTrainGraph(m, opt, _batches(dev, 1)[0].clone(), sync=True)
+    assert all(torch.equal(a, b) for a, b in zip(before, m.buffers()))
