@@ -64,33 +64,5 @@ def build(verbose=False, force=False):
     return LIB
 
 
-def build_stamps(verbose=False, extra=(), suffix=""):
-    """Diagnostic variant with in-kernel s_memtime stamps (-DGR_STAMPS) -> lib/libgr_amd_stamps*.so.
-    Never loaded by the product path; used by scripts/stamps_rq.py only.  ``extra`` adds ablation
-    macros (GR_ABL_*) for one-factor experiments."""
-    os.makedirs(OBJDIR, exist_ok=True)
-    out = os.path.join(LIBDIR, f"libgr_amd_stamps{suffix}.so")
-    objs = []
-    for src in sources():
-        obj = os.path.join(OBJDIR, os.path.basename(src) + f".stamps{suffix}.o")
-        cmd = [HIPCC] + (["-x", "hip"] if src.endswith(".cpp") else []) + CFLAGS + ["-DGR_STAMPS", *extra, "-c", src, "-o", obj]
-        if verbose:
-            print(" ".join(cmd), flush=True)
-        subprocess.run(cmd, check=True)
-        objs.append(obj)
-    subprocess.run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", out], check=True)
-    return out
-
-
 if __name__ == "__main__":
-    import sys
-    if "--abl" in sys.argv:   # diagnostic library with one GR_ABL_* macro (never loaded by the product)
-        print(build_stamps(extra=[f"-D{sys.argv[sys.argv.index('--abl') + 1]}"], suffix="_abl"))
-    elif "--stamps" in sys.argv:
-        print(build_stamps())
-        print(build_stamps(extra=["-DGR_ABL_NOW1"], suffix="_now1"))
-        print(build_stamps(extra=["-DGR_ABL_NOX"], suffix="_nox"))
-        print(build_stamps(extra=["-DGR_ABL_NOX", "-DGR_ABL_NOW1"], suffix="_noxw"))
-        print(build_stamps(extra=["-DGR_ABL_W1COAL"], suffix="_w1coal"))
-    else:
-        print(build(verbose=True))
+    print(build(verbose=True))

@@ -15,13 +15,6 @@ void clear_error() { g_last_error.clear(); }
 static std::atomic<int64_t> g_rq_fused{1};
 // sas_fused (1: register-resident fused SASRec forward when n <= 64 and d <= 64, 0: layer-wise).
 static std::atomic<int64_t> g_sas_fused{1};
-// score_ablate (diagnostic, results INVALID when != 0): 1 = scoring kernel skips its logits
-// stores, 2 = skips its matrix work, 3 = skips the matrix work and the logits ring writes, 4 = as
-// 3 and the store waves store constants (no ring reads).  scripts/ab_score.py splits the time.
-static std::atomic<int64_t> g_score_ablate{0};
-// topk_ablate (diagnostic, results INVALID when != 0): the fused score + top-k kernel skips 1 = all
-// top-k work (counts only), 2 = the appends and folds (keeps the per-chunk max test).
-static std::atomic<int64_t> g_topk_ablate{0};
 // topk_sample (1: gr_score_topk_f32 takes its threshold from a strided sample pass when the
 // catalog is long enough, 0: always one pass).  Same results either way; used for A/B timing.
 static std::atomic<int64_t> g_topk_sample{1};
@@ -61,8 +54,6 @@ static std::atomic<int64_t> g_attn_lazy{1};
 // topk_impl (1 (default): gr_score_topk_f32 = tile-max counting pass + select/re-score kernel;
 // 0: sample pass + exact list pass + merges)
 static std::atomic<int64_t> g_topk_impl{1};
-// topk_sel_abl (diagnostic only, wrong results: bit 1 no re-scoring, 2 no k-th tile select, 4 no final select)
-static std::atomic<int64_t> g_topk_sel_abl{0};
 // rt_w8 (1 (default): the post-attention row tile runs 8 waves per 64-row tile; 0: 4 waves)
 static std::atomic<int64_t> g_rt_w8{1};
 // lin_w8 (1 (default): gr_linear_f32's 128x128 / 128x64 tiles run 8 waves per workgroup; 0: 4)
@@ -71,8 +62,6 @@ static std::atomic<int64_t> g_lin_w8{1};
 int64_t option(const char* name) {
   if (!strcmp(name, "rq_fused")) return g_rq_fused.load();
   if (!strcmp(name, "sas_fused")) return g_sas_fused.load();
-  if (!strcmp(name, "score_ablate")) return g_score_ablate.load();
-  if (!strcmp(name, "topk_ablate")) return g_topk_ablate.load();
   if (!strcmp(name, "topk_sample")) return g_topk_sample.load();
   if (!strcmp(name, "score_flags")) return g_score_flags.load();
   if (!strcmp(name, "score_ubmajor")) return g_score_ubmajor.load();
@@ -86,7 +75,6 @@ int64_t option(const char* name) {
   if (!strcmp(name, "attn_alt")) return g_attn_alt.load();
   if (!strcmp(name, "attn_lazy")) return g_attn_lazy.load();
   if (!strcmp(name, "topk_impl")) return g_topk_impl.load();
-  if (!strcmp(name, "topk_sel_abl")) return g_topk_sel_abl.load();
   if (!strcmp(name, "rt_w8")) return g_rt_w8.load();
   if (!strcmp(name, "lin_w8")) return g_lin_w8.load();
   return -1;
@@ -98,8 +86,6 @@ extern "C" int gr_set_option(const char* name, int64_t value) {
   if (!name) return gr::fail(GR_ERR_ARG, "gr_set_option: null name");
   if (!strcmp(name, "rq_fused") && (value == 0 || value == 1)) { gr::g_rq_fused = value; return GR_OK; }
   if (!strcmp(name, "sas_fused") && (value == 0 || value == 1)) { gr::g_sas_fused = value; return GR_OK; }
-  if (!strcmp(name, "score_ablate") && value >= 0 && value <= 4) { gr::g_score_ablate = value; return GR_OK; }
-  if (!strcmp(name, "topk_ablate") && value >= 0 && value <= 2) { gr::g_topk_ablate = value; return GR_OK; }
   if (!strcmp(name, "topk_sample") && (value == 0 || value == 1)) { gr::g_topk_sample = value; return GR_OK; }
   if (!strcmp(name, "score_flags") && (value == 0 || value == 1)) { gr::g_score_flags = value; return GR_OK; }
   if (!strcmp(name, "score_ubmajor") && (value == 0 || value == 1)) { gr::g_score_ubmajor = value; return GR_OK; }
@@ -113,7 +99,6 @@ extern "C" int gr_set_option(const char* name, int64_t value) {
   if (!strcmp(name, "attn_alt") && (value == 0 || value == 1)) { gr::g_attn_alt = value; return GR_OK; }
   if (!strcmp(name, "attn_lazy") && (value == 0 || value == 1)) { gr::g_attn_lazy = value; return GR_OK; }
   if (!strcmp(name, "topk_impl") && (value == 0 || value == 1)) { gr::g_topk_impl = value; return GR_OK; }
-  if (!strcmp(name, "topk_sel_abl") && value >= 0 && value <= 7) { gr::g_topk_sel_abl = value; return GR_OK; }
   if (!strcmp(name, "rt_w8") && (value == 0 || value == 1)) { gr::g_rt_w8 = value; return GR_OK; }
   if (!strcmp(name, "lin_w8") && (value == 0 || value == 1)) { gr::g_lin_w8 = value; return GR_OK; }
   return gr::fail(GR_ERR_ARG, std::string("gr_set_option: unknown option or value: ") + name);

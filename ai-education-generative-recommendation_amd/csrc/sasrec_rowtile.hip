@@ -40,9 +40,6 @@ template <int K>
 __device__ __forceinline__ void rt_gemm(f32x16 (&acc)[2], const float* A, int ap, const float* __restrict__ W,
                                         int wrow, int r, int h) {
   constexpr int NK = K / 8, PF = RT_PF < NK ? RT_PF : NK;
-#ifdef GR_ABL_WROW   // diagnostic build only: every lane of a half reads the tile's first row (wrong data)
-  wrow &= ~31;
-#endif
   const float* wr = W + (int64_t)wrow * K + 4 * h;
   const float* a0 = A + r * ap + 4 * h;
   f32x4 wb[PF];

@@ -80,7 +80,7 @@ template <int D, bool FLAGS>
 __global__ __launch_bounds__(64 * (ScCW<D, FLAGS>::value + ScSW<D, FLAGS>::value), 1) void score_kernel(const float* __restrict__ h, int64_t B,
                                                    const float* __restrict__ table, int64_t rows,
                                                    float* __restrict__ out, int64_t ld,
-                                                   int ublocks, int slices, int ablate, int ubmajor) {
+                                                   int ublocks, int slices, int ubmajor) {
   constexpr int KG = D / 32;                       // 32-deep k groups
   constexpr int P = D + 4;                         // LDS table row pitch (floats)
   constexpr int CW = ScCW<D, FLAGS>::value, SC_USERS = 256;   // compute waves; users per workgroup
@@ -177,8 +177,7 @@ __global__ __launch_bounds__(64 * (ScCW<D, FLAGS>::value + ScSW<D, FLAGS>::value
     } else {
       __syncthreads();   // table chunk c_begin staged by the store waves
     }
-    auto run = [&](auto nomfma_sel) {
-      constexpr bool NOMFMA = decltype(nomfma_sel)::value;
+    {
       int cm = (int)((c_begin * SC_CHUNK) % RW);   // 32k mod RW
 #pragma unroll 1
       for (int64_t k = c_begin; k < c_end; ++k) {
@@ -199,10 +198,7 @@ __global__ __launch_bounds__(64 * (ScCW<D, FLAGS>::value + ScSW<D, FLAGS>::value
 #pragma unroll
             for (int s = 0; s < 4; ++s)
 #pragma unroll
-              for (int ut = 0; ut < UT; ++ut) {
-                if (NOMFMA) acc[ut][4 * q + s] += bt[s];   // diagnostic: no matrix work
-                else acc[ut] = mfma32(hf[ut][g][q][s], bt[s], acc[ut]);
-              }
+              for (int ut = 0; ut < UT; ++ut) acc[ut] = mfma32(hf[ut][g][q][s], bt[s], acc[ut]);
           }
         if (FLAGS) {
           lds_publish_set(&sy[CW + wave], j + 1, lane);   // done reading table chunk j
@@ -217,7 +213,7 @@ __global__ __launch_bounds__(64 * (ScCW<D, FLAGS>::value + ScSW<D, FLAGS>::value
         }
         // logits tile -> ring (row-shifted); a position past the row's RW wraps back by RW
 #pragma unroll
-        for (int ut = 0; ut < UT && ablate < 3; ++ut)
+        for (int ut = 0; ut < UT; ++ut)
 #pragma unroll
           for (int v = 0; v < 16; ++v) {
             const int ul_end = (wave * UPW + ut * 32 + (v & 3) + 8 * (v >> 2) + 4 * hh + 1) * RW;
@@ -229,11 +225,9 @@ __global__ __launch_bounds__(64 * (ScCW<D, FLAGS>::value + ScSW<D, FLAGS>::value
         cm = cm + SC_CHUNK == RW ? 0 : cm + SC_CHUNK;
       }
       if (!FLAGS) __syncthreads();   // the store waves' final iteration
-    };
+    }
     // (Spreading the ring writes of chunk j-1 between the MFMAs of chunk j was measured slower:
     // 341 vs 296 us at C3.)
-    if (ablate >= 2) run(std::true_type{});
-    else run(std::false_type{});
   } else {
     // ------------------------------------------------------------------ store waves
     const int sw = wave - CW, stid = tid - 64 * CW;
@@ -306,14 +300,13 @@ __global__ __launch_bounds__(64 * (ScCW<D, FLAGS>::value + ScSW<D, FLAGS>::value
 #pragma unroll
         for (int q = 0; q < CPS; ++q) lds_wait_ge(&sy[2 * CW + cw_of + q], j);
       }
-      if (k > c_begin && ablate != 1) {   // the line ending inside chunk c = k-1 (k-2 still held)
+      if (k > c_begin) {   // the line ending inside chunk c = k-1 (k-2 still held)
         const int64_t c = k - 1, c0 = c * SC_CHUNK;
         const int soff = (int)(c0 * 4);
         if (all_rows && c0 - SC_CHUNK >= s_lo && c0 + SC_CHUNK <= s_hi) {   // steady state
 #pragma unroll
           for (int i = 0; i < SI; ++i) {
-            const f32x4 v = ablate == 4 ? f32x4{1.f, 2.f, 3.f, 4.f}
-                                        : *reinterpret_cast<const f32x4*>(&ring[lrow[i] + lm]);
+            const f32x4 v = *reinterpret_cast<const f32x4*>(&ring[lrow[i] + lm]);
             __builtin_amdgcn_raw_buffer_store_b128(
                 __builtin_bit_cast(HIP_vector_type<unsigned int, 4>::Native_vec_, v), rs, voff[i], soff, 0);
           }
@@ -488,7 +481,6 @@ int gr_score_launch(const float* h, int64_t B, int32_t d, const float* table, in
   if (slices < 1) slices = 1;
   if (ublocks * slices > 0x7fffffffLL) return fail(GR_ERR_UNSUPPORTED, "gr_score_f32: grid too large");
   const dim3 g((unsigned)(ublocks * slices));
-  const int ablate = (int)option("score_ablate");   // diagnostic only (gr_set_option)
   const bool flags = option("score_flags") != 0 && d <= 64;   // d = 128 spills at 2 waves / SIMD
   const int ubmajor = (int)option("score_ubmajor");
   // Direct accumulator stores when every logits row starts on a 128-byte line (row stride a
@@ -511,9 +503,9 @@ int gr_score_launch(const float* h, int64_t B, int32_t d, const float* table, in
   }
 #define GR_SC_LAUNCH(DD)                                                                           \
   if (flags) hipLaunchKernelGGL((score_kernel<DD, true>), g, dim3(64 * (ScCW<DD, true>::value + ScSW<DD, true>::value)), \
-                                0, st, h, B, table, rows, logits, ld, (int)ublocks, (int)slices, ablate, ubmajor); \
+                                0, st, h, B, table, rows, logits, ld, (int)ublocks, (int)slices, ubmajor); \
   else hipLaunchKernelGGL((score_kernel<DD, false>), g, dim3(64 * (ScCW<DD, false>::value + ScSW<DD, false>::value)), 0, \
-                          st, h, B, table, rows, logits, ld, (int)ublocks, (int)slices, ablate, ubmajor);
+                          st, h, B, table, rows, logits, ld, (int)ublocks, (int)slices, ubmajor);
   switch (d) {
     case 32: GR_SC_LAUNCH(32) break;
     case 64: GR_SC_LAUNCH(64) break;

@@ -31,6 +31,11 @@
 namespace gr {
 
 constexpr int TK_CHUNK = 64;     // items per chunk (two 32-item MFMA tiles)
+// Tile pass: the tile maxima of TK_FL chunks per user are staged in LDS and written out as one
+// 64-byte run per user (2 TK_FL floats), instead of one 4-byte store per (user, tile) scattered over
+// 32 users' rows per wave instruction.
+constexpr int TK_FL = 8;
+constexpr int TK_FS = 2 * TK_FL + 1;   // LDS pitch per user (floats)
 constexpr float TK_MASK = -1e9f; // evaluate.py:27
 
 template <int KC>
@@ -119,12 +124,13 @@ __global__ __launch_bounds__(256, 2) void score_topk_kernel(
     const float* __restrict__ thr, int mask_col0, unsigned long long* __restrict__ cnt_out,
     const float* __restrict__ tinit, int tstride, int64_t vchunks, int s,
     float* __restrict__ cv, int64_t* __restrict__ ci, int64_t seg_stride, int seg_off, int ublocks,
-    int slices, int ablate) {
+    int slices) {
   constexpr int KG = D / 32;
   constexpr int P = D + 4;
   constexpr int LV = TK_CHUNK * D / 4 / 256;
   constexpr int mode = MODE;
   __shared__ __attribute__((aligned(16))) float tab[2][TK_CHUNK * P];
+  __shared__ float tmb[MODE == 2 ? 128 * TK_FS : 1];   // tile pass: staged tile maxima
   const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, hh = lane >> 5;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wgid = xcd_remap(blockIdx.x, gridDim.x);
@@ -229,25 +235,32 @@ __global__ __launch_bounds__(256, 2) void score_topk_kernel(
         }
     }
     if (mode == 2) {   // tile pass: strict counts + the max logit of every 32-row tile per user
+      static_assert(MODE != 2 || UT == 1, "tile pass: one user tile per wave");
 #pragma unroll
-      for (int ut = 0; ut < UT; ++ut) {
-        const int64_t u = u0 + ut * 32 + r;
+      for (int it = 0; it < 2; ++it) {
+        float m = -INFINITY;   // fmaxf skips the NaN of rows past the catalog
 #pragma unroll
-        for (int it = 0; it < 2; ++it) {
-          float m = -INFINITY;   // fmaxf skips the NaN of rows past the catalog
-#pragma unroll
-          for (int v = 0; v < 16; ++v) {
-            const float x = acc[ut][it][v];
-            cgt[ut] += x > th[ut] ? 1 : 0;
-            m = fmaxf(m, x);
-          }
-          m = fmaxf(m, __shfl_xor(m, 32));
-          if (hh == 0 && u < B) cv[u * seg_stride + 2 * vc + it] = m;
+        for (int v = 0; v < 16; ++v) {
+          const float x = acc[0][it][v];
+          cgt[0] += x > th[0] ? 1 : 0;
+          m = fmaxf(m, x);
         }
+        m = fmaxf(m, __shfl_xor(m, 32));
+        if (hh == 0) tmb[(w * 32 + r) * TK_FS + 2 * (int)(vc % TK_FL) + it] = m;
       }
       if (vc + 1 < v_end) swrite(buf ^ 1);
       __syncthreads();
       buf ^= 1;
+      if (vc % TK_FL == TK_FL - 1 || vc + 1 == v_end) {   // write the staged runs, 16 lanes per user
+        const int64_t fs = vc - vc % TK_FL > v_begin ? vc - vc % TK_FL : v_begin;
+        const int qlo = 2 * (int)(fs % TK_FL), qhi = 2 * (int)(vc % TK_FL) + 2;
+        for (int f = tid; f < 128 * 2 * TK_FL; f += 256) {
+          const int ul = f / (2 * TK_FL), q = f % (2 * TK_FL);
+          const int64_t u = (int64_t)ub * 128 + ul;
+          if (q >= qlo && q < qhi && u < B) cv[u * seg_stride + 2 * (vc - vc % TK_FL) + q] = tmb[ul * TK_FS + q];
+        }
+        __syncthreads();   // the next chunk's maxima reuse the staging rows
+      }
       continue;
     }
     if (mode == 1) {   // sample pass: bucket maxima (bucket = position mod KC), nothing else
@@ -276,7 +289,6 @@ __global__ __launch_bounds__(256, 2) void score_topk_kernel(
           cgt[ut] += x > th[ut] ? 1 : 0;
           mx = fmaxf(mx, x);
         }
-      if (ablate == 1) continue;
       if (__any(mx > Tm[ut])) {
 #pragma unroll
         for (int it = 0; it < 2; ++it)
@@ -335,11 +347,11 @@ template <int D, int KC>
 __global__ __launch_bounds__(256, 2) void topk_select_kernel(const float* __restrict__ h, int64_t B,
                                                           const float* __restrict__ table, int64_t rows,
                                                           int mask_col0, int k, int64_t id_offset,
-                                                          const float* __restrict__ tmax, int64_t T,
+                                                          const float* __restrict__ tmax, int64_t T, int64_t Ts,
                                                           const unsigned* __restrict__ cpart, int slices,
                                                           unsigned long long* __restrict__ cnt_out,
                                                           float* __restrict__ vals, int64_t* __restrict__ ids,
-                                                          int abl) {
+                                                          int) {
   constexpr int KG = D / 32;
   __shared__ int list[256];
   __shared__ int nlist, saturated;
@@ -347,7 +359,7 @@ __global__ __launch_bounds__(256, 2) void topk_select_kernel(const float* __rest
   __shared__ unsigned long long csum;
   const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, hh = lane >> 5, w = tid >> 6;
   const int64_t u = blockIdx.x;
-  const float* tm = tmax + u * T;
+  const float* tm = tmax + u * Ts;
   if (tid == 0) {
     nlist = 0;
     saturated = 0;
@@ -377,13 +389,9 @@ __global__ __launch_bounds__(256, 2) void topk_select_kernel(const float* __rest
       for (int b = 0; b < MB; ++b)
         if (q0 + 256 * b < T) tl.push(v[b], q0 + 256 * b);
     }
-    if (abl & 2) {   // diagnostic only (topk_sel_abl): the list head instead of a block select
-      if (tid == 0) mk_s = tl.v[0];
-    } else {
-      tl.block_select(k, [&](int q, float v, int64_t) {
-        if (q == k - 1) mk_s = v;
-      });
-    }
+    tl.block_select(k, [&](int q, float v, int64_t) {
+      if (q == k - 1) mk_s = v;
+    });
   }
   __syncthreads();
   const float mk = mk_s;
@@ -423,7 +431,7 @@ __global__ __launch_bounds__(256, 2) void topk_select_kernel(const float* __rest
       if (t < T && tm[t] >= mk) list[atomicAdd(&nlist, 1)] = (int)t;
     }
     __syncthreads();
-    const int n = (abl & 1) ? 0 : nlist;   // diagnostic only: no re-scoring
+    const int n = nlist;
     for (int e = 2 * w + (lane >> 5); e < n; e += 8) {
       const int64_t row = (int64_t)list[e] * 32 + r;
       const int64_t rc = row < rows ? row : rows - 1;
@@ -458,13 +466,6 @@ __global__ __launch_bounds__(256, 2) void topk_select_kernel(const float* __rest
         if (x == x) best.push(x, row);   // NaN never enters (as in the list passes)
       }
     }
-  }
-  if (abl & 4) {   // diagnostic only: no final block select
-    if (tid < k) {
-      vals[u * k + tid] = best.v[0];
-      ids[u * k + tid] = best.i[0];
-    }
-    return;
   }
   best.block_select(k, [&](int q, float v, int64_t i) {
     vals[u * k + q] = v;
@@ -532,11 +533,12 @@ static TopkPlan topk_plan(int64_t B, int64_t rows, int k, int d) {
 }
 
 // Tile design (topk_impl 1): one counting pass over every chunk writing per-user tile maxima, then
-// the select kernel.  Workspace: tile maxima [B][2 * chunks] floats + partial counts [B][slices].
+// the select kernel.  Workspace: tile maxima [B][Ts] floats (2 * chunks used, rows padded to 64
+// bytes) + partial counts [B][slices].
 static bool tile_design() { return option("topk_impl") != 0; }
 
 struct TileWs {
-  int64_t T, slices, ublocks, chunks;
+  int64_t T, Ts, slices, ublocks, chunks;   // tiles per user, row stride (64-byte multiple)
   size_t tmax, cpart, total;
 };
 static TileWs tile_ws(int64_t B, int64_t rows, int d) {
@@ -546,7 +548,8 @@ static TileWs tile_ws(int64_t B, int64_t rows, int d) {
   w.chunks = (rows + TK_CHUNK - 1) / TK_CHUNK;
   w.slices = slices_for(w.ublocks, w.chunks, d);
   w.T = 2 * w.chunks;
-  w.tmax = align_up((size_t)B * w.T * sizeof(float), 256);
+  w.Ts = (w.T + 2 * TK_FL - 1) / (2 * TK_FL) * (2 * TK_FL);
+  w.tmax = align_up((size_t)B * w.Ts * sizeof(float), 256);
   w.cpart = align_up((size_t)B * w.slices * sizeof(unsigned), 256);
   w.total = w.tmax + w.cpart + 256;
   return w;
@@ -570,10 +573,10 @@ template <int KC>
 static void launch_pass(int d, dim3 grid, hipStream_t st, const float* h, int64_t B, const float* table,
                         int64_t rows, const float* thr, int mask_col0, unsigned long long* cnt,
                         const float* tinit, int tstride, int64_t vchunks, int mode, int s, float* cv,
-                        int64_t* ci, int64_t seg_stride, int seg_off, int ub, int sl, int ablate) {
+                        int64_t* ci, int64_t seg_stride, int seg_off, int ub, int sl) {
   const dim3 blk(256);
 #define GR_TK_PASS(DD, MM) hipLaunchKernelGGL((score_topk_kernel<DD, KC, MM>), grid, blk, 0, st, h, B, table, rows, thr, \
-                                             mask_col0, cnt, tinit, tstride, vchunks, s, cv, ci, seg_stride, seg_off, ub, sl, ablate)
+                                             mask_col0, cnt, tinit, tstride, vchunks, s, cv, ci, seg_stride, seg_off, ub, sl)
   if (mode == 1) {
     switch (d) {
       case 32: GR_TK_PASS(32, 1); break;
@@ -659,13 +662,13 @@ extern "C" int gr_score_topk_f32(const float* h, int64_t B, int32_t d, const flo
     auto runt = [&](auto kc_tag) -> int {
       constexpr int KC = decltype(kc_tag)::value;
       launch_pass<KC>(d, dim3((unsigned)(tw.ublocks * tw.slices)), st, h, B, table, rows, thresholds, mask_col0,
-                      nullptr, nullptr, 0, tw.chunks, 2, 1, tmax, reinterpret_cast<int64_t*>(cpart), tw.T, 0,
-                      (int)tw.ublocks, (int)tw.slices, 0);
+                      nullptr, nullptr, 0, tw.chunks, 2, 1, tmax, reinterpret_cast<int64_t*>(cpart), tw.Ts, 0,
+                      (int)tw.ublocks, (int)tw.slices);
       int rc = check_launch("gr_score_topk_f32 (tile pass)");
       if (rc) return rc;
 #define GR_TK_SEL(DD) hipLaunchKernelGGL((topk_select_kernel<DD, KC>), dim3((unsigned)B), dim3(256), 0, st, h, B, \
-                                         table, rows, mask_col0, k, id_offset, tmax, tw.T, cpart, (int)tw.slices, \
-                                         cnt, vals_out, ids_out, (int)option("topk_sel_abl"))
+                                         table, rows, mask_col0, k, id_offset, tmax, tw.T, tw.Ts, cpart, (int)tw.slices, \
+                                         cnt, vals_out, ids_out, 0)
       switch (d) {
         case 32: GR_TK_SEL(32); break;
         case 64: GR_TK_SEL(64); break;
@@ -696,7 +699,6 @@ extern "C" int gr_score_topk_f32(const float* h, int64_t B, int32_t d, const flo
   auto* v1 = reinterpret_cast<float*>(base + wl.cv + wl.ci);
   auto* i1 = reinterpret_cast<int64_t*>(base + wl.cv + wl.ci + wl.v1);
   auto* cnt = reinterpret_cast<unsigned long long*>(counts_out);
-  const int ablate = (int)option("topk_ablate");   // diagnostic only (gr_set_option)
   const int64_t seg_stride = p.seg_per_user() * p.kc;
   const int ub = (int)p.ublocks;
   auto run = [&](auto kc_tag) -> int {
@@ -705,7 +707,7 @@ extern "C" int gr_score_topk_f32(const float* h, int64_t B, int32_t d, const flo
     int rc;
     if (p.s) {   // sample pass -> T_S = the k-th largest bucket maximum per user
       launch_pass<KC>(d, dim3((unsigned)(p.ublocks * p.slices1)), st, h, B, table, rows, nullptr, mask_col0,
-                      cnt, nullptr, 0, p.v1, 1, p.s, cv, ci, seg_stride, 0, ub, (int)p.slices1, ablate);
+                      cnt, nullptr, 0, p.v1, 1, p.s, cv, ci, seg_stride, 0, ub, (int)p.slices1);
       rc = check_launch("gr_score_topk_f32 (sample pass)");
       if (rc) return rc;
       launch_merge<KC>(st, B, seg_stride, 2 * p.slices1 * KC, k, 0, cv, ci, v1, i1);
@@ -715,7 +717,7 @@ extern "C" int gr_score_topk_f32(const float* h, int64_t B, int32_t d, const flo
     }
     launch_pass<KC>(d, dim3((unsigned)(p.ublocks * p.slices2)), st, h, B, table, rows, thresholds, mask_col0,
                     cnt, tinit, k, p.chunks, 0, 1, cv, ci, seg_stride, (int)(2 * p.slices1), ub,
-                    (int)p.slices2, ablate);
+                    (int)p.slices2);
     rc = check_launch("gr_score_topk_f32 (pass)");
     if (rc) return rc;
     // final merge over the full pass's segments only (the sample's maxima are not candidates)

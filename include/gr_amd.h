@@ -56,9 +56,6 @@ const char* gr_last_error(void);
  *                   register-resident forward kernel when n <= 64, d <= 64 (d and the head width
  *                   multiples of 8), mlp <= 128, num_blocks <= 8; 0: the layer-wise pipeline
  *                   (the workspace query follows the option in force when it is called)
- *   "score_ablate"  0 (default).  DIAGNOSTIC ONLY, outputs invalid otherwise: 1 = the scoring
- *                   kernel skips the logits stores, 2 = it skips the matrix work, 3 = also the
- *                   logits ring writes, 4 = also the ring reads (constants stored)
  *   "score_flags"   1 (default): the scoring kernel (d <= 64) hands chunks between its compute and
  *                   store waves through LDS words; 0: one barrier per chunk.  Identical results.
  *   "score_ubmajor" 1 (default): one XCD's workgroups share a user block; 0: a catalog slice.
@@ -66,8 +63,6 @@ const char* gr_last_error(void);
  *                   logits row starts on a 128-byte line (row stride % 32 == 0, aligned base),
  *                   else compute / store wave specialisation with an LDS ring; 0: always the ring;
  *                   1: always direct.  Identical results.
- *   "topk_ablate"   0 (default).  DIAGNOSTIC ONLY, outputs invalid otherwise: the fused score +
- *                   top-k kernel skips 1 = all top-k work (counts stay valid)
  *   "topk_sample"   1 (default): gr_score_topk_f32 prunes with a threshold from a strided sample
  *                   pass when the catalog is long enough; 0: one pass.  Identical results.
  * gr_set_option returns GR_ERR_ARG for an unknown name/value; gr_get_option returns -1 for an

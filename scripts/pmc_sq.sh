@@ -1,7 +1,7 @@
 #!/bin/bash
 # SQ / TCC counters of every gr:: kernel a command launches, one --pmc pass per counter group (each
 # pass under its own time limit; no trace domains are combined with --pmc).
-#   scripts/pmc_sq.sh TAG python3 scripts/ab_opt.py --what quant --opt rq_resident=0
+#   scripts/pmc_sq.sh TAG python3 scripts/ab_lib.py ai-education-generative-recommendation_amd/lib/libgr_amd.so --calls 5
 # Summaries: python scripts/pmc_summary.py gpurun_out/TAG/pmcN
 set -u
 ROOT=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
