@@ -21,7 +21,7 @@
 //       the bias moves to registers and the chain restarts from zero.
 //   L2  h2^T[128 x 32FP] = W2 . relu(h1)^T   waves 0-3, wave w owns features [32w, 32w+32)
 //   L3  z^T[32 x 32FP] = W3 . relu(h2)^T     16x16x4 MFMA tiles (also an fma chain in k order),
-//       one per wave, each the whole k = 128 chain
+//       one per wave, each the whole k = 128 chain, W3 from an LDS copy staged at kernel start
 #include <type_traits>
 
 #include "gr_common.h"
@@ -38,10 +38,10 @@ template <int H1, int H2>
 struct FusedCfg {
   static constexpr int E = 32;
   static constexpr int NTH = 64 * FWV;   // threads per workgroup
-  static constexpr int P1 = H1 + 4, P2 = H2 + 4;
+  static constexpr int P1 = H1 + 4, P2 = H2 + 4, P3 = H2 + 4;
   static constexpr int PI = FP * FT;     // items per (full) pass
   static constexpr int XV = PI * 16 / NTH;
-  static constexpr int LDS = 2 * PI * FXP + PI * P1 + PI * P2;
+  static constexpr int LDS = 2 * PI * FXP + PI * P1 + PI * P2 + E * P3;
   static_assert(H1 == 32 * FWV && H2 == 128, "8-wave form: H1 = 256, H2 = 128");
 };
 
@@ -68,7 +68,7 @@ struct FusedCtx {
   int D0, NC, csplit, t_end;
   const float *W2, *b1, *b2, *W3, *b3;
   float* z_out;
-  float *xs, *h1s, *h2s;
+  float *xs, *h1s, *h2s, *w3s;
   int tid, w, r, h;
   const float* w1row;
   f32x4 awc[4];           // W1 fragments of the current 32-deep group
@@ -225,8 +225,9 @@ __device__ __forceinline__ void rq_fused_pass(FusedCtx<H1, H2>& cx, int tb) {
   int c = 0;
 #pragma unroll 1
   for (; c < cx.csplit; ++c) chunk(c);
-  // MKL's second k block (in = 768: k >= 384): keep b1 + block 0, restart the chain from zero
-  const bool split = cx.csplit < NC;
+  // MKL's second k block (in = 768: k >= 384): keep b1 + block 0, restart the chain from zero.
+  // Unsplit layers (csplit = NC) take the same path: part = b1 + the whole chain, and the final
+  // part + 0 below is exact (part is never -0: the chain starts from +0).
   f32x16 part[NP];
 #pragma unroll
   for (int g4 = 0; g4 < 4; ++g4) {
@@ -234,11 +235,12 @@ __device__ __forceinline__ void rq_fused_pass(FusedCtx<H1, H2>& cx, int tb) {
 #pragma unroll
     for (int it = 0; it < NP; ++it)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        part[it][4 * g4 + i] = split ? bb[i] + acc1[it][4 * g4 + i] : bb[i];
-        if (split) acc1[it][4 * g4 + i] = 0.f;
-      }
+      for (int i = 0; i < 4; ++i) part[it][4 * g4 + i] = bb[i] + acc1[it][4 * g4 + i];
   }
+#pragma unroll
+  for (int it = 0; it < NP; ++it)
+#pragma unroll
+    for (int v = 0; v < 16; ++v) acc1[it][v] = 0.f;
 #pragma unroll 1
   for (; c < NC; ++c) chunk(c);
   // y = (b1 + block 0) + block 1 (or b1 + the single block), ReLU, h1 -> LDS packed
@@ -335,7 +337,7 @@ __device__ __forceinline__ void rq_fused_pass(FusedCtx<H1, H2>& cx, int tb) {
     const int lane = cx.tid & 63, j = lane & 15, g = lane >> 4;
     f32x4 acc3 = {0.f, 0.f, 0.f, 0.f};
     const float* hb = cx.h2s + (it * FT + 16 * ih + j) * P2 + 4 * g;
-    const float* w3row = cx.W3 + (int64_t)(16 * oh + j) * H2 + 4 * g;
+    const float* w3row = cx.w3s + (16 * oh + j) * C::P3 + 4 * g;   // LDS: rows 4 banks apart
 #pragma unroll
     for (int b = 0; b < H2 / 16; ++b) {
       const f32x4 aw = *reinterpret_cast<const f32x4*>(w3row + 16 * b);
@@ -362,7 +364,7 @@ __global__ __launch_bounds__(64 * FWV, 1) void rq_encoder_kernel(
     const float* __restrict__ W3, const float* __restrict__ b3, float* __restrict__ z_out,
     int tiles) {
   using C = FusedCfg<H1, H2>;
-  __shared__ __attribute__((aligned(16))) float sm[C::LDS];
+  extern __shared__ __attribute__((aligned(16))) float sm[];
   const int t_begin = (int)((int64_t)blockIdx.x * tiles / gridDim.x);
   const int t_end = (int)((int64_t)(blockIdx.x + 1) * tiles / gridDim.x);
   if (t_begin >= t_end) return;
@@ -372,6 +374,11 @@ __global__ __launch_bounds__(64 * FWV, 1) void rq_encoder_kernel(
   cx.xs = sm;                              // [2][PI][FXP]
   cx.h1s = sm + 2 * C::PI * FXP;           // [PI][P1]
   cx.h2s = cx.h1s + C::PI * C::P1;         // [PI][P2]
+  cx.w3s = cx.h2s + C::PI * C::P2;         // [32][P3] the packed W3, staged once
+  for (int f = threadIdx.x; f < C::E * H2 / 4; f += C::NTH) {
+    const int row = f / (H2 / 4), q = f % (H2 / 4);
+    *reinterpret_cast<f32x4*>(cx.w3s + row * C::P3 + 4 * q) = *reinterpret_cast<const f32x4*>(W3 + row * H2 + 4 * q);
+  }
   const int tid = threadIdx.x, lane = tid & 63;
   cx.tid = tid; cx.w = tid >> 6; cx.r = lane & 31; cx.h = lane >> 5;
   cx.w1row = W1 + (int64_t)(cx.w * 32 + cx.r) * D0 + 16 * cx.h;
@@ -467,7 +474,12 @@ int gr_rq_encoder_fused_launch(const float* x, int64_t n, int32_t n_linear, cons
   }
   const int64_t grid = tiles < cus ? tiles : cus;
   const int csplit = kb < dims[0] ? kb / FXC : dims[0] / FXC;
-  hipLaunchKernelGGL((rq_encoder_kernel<256, 128>), dim3((unsigned)grid), dim3(64 * FWV), 0, st, x, n,
+  using Cfg = FusedCfg<256, 128>;
+  static bool lds_ok = hipFuncSetAttribute(reinterpret_cast<const void*>(rq_encoder_kernel<256, 128>),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           (int)(Cfg::LDS * sizeof(float))) == hipSuccess;
+  if (!lds_ok) return fail(GR_ERR_HIP, "rq fused encoder: cannot raise the LDS limit");
+  hipLaunchKernelGGL((rq_encoder_kernel<256, 128>), dim3((unsigned)grid), dim3(64 * FWV), Cfg::LDS * sizeof(float), st, x, n,
                      dims[0], csplit, wp[0], biases[0], wp[1], biases[1], wp[2], biases[2], z_out, (int)tiles);
   return check_launch("rq fused encoder");
 }

@@ -31,11 +31,6 @@
 namespace gr {
 
 constexpr int TK_CHUNK = 64;     // items per chunk (two 32-item MFMA tiles)
-// Tile pass: the tile maxima of TK_FL chunks per user are staged in LDS and written out as one
-// 64-byte run per user (2 TK_FL floats), instead of one 4-byte store per (user, tile) scattered over
-// 32 users' rows per wave instruction.
-constexpr int TK_FL = 8;
-constexpr int TK_FS = 2 * TK_FL + 1;   // LDS pitch per user (floats)
 constexpr float TK_MASK = -1e9f; // evaluate.py:27
 
 template <int KC>
@@ -130,7 +125,6 @@ __global__ __launch_bounds__(256, 2) void score_topk_kernel(
   constexpr int LV = TK_CHUNK * D / 4 / 256;
   constexpr int mode = MODE;
   __shared__ __attribute__((aligned(16))) float tab[2][TK_CHUNK * P];
-  __shared__ float tmb[MODE == 2 ? 128 * TK_FS : 1];   // tile pass: staged tile maxima
   const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, hh = lane >> 5;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wgid = xcd_remap(blockIdx.x, gridDim.x);
@@ -234,33 +228,31 @@ __global__ __launch_bounds__(256, 2) void score_topk_kernel(
           }
         }
     }
-    if (mode == 2) {   // tile pass: strict counts + the max logit of every 32-row tile per user
-      static_assert(MODE != 2 || UT == 1, "tile pass: one user tile per wave");
+    // tile pass: strict counts + the max logit of every 32-row tile per user.  The maxima are stored
+    // [user][tile], one 4-byte store per (user, tile) from lane = user; staging them in LDS and
+    // writing 32- or 64-byte runs per user measured slower (1097-1101 vs 1078-1080 us at C5,
+    // 175.6-176.4 vs 172 us on a shard, same results; profiles/r03_ab_topk_staged.txt): the call is
+    // MFMA-bound and the extra LDS traffic / barriers cost more than the write traffic saved
+    if (mode == 2) {
 #pragma unroll
-      for (int it = 0; it < 2; ++it) {
-        float m = -INFINITY;   // fmaxf skips the NaN of rows past the catalog
+      for (int ut = 0; ut < UT; ++ut) {
+        const int64_t u = u0 + ut * 32 + r;
 #pragma unroll
-        for (int v = 0; v < 16; ++v) {
-          const float x = acc[0][it][v];
-          cgt[0] += x > th[0] ? 1 : 0;
-          m = fmaxf(m, x);
+        for (int it = 0; it < 2; ++it) {
+          float m = -INFINITY;   // fmaxf skips the NaN of rows past the catalog
+#pragma unroll
+          for (int v = 0; v < 16; ++v) {
+            const float x = acc[ut][it][v];
+            cgt[ut] += x > th[ut] ? 1 : 0;
+            m = fmaxf(m, x);
+          }
+          m = fmaxf(m, __shfl_xor(m, 32));
+          if (hh == 0 && u < B) cv[u * seg_stride + 2 * vc + it] = m;
         }
-        m = fmaxf(m, __shfl_xor(m, 32));
-        if (hh == 0) tmb[(w * 32 + r) * TK_FS + 2 * (int)(vc % TK_FL) + it] = m;
       }
       if (vc + 1 < v_end) swrite(buf ^ 1);
       __syncthreads();
       buf ^= 1;
-      if (vc % TK_FL == TK_FL - 1 || vc + 1 == v_end) {   // write the staged runs, 16 lanes per user
-        const int64_t fs = vc - vc % TK_FL > v_begin ? vc - vc % TK_FL : v_begin;
-        const int qlo = 2 * (int)(fs % TK_FL), qhi = 2 * (int)(vc % TK_FL) + 2;
-        for (int f = tid; f < 128 * 2 * TK_FL; f += 256) {
-          const int ul = f / (2 * TK_FL), q = f % (2 * TK_FL);
-          const int64_t u = (int64_t)ub * 128 + ul;
-          if (q >= qlo && q < qhi && u < B) cv[u * seg_stride + 2 * (vc - vc % TK_FL) + q] = tmb[ul * TK_FS + q];
-        }
-        __syncthreads();   // the next chunk's maxima reuse the staging rows
-      }
       continue;
     }
     if (mode == 1) {   // sample pass: bucket maxima (bucket = position mod KC), nothing else
@@ -347,7 +339,7 @@ template <int D, int KC>
 __global__ __launch_bounds__(256, 2) void topk_select_kernel(const float* __restrict__ h, int64_t B,
                                                           const float* __restrict__ table, int64_t rows,
                                                           int mask_col0, int k, int64_t id_offset,
-                                                          const float* __restrict__ tmax, int64_t T, int64_t Ts,
+                                                          const float* __restrict__ tmax, int64_t T,
                                                           const unsigned* __restrict__ cpart, int slices,
                                                           unsigned long long* __restrict__ cnt_out,
                                                           float* __restrict__ vals, int64_t* __restrict__ ids,
@@ -359,7 +351,7 @@ __global__ __launch_bounds__(256, 2) void topk_select_kernel(const float* __rest
   __shared__ unsigned long long csum;
   const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, hh = lane >> 5, w = tid >> 6;
   const int64_t u = blockIdx.x;
-  const float* tm = tmax + u * Ts;
+  const float* tm = tmax + u * T;
   if (tid == 0) {
     nlist = 0;
     saturated = 0;
@@ -533,12 +525,11 @@ static TopkPlan topk_plan(int64_t B, int64_t rows, int k, int d) {
 }
 
 // Tile design (topk_impl 1): one counting pass over every chunk writing per-user tile maxima, then
-// the select kernel.  Workspace: tile maxima [B][Ts] floats (2 * chunks used, rows padded to 64
-// bytes) + partial counts [B][slices].
+// the select kernel.  Workspace: tile maxima [B][2 * chunks] floats + partial counts [B][slices].
 static bool tile_design() { return option("topk_impl") != 0; }
 
 struct TileWs {
-  int64_t T, Ts, slices, ublocks, chunks;   // tiles per user, row stride (64-byte multiple)
+  int64_t T, slices, ublocks, chunks;
   size_t tmax, cpart, total;
 };
 static TileWs tile_ws(int64_t B, int64_t rows, int d) {
@@ -548,8 +539,7 @@ static TileWs tile_ws(int64_t B, int64_t rows, int d) {
   w.chunks = (rows + TK_CHUNK - 1) / TK_CHUNK;
   w.slices = slices_for(w.ublocks, w.chunks, d);
   w.T = 2 * w.chunks;
-  w.Ts = (w.T + 2 * TK_FL - 1) / (2 * TK_FL) * (2 * TK_FL);
-  w.tmax = align_up((size_t)B * w.Ts * sizeof(float), 256);
+  w.tmax = align_up((size_t)B * w.T * sizeof(float), 256);
   w.cpart = align_up((size_t)B * w.slices * sizeof(unsigned), 256);
   w.total = w.tmax + w.cpart + 256;
   return w;
@@ -662,12 +652,12 @@ extern "C" int gr_score_topk_f32(const float* h, int64_t B, int32_t d, const flo
     auto runt = [&](auto kc_tag) -> int {
       constexpr int KC = decltype(kc_tag)::value;
       launch_pass<KC>(d, dim3((unsigned)(tw.ublocks * tw.slices)), st, h, B, table, rows, thresholds, mask_col0,
-                      nullptr, nullptr, 0, tw.chunks, 2, 1, tmax, reinterpret_cast<int64_t*>(cpart), tw.Ts, 0,
+                      nullptr, nullptr, 0, tw.chunks, 2, 1, tmax, reinterpret_cast<int64_t*>(cpart), tw.T, 0,
                       (int)tw.ublocks, (int)tw.slices);
       int rc = check_launch("gr_score_topk_f32 (tile pass)");
       if (rc) return rc;
 #define GR_TK_SEL(DD) hipLaunchKernelGGL((topk_select_kernel<DD, KC>), dim3((unsigned)B), dim3(256), 0, st, h, B, \
-                                         table, rows, mask_col0, k, id_offset, tmax, tw.T, tw.Ts, cpart, (int)tw.slices, \
+                                         table, rows, mask_col0, k, id_offset, tmax, tw.T, cpart, (int)tw.slices, \
                                          cnt, vals_out, ids_out, 0)
       switch (d) {
         case 32: GR_TK_SEL(32); break;

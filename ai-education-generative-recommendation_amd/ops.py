@@ -843,14 +843,20 @@ class SasTrainGraph:
     afterwards, so the first replay is the first real training step.  Dropout draws from torch's
     graph-safe generator (fresh masks each replay)."""
 
-    def __init__(self, model, optimizer, inputs, targets, item_num, num_neg, eps, seed=0, warmup=3):
+    def __init__(self, model, optimizer, inputs, targets, item_num, num_neg, eps, seed=0, warmup=3,
+                 capture=None):
         L.require_gpu(inputs, targets)
         self.model, self.opt = model, optimizer
-        self._sync = not (getattr(model, "fused_train", False) and sasrec_train_supported(model, inputs.shape[1]))
+        if capture is None:   # capture the fused-kernel step; the autograd fallback runs eagerly
+            capture = bool(getattr(model, "fused_train", False) and sasrec_train_supported(model, inputs.shape[1]))
         self.inputs, self.targets = inputs, targets
         self.item_num, self.num_neg, self.eps = int(item_num), int(num_neg), float(eps)
+        self._check = CHECK or 2 * (inputs.shape[1] + self.num_neg) > self.item_num
         dev = inputs.device
         self.seed = torch.tensor([int(seed)], dtype=torch.int64, device=dev)
+        self.graph = None
+        if not capture:
+            return
         params = [p for g in optimizer.param_groups for p in g["params"]]
         saved_p = [p.detach().clone() for p in params]
         saved_s = {id(p): {k: (v.detach().clone() if torch.is_tensor(v) else v)
@@ -880,21 +886,26 @@ class SasTrainGraph:
             self.seed.fill_(int(seed))
 
     def replay(self):
-        """Run one captured step; returns the static ``(batch_loss, batch_valid_t)``.
+        """Run one step; returns ``(batch_loss, batch_valid_t)`` (the captured step's static
+        tensors).
 
-        With the transformer under torch autograd (``fused_train = False`` or a shape the fused
-        kernels do not take), replay synchronises the device after each step.  That graph holds
-        memset nodes (rocprim's sort / unique-by-key temporaries in the embedding backward), and on
-        this ROCm a captured memset node does not reliably clear its buffer once replays queue
-        back to back: 4 of 4 bench runs faulted in the unique-by-key kernel within ~600 steps,
-        replay + ``torch.cuda.synchronize()`` ran 725 and 1500 steps clean, and the library's own
-        memset (the sampled BCE's dM) measurably kept stale data on the 2nd replay until it became
-        a kernel (profiles/r02_train_graph_diag.txt).  The fused path's graph has no memset node
-        and replays back to back."""
-        self.graph.replay()
-        if self._sync:
-            torch.cuda.synchronize(self.inputs.device)
-        return self.out
+        The fused-kernel step (``fused_train`` and a shape sasrec_train_supported takes) is one
+        captured graph, replayed back to back with no host synchronisation.  With the transformer
+        under torch autograd the step runs eagerly instead: back-to-back replays of that graph
+        faulted (HSA memory aperture violation) in rocPRIM's unique-by-key partition kernel of the
+        item-embedding backward (profiles/r02_train_graph_diag.txt); a graph of captured memsets
+        and kernels replays correctly back to back (profiles/r03_graph_memset.txt), so round 2's
+        memset-node explanation does not hold, and the fault stays inside that rocPRIM kernel.
+        Round 2 synchronised the device after every replay; not capturing that path at all makes
+        every path run without a host synchronisation and without the faulting configuration."""
+        if self.graph is None:
+            out = tuple(x.detach() for x in self._body())
+        else:
+            self.graph.replay()
+            out = self.out
+        if self._check:   # a row whose negative population may be short: the reference raises
+            check_errors(self.inputs.device)
+        return out
 
     def _body(self):
         self.opt.zero_grad(set_to_none=True)
@@ -926,28 +937,29 @@ class RqTrainGraph:
     capture.  Warm-up steps (allocator, autograd, the optimizer's lazily created state) are undone
     afterwards, so the first replay is the first real training step.  Dropout draws from torch's
     graph-safe generator (fresh masks each replay).  On the kernel path (fused MLPs and quantizer)
-    replays run back to back (300 replays bitwise equal to synchronised ones,
-    scripts/diag_rq_graph_sync.py); with the torch modules (``fused_train = False``), whose embedding
-    backward holds memset nodes, replay synchronises the device after each step (SasTrainGraph.replay
-    explains why).  ``sync`` overrides the choice."""
+    replays run back to back (tests/test_rq_train_gpu.py); with the torch modules (``fused_train =
+    False``, BatchNorm) the step runs eagerly (SasTrainGraph.replay explains why).  ``capture``
+    overrides the choice."""
 
-    def __init__(self, model, optimizer, inputs, max_norm=1.0, use_sk=True, warmup=3, sync=None):
+    def __init__(self, model, optimizer, inputs, max_norm=1.0, use_sk=True, warmup=3, capture=None):
         L.require_gpu(inputs)
         for g in optimizer.param_groups:
             if not g.get("capturable", False) or not torch.is_tensor(g["lr"]):
                 raise RuntimeError("RqTrainGraph: the optimizer must be capturable with a tensor lr "
                                    "(e.g. AdamW(params, lr=torch.tensor(1e-3, device=dev), capturable=True))")
         self.model, self.opt, self.inputs = model, optimizer, inputs
-        if sync is None:   # the kernel path's graph replays back to back (tested bitwise); torch
-            kern = (getattr(model.encoder, "fused_train", False) and getattr(model.decoder, "fused_train", False)
-                    and getattr(model.rq, "fused_train", False) and mlp_train_supported(model.encoder, inputs)
-                    and not model.bn)
-            sync = not kern   # autograd's embedding backward holds memset nodes: synchronise
-        self.max_norm, self.use_sk, self._sync = float(max_norm), bool(use_sk), bool(sync)
+        if capture is None:   # capture the kernel path; the torch-module fallback runs eagerly
+            capture = bool(getattr(model.encoder, "fused_train", False) and getattr(model.decoder, "fused_train", False)
+                           and getattr(model.rq, "fused_train", False) and mlp_train_supported(model.encoder, inputs)
+                           and not model.bn)
+        self.max_norm, self.use_sk = float(max_norm), bool(use_sk)
         dev = inputs.device
         if model.training and any(not q.initted for q in model.rq.vq_layers):
             with torch.no_grad():   # vq.py:66-67: k-means init on the first batch's residuals
                 model(inputs, use_sk=self.use_sk)
+        self.graph = None
+        if not capture:
+            return
         params = [p for g in optimizer.param_groups for p in g["params"]]
         saved_p = [p.detach().clone() for p in params]
         saved_s = {id(p): {k: (v.detach().clone() if torch.is_tensor(v) else v)
@@ -985,10 +997,12 @@ class RqTrainGraph:
                 b.copy_(sb)
 
     def replay(self):
-        """Run one captured step; returns the static ``(loss, loss_recon, indices)``."""
+        """Run one step; returns ``(loss, loss_recon, indices)`` (the captured step's static tensors).
+        The kernel path is one captured graph replayed back to back; the torch-module fallback runs
+        eagerly (SasTrainGraph.replay explains why)."""
+        if self.graph is None:
+            return tuple(x.detach() for x in self._body())
         self.graph.replay()
-        if self._sync:
-            torch.cuda.synchronize(self.inputs.device)
         return self.out
 
     def _body(self):

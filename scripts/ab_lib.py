@@ -20,13 +20,10 @@ ap.add_argument("--n", type=int, default=100_000)
 ap.add_argument("--L", type=int, default=3)
 ap.add_argument("--K", type=int, default=256)
 ap.add_argument("--calls", type=int, default=0, help="just issue this many plain calls per library (for rocprofv3)")
+ap.add_argument("--what", default="rq", help="rq: encoder + quantizer; topk: gr_score_topk_f32 (d 128, 512 users)")
+ap.add_argument("--rows", type=int, default=1_000_001, help="topk: catalog rows")
 a = ap.parse_args()
 dev = torch.device("cuda:0")
-m = synth.rqvae_model(a.L, a.K, dev)
-b = m.encode_binding()
-x = synth.items(a.n, 1000, dev)
-
-
 def cur():
     """The stream the caller is on NOW (a graph capture runs on a side stream)."""
     return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
@@ -52,6 +49,44 @@ def graph_us(fn, calls=20, reps=10):
     e1.record()
     torch.cuda.synchronize()
     return e0.elapsed_time(e1) / (reps * calls) * 1e3
+
+
+if a.what == "topk":   # fused score + top-10 + strict counts over a catalog (SASRec C5 / shard)
+    B, d, k = 512, 128, 10
+    g = torch.Generator(device=dev).manual_seed(0)
+    h = torch.randn(B, d, generator=g, device=dev) * 0.1
+    table = torch.randn(a.rows, d, generator=g, device=dev) * 0.1
+    thr = torch.randn(B, generator=g, device=dev) * 0.1
+    ref = None
+    for path in a.libs:
+        lib = ctypes.CDLL(os.path.abspath(path))
+        lib.gr_score_topk_workspace_bytes.restype = ctypes.c_size_t
+        lib.gr_score_topk_workspace_bytes.argtypes = [ctypes.c_int64, ctypes.c_int32, ctypes.c_int64, ctypes.c_int32]
+        nb = lib.gr_score_topk_workspace_bytes(B, d, a.rows, k)
+        ws = torch.empty(nb, dtype=torch.uint8, device=dev)
+        vals = torch.empty((B, k), device=dev)
+        ids = torch.empty((B, k), dtype=torch.int64, device=dev)
+        cnt = torch.empty(B, dtype=torch.int64, device=dev)
+        vp = ctypes.c_void_p
+        fn = lambda: lib.gr_score_topk_f32(vp(h.data_ptr()), ctypes.c_int64(B), d, vp(table.data_ptr()),  # noqa
+                                           ctypes.c_int64(a.rows), ctypes.c_int64(0), 1, k, vp(thr.data_ptr()),
+                                           vp(cnt.data_ptr()), vp(vals.data_ptr()), vp(ids.data_ptr()),
+                                           vp(ws.data_ptr()), ctypes.c_size_t(nb), cur())
+        assert fn() == 0
+        torch.cuda.synchronize()
+        same = "" if ref is None else f"  same results: {torch.equal(ids, ref[0]) and torch.equal(cnt, ref[1])}"
+        ref = (ids.clone(), cnt.clone()) if ref is None else ref
+        if a.calls:
+            for _ in range(a.calls):
+                fn()
+            torch.cuda.synchronize()
+            continue
+        print(f"{os.path.basename(path):24s} topk B={B} d={d} rows={a.rows}: {graph_us(fn, calls=5):9.2f} us{same}",
+              flush=True)
+    sys.exit(0)
+m = synth.rqvae_model(a.L, a.K, dev)
+b = m.encode_binding()
+x = synth.items(a.n, 1000, dev)
 
 
 ref_idx = None

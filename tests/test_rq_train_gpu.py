@@ -129,9 +129,9 @@ def test_fused_quantizer_equals_level_by_level(K, use_sk, dev):
 
 
 def test_graph_replays_back_to_back_equal_synchronised(dev):
-    """The kernel path's captured step replays without a device synchronisation (no memset node
-    whose clearing could race a queued replay): 60 back-to-back training replays end in the same
-    parameters, bit for bit, as 60 replays with a synchronisation after each."""
+    """The kernel path's captured step replays without a host synchronisation: 60 back-to-back
+    training replays end in the same parameters, bit for bit, as 60 replays each followed by a
+    device synchronisation."""
     from gr_amd import ops
     base = _model(dev, 0.0, False)
     x = _batches(dev, 1)[0]
@@ -139,15 +139,42 @@ def test_graph_replays_back_to_back_equal_synchronised(dev):
     for sync in (True, False):
         m = copy.deepcopy(base)
         opt, _ = _opt(m, dev, warm=0, total=100000, fused=True)
-        step = ops.RqTrainGraph(m, opt, x.clone(), sync=sync)
-        assert step._sync == sync
+        step = ops.RqTrainGraph(m, opt, x.clone())
+        assert step.graph is not None   # kernel path: captured
         for _ in range(60):
             step.replay()
+            if sync:
+                torch.cuda.synchronize()
         torch.cuda.synchronize()
         res.append([p.detach().clone() for p in m.parameters()])
     assert all(torch.equal(a, b) for a, b in zip(*res))
-    m = copy.deepcopy(base)
-    assert not ops.RqTrainGraph(m, _opt(m, dev, fused=True)[0], x.clone())._sync   # kernel path default
+
+
+def test_module_fallback_runs_eagerly_and_matches(dev):
+    """fused_train = False (torch modules): the step is not captured (see SasTrainGraph.replay) and
+    back-to-back replays equal the same steps issued by hand."""
+    from gr_amd import ops
+    base = _model(dev, 0.0, False)
+    for mod in (base.encoder, base.decoder, base.rq):
+        mod.fused_train = False
+    data = _batches(dev, 3)
+    m, ref = copy.deepcopy(base), copy.deepcopy(base)
+    opt, _ = _opt(m, dev, warm=0, total=100000, fused=True)
+    ropt, _ = _opt(ref, dev, warm=0, total=100000, fused=True)
+    inputs = data[0].clone()
+    step = ops.RqTrainGraph(m, opt, inputs)
+    assert step.graph is None
+    for x in data:
+        inputs.copy_(x)
+        loss, recon, idx = step.replay()
+        ropt.zero_grad(set_to_none=True)
+        o, rq_loss, ridx = ref(x)
+        rloss, _ = ref.compute_loss(o, rq_loss, xs=x)
+        rloss.backward()
+        torch.nn.utils.clip_grad_norm_(ref.parameters(), 1.0)
+        ropt.step()
+        assert torch.equal(idx, ridx) and loss.item() == rloss.item()
+    assert all(torch.equal(a, b) for a, b in zip(m.parameters(), ref.parameters()))
 
 
 def test_capture_restores_module_buffers(dev):
@@ -163,5 +190,5 @@ def test_capture_restores_module_buffers(dev):
     before = [b.detach().clone() for b in m.buffers()]
     assert len(before) > 0
     opt, _ = _opt(m, dev)
-    ops.RqTrainGraph(m, opt, _batches(dev, 1)[0].clone(), sync=True)
+    ops.RqTrainGraph(m, opt, _batches(dev, 1)[0].clone(), capture=True)
     assert all(torch.equal(a, b) for a, b in zip(before, m.buffers()))
