@@ -58,6 +58,50 @@ def sas_flop_per_user(d, n, items, mlp=64, blocks=2):
     return blocks * per_block + 2 * d * (items + 1)
 
 
+def sas_exec_flop_per_user(d, n, items, mlp=64, blocks=2, causal=True):
+    """Flops the kernels execute per user: every block but the last in full,
+    attention over the causal n(n+1)/2 query-key pairs (``causal``; the one-wave C3 kernel computes
+    the whole n x n tile, ``causal=False``); the last block's K|V projection for all n tokens and
+    everything else at position n-1 only (q, one query's attention, out-proj, FFN); scoring
+    2*d*(items+1) (``items`` = -1: forward only)."""
+    pairs = n * (n + 1) // 2 if causal else n * n
+    full = 2 * n * d * 3 * d + 4 * pairs * d + 2 * n * d * d + 4 * n * d * mlp
+    last = 2 * n * d * 2 * d + 2 * d * d + 4 * n * d + 2 * d * d + 4 * d * mlp
+    return (blocks - 1) * full + last + 2 * d * (items + 1)
+
+
+def per_rank(x, world):
+    """``x`` (this rank's float) from every rank, in rank order (a collective at world > 1)."""
+    if world <= 1 or not dist.is_initialized():
+        return [x]
+    t = torch.zeros(world, dtype=torch.float64, device="cuda")
+    t[dist.get_rank()] = x
+    dist.all_reduce(t)
+    return t.tolist()
+
+
+def result_checksum(res, world):
+    """a digest of the merged C5 result (1-based ranks, top-k values and ids, all
+    [B]-sized and identical on every rank after the exchange), gathered from every rank so the line
+    shows the ranks agreed; the digest is independent of the world size (the same bits at N = 1)."""
+    import hashlib
+    rk, v, i = res
+    hsh = hashlib.sha256()
+    for t in (rk.to(torch.int64), v.to(torch.float32), i.to(torch.int64)):
+        hsh.update(t.contiguous().cpu().numpy().tobytes())
+    dg = hsh.hexdigest()[:16]
+    mine = int(dg, 16) & ((1 << 62) - 1)
+    allr = [mine]
+    if world > 1 and dist.is_initialized():
+        t = torch.zeros(world, dtype=torch.int64, device="cuda")
+        t[dist.get_rank()] = mine
+        dist.all_reduce(t)
+        allr = t.tolist()
+    return {"sha256_16": dg, "ranks_agree": all(c == mine for c in allr), "n_ranks_reporting": len(allr),
+            "sum_rank": int(rk.to(torch.int64).sum()), "hr10": float((rk <= 10).double().mean()),
+            "topk_id_sum": int(i.to(torch.int64).sum())}
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -234,10 +278,13 @@ def cpu_rq_baseline(model, n_items, tag):
                       f"oracle/rq_oracle.get_indices, {tag}: batch of {n_items} synthetic items (fp32 torch CPU)")
 
 
-def cpu_sas_baseline(model, B, n, items, tag):
-    """Oracle restatement of predict (oracle/sasrec_oracle.py) on host cores, one call of B users."""
+def cpu_sas_baseline(model, B, n, items, tag, table=None):
+    """Oracle restatement of predict (oracle/sasrec_oracle.py) on host cores, one call of B users
+    (``table``: the full [items+1, d] item table when the model holds a compact one)."""
     from oracle import sasrec_oracle
     sd = {k: v.detach().cpu() for k, v in model.state_dict().items()}
+    if table is not None:
+        sd["item_emb.weight"] = table.detach().cpu()
     seqs = synth.sequences(B, n, items, 777, "cuda").cpu()
     return cpu_median(lambda: sasrec_oracle.predict(seqs, sd, model.num_blocks, model.num_heads, 1e-8),
                       B, "seqs/s", f"oracle/sasrec_oracle.predict, {tag}: batch of {B} users "
@@ -263,6 +310,7 @@ def bench_rq_c2(a, world, rank, dev):
                    "parallelism": f"item-sharded x{world}, no collective"},
         "roofline": roofline("rq_encoder_kernel<256,128,8>", ENC_FLOP_PER_ITEM * a.rq_items, enc_ms, "c2"),
         "call": {"kernels": "rq_encoder_kernel + rq_quantize_kernel", "device_ms": dev_ms,
+                 "device_ms_per_rank": per_rank(dev_ms, world),
                  "flop_per_item": rq_flop_per_item(L, K),
                  "frac_of_fp32_peak": rq_flop_per_item(L, K) * a.rq_items / (dev_ms * 1e-3) / 1e12 / FP32_PEAK_TFLOPS,
                  "hbm_algorithmic_GBs": rq_bytes_per_item(L) * a.rq_items / (dev_ms * 1e-3) / 1e9,
@@ -286,7 +334,8 @@ def bench_rq_c4(a, world, rank, dev):
             "config": {"workload": "rq_c4: RQ-VAE get_indices, 4x1024 codebooks, in 768 -> [256,128] -> e 32",
                        "catalog_items": a.c4_items, "items_per_rank": hi - lo,
                        "parallelism": f"item-sharded x{world}, no collective"},
-            "call": {"device_ms": dev_ms, "flop_per_item": rq_flop_per_item(L, K),
+            "call": {"device_ms": dev_ms, "device_ms_per_rank": per_rank(dev_ms, world),
+                     "flop_per_item": rq_flop_per_item(L, K),
                      "frac_of_fp32_peak": rq_flop_per_item(L, K) * (hi - lo) / (dev_ms * 1e-3) / 1e12 / FP32_PEAK_TFLOPS,
                      "encode_call_ms_50rep_mean": enc_ms}}
     return res, model
@@ -308,15 +357,24 @@ def bench_sas_c3(a, world, rank, dev):
     targets = torch.randint(1, items + 1, (a.sas_batch,), generator=torch.Generator(device=dev).manual_seed(5), device=dev)
     rank_ms = kernel_ms(lambda: ops.score_rank(h, table, targets))
     fl = sas_flop_per_user(d, n, items)
+    fl_exe = sas_exec_flop_per_user(d, n, items, causal=False)
+    fwd_exe = sas_exec_flop_per_user(d, n, -1, causal=False)
     res = {"metric": "seqs_scored/s", "value": a.sas_batch * world * a.steps / wall, "unit": "seqs/s",
            "ms_per_step": wall / a.steps * 1e3, "scaling": "weak",
            "config": {"workload": "sas_c3: SASRec predict, 2 blocks, d 64, n 50, H 1, mlp 64, "
                                   "100k-item full-catalog logits written", "users_per_rank_per_step": a.sas_batch,
                       "parallelism": f"user-sharded x{world}, no collective"},
            "roofline": roofline("score_direct_kernel<64>", 2 * d * (items + 1) * a.sas_batch, score_ms, "sasrec"),
-           "call": {"device_ms": dev_ms, "flop_per_user": fl,
+           "call": {"device_ms": dev_ms, "device_ms_per_rank": per_rank(dev_ms, world), "flop_per_user": fl,
                     "frac_of_fp32_peak": fl * a.sas_batch / (dev_ms * 1e-3) / 1e12 / FP32_PEAK_TFLOPS,
-                    "forward_ms": fwd_ms, "score_ms": score_ms,
+                    "flop_per_user_executed": fl_exe,
+                    "frac_of_fp32_peak_executed": fl_exe * a.sas_batch / (dev_ms * 1e-3) / 1e12 / FP32_PEAK_TFLOPS,
+                    "forward_ms": fwd_ms, "forward_flop_per_user_executed": fwd_exe,
+                    "forward_frac_executed": fwd_exe * a.sas_batch / (fwd_ms * 1e-3) / 1e12 / FP32_PEAK_TFLOPS,
+                    "executed_note": "block 0 in full (the one-wave kernel computes the whole n x n "
+                                     "attention tile), the last block's K|V for all n tokens and the "
+                                     "rest at position n-1 only",
+                    "score_ms": score_ms,
                     "logits_write_GBs": a.sas_batch * (items + 1) * 4 / (score_ms * 1e-3) / 1e9},
            "rank_fused": {"note": "forward + target logit + strict count, logits never written",
                           "value": a.sas_batch / ((fwd_ms + rank_ms) * 1e-3), "unit": "seqs/s",
@@ -332,20 +390,28 @@ def bench_sas_c5(a, world, rank, dev, time_it=True):
     from gr_amd import dist as D
     d, n, items, B = 128, 200, a.c5_items, a.c5_batch
     p = synth.sasrec_params(d, n, 2, 1, 64, dev)
-    model = synth.sasrec_model(items, p, dev, seed=5)
     seqs = synth.sequences(B, n, items, 5000, dev)            # same users on every rank
     targets = torch.randint(1, items + 1, (B,), generator=torch.Generator(device=dev).manual_seed(6), device=dev)
     ulo, uhi = D.shard_range(B, rank, world)
     usizes = [D.shard_range(B, r_, world)[1] - D.shard_range(B, r_, world)[0] for r_ in range(world)]
     lo, hi = D.shard_range(items + 1, rank, world)
-    shard = model.item_emb.weight.detach()[lo:hi]
+    # each rank builds only its catalog shard (scored) and the rows its own users' histories gather
+    # (forward), both from the position-keyed synth.table_rows: every world size scores the same table
+    t0 = time.perf_counter()
+    shard = synth.table_rows(torch.arange(lo, hi, device=dev), d, 7, dev)
+    model, lseqs = synth.sasrec_rank_model(items, p, seqs[ulo:uhi], dev, seed=5)
+    torch.cuda.synchronize()
+    setup_s = time.perf_counter() - t0
 
     P = max(1, a.c5_pipeline)
     cuts = [B * j // P for j in range(P + 1)]
 
+    def gather_h():
+        hl = model.last_hidden(lseqs)
+        return D.all_gather_rows(hl, sizes=usizes) if dist.is_initialized() else hl
+
     def step():
-        hl = model.last_hidden(seqs[ulo:uhi])
-        h = D.all_gather_rows(hl, sizes=usizes) if dist.is_initialized() else hl
+        h = gather_h()
         if P == 1:
             return D.sharded_rank_topk(h, shard, lo, targets, k=10)
         # the exchange of sub-batch j overlapped with the scoring of sub-batch j+1
@@ -353,30 +419,45 @@ def bench_sas_c5(a, world, rank, dev, time_it=True):
                                            [targets[x:y] for x, y in zip(cuts[:-1], cuts[1:])], k=10)
 
     if not time_it:   # setup only (the shard leg alone): no C5 launches in its profile
-        return None, model, model.last_hidden(seqs), targets
+        return None, model, gather_h(), targets, shard
     steps, warm = max(2, min(a.steps, 10)), 2
     wall, dev_ms = timed(step, steps, warm, world)
-    h = model.last_hidden(seqs)
+    r = step()
+    check = result_checksum(r if P == 1 else tuple(torch.cat(t) for t in zip(*r)), world)
+    h = gather_h()
     ts = torch.zeros(B, device=dev)
     topk_ms = kernel_ms(lambda: ops.score_topk(h, shard, 10, lo, thresholds=ts, mask_col0=(lo == 0)))
-    fwd_ms = kernel_ms(lambda: model.last_hidden(seqs[ulo:uhi]))
+    fwd_ms = kernel_ms(lambda: model.last_hidden(lseqs))
+    fl_ref = sas_flop_per_user(d, n, items)
+    fl_exe = sas_exec_flop_per_user(d, n, items, causal=True)
+    fwd_exe = sas_exec_flop_per_user(d, n, -1, causal=True)
     res = {"metric": "seqs_scored/s", "value": B * steps / wall, "unit": "seqs/s", "scaling": "strong",
             "ms_per_step": wall / steps * 1e3, "steps": steps,
             "config": {"workload": "sas_c5: SASRec d 128, n 200, 2 blocks, 1M-item catalog, rank + top-10",
                        "users_per_step": B, "catalog_rows": items + 1, "rows_per_rank": hi - lo,
+                       "users_forwarded_per_rank": uhi - ulo, "table_rows_built_per_rank": (hi - lo) + model.item_num,
+                       "setup_s": setup_s,
                        "parallelism": f"catalog-sharded x{world}: RCCL all-gather h + top-k, all-reduce counts"
                        + (f", {P} pipelined sub-batches" if P > 1 else "") if world > 1 else "single shard"},
+            "result_checksum": check,
             "roofline": roofline(TOPK_PASS, 2 * d * (hi - lo) * B, topk_ms, "c5",
                                  call_kernels=TOPK_CALL_KERNELS,
                                  note="one gr_score_topk_f32 call: the tile pass (scores, strict counts, "
                                       "per-user 32-row tile maxima) + the select kernel (re-scores the tiles "
                                       "at or above the k-th tile max); flop counts the scoring GEMM once; "
                                       "traffic is the whole call's"),
-            "call": {"device_ms_rank0": dev_ms, "flop_per_user": sas_flop_per_user(d, n, items),
-                     "forward_ms": fwd_ms, "score_topk_ms": topk_ms,
+            "call": {"device_ms_rank0": dev_ms, "device_ms_per_rank": per_rank(dev_ms, world),
+                     "flop_per_user": fl_ref, "flop_per_user_executed": fl_exe,
+                     "frac_of_fp32_peak": fl_ref * B / world / (wall / steps) / 1e12 / FP32_PEAK_TFLOPS,
+                     "frac_of_fp32_peak_executed": fl_exe * B / world / (wall / steps) / 1e12 / FP32_PEAK_TFLOPS,
+                     "forward_ms": fwd_ms, "forward_flop_per_user_executed": fwd_exe,
+                     "forward_frac_executed": fwd_exe * (uhi - ulo) / (fwd_ms * 1e-3) / 1e12 / FP32_PEAK_TFLOPS,
+                     "score_topk_ms": topk_ms,
                      "note": "rank + top-10 fused into the scoring pass (gr_score_topk_f32): the "
-                             "[B, rows] logits are never written"}}
-    return res, model, h, targets
+                             "[B, rows] logits are never written; 'executed' counts causal attention "
+                             "(n(n+1)/2 query-key pairs) and the final block at position n-1 only, as "
+                             "the kernels run it; frac from the max-over-ranks wall time per step"}}
+    return res, model, h, targets, shard
 
 
 def sas_train_bytes(B, n, d, rows, J):
@@ -687,16 +768,16 @@ def bench_rq_train_step(a, world, rank, dev, cpu=False):
     return res
 
 
-def bench_c5_shard(a, model, h, targets, dev, shards=8):
+def bench_c5_shard(a, table, h, targets, dev, shards=8):
     """The per-GPU work of the 8-GPU C5 point, timed on one GPU: 512 users against one catalog
-    shard of 125,001 rows (rows [lo, hi) of the 1M-item table; the first shard, which also masks
+    shard of 125,001 rows (rows [lo, hi) of the 1M-item ``table``; the first shard, which also masks
     row 0): the owner's target logits (gr_score_pairs_f32) + fused score + top-10 + strict counts
     (gr_score_topk_f32).  The collectives around it (all-reduce of B floats and B counts,
     all-gather of B x 10 candidates) are latency-bound and not included."""
     from gr_amd import dist as D
     d, B, k = h.shape[1], h.shape[0], 10
-    lo, hi = D.shard_range(model.item_emb.weight.shape[0], 0, shards)
-    shard = model.item_emb.weight.detach()[lo:hi]
+    lo, hi = D.shard_range(table.shape[0], 0, shards)
+    shard = table[lo:hi]
     t = targets.reshape(-1)
     own = (t >= lo) & (t < hi)
     loc = torch.where(own, t - lo, torch.zeros_like(t))
@@ -713,7 +794,7 @@ def bench_c5_shard(a, model, h, targets, dev, shards=8):
     return {"metric": "seqs_scored/s", "value": B * a.steps / wall, "unit": "seqs/s",
             "ms_per_step": wall / a.steps * 1e3, "scaling": "per-rank shard of the 8-GPU C5 point",
             "config": {"workload": f"c5_shard: {B} users x one {hi - lo}-row catalog shard (1/{shards} of "
-                                   f"{model.item_emb.weight.shape[0]}), d {d}, target logit + rank + top-{k}",
+                                   f"{table.shape[0]}), d {d}, target logit + rank + top-{k}",
                        "rows": hi - lo, "users": B},
             "roofline": roofline(TOPK_PASS, flop, topk_ms, "shard",
                                  call_kernels=TOPK_CALL_KERNELS,
@@ -832,14 +913,15 @@ def main():
         del c4_model
         torch.cuda.empty_cache()
     if "c5" in legs or "shard" in legs:
-        c5, c5_model, h5, t5 = bench_sas_c5(a, world, rank, dev, time_it="c5" in legs)
+        c5, c5_model, h5, t5, table5 = bench_sas_c5(a, world, rank, dev, time_it="c5" in legs)
         if "c5" in legs:
             line["sasrec_c5"] = c5
-            if cpu:
-                line["sasrec_c5"]["cpu_baseline"] = cpu_sas_baseline(c5_model, 128, 200, a.c5_items, "C5")
+            if cpu:   # at N = 1 the rank's shard is the whole table
+                line["sasrec_c5"]["cpu_baseline"] = cpu_sas_baseline(c5_model, 128, 200, a.c5_items, "C5",
+                                                                     table=table5)
         if "shard" in legs and world == 1:
-            line["c5_shard"] = bench_c5_shard(a, c5_model, h5, t5, dev)
-        del c5_model, h5
+            line["c5_shard"] = bench_c5_shard(a, table5, h5, t5, dev)
+        del c5_model, h5, table5
         torch.cuda.empty_cache()
     if "train_step" in legs:
         line["sasrec_train_step"] = bench_sas_train_step(a, world, rank, dev)
@@ -847,6 +929,14 @@ def main():
         line["rq_train_step"] = bench_rq_train_step(a, world, rank, dev, cpu)
     if "train" in legs:
         line["sasrec_train"] = bench_sas_train(a, world, rank, dev)
+    # what the process group saw, so a multi-GPU line proves its ranks took part
+    if dist.is_initialized():
+        devs = per_rank(float(local), world)
+        line["dist"] = {"backend": str(dist.get_backend()), "world_size": dist.get_world_size(),
+                        "local_device_per_rank": [int(x) for x in devs],
+                        "device_name": torch.cuda.get_device_name(dev)}
+    else:
+        line["dist"] = {"backend": None, "world_size": 1, "note": "no process group (N = 1)"}
     if rank == 0:
         print(json.dumps(line), flush=True)
     if dist.is_initialized():

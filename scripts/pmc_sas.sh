@@ -1,17 +1,19 @@
 #!/bin/bash
-# SQ / TCC counters of the C5 forward kernels (one --pmc pass per counter group, each with its own
-# time limit; the box refuses combined trace domains).  Usage: scripts/pmc_sas.sh TAG
+# SQ / GRBM counters of the C5 forward and C2 encode kernels: one --pmc pass per counter group, each
+# under its own time limit (the box refuses combined trace domains), over scripts/prof_kernels.py.
+# Usage: scripts/pmc_sas.sh TAG [WHAT]   (WHAT: c5fwd,c2 by default)
 set -u
 ROOT=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 OUT=$ROOT/gpurun_out/$1
+WHAT=${2:-c5fwd,c2}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 cd /tmp
 i=0
 for c in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS" \
-         "SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE" "FETCH_SIZE" "WRITE_SIZE"; do
+         "SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE GRBM_COUNT"; do
   i=$((i+1))
-  timeout -s KILL 120 rocprofv3 --pmc $c --output-format csv -d "$OUT/pmc$i" -o run -- python3 "$ROOT/scripts/ab_sas.py" --opt sas_rowtile=1 > "$OUT/pmc$i.log" 2>&1
+  timeout -s KILL 90 rocprofv3 --pmc $c -d "$OUT/p$i" -o p$i -- python3 "$ROOT/scripts/prof_kernels.py" --what "$WHAT" > "$OUT/p$i.log" 2>&1
   rc=$?
   echo "pass $i rc=$rc"
   if [ $rc -ne 0 ]; then exit $rc; fi

@@ -1,0 +1,33 @@
+"""A short, fixed workload for rocprofv3 PMC passes: a few calls of the C5 forward
+(model.last_hidden, d 128, n 200, B 512) and/or the C2 encode (get_indices, 100k items).
+
+    rocprofv3 --pmc ... -d OUT -- python3 scripts/prof_kernels.py --what c5fwd,c2 --calls 5
+"""
+import argparse
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from gr_amd import synth  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--what", default="c5fwd,c2")
+ap.add_argument("--calls", type=int, default=5)
+a = ap.parse_args()
+dev = torch.device("cuda:0")
+what = a.what.split(",")
+if "c5fwd" in what:
+    seqs = synth.sequences(512, 200, 1_000_000, 5000, dev)
+    m, ls = synth.sasrec_rank_model(1_000_000, synth.sasrec_params(128, 200, 2, 1, 64, dev), seqs, dev, seed=5)
+    for _ in range(a.calls):
+        m.last_hidden(ls)
+    torch.cuda.synchronize()
+if "c2" in what:
+    rq = synth.rqvae_model(3, 256, dev)
+    x = synth.items(100_000, 1000, dev)
+    for _ in range(a.calls):
+        rq.get_indices(x)
+    torch.cuda.synchronize()
+print("done", what, flush=True)

@@ -150,3 +150,33 @@ def test_c5_full_catalog_vs_oracle(dev, parity_log):
                ranks_isolated=int(iso.sum()), top10_exact_users=n_exact1,
                hr10_oracle=float((exact <= 10).mean()))
     assert err <= TOL
+
+
+def test_c5_per_rank_construction_matches_full_table(dev):
+    """bench.py's C5 leg builds, per rank, only its catalog shard and the table rows its own users
+    gather (synth.sasrec_rank_model).  The hidden states of every world size's user shards, stitched
+    together, equal the full-table model's bit for bit, and so does the merged rank / top-10."""
+    import copy
+    from gr_amd import dist as D, synth
+    items, n, B, d = 1_000_000, 200, 512, 128
+    p = synth.sasrec_params(d, n, 2, 1, 64, dev)
+    seqs = synth.sequences(B, n, items, 5000, dev)
+    table = synth.table_rows(torch.arange(items + 1, device=dev), d, 7, dev)
+    m1, s1 = synth.sasrec_rank_model(items, p, seqs, dev, seed=5)
+    full = copy.deepcopy(m1)
+    full.item_emb = torch.nn.Embedding(items + 1, d, padding_idx=0).to(dev)
+    with torch.no_grad():
+        full.item_emb.weight.copy_(table)
+    full.item_num = items
+    h = full.last_hidden(seqs)
+    assert torch.equal(m1.last_hidden(s1), h)
+    for world in (2, 8):
+        hs = []
+        for r in range(world):
+            lo, hi = D.shard_range(B, r, world)
+            mr, sr = synth.sasrec_rank_model(items, p, seqs[lo:hi], dev, seed=5)
+            hs.append(mr.last_hidden(sr))
+        assert torch.equal(torch.cat(hs), h), world
+        shards = [D.shard_range(items + 1, r, world) for r in range(world)]
+        parts = [synth.table_rows(torch.arange(lo, hi, device=dev), d, 7, dev) for lo, hi in shards]
+        assert torch.equal(torch.cat(parts), table)
