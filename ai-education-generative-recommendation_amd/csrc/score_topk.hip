@@ -332,7 +332,8 @@ __global__ __launch_bounds__(256, 2) void score_topk_kernel(
 // and records per user the max logit of every 32-row tile.  Let M_k be the k-th largest tile max:
 // those k tiles hold k distinct items >= M_k, so the user's k-th best logit is >= M_k and every
 // top-k item lies in a tile whose max is >= M_k (about k tiles; more only on exact ties).  This
-// kernel (one workgroup per user) finds M_k, re-scores just those tiles with the tile pass's exact
+// kernel (one workgroup per user) finds a threshold tau <= M_k (below), re-scores just the tiles
+// whose max is >= tau with the tile pass's exact
 // MFMA chain (table rows as the A operand, the user as B: bitwise the same logits), and selects
 // the top k by (value desc, column asc); it also sums the partial counts.
 template <int D, int KC>
@@ -346,7 +347,7 @@ __global__ __launch_bounds__(256, 2) void topk_select_kernel(const float* __rest
                                                           int) {
   constexpr int KG = D / 32;
   __shared__ int list[256];
-  __shared__ int nlist, saturated;
+  __shared__ int nlist;
   __shared__ float mk_s;
   __shared__ unsigned long long csum;
   const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, hh = lane >> 5, w = tid >> 6;
@@ -354,7 +355,6 @@ __global__ __launch_bounds__(256, 2) void topk_select_kernel(const float* __rest
   const float* tm = tmax + u * T;
   if (tid == 0) {
     nlist = 0;
-    saturated = 0;
     csum = 0ull;
     mk_s = -INFINITY;
   }
@@ -365,22 +365,27 @@ __global__ __launch_bounds__(256, 2) void topk_select_kernel(const float* __rest
     for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
     if (lane == 0 && c) atomicAdd(&csum, c);
   }
-  // M_k = the k-th largest tile max; each thread keeps its own KC best tiles (batches of MB loads)
-  TopList<KC> tl;
-  tl.init();
-  {
-    constexpr int MB = 16;
-    for (int64_t q0 = tid; q0 < T; q0 += 256 * MB) {
-      float v[MB];
+  // The threshold: tau = the k-th largest of the 256 per-thread maxima of the user's tile maxima
+  // (thread t reads tiles t, t + 256, ...).  k distinct threads hold a tile >= tau, so M_k >= tau:
+  // every top-k item lies in a tile whose max is >= tau (about k + 1 tiles: the k largest tiles
+  // rarely share a thread).  One fmax per tile, no per-thread sorted lists (their insertions took
+  // most of this kernel's 89 us at C5, profiles/r03_ab_topk_select_tau.txt).
+  constexpr int MB = 16;
+  float mx = -INFINITY;
+  for (int64_t q0 = tid; q0 < T; q0 += 256 * MB) {
+    float v[MB];
 #pragma unroll
-      for (int b = 0; b < MB; ++b) {
-        const int64_t q = q0 + 256 * b;
-        v[b] = tm[q < T ? q : q0];
-      }
-#pragma unroll
-      for (int b = 0; b < MB; ++b)
-        if (q0 + 256 * b < T) tl.push(v[b], q0 + 256 * b);
+    for (int b = 0; b < MB; ++b) {
+      const int64_t q = q0 + 256 * b;
+      v[b] = q < T ? tm[q] : -INFINITY;
     }
+#pragma unroll
+    for (int b = 0; b < MB; ++b) mx = fmaxf(mx, v[b]);
+  }
+  {
+    TopList<1> tl;
+    tl.init();
+    tl.push(mx, tid);
     tl.block_select(k, [&](int q, float v, int64_t) {
       if (q == k - 1) mk_s = v;
     });
@@ -388,24 +393,26 @@ __global__ __launch_bounds__(256, 2) void topk_select_kernel(const float* __rest
   __syncthreads();
   const float mk = mk_s;
   if (cnt_out && tid == 0) cnt_out[u] = csum;
-  // The qualifying tiles (max >= M_k) are the threads' list entries >= M_k, unless a thread's list
-  // is all >= M_k (it may hold more: exact ties) or they overflow the list -- then every tile is
-  // re-checked, 256 at a time.
-  int mine = 0;
+  // The qualifying tiles (max >= tau), from a second read of the thread's tiles (cache-resident);
+  // more than the LDS list holds (ties) -> every tile is re-checked, 256 at a time.
+  if (mx >= mk) {
+    for (int64_t q0 = tid; q0 < T; q0 += 256 * MB) {
+      float v[MB];
 #pragma unroll
-  for (int q = 0; q < KC; ++q) mine += (tl.i[q] != INT64_MAX && tl.v[q] >= mk) ? 1 : 0;
-  if (mine == KC) saturated = 1;
-  if (mine) atomicAdd(&nlist, mine);
-  __syncthreads();
-  const bool slow = saturated != 0 || nlist > 256;   // (ties past the list's capacity)
-  __syncthreads();
-  if (tid == 0) nlist = 0;
-  __syncthreads();
-  if (!slow) {
+      for (int b = 0; b < MB; ++b) {
+        const int64_t q = q0 + 256 * b;
+        v[b] = q < T ? tm[q] : -INFINITY;
+      }
 #pragma unroll
-    for (int q = 0; q < KC; ++q)
-      if (tl.i[q] != INT64_MAX && tl.v[q] >= mk) list[atomicAdd(&nlist, 1)] = (int)tl.i[q];
+      for (int b = 0; b < MB; ++b)
+        if (q0 + 256 * b < T && v[b] >= mk) {
+          const int at = atomicAdd(&nlist, 1);
+          if (at < 256) list[at] = (int)(q0 + 256 * b);
+        }
+    }
   }
+  __syncthreads();
+  const bool slow = nlist > 256;
   __shared__ __attribute__((aligned(16))) float hs[D];   // the user's vector (LDS broadcast reads)
   if (tid < D / 4) *reinterpret_cast<f32x4*>(hs + 4 * tid) = *reinterpret_cast<const f32x4*>(h + u * D + 4 * tid);
   TopList<KC> best;
