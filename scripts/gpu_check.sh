@@ -27,11 +27,6 @@ for s in $STEPS; do
     tests) step pytest_gpu 1200 python -m pytest tests -m gpu -q -rs ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 900 python bench.py ;;
-    stamps) step stamps_rq 300 python scripts/stamps_rq.py 3 256 && step stamps_rq4 300 python scripts/stamps_rq.py 4 1024 ;;
-    ablate) GR_STAMPS_VARIANT=_now1 step stamps_now1 300 python scripts/stamps_rq.py 3 256 && \
-            GR_STAMPS_VARIANT=_nox step stamps_nox 300 python scripts/stamps_rq.py 3 256 && \
-            GR_STAMPS_VARIANT=_noxw step stamps_noxw 300 python scripts/stamps_rq.py 3 256 && \
-            GR_STAMPS_VARIANT=_w1coal step stamps_w1coal 300 python scripts/stamps_rq.py 3 256 ;;
     trace_rq)
       export TMPDIR=/tmp
       cd /tmp
@@ -43,8 +38,14 @@ for s in $STEPS; do
       export TMPDIR=/tmp
       cd /tmp
       step rocprof 900 rocprofv3 --kernel-trace --stats --output-format csv \
-          -d "$OUT/rocprof" -o run -- python3 "$ROOT/bench.py" --steps 10 --warmup 3 --no-cpu-baseline
+          -d /tmp/gr_rocprof -o run -- python3 "$ROOT/bench.py" --steps 10 --warmup 3 --no-cpu-baseline
+      # the full trace is tens of MB (gpurun copies back <= 64 MiB): keep the stats and a per-launch-shape summary
+      mkdir -p "$OUT/rocprof"
+      cp /tmp/gr_rocprof/run_kernel_stats.csv "$OUT/rocprof/" 2>/dev/null
+      python3 "$ROOT/scripts/trace_stats.py" /tmp/gr_rocprof/run_kernel_trace.csv --top 60 > "$OUT/rocprof/trace_stats.csv" 2>&1
       cd "$ROOT" ;;
+    micro)
+      step micro_valu 300 python scripts/micro/mfma_valu.py ;;
     pmc)  # HBM traffic: FETCH_SIZE and WRITE_SIZE in separate passes (MI355X_MICROARCH.md §HBM)
       export TMPDIR=/tmp
       for c in FETCH_SIZE WRITE_SIZE; do
