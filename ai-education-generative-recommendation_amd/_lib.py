@@ -9,7 +9,8 @@ import os
 import torch
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_PKG, "lib", "libgr_amd.so")
+# GR_AMD_LIB: another in-tree build of the same ABI (A/B variants from scripts/build_variant.sh)
+LIB_PATH = os.environ.get("GR_AMD_LIB") or os.path.join(_PKG, "lib", "libgr_amd.so")
 
 GR_ACT_NONE = 0
 GR_ACT_RELU = 1

@@ -30,6 +30,7 @@
 // larger than one LDS chunk are streamed in chunks.  e <= 64 (padded with zero features to 16, 32
 // or 64: zero terms at the end of the fma chain change nothing).
 #include "gr_common.h"
+#include "rq_quant.h"
 
 namespace gr {
 
@@ -45,86 +46,6 @@ constexpr size_t RQ_PART_BYTES = 2 * RQ_SPLIT_MAX * 4 * 32 * 3 * sizeof(float);
 // item tiles per wave held in registers: fewer at e = 64 to stay spill-free
 template <int EP>
 struct RQMaxT { static constexpr int value = EP >= 64 ? 2 : 4; };
-
-// Float offset of 16-byte slot q of row c of an LDS codebook image with EP/4 slots per row.
-template <int EP>
-__device__ __forceinline__ int cb_off(int c, int q) {
-  constexpr int S = EP / 4;
-  constexpr int M = S >= 8 ? 7 : S - 1;
-  return c * EP + 4 * (q ^ (c & M));
-}
-
-// LDS float offset of feature f of row c: lane half f & 1, float4 f >> 3, element (f >> 1) & 3.
-template <int EP>
-__device__ __forceinline__ int feat_off(int c, int f) {
-  return cb_off<EP>(c, (f & 1) * (EP / 8) + (f >> 3)) + ((f >> 1) & 3);
-}
-
-// ||r||^2 of this lane's item in ATen's order (aten_rowsq) with the features split over the lane
-// halves (half h: features 8j + 2s + h in rr[j][s]); every lane of the pair returns the same value.
-template <int EP>
-__device__ __forceinline__ float rn_exact(const f32x4 (&rr)[EP / 8], int e, int h) {
-#pragma clang fp contract(off)
-  constexpr int HQ = EP / 8;
-  const int nv = e >> 3, full = (nv >> 2) << 2, tail = e & 7;
-  float A[4], T[4];
-#pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
-    T[s] = 0.f;
-#pragma unroll
-    for (int v = 0; v < HQ; ++v) {
-      const float x = rr[v][s];
-      const float q = x * x;
-      if (v < nv) {
-        const int a = v < full ? (v & 3) : 0;
-        if (a == 0) a0 = a0 + q;
-        else if (a == 1) a1 = a1 + q;
-        else if (a == 2) a2 = a2 + q;
-        else a3 = a3 + q;
-      } else if (v == nv) {
-        T[s] = q;                      // tail element 8 nv + 2s + h (zero past e)
-      }
-    }
-    A[s] = ((a0 + a1) + a2) + a3;
-  }
-  float PA[4], PT[4];
-#pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    PA[s] = __shfl_xor(A[s], 32);
-    PT[s] = __shfl_xor(T[s], 32);
-  }
-  if (e < 8) {   // ATen's scalar row sum (4 accumulators over rows of 4, leftovers into the first)
-    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
-#pragma unroll
-    for (int i = 0; i < 7; ++i)
-      if (i < e) {
-        const float q = ((i & 1) == h) ? T[i >> 1] : PT[i >> 1];
-        const int k = i < ((e >> 2) << 2) ? (i & 3) : 0;
-        if (k == 0) a0 = a0 + q;
-        else if (k == 1) a1 = a1 + q;
-        else if (k == 2) a2 = a2 + q;
-        else a3 = a3 + q;
-      }
-    return ((a0 + a1) + a2) + a3;
-  }
-  float f = 0.f;
-#pragma unroll
-  for (int jj = 0; jj < 7; ++jj)
-    if (jj < tail) f = f + (((jj & 1) == h) ? T[jj >> 1] : PT[jj >> 1]);
-#pragma unroll
-  for (int jj = 0; jj < 8; ++jj) f = f + (((jj & 1) == h) ? A[jj >> 1] : PA[jj >> 1]);
-  return f;
-}
-
-// (best, second, index) merge: the lower distance, then the lower index (branch-free selects).
-template <bool SECOND>
-__device__ __forceinline__ void merge_min(float& best, float& second, int& bi, float ob, float os, int oi) {
-  const bool take = (ob < best) | ((ob == best) & (oi < bi));
-  if (SECOND) second = take ? fminf(os, best) : fminf(second, ob);
-  best = take ? ob : best;
-  bi = take ? oi : bi;
-}
 
 // Stage codes [c0, c0 + cnt) of a level into the LDS image (de-interleaved rows) and their norms.
 template <int EP, int NT, bool FULL>
@@ -505,10 +426,13 @@ static int mlp_exact(const float* x, int64_t n, int32_t n_linear, const int32_t*
   return GR_OK;
 }
 
+// Workspace: the MLP's part, then z [n, e] (when the caller passes no z_out), then the fused
+// encode's hand-off words.
 extern "C" size_t gr_rq_encode_workspace_bytes(int64_t n, int32_t n_linear, const int32_t* dims,
                                                int32_t L, const int32_t* K) {
   if (n < 0 || n_linear < 1 || !dims || L < 1 || !K) return 0;
-  return mlp_ws_bytes(n, n_linear, dims) + gr::align_up((size_t)n * dims[n_linear] * 4, 256);
+  return mlp_ws_bytes(n, n_linear, dims) + gr::align_up((size_t)n * dims[n_linear] * 4, 256) +
+         gr::align_up((size_t)gr_rq_encode_sync_words(n) * 4, 256);
 }
 
 extern "C" size_t gr_rq_encoder_pack_floats(int32_t n_linear, const int32_t* dims) {
@@ -547,10 +471,17 @@ extern "C" int gr_rq_encode_packed_f32(const float* x, int64_t n, int32_t n_line
     return fail(GR_ERR_WORKSPACE, "gr_rq_encode_f32: workspace too small (need " + std::to_string(need) + " bytes)");
   if (n == 0) return GR_OK;
   if (!x || !idx_out) return fail(GR_ERR_ARG, "gr_rq_encode_f32: null x / idx_out");
-  float* zb = z_out;
-  if (!zb) {   // z in the workspace, after the MLP's part
-    char* ws = reinterpret_cast<char*>(align_up(reinterpret_cast<uintptr_t>(workspace), 256));
-    zb = reinterpret_cast<float*>(ws + mlp_ws_bytes(n, n_linear, dims) - 256);
+  char* wsa = reinterpret_cast<char*>(align_up(reinterpret_cast<uintptr_t>(workspace), 256));
+  char* zws = wsa + mlp_ws_bytes(n, n_linear, dims) - 256;   // z in the workspace, after the MLP's part
+  float* zb = z_out ? z_out : reinterpret_cast<float*>(zws);
+  uint32_t* sync = reinterpret_cast<uint32_t*>(zws + align_up((size_t)n * e * 4, 256));
+  if (!best_out && !gap_out && option("rq_encq") == 1 && option("rq_fused") == 1) {
+    rc = gr_rq_encode_fused_launch(x, n, n_linear, dims, weights, biases,
+                                   packed ? const_cast<float*>(packed)
+                                          : reinterpret_cast<float*>(wsa + 2 * act_bytes(n, n_linear, dims)),
+                                   packed != nullptr, L, K, codebooks, idx_out, zb, sync, st);
+    if (rc != GR_ERR_UNSUPPORTED) return rc;
+    clear_error();
   }
   RQLevels lv{};
   for (int l = 0; l < L; ++l) {
