@@ -56,10 +56,6 @@ static std::atomic<int64_t> g_attn_lazy{1};
 static std::atomic<int64_t> g_topk_impl{1};
 // rt_w8 (1 (default): the post-attention row tile runs 8 waves per 64-row tile; 0: 4 waves)
 static std::atomic<int64_t> g_rt_w8{1};
-// rq_encq (1 (default): at the fused encoder shape, get_indices is ONE launch -- the encoder plus a
-// dynamically claimed quantize phase (rq_fused.hip rq_encode_kernel); 0: encoder and quantize
-// kernels back to back).  Bitwise the same IDs; A/B timing.
-static std::atomic<int64_t> g_rq_encq{1};
 // lin_w8 (1 (default): gr_linear_f32's 128x128 / 128x64 tiles run 8 waves per workgroup; 0: 4)
 static std::atomic<int64_t> g_lin_w8{1};
 
@@ -81,7 +77,6 @@ int64_t option(const char* name) {
   if (!strcmp(name, "topk_impl")) return g_topk_impl.load();
   if (!strcmp(name, "rt_w8")) return g_rt_w8.load();
   if (!strcmp(name, "lin_w8")) return g_lin_w8.load();
-  if (!strcmp(name, "rq_encq")) return g_rq_encq.load();
   return -1;
 }
 }  // namespace gr
@@ -106,7 +101,6 @@ extern "C" int gr_set_option(const char* name, int64_t value) {
   if (!strcmp(name, "topk_impl") && (value == 0 || value == 1)) { gr::g_topk_impl = value; return GR_OK; }
   if (!strcmp(name, "rt_w8") && (value == 0 || value == 1)) { gr::g_rt_w8 = value; return GR_OK; }
   if (!strcmp(name, "lin_w8") && (value == 0 || value == 1)) { gr::g_lin_w8 = value; return GR_OK; }
-  if (!strcmp(name, "rq_encq") && (value == 0 || value == 1)) { gr::g_rq_encq = value; return GR_OK; }
   return gr::fail(GR_ERR_ARG, std::string("gr_set_option: unknown option or value: ") + name);
 }
 

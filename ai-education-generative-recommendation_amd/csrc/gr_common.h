@@ -137,12 +137,6 @@ int gr_rq_encoder_fused_launch(const float* x, int64_t n, int32_t n_linear, cons
 int gr_rq_encoder_pack_launch(int32_t n_linear, const int32_t* dims, const float* const* weights, float* pack,
                               hipStream_t st);
 size_t gr_rq_fused_pack_floats(int32_t n_linear, const int32_t* dims);
-int gr_rq_encode_fused_launch(const float* x, int64_t n, int32_t n_linear, const int32_t* dims,
-                              const float* const* weights, const float* const* biases, float* pack,
-                              bool pack_is_ready, int32_t L, const int32_t* K, const float* const* cbs,
-                              int64_t* idx, float* z, uint32_t* sync, hipStream_t st);
-// 32-bit words of the fused encode's hand-off state for n items (claim counter, timeout, tile flags).
-inline int64_t gr_rq_encode_sync_words(int64_t n) { return (n + 31) / 32 + 2; }
 int gr_sasrec_fused_launch(const gr_sasrec_params* p, const int64_t* seqs, int64_t B, int32_t n,
                            float* out, int32_t last_only, int32_t* err, hipStream_t st);
 int gr_attn_mfma_launch(const float* qkv, float* out, int64_t B, int n, int H, int hd, float scale,

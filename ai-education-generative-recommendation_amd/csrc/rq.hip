@@ -426,13 +426,10 @@ static int mlp_exact(const float* x, int64_t n, int32_t n_linear, const int32_t*
   return GR_OK;
 }
 
-// Workspace: the MLP's part, then z [n, e] (when the caller passes no z_out), then the fused
-// encode's hand-off words.
 extern "C" size_t gr_rq_encode_workspace_bytes(int64_t n, int32_t n_linear, const int32_t* dims,
                                                int32_t L, const int32_t* K) {
   if (n < 0 || n_linear < 1 || !dims || L < 1 || !K) return 0;
-  return mlp_ws_bytes(n, n_linear, dims) + gr::align_up((size_t)n * dims[n_linear] * 4, 256) +
-         gr::align_up((size_t)gr_rq_encode_sync_words(n) * 4, 256);
+  return mlp_ws_bytes(n, n_linear, dims) + gr::align_up((size_t)n * dims[n_linear] * 4, 256);
 }
 
 extern "C" size_t gr_rq_encoder_pack_floats(int32_t n_linear, const int32_t* dims) {
@@ -471,17 +468,10 @@ extern "C" int gr_rq_encode_packed_f32(const float* x, int64_t n, int32_t n_line
     return fail(GR_ERR_WORKSPACE, "gr_rq_encode_f32: workspace too small (need " + std::to_string(need) + " bytes)");
   if (n == 0) return GR_OK;
   if (!x || !idx_out) return fail(GR_ERR_ARG, "gr_rq_encode_f32: null x / idx_out");
-  char* wsa = reinterpret_cast<char*>(align_up(reinterpret_cast<uintptr_t>(workspace), 256));
-  char* zws = wsa + mlp_ws_bytes(n, n_linear, dims) - 256;   // z in the workspace, after the MLP's part
-  float* zb = z_out ? z_out : reinterpret_cast<float*>(zws);
-  uint32_t* sync = reinterpret_cast<uint32_t*>(zws + align_up((size_t)n * e * 4, 256));
-  if (!best_out && !gap_out && option("rq_encq") == 1 && option("rq_fused") == 1) {
-    rc = gr_rq_encode_fused_launch(x, n, n_linear, dims, weights, biases,
-                                   packed ? const_cast<float*>(packed)
-                                          : reinterpret_cast<float*>(wsa + 2 * act_bytes(n, n_linear, dims)),
-                                   packed != nullptr, L, K, codebooks, idx_out, zb, sync, st);
-    if (rc != GR_ERR_UNSUPPORTED) return rc;
-    clear_error();
+  float* zb = z_out;
+  if (!zb) {   // z in the workspace, after the MLP's part
+    char* ws = reinterpret_cast<char*>(align_up(reinterpret_cast<uintptr_t>(workspace), 256));
+    zb = reinterpret_cast<float*>(ws + mlp_ws_bytes(n, n_linear, dims) - 256);
   }
   RQLevels lv{};
   for (int l = 0; l < L; ++l) {

@@ -25,7 +25,6 @@
 #include <type_traits>
 
 #include "gr_common.h"
-#include "rq_quant.h"
 
 namespace gr {
 
@@ -45,13 +44,6 @@ struct FusedCfg {
   static constexpr int LDS = 2 * PI * FXP + PI * P1 + PI * P2 + E * P3;
   static_assert(H1 == 32 * FWV && H2 == 128, "8-wave form: H1 = 256, H2 = 128");
 };
-
-typedef __attribute__((address_space(1))) unsigned int gu32;
-typedef __attribute__((address_space(1))) unsigned long long gu64;
-
-__device__ __forceinline__ unsigned long long pack2(float a, float b) {
-  return (unsigned long long)__float_as_uint(a) | ((unsigned long long)__float_as_uint(b) << 32);
-}
 
 // Packed-order position of the 4 consecutive features k0..k0+3 (k0 % 4 == 0) of a 32-deep group:
 // feature 8j + 2s + h sits at 16h + 4j + s, so a float4 splits into two 8-byte halves.
@@ -76,7 +68,6 @@ struct FusedCtx {
   int D0, NC, csplit, t_end;
   const float *W2, *b1, *b2, *W3, *b3;
   float* z_out;
-  gu32* flags;            // fused encode: per-tile "z published" words (else null)
   float *xs, *h1s, *h2s, *w3s;
   int tid, w, r, h;
   const float* w1row;
@@ -123,7 +114,7 @@ __device__ __forceinline__ void store_h_packed(float* row, int g4, int h, const 
 // so a workgroup's odd last tile runs half the chunk iterations at two chains per wave instead of a
 // one-chain pass over all of them; y = (b1 + block 0) + block 1 as in every other pass.
 // next_ks: the pass after this one is a k-split pass (its first x chunk is staged in that layout).
-template <int NP, int H1, int H2, bool PUB = false, bool KS = false>
+template <int NP, int H1, int H2, bool KS = false>
 __device__ __forceinline__ void rq_fused_pass(FusedCtx<H1, H2>& cx, int tb, bool next_ks = false) {
 #pragma clang fp contract(off)
   using C = FusedCfg<H1, H2>;
@@ -397,27 +388,10 @@ __device__ __forceinline__ void rq_fused_pass(FusedCtx<H1, H2>& cx, int tb, bool
       f32x4 o;
 #pragma unroll
       for (int i = 0; i < 4; ++i) o[i] = bb[i] + acc3[i];
-      float* zp = cx.z_out + item * E + 16 * oh + 4 * g;
-      if constexpr (PUB) {   // write-through (sc1) stores: other CUs quantize these rows
-        gu64* zq = (gu64*)zp;
-        __hip_atomic_store(zq, pack2(o[0], o[1]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(zq + 1, pack2(o[2], o[3]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      } else {
-        *reinterpret_cast<f32x4*>(zp) = o;
-      }
+      *reinterpret_cast<f32x4*>(cx.z_out + item * E + 16 * oh + 4 * g) = o;
     }
   }
   // no barrier: h2 is next written after the next pass's L1 barriers
-}
-
-// Publish z tiles [t0, t1) of this workgroup (cdna_hip_programming.md Guideline 16, R1): every
-// storing wave drains its sc1 stores (vmcnt also waits for the loads in flight, so this is done
-// once or twice per workgroup, not per pass), the workgroup barrier, then ONE lane per tile flag.
-__device__ __forceinline__ void publish_tiles(gu32* flags, int t0, int t1, int tid) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  for (int t = t0 + tid; t < t1; t += 64 * FWV)
-    __hip_atomic_store(flags + t, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 template <int H1, int H2>
@@ -456,339 +430,9 @@ __global__ __launch_bounds__(64 * FWV, 1) void rq_encoder_kernel(
   int tb = t_begin;
   for (; tb + FP <= t_end; tb += FP) rq_fused_pass<FP, H1, H2>(cx, tb, ks && tb + FP + 1 == t_end);
   if (tb < t_end) {   // FP == 2: at most one tile left
-    if (ks) rq_fused_pass<2, H1, H2, false, true>(cx, tb);
+    if (ks) rq_fused_pass<2, H1, H2, true>(cx, tb);
     else rq_fused_pass<1, H1, H2>(cx, tb);
   }
-}
-
-// ---------------------------------------------------------------------------------------------
-// Fused encode (RQVAE.get_indices at the fused encoder shape, rqvae.py:67-71): one persistent launch
-// runs the encoder above over a static tile partition, publishing each pass's z tiles, and then every
-// wave turns into a quantizer that CLAIMS tiles from a global counter (position-major: the tiles every
-// workgroup finished first come first), waits for the tile's flag, and assigns all L levels of its 32
-// items with the level codebooks resident in LDS -- no workgroup barrier in that phase.  Workgroups
-// whose encoder range is one tile shorter start quantizing while the longer ones finish, so the
-// encoder's tile-granularity tail and the separate quantize launch's per-level barriers are gone.
-// Per item the arithmetic is rq_quantize_kernel's (rq.hip: the reference's CPU order, exact ties).
-struct EncQ {
-  const float* cb[GR_MAX_LEVELS];
-  int K[GR_MAX_LEVELS];
-  int row0[GR_MAX_LEVELS];   // first LDS row of each level's image (multiples of 32)
-  int L, rows;               // levels, padded rows in total
-  int64_t* idx;
-  unsigned long long* stamps;   // diagnostics (gr_rq_encode_stamps): per workgroup 8 words, or null
-  gu32* sync;                // [0] claim counter, [1] timeout word, [2..] per-tile flags (zeroed per launch)
-};
-
-constexpr unsigned RQE_SPIN_MAX = 1u << 22;   // ~0.5 s of s_sleep: a lost flag ends as idx -1, not a hang
-
-// Tile of claim c under the encoder's partition (workgroup b owns [b q + min(b, r), ..) with
-// tiles = q G + r): positions 0..q-1 of every workgroup first, then the r workgroups' extra tile.
-__device__ __forceinline__ int claim_tile(int c, int G, int q, int r) {
-  if (c < q * G) {
-    const int b = c % G;
-    return b * q + (b < r ? b : r) + c / G;
-  }
-  const int b = c - q * G;
-  return b * (q + 1) + q;
-}
-
-// Residual of item r of tile t in lane (r, h): features 8j + 2s + h in res[j][s] (zeros past n).
-__device__ __forceinline__ void load_residual(f32x4 (&res)[4], const float* z, int64_t n, int t, int r, int h) {
-  const int64_t item = (int64_t)t * 32 + r;
-  const bool ok = item < n;
-  const float* zr = z + (ok ? item : 0) * 32;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const f32x4 lo = *reinterpret_cast<const f32x4*>(zr + 8 * j);
-    const f32x4 hi = *reinterpret_cast<const f32x4*>(zr + 8 * j + 4);
-    const f32x4 v = h ? f32x4{lo[1], lo[3], hi[1], hi[3]} : f32x4{lo[0], lo[2], hi[0], hi[2]};
-    res[j] = ok ? v : f32x4{0.f, 0.f, 0.f, 0.f};
-  }
-}
-
-// First minima of codes [32 ct0, 32 ct1) of one level for NT item tiles (res[u], lane (r, h)):
-// (best, index) per tile merged over the lane halves, the same value in both halves.  16 running
-// minima per lane and tile, one per accumulator register v (codes 32 ct + (v & 3) + 8 (v >> 2) + 4h,
-// ascending with ct), so the compare / select chains are independent and the stored index is the
-// code tile alone (wave-uniform); merged in code order after the sweep.  The NT chains share each
-// code tile's A fragments, which are read from LDS one code tile ahead.
-template <int NT>
-__device__ __forceinline__ void argmin_codes(const f32x4 (&res)[NT][4], const float (&rn)[NT], const float* cbs,
-                                             const float* cns, int base, int ct0, int ct1, int r, int h,
-                                             float (&bb)[NT], int (&bi)[NT]) {
-#pragma clang fp contract(off)
-  constexpr int EP = 32, HQ = 4;
-  float best[NT][16];
-  int bct[NT][16];
-#pragma unroll
-  for (int u = 0; u < NT; ++u)
-#pragma unroll
-    for (int v = 0; v < 16; ++v) {
-      best[u][v] = __builtin_inff();
-      bct[u][v] = 1 << 20;   // never written: the merged index stays >= K (-> 0 like torch.argmin on inf / NaN rows)
-    }
-  const float* nrow = cns + base + 4 * h;
-  f32x4 an[HQ];
-  if (ct0 < ct1) {
-#pragma unroll
-    for (int j = 0; j < HQ; ++j)
-      an[j] = *reinterpret_cast<const f32x4*>(cbs + cb_off<EP>(base + ct0 * 32 + r, HQ * h + j));
-  }
-  for (int ct = ct0; ct < ct1; ++ct) {
-    f32x4 a[HQ];
-#pragma unroll
-    for (int j = 0; j < HQ; ++j) a[j] = an[j];
-    if (ct + 1 < ct1) {
-#pragma unroll
-      for (int j = 0; j < HQ; ++j)
-        an[j] = *reinterpret_cast<const f32x4*>(cbs + cb_off<EP>(base + (ct + 1) * 32 + r, HQ * h + j));
-    }
-    f32x4 cn[4];
-#pragma unroll
-    for (int g4 = 0; g4 < 4; ++g4) cn[g4] = *reinterpret_cast<const f32x4*>(nrow + ct * 32 + 8 * g4);
-    f32x16 acc[NT];
-#pragma unroll
-    for (int u = 0; u < NT; ++u)
-#pragma unroll
-      for (int v = 0; v < 16; ++v) acc[u][v] = 0.f;
-#pragma unroll
-    for (int j = 0; j < HQ; ++j)
-#pragma unroll
-      for (int s = 0; s < 4; ++s)
-#pragma unroll
-        for (int u = 0; u < NT; ++u) acc[u] = mfma32(a[j][s], res[u][j][s], acc[u]);
-#pragma unroll
-    for (int u = 0; u < NT; ++u)
-#pragma unroll
-      for (int v = 0; v < 16; ++v) {
-        // (|r|^2 + |c|^2) - 2 r.c: 2 r.c is exact, so one fma rounds the same value (vq.py:71-73)
-        const float dd = fmaf(-2.f, acc[u][v], rn[u] + cn[v >> 2][v & 3]);
-        const bool lt = dd < best[u][v];
-        bct[u][v] = lt ? ct : bct[u][v];
-        best[u][v] = lt ? dd : best[u][v];
-      }
-  }
-#pragma unroll
-  for (int u = 0; u < NT; ++u) {
-    bb[u] = best[u][0];
-    bi[u] = bct[u][0] * 32 + 4 * h;
-#pragma unroll
-    for (int v = 1; v < 16; ++v) {
-      float dummy = 0.f;
-      merge_min<false>(bb[u], dummy, bi[u], best[u][v], 0.f, bct[u][v] * 32 + (v & 3) + 8 * (v >> 2) + 4 * h);
-    }
-    float dummy = 0.f;
-    const float ob = __shfl_xor(bb[u], 32);
-    const int oi = __shfl_xor(bi[u], 32);
-    merge_min<false>(bb[u], dummy, bi[u], ob, 0.f, oi);
-  }
-}
-
-#ifndef RQE_TPW
-#define RQE_TPW 2   // item tiles per wave in the quantize phase (a claim = 4 x RQE_TPW tiles)
-#endif
-
-template <int H1, int H2>
-__global__ __launch_bounds__(64 * FWV, 1) void rq_encode_kernel(
-    const float* __restrict__ x, int64_t n, int D0, int csplit, const float* __restrict__ W1,
-    const float* __restrict__ b1, const float* __restrict__ W2, const float* __restrict__ b2,
-    const float* __restrict__ W3, const float* __restrict__ b3, float* __restrict__ z_out,
-    int tiles, EncQ q) {
-  using C = FusedCfg<H1, H2>;
-  extern __shared__ __attribute__((aligned(16))) float sm[];
-  const int G = gridDim.x, tq = tiles / G, tr = tiles % G, bx = blockIdx.x;
-  const int t_begin = bx * tq + (bx < tr ? bx : tr);
-  const int t_end = t_begin + tq + (bx < tr ? 1 : 0);
-  const int tid = threadIdx.x, lane = tid & 63;
-  gu32* flags = q.sync + 2;
-  unsigned long long st0 = 0, st1 = 0, st2 = 0, st3 = 0;
-  unsigned spins_all = 0, groups = 0;
-  if (q.stamps) st0 = __builtin_amdgcn_s_memrealtime();
-  // ------------------------------------------------------------------ encoder phase
-  if (t_begin < t_end) {
-    FusedCtx<H1, H2> cx;
-    cx.x = x; cx.n = n; cx.D0 = D0; cx.NC = D0 / FXC; cx.csplit = csplit; cx.t_end = t_end;
-    cx.W2 = W2; cx.b1 = b1; cx.b2 = b2; cx.W3 = W3; cx.b3 = b3; cx.z_out = z_out; cx.flags = flags;
-    cx.xs = sm;
-    cx.h1s = sm + 2 * C::PI * FXP;
-    cx.h2s = cx.h1s + C::PI * C::P1;
-    cx.w3s = cx.h2s + C::PI * C::P2;
-    for (int f = tid; f < C::E * H2 / 4; f += C::NTH) {
-      const int row = f / (H2 / 4), qq = f % (H2 / 4);
-      *reinterpret_cast<f32x4*>(cx.w3s + row * C::P3 + 4 * qq) = *reinterpret_cast<const f32x4*>(W3 + row * H2 + 4 * qq);
-    }
-    cx.tid = tid; cx.w = tid >> 6; cx.r = lane & 31; cx.h = lane >> 5;
-    cx.w1row = W1 + (int64_t)(cx.w * 32 + cx.r) * D0 + 16 * cx.h;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) cx.awc[j] = *reinterpret_cast<const f32x4*>(cx.w1row + 4 * j);
-    cx.buf = 0;
-    const bool ks = 2 * csplit == cx.NC && ((t_end - t_begin) & 1);
-    cx.gload_x(t_begin, 0, ks && t_end - t_begin == 1);
-    cx.swrite_x(0);
-    __syncthreads();
-    int tb = t_begin;
-    for (; tb + FP <= t_end; tb += FP) rq_fused_pass<FP, H1, H2, true>(cx, tb, ks && tb + FP + 1 == t_end);
-    // claims are position-major, so the tiles before a one-tile last pass are wanted before it
-    if (tb < t_end) {
-      publish_tiles(flags, t_begin, tb, tid);
-      if (q.stamps) st3 = __builtin_amdgcn_s_memrealtime();
-      if (ks) rq_fused_pass<2, H1, H2, true, true>(cx, tb);
-      else rq_fused_pass<1, H1, H2, true>(cx, tb);
-      publish_tiles(flags, tb, t_end, tid);
-    } else {
-      publish_tiles(flags, t_begin, t_end, tid);
-    }
-  }
-
-  // ------------------------------------------------------------------ quantize phase
-  if (q.stamps) st1 = __builtin_amdgcn_s_memrealtime();
-  __syncthreads();   // the encoder's LDS images are no longer read
-  constexpr int EP = 32, HQ = 4;
-  float* cbs = sm;
-  float* cns = sm + q.rows * EP;
-  for (int l = 0; l < q.L; ++l) {   // every level's codebook, rows padded to 32 (zeros, norm +inf)
-    const int K = q.K[l], kp = (K + 31) & ~31, base = q.row0[l];
-    for (int f = tid; f < kp * (EP / 4); f += C::NTH) {
-      const int c = f >> 3, u = f & 7, j = u >> 1, e2 = 2 * (u & 1);
-      const f32x4 v = c < K ? *reinterpret_cast<const f32x4*>(q.cb[l] + (int64_t)c * EP + 4 * u)
-                            : f32x4{0.f, 0.f, 0.f, 0.f};
-      *reinterpret_cast<f32x2*>(cbs + cb_off<EP>(base + c, j) + e2) = f32x2{v[0], v[2]};
-      *reinterpret_cast<f32x2*>(cbs + cb_off<EP>(base + c, HQ + j) + e2) = f32x2{v[1], v[3]};
-    }
-  }
-  __syncthreads();
-  for (int l = 0; l < q.L; ++l) {
-    const int K = q.K[l], kp = (K + 31) & ~31, base = q.row0[l];
-    for (int c = tid; c < kp; c += C::NTH) {
-      float s = __builtin_inff();   // padding rows never win
-      if (c < K) {
-        float v[EP];
-#pragma unroll
-        for (int qq = 0; qq < 2 * HQ; ++qq) {
-          const f32x4 t4 = *reinterpret_cast<const f32x4*>(cbs + cb_off<EP>(base + c, qq));
-#pragma unroll
-          for (int i = 0; i < 4; ++i) v[8 * (qq % HQ) + 2 * i + qq / HQ] = t4[i];
-        }
-        s = aten_rowsq([&](int f) { return v[f]; }, EP);
-      }
-      cns[base + c] = s;
-    }
-  }
-  __syncthreads();
-  // Groups of 4 x TPW tiles per claim: wave w works on the TPW tiles of slot w & 3 (TPW chains
-  // sharing each code tile's fragments) with the other wave of that slot (w ^ 4) splitting each
-  // level's code tiles in halves; the halves' minima meet in LDS after every level (lower distance,
-  // then lower index: the first minimum), and both waves carry the same residuals on.  The claim
-  // for the next group is issued during the last level.
-  constexpr int TPW = RQE_TPW, TG = 4 * TPW;
-  const int r = lane & 31, h = lane >> 5, w = tid >> 6, s4 = w & 3, kh = w >> 2;
-  gu32* counter = q.sync;
-  float* part = cns + q.rows;              // [2 (level parity)][4 slots][TPW][2 halves][32 items][2]
-  constexpr int PSLOT = TPW * 2 * 32 * 2, PLEV = 4 * PSLOT;
-  int* claim_s = reinterpret_cast<int*>(part + 2 * PLEV);
-  if (q.stamps) st2 = __builtin_amdgcn_s_memrealtime();
-  if (tid == 0) *claim_s = (int)__hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __syncthreads();
-  int g = *claim_s;
-#ifdef GR_ENCQ_NOQ   // diagnostic build (scripts/build_variant.sh): the encoder phase alone
-  g = tiles;
-#endif
-  while (TG * g < tiles) {
-    int tt[TPW];
-    bool act[TPW];
-    f32x4 res[TPW][HQ];
-    bool okf = true;
-#pragma unroll
-    for (int u = 0; u < TPW; ++u) {
-      const int c = TG * g + TPW * s4 + u;
-      act[u] = c < tiles;
-      tt[u] = act[u] ? claim_tile(c, G, tq, tr) : 0;
-      if (act[u]) {
-        // consume (Guideline 16, R1): one relaxed poll of the tile's flag, then ONE agent acquire;
-        // this wave reads the tile itself, so its own plain loads follow
-        unsigned spins = 0;
-        while (__hip_atomic_load(flags + tt[u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
-          __builtin_amdgcn_s_sleep(2);
-          ++spins_all;
-          if (++spins > RQE_SPIN_MAX) {   // never seen in a correct run: flag it, do not hang
-            if (lane == 0) __hip_atomic_store(q.sync + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            okf = false;
-            break;
-          }
-        }
-      }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-#pragma unroll
-    for (int u = 0; u < TPW; ++u) load_residual(res[u], z_out, act[u] ? n : 0, tt[u], r, h);
-    const bool any = act[0];   // slot's first tile active <=> any of its tiles is
-    unsigned nxt = 0;
-    for (int l = 0; l < q.L; ++l) {
-      if (l == q.L - 1 && tid == 0)
-        nxt = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const int K = q.K[l], base = q.row0[l], nct = (K + 31) >> 5, half = (nct + 1) >> 1;
-      float* pl = part + (l & 1) * PLEV + s4 * PSLOT;
-      if (any) {
-        float rn[TPW], bb[TPW];
-        int bi[TPW];
-#pragma unroll
-        for (int u = 0; u < TPW; ++u) rn[u] = rn_exact<EP>(res[u], EP, h);
-        argmin_codes<TPW>(res, rn, cbs, cns, base, kh ? half : 0, kh ? nct : half, r, h, bb, bi);
-        if (h == 0) {
-#pragma unroll
-          for (int u = 0; u < TPW; ++u) {
-            pl[((u * 2 + kh) * 32 + r) * 2] = bb[u];
-            pl[((u * 2 + kh) * 32 + r) * 2 + 1] = __int_as_float(bi[u]);
-          }
-        }
-      }
-      __syncthreads();
-      if (any) {
-#pragma unroll
-        for (int u = 0; u < TPW; ++u) {
-          const float* pu = pl + u * (2 * 32 * 2);
-          float b0 = pu[r * 2], dummy = 0.f;
-          int i0 = __float_as_int(pu[r * 2 + 1]);
-          merge_min<false>(b0, dummy, i0, pu[(32 + r) * 2], 0.f, __float_as_int(pu[(32 + r) * 2 + 1]));
-          const int b = (i0 >= K || i0 < 0) ? 0 : i0;   // no finite distance: torch.argmin -> 0
-          const int64_t item = (int64_t)tt[u] * 32 + r;
-          if (act[u] && kh == 0 && h == 0 && item < n) q.idx[item * q.L + l] = (okf ? (int64_t)b : -1);
-          f32x4 cw[HQ];
-#pragma unroll
-          for (int j = 0; j < HQ; ++j) cw[j] = *reinterpret_cast<const f32x4*>(cbs + cb_off<EP>(base + b, HQ * h + j));
-#pragma unroll
-          for (int j = 0; j < HQ; ++j)
-#pragma unroll
-            for (int s = 0; s < 4; ++s) {
-              const float xq = res[u][j][s] + (cw[j][s] - res[u][j][s]);   // vq.py:95
-              res[u][j][s] = res[u][j][s] - xq;                            // rq.py:47
-            }
-        }
-      }
-    }
-    if (tid == 0) *claim_s = (int)nxt;
-    __syncthreads();
-    g = *claim_s;
-    __syncthreads();   // every wave has read the claim before thread 0 may overwrite it
-    ++groups;
-  }
-  if (q.stamps && tid == 0) {
-    unsigned long long* o = q.stamps + 8 * blockIdx.x;
-    o[0] = st0; o[1] = st1; o[2] = st2; o[3] = __builtin_amdgcn_s_memrealtime();
-    o[4] = groups; o[5] = spins_all; o[6] = (unsigned long long)(t_end - t_begin); o[7] = st3;
-  }
-}
-
-// LDS floats of the fused encode's quantize phase for these levels (0: does not fit).
-static int rqe_layout(int32_t L, const int32_t* K, EncQ* q) {
-  int rows = 0;
-  for (int l = 0; l < L; ++l) {
-    if (q) q->row0[l] = rows;
-    rows += (K[l] + 31) & ~31;
-  }
-  if (q) q->rows = rows;
-  return rows * 33 + 2 * 4 * RQE_TPW * 2 * 32 * 2 + 4;   // codebooks, norms, the halves' minima, the claim word
 }
 
 // Packed weight images of the three layers (one launch): W1 and W2 for the 32x32x2 chains (within
@@ -881,65 +525,3 @@ int gr_rq_encoder_fused_launch(const float* x, int64_t n, int32_t n_linear, cons
                      dims[0], csplit, wp[0], biases[0], wp[1], biases[1], wp[2], biases[2], z_out, (int)tiles);
   return check_launch("rq fused encoder");
 }
-
-static unsigned long long* g_rqe_stamps = nullptr;
-
-// One-launch get_indices at the fused encoder shape (rq_encode_kernel).  `sync`: workspace of
-// gr_rq_encode_sync_words(n) 32-bit words, zeroed here by a fill kernel (graph-safe).  Returns
-// GR_ERR_UNSUPPORTED (message untouched) off that shape or when the level codebooks do not fit.
-int gr_rq_encode_fused_launch(const float* x, int64_t n, int32_t n_linear, const int32_t* dims,
-                              const float* const* weights, const float* const* biases, float* pack,
-                              bool pack_is_ready, int32_t L, const int32_t* K, const float* const* cbs,
-                              int64_t* idx, float* z, uint32_t* sync, hipStream_t st) {
-  using namespace gr;
-  using Cfg = FusedCfg<256, 128>;
-  if (gr_rq_fused_pack_floats(n_linear, dims) == 0 || dims[0] % FXC != 0 || !biases) return GR_ERR_UNSUPPORTED;
-  const int kb = mkl_kblock(dims[0]);
-  if (kb < 0 || (kb < dims[0] && kb % FXC != 0)) return GR_ERR_UNSUPPORTED;
-  for (int i = 0; i < 3; ++i)
-    if (!weights[i] || !biases[i] || !aligned16(biases[i])) return GR_ERR_UNSUPPORTED;
-  if (!aligned16(x) || !aligned16(z) || !pack || !aligned16(pack) || !sync) return GR_ERR_UNSUPPORTED;
-  if (L < 1 || L > GR_MAX_LEVELS) return GR_ERR_UNSUPPORTED;
-  EncQ q{};
-  if (rqe_layout(L, K, &q) > Cfg::LDS) return GR_ERR_UNSUPPORTED;
-  for (int l = 0; l < L; ++l) {
-    if (!cbs[l] || !aligned16(cbs[l]) || K[l] < 1) return GR_ERR_UNSUPPORTED;
-    q.cb[l] = cbs[l];
-    q.K[l] = K[l];
-  }
-  q.L = L;
-  q.idx = idx;
-  q.stamps = g_rqe_stamps;
-  q.sync = (gu32*)sync;
-  if (n == 0) return GR_OK;
-  const int64_t tiles = (n + FT - 1) / FT;
-  if (tiles > (1LL << 30)) return GR_ERR_UNSUPPORTED;
-  float* wp[3] = {pack, pack + (size_t)dims[0] * 256, pack + (size_t)dims[0] * 256 + 256 * 128};
-  if (!pack_is_ready) {
-    const int rc = gr_rq_encoder_pack_launch(n_linear, dims, weights, pack, st);
-    if (rc) return rc;
-  }
-  int rc = gr_fill32_launch(sync, 0u, tiles + 2, st);
-  if (rc) return rc;
-  static int cus = 0;
-  if (!cus) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) dev = 0;
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
-      cus = 256;
-  }
-  const int64_t grid = tiles < cus ? tiles : cus;
-  const int csplit = kb < dims[0] ? kb / FXC : dims[0] / FXC;
-  static bool lds_ok = hipFuncSetAttribute(reinterpret_cast<const void*>(rq_encode_kernel<256, 128>),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize,
-                                           (int)(Cfg::LDS * sizeof(float))) == hipSuccess;
-  if (!lds_ok) return fail(GR_ERR_HIP, "rq fused encode: cannot raise the LDS limit");
-  hipLaunchKernelGGL((rq_encode_kernel<256, 128>), dim3((unsigned)grid), dim3(64 * FWV), Cfg::LDS * sizeof(float), st,
-                     x, n, dims[0], csplit, wp[0], biases[0], wp[1], biases[1], wp[2], biases[2], z, (int)tiles, q);
-  return check_launch("rq fused encode");
-}
-
-// Diagnostics: per-workgroup timestamps of the next fused-encode launches (s_memrealtime, 100 MHz):
-// [start, encoder phase done, codebooks staged, end, groups quantized, flag polls, encoder tiles, 0]
-// x gridDim words; null turns them off.  Not part of the product path.
-extern "C" void gr_rq_encode_stamps(unsigned long long* stamps) { g_rqe_stamps = stamps; }

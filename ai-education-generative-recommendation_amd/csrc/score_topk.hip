@@ -350,7 +350,7 @@ __global__ __launch_bounds__(256, 2) void topk_select_kernel(const float* __rest
   __shared__ int nlist;
   __shared__ float mk_s;
   __shared__ unsigned long long csum;
-  const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, hh = lane >> 5, w = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, w = tid >> 6;
   const int64_t u = blockIdx.x;
   const float* tm = tmax + u * T;
   if (tid == 0) {

@@ -65,10 +65,6 @@ const char* gr_last_error(void);
  *                   1: always direct.  Identical results.
  *   "topk_sample"   1 (default): gr_score_topk_f32 prunes with a threshold from a strided sample
  *                   pass when the catalog is long enough; 0: one pass.  Identical results.
- *   "rq_encq"       1 (default): at the fused encoder shape (in -> 256 -> 128 -> 32, level codebooks
- *                   that fit one CU's LDS) gr_rq_encode_f32 without best/gap outputs is ONE launch:
- *                   the encoder hands finished z tiles to waves that claim and quantize them; 0:
- *                   encoder and quantize kernels back to back.  Identical IDs.
  * gr_set_option returns GR_ERR_ARG for an unknown name/value; gr_get_option returns -1 for an
  * unknown name. */
 int gr_set_option(const char* name, int64_t value);
@@ -145,12 +141,6 @@ int gr_rq_encode_packed_f32(const float* x, int64_t n, int32_t n_linear, const i
                             const float* const* codebooks, int64_t* idx_out, float* best_out,
                             float* gap_out, float* z_out, void* workspace, size_t workspace_bytes,
                             void* stream);
-
-/* Diagnostics (not on the product path): per-workgroup timestamps of the following one-launch
- * encodes (rq_encq), 8 uint64 words per workgroup (s_memrealtime, 100 MHz): start, encoder phase
- * done, level codebooks staged, end, 4-tile groups quantized, flag polls, encoder tiles, start of the odd last pass (0: none).
- * stamps: device buffer of >= 8 * (CU count) words, or NULL (off). */
-void gr_rq_encode_stamps(unsigned long long* stamps);
 
 /* MLPLayers.forward in eval mode (RQ-VAE/models/layers.py:42-43): z_out[n, dims[n_linear]] = the
  * encoder output alone (ReLU after every Linear but the last).  Same kernels as gr_rq_encode_f32. */

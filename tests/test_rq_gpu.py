@@ -18,17 +18,14 @@ RQ = ["rq_csv_3x8", "rq_syn_3x256", "rq_syn_4x1024", "rq_syn_randinit_3x256", "r
       "rq_calib_wide_3x256"]
 
 
-@pytest.fixture(params=[2, 1, 0], ids=["encode1", "fused", "layerwise"])
+@pytest.fixture(params=[1, 0], ids=["fused", "layerwise"])
 def rq_path(request):
-    """Run a test through the one-launch encode (fused encoder + claimed quantize phase, the
-    default), the fused encoder followed by the quantize kernel, and the layer-wise path (exact
-    gr_linear + gr_rq_quantize): all must be bitwise the reference."""
+    """Run a test through the fused persistent kernel and through the layer-wise path
+    (exact gr_linear + gr_rq_quantize): both must be bitwise the reference."""
     from gr_amd import _lib
-    _lib.set_option("rq_fused", 1 if request.param else 0)
-    _lib.set_option("rq_encq", 1 if request.param == 2 else 0)
+    _lib.set_option("rq_fused", request.param)
     yield request.param
     _lib.set_option("rq_fused", 1)
-    _lib.set_option("rq_encq", 1)
 
 
 def build_model(meta, sd, dev, bn=False):
@@ -42,7 +39,7 @@ def build_model(meta, sd, dev, bn=False):
 
 
 def _path(p):
-    return {2: "encode1", 1: "fused", 0: "layerwise"}[p]
+    return "fused" if p else "layerwise"
 
 
 @pytest.mark.parametrize("name", RQ)
@@ -172,32 +169,24 @@ def test_full_population_c2_bench_workload(dev, rq_path, parity_log):
     assert diff.sum() == 0, f"{diff.sum()} of {n} rows differ: {np.nonzero(diff)[0][:10]}"
 
 
-@pytest.mark.parametrize("n", [1, 31, 33, 255 * 32 + 7, 256 * 32, 256 * 33 + 1, 409_600])
-def test_one_launch_encode_equals_two_kernels(n, dev, parity_log):
-    """The one-launch encode (rq_encq=1: tiles handed from the encoder phase to waves that claim
-    them) against the encoder + quantize kernels, bitwise, at batch sizes around the partition's
-    edges (fewer tiles than CUs, one extra tile, q tiles each plus a remainder); 409,600 rows (the
-    size at which round 2's 16-wave quantizer diverged) also against the exact-order oracle."""
-    from gr_amd import _lib, synth
+@pytest.mark.parametrize("n", [1, 31, 33, 64, 255 * 32 + 7, 256 * 32, 256 * 33 + 1, 256 * 34 + 5])
+def test_partition_edges_vs_oracle(n, dev, parity_log):
+    """Batch sizes around the fused encoder's tile partition: fewer tiles than CUs (every workgroup
+    runs ONE k-split pass -- the tile's two MKL k blocks as its two chains), an odd last tile after
+    full passes, exact multiples; every row against the exact-order oracle, and back-to-back calls
+    equal."""
+    from gr_amd import synth
     m = synth.rqvae_model(3, 256, dev)
     x = synth.items(n, 77, dev)
-    try:
-        _lib.set_option("rq_encq", 0)
-        two = m.get_indices(x)
-        _lib.set_option("rq_encq", 1)
-        one = m.get_indices(x)
-        again = [m.get_indices(x) for _ in range(8)]   # back to back, no host sync in between
-    finally:
-        _lib.set_option("rq_encq", 1)
-    assert torch.equal(one, two)
+    one = m.get_indices(x)
+    again = [m.get_indices(x) for _ in range(4)]   # back to back, no host sync in between
     assert all(torch.equal(one, a) for a in again)
-    if n == 409_600:
-        ws, bs, cbs = _weights(m)
-        ref = rq_exact.encode(x.cpu().numpy(), ws, bs, cbs)
-        diff = (one.cpu().numpy() != ref).any(1)
-        parity_log(kind="rq_ids_full_population", config="C2 model, 409,600 items", path="encode1", rows=n,
-                   rows_differ=int(diff.sum()))
-        assert diff.sum() == 0
+    ws, bs, cbs = _weights(m)
+    ref = rq_exact.encode(x.cpu().numpy(), ws, bs, cbs)
+    diff = (one.cpu().numpy() != ref).any(1)
+    parity_log(kind="rq_ids_vs_oracle", shape=f"C2 model, n {n} (partition edges)", path="fused", rows=n,
+               rows_differ=int(diff.sum()))
+    assert diff.sum() == 0, f"{diff.sum()} of {n} rows differ"
 
 
 def test_full_population_c4_contiguous(dev, parity_log):
