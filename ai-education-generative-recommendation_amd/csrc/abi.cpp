@@ -58,6 +58,10 @@ static std::atomic<int64_t> g_topk_impl{1};
 static std::atomic<int64_t> g_rt_w8{1};
 // lin_w8 (1 (default): gr_linear_f32's 128x128 / 128x64 tiles run 8 waves per workgroup; 0: 4)
 static std::atomic<int64_t> g_lin_w8{1};
+// lin_wres (1 (default): gr_linear_f32 with k = 128, n % 128 == 0, no residual and m >= 64 x 256
+// runs the persistent kernel that keeps 32-column slices of w resident in registers; 0: the tiled
+// kernel).  Bitwise the same results; A/B timing.
+static std::atomic<int64_t> g_lin_wres{1};
 
 int64_t option(const char* name) {
   if (!strcmp(name, "rq_fused")) return g_rq_fused.load();
@@ -77,6 +81,7 @@ int64_t option(const char* name) {
   if (!strcmp(name, "topk_impl")) return g_topk_impl.load();
   if (!strcmp(name, "rt_w8")) return g_rt_w8.load();
   if (!strcmp(name, "lin_w8")) return g_lin_w8.load();
+  if (!strcmp(name, "lin_wres")) return g_lin_wres.load();
   return -1;
 }
 }  // namespace gr
@@ -101,6 +106,7 @@ extern "C" int gr_set_option(const char* name, int64_t value) {
   if (!strcmp(name, "topk_impl") && (value == 0 || value == 1)) { gr::g_topk_impl = value; return GR_OK; }
   if (!strcmp(name, "rt_w8") && (value == 0 || value == 1)) { gr::g_rt_w8 = value; return GR_OK; }
   if (!strcmp(name, "lin_w8") && (value == 0 || value == 1)) { gr::g_lin_w8 = value; return GR_OK; }
+  if (!strcmp(name, "lin_wres") && (value == 0 || value == 1)) { gr::g_lin_wres = value; return GR_OK; }
   return gr::fail(GR_ERR_ARG, std::string("gr_set_option: unknown option or value: ") + name);
 }
 

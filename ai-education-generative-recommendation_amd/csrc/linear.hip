@@ -198,6 +198,95 @@ __global__ __launch_bounds__(NT, NT / 128) void linear_f32_kernel(
   }
 }
 
+// ---- K = 128, n % 128 == 0, no residual (the C5 block-0 in-projection [B n, 128] x [384, 128]^T):
+// persistent workgroups, each owning one 128-column slice of w and a contiguous range of 96-row
+// tiles of x streamed through a double-buffered LDS image.  12 waves (3 per SIMD): wave w owns
+// output rows 32 (w >> 2).. and columns 32 (w & 3).. of every tile and keeps its 32 columns of w in
+// registers for the whole range (64 floats per lane, loaded once: the tiled kernel above re-reads
+// a 64 KB w tile for every 128 x 128 output tile with only 4 k slabs to amortise it over).  One
+// 64-MFMA chain per tile in linear_f32_kernel's k order (step s of slice kc feeds k = 8kc + s, then
+// 8kc + 4 + s), bias added last -- bitwise the tiled kernel's result.
+constexpr int WR_K = 128, WR_P = WR_K + 4, WR_RT = 3, WR_BM = 32 * WR_RT, WR_BN = 128, WR_NT = 256 * WR_RT;
+
+template <int ACT>
+__global__ __launch_bounds__(WR_NT, 1) void linear_wres_kernel(const float* __restrict__ x, const float* __restrict__ w,
+                                                               const float* __restrict__ bias, float* __restrict__ y,
+                                                               int64_t M, int N, int64_t ldy, int groups) {
+#pragma clang fp contract(off)
+  __shared__ __attribute__((aligned(16))) float xs[2][WR_BM * WR_P];
+  constexpr int XV = WR_BM * WR_K / 4 / WR_NT;   // float4 per thread per x tile
+  const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, h = lane >> 5;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6), rt = wv >> 2, ct = wv & 3;
+  const int cg = blockIdx.x % groups, j = blockIdx.x / groups, per = gridDim.x / groups;
+  const int n0 = cg * WR_BN;
+  const int64_t tiles = (M + WR_BM - 1) / WR_BM;
+  const int64_t t0 = (int64_t)j * tiles / per, t1 = (int64_t)(j + 1) * tiles / per;
+  if (t0 >= t1) return;
+  const int col = n0 + 32 * ct + r;
+  f32x4 wf[WR_K / 8];   // this lane's w fragments: w[col][8kc + 4h .. +3]
+#pragma unroll
+  for (int kc = 0; kc < WR_K / 8; ++kc)
+    wf[kc] = *reinterpret_cast<const f32x4*>(w + (int64_t)col * WR_K + 8 * kc + 4 * h);
+  const float bv = bias ? bias[col] : 0.f;
+  f32x4 xr[XV];
+  // addresses: a uniform 64-bit tile base plus 32-bit per-lane offsets (96 x K and 96 x ldy < 2^31)
+  auto gload = [&](int64_t t) {
+    const float* xt = x + t * WR_BM * WR_K;
+    const int last = (int)(M - 1 - t * WR_BM);   // rows past it are clamped: loaded, never stored
+#pragma unroll
+    for (int i = 0; i < XV; ++i) {
+      const int f = tid + WR_NT * i, row = f >> 5, c = (f & 31) * 4;
+      xr[i] = *reinterpret_cast<const f32x4*>(xt + (row < last ? row : last) * WR_K + c);
+    }
+  };
+  auto swrite = [&](int b) {
+#pragma unroll
+    for (int i = 0; i < XV; ++i) {
+      const int f = tid + WR_NT * i, row = f >> 5, c = (f & 31) * 4;
+      *reinterpret_cast<f32x4*>(&xs[b][row * WR_P + c]) = xr[i];
+    }
+  };
+  gload(t0);
+  swrite(0);
+  __syncthreads();
+  const int ld = (int)ldy;
+  const int lo = (32 * rt + 4 * h) * ld + col;
+  int b = 0;
+  for (int64_t t = t0; t < t1; ++t) {
+    if (t + 1 < t1) gload(t + 1);
+    const float* xrow = &xs[b][(32 * rt + r) * WR_P + 4 * h];
+    f32x16 acc;
+#pragma unroll
+    for (int v = 0; v < 16; ++v) acc[v] = 0.f;
+#pragma unroll
+    for (int kc = 0; kc < WR_K / 8; ++kc) {
+      const f32x4 a = *reinterpret_cast<const f32x4*>(xrow + 8 * kc);
+#pragma unroll
+      for (int s2 = 0; s2 < 4; ++s2) acc = mfma32(a[s2], wf[kc][s2], acc);
+    }
+    float* yt = y + t * WR_BM * ldy;
+    float o[16];
+#pragma unroll
+    for (int v = 0; v < 16; ++v) {
+      o[v] = acc[v];
+      if (bias) o[v] = o[v] + bv;
+      if (ACT == GR_ACT_RELU) o[v] = (o[v] < 0.f) ? 0.f : o[v];
+    }
+    if (t * WR_BM + WR_BM <= M) {   // every tile but a ragged last one: no per-row test
+#pragma unroll
+      for (int v = 0; v < 16; ++v) yt[lo + ((v & 3) + 8 * (v >> 2)) * ld] = o[v];
+    } else {
+      const int rows = (int)(M - t * WR_BM) - 32 * rt - 4 * h;
+#pragma unroll
+      for (int v = 0; v < 16; ++v)
+        if ((v & 3) + 8 * (v >> 2) < rows) yt[lo + ((v & 3) + 8 * (v >> 2)) * ld] = o[v];
+    }
+    if (t + 1 < t1) swrite(b ^ 1);
+    __syncthreads();
+    b ^= 1;
+  }
+}
+
 template <int BM, int BN, int WM, int WN, int NT = 256, bool EXACT = false>
 static int launch_tile(const float* x, int64_t m, int k, const float* w, int n, const float* bias,
                        const float* residual, int64_t ldr, int act, float* y, int64_t ldy,
@@ -251,6 +340,22 @@ int gr_linear_launch(const float* x, int64_t m, int32_t k, const float* w, int32
   if (ldy < n || (residual && ldr < n)) return fail(GR_ERR_ARG, "gr_linear_f32: bad row stride");
   if (act < GR_ACT_NONE || act > GR_ACT_LEAKYRELU) return fail(GR_ERR_ARG, "gr_linear_f32: bad act");
   if (act > GR_ACT_RELU && residual) return fail(GR_ERR_UNSUPPORTED, "gr_linear_f32: this act takes no residual");
+  // K = 128, n % 128 == 0, long m: w slices resident in registers (linear_wres_kernel; option lin_wres)
+  if (k == WR_K && n % WR_BN == 0 && !residual && (act == GR_ACT_NONE || act == GR_ACT_RELU) &&
+      m >= (int64_t)WR_BM * 256 && ldy * WR_BM < (1LL << 31) && option("lin_wres") != 0) {
+    static int cus = 0;
+    if (!cus) {
+      int dev = 0;
+      if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+      if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
+        cus = 256;
+    }
+    const int groups = n / WR_BN;
+    const int per = cus / groups > 0 ? cus / groups : 1;   // one workgroup per CU
+    auto kern = act == GR_ACT_RELU ? linear_wres_kernel<GR_ACT_RELU> : linear_wres_kernel<GR_ACT_NONE>;
+    hipLaunchKernelGGL(kern, dim3((unsigned)(groups * per)), dim3(WR_NT), 0, stream, x, w, bias, y, m, n, ldy, groups);
+    return check_launch("gr_linear_f32 (resident w)");
+  }
   // 8 waves per 128-row tile (4 per SIMD at two workgroups per CU; option lin_w8, the default):
   // C5 block-0 in-projection 137 -> 124 us, bitwise the same chain
   const bool w8 = option("lin_w8") != 0;

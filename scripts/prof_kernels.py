@@ -15,7 +15,13 @@ from gr_amd import synth  # noqa: E402
 ap = argparse.ArgumentParser()
 ap.add_argument("--what", default="c5fwd,c2")
 ap.add_argument("--calls", type=int, default=5)
+ap.add_argument("--opt", default="", help="gr_set_option settings, e.g. lin_wres=0,attn_lazy=1")
 a = ap.parse_args()
+if a.opt:
+    from gr_amd import _lib
+    for kv in a.opt.split(","):
+        k, v = kv.split("=")
+        _lib.set_option(k, int(v))
 dev = torch.device("cuda:0")
 what = a.what.split(",")
 if "c5fwd" in what:

@@ -169,6 +169,25 @@ def test_linear_vs_fp64(m_, k, n, act, res, dev):
     assert ((y - ref).abs() <= bound).all()
 
 
+@pytest.mark.parametrize("m_,n,act", [(102_400, 384, "none"), (64 * 256 + 37, 128, "relu"), (64 * 300 - 1, 256, "none")])
+def test_linear_resident_w_equals_tiled(m_, n, act, dev):
+    """k = 128, n % 128 == 0 (the C5 block-0 in-projection shape): the persistent kernel with w
+    slices resident in LDS (option lin_wres) is bitwise the tiled kernel, ragged m included."""
+    from gr_amd import _lib, ops
+    g = torch.Generator(device=dev).manual_seed(m_ + n)
+    x = torch.randn(m_, 128, generator=g, device=dev)
+    w = torch.randn(n, 128, generator=g, device=dev) * 0.1
+    b = torch.randn(n, generator=g, device=dev)
+    try:
+        _lib.set_option("lin_wres", 0)
+        tiled = ops.linear(x, w, b, act=act)
+        _lib.set_option("lin_wres", 1)
+        res = ops.linear(x, w, b, act=act)
+    finally:
+        _lib.set_option("lin_wres", 1)
+    assert torch.equal(tiled, res)
+
+
 def test_score_matches_linear_and_rank_consistency(dev):
     """Fused-rank hard part 3: every logit sees the same fp32 fma chain, so the target's score
     recomputed on any tile equals its entry in the logits (strict '>' never counts the target)."""
