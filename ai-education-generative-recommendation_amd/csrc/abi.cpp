@@ -62,6 +62,10 @@ static std::atomic<int64_t> g_lin_w8{1};
 // runs the persistent kernel that keeps 32-column slices of w resident in registers; 0: the tiled
 // kernel).  Bitwise the same results; A/B timing.
 static std::atomic<int64_t> g_lin_wres{1};
+// rq_pieces (1 (default): the fused encoder's tiles past q x grid run as feature-half pieces on
+// twice as many workgroups plus a layers-2-3 kernel; 0: a one-tile pass on r workgroups).  Bitwise
+// the same z; A/B timing.
+static std::atomic<int64_t> g_rq_pieces{1};
 
 int64_t option(const char* name) {
   if (!strcmp(name, "rq_fused")) return g_rq_fused.load();
@@ -82,6 +86,7 @@ int64_t option(const char* name) {
   if (!strcmp(name, "rt_w8")) return g_rt_w8.load();
   if (!strcmp(name, "lin_w8")) return g_lin_w8.load();
   if (!strcmp(name, "lin_wres")) return g_lin_wres.load();
+  if (!strcmp(name, "rq_pieces")) return g_rq_pieces.load();
   return -1;
 }
 }  // namespace gr
@@ -107,6 +112,7 @@ extern "C" int gr_set_option(const char* name, int64_t value) {
   if (!strcmp(name, "rt_w8") && (value == 0 || value == 1)) { gr::g_rt_w8 = value; return GR_OK; }
   if (!strcmp(name, "lin_w8") && (value == 0 || value == 1)) { gr::g_lin_w8 = value; return GR_OK; }
   if (!strcmp(name, "lin_wres") && (value == 0 || value == 1)) { gr::g_lin_wres = value; return GR_OK; }
+  if (!strcmp(name, "rq_pieces") && (value == 0 || value == 1)) { gr::g_rq_pieces = value; return GR_OK; }
   return gr::fail(GR_ERR_ARG, std::string("gr_set_option: unknown option or value: ") + name);
 }
 

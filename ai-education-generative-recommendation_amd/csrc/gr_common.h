@@ -133,7 +133,7 @@ __device__ __forceinline__ f32x4 mfma16(float a, float b, f32x4 c) {
 // Internal launchers shared between translation units (all enqueue on `stream`, no sync).
 int gr_rq_encoder_fused_launch(const float* x, int64_t n, int32_t n_linear, const int32_t* dims,
                                const float* const* weights, const float* const* biases,
-                               float* z_out, float* pack, hipStream_t st, bool pack_is_ready);
+                               float* z_out, float* pack, hipStream_t st, bool pack_is_ready, float* scratch);
 int gr_rq_encoder_pack_launch(int32_t n_linear, const int32_t* dims, const float* const* weights, float* pack,
                               hipStream_t st);
 size_t gr_rq_fused_pack_floats(int32_t n_linear, const int32_t* dims);

@@ -407,7 +407,7 @@ static int mlp_exact(const float* x, int64_t n, int32_t n_linear, const int32_t*
   if (!bn_mean && act == GR_ACT_RELU && option("rq_fused") == 1) {
     const int rc = gr_rq_encoder_fused_launch(x, n, n_linear, dims, weights, biases, z_out,
                                               packed ? const_cast<float*>(packed) : reinterpret_cast<float*>(ws + 2 * ab),
-                                              st, packed != nullptr);
+                                              st, packed != nullptr, buf[0]);
     if (rc != GR_ERR_UNSUPPORTED) return rc;
     clear_error();
   }

@@ -107,24 +107,130 @@ __device__ __forceinline__ void store_h_packed(float* row, int g4, int h, const 
   *reinterpret_cast<f32x2*>(row + 16 + 4 * g4 + 2 * h) = f32x2{o[1], o[3]};
 }
 
+// Layers 2 and 3 of NR item tiles whose relu(h1) sits packed in cx.h1s: z = W3 . relu(W2 . h1 + b2)
+// + b3 for tiles tb .. tb + NR - 1, written to cx.z_out.
+template <int NR, int H1, int H2>
+__device__ __forceinline__ void rq_l23(FusedCtx<H1, H2>& cx, int tb) {
+#pragma clang fp contract(off)
+  using C = FusedCfg<H1, H2>;
+  constexpr int E = C::E, P1 = C::P1, P2 = C::P2;
+  const int w = cx.w, r = cx.r, h = cx.h;
+  // ------------------------------------------------------------------ L2: W2 . h1^T
+  // waves 0-3: wave w, features [32w, 32w + 32) for all NR item tiles (NR accumulator chains per
+  // wave); waves 4-7 skip L2 (splitting it into one chain per wave over all 8 measured 483 vs 462
+  // us per C2 call, profiles/r02_ab_quant_ablation.txt)
+  if (w < 4) {
+    f32x16 acc2[NR];
+#pragma unroll
+    for (int it = 0; it < NR; ++it)
+#pragma unroll
+      for (int v = 0; v < 16; ++v) acc2[it][v] = 0.f;
+    const float* hb = cx.h1s + r * P1 + 16 * h;
+    const float* w2row = cx.W2 + (int64_t)(w * 32 + r) * H1 + 16 * h;
+    f32x4 aw2[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) aw2[j] = *reinterpret_cast<const f32x4*>(w2row + 4 * j);
+#pragma unroll 1
+    for (int g = 0; g < H1 / 32; ++g) {
+      const int gn = (g + 1 < H1 / 32) ? g + 1 : g;
+      f32x4 awn[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) awn[j] = *reinterpret_cast<const f32x4*>(w2row + gn * 32 + 4 * j);
+      f32x4 bx[NR][4];
+#pragma unroll
+      for (int it = 0; it < NR; ++it)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) bx[it][j] = *reinterpret_cast<const f32x4*>(hb + it * FT * P1 + g * 32 + 4 * j);
+#pragma unroll
+      for (int it = 0; it < NR; ++it)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int s = 0; s < 4; ++s) acc2[it] = mfma32(aw2[j][s], bx[it][j][s], acc2[it]);
+      // same interleave as L1: item tile 0's h1 fragments first, then one load per MFMA
+      __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+      }
+#pragma unroll
+      for (int i = 0; i < 4 * (NR - 1); ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, 16 * NR - 4 - 4 * (NR - 1), 0);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) aw2[j] = awn[j];
+    }
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      const f32x4 bb = *reinterpret_cast<const f32x4*>(cx.b2 + w * 32 + 8 * g4 + 4 * h);
+#pragma unroll
+      for (int it = 0; it < NR; ++it) {
+        f32x4 o;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float u = bb[i] + acc2[it][4 * g4 + i];
+          o[i] = u < 0.f ? 0.f : u;
+        }
+        // L3 layout: within each 16-feature block, feature 4t + g at 4g + t (a lane of k group g
+        // reads four consecutive 16x16x4 steps as one float4)
+        float* row = cx.h2s + (it * FT + r) * P2 + w * 32 + 16 * (g4 >> 1);
+        const int t = (2 * g4 + h) & 3;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) row[4 * i + t] = o[i];
+      }
+    }
+  }
+  __syncthreads();
+
+  // ------------------------------------------------------------------ L3: W3 . h2^T
+  // 16x16x4 tiles (16 outputs x 16 items), one per wave: item tile w >> 2, item half (w >> 1) & 1,
+  // output half w & 1; one k-ordered chain over k = 0..127 (32 MFMAs), z = b3 + chain, to HBM.
+  // W3 arrives packed for this form: feature 16b + 4t + g of a row at 16b + 4g + t.
+  if (w < 4 * NR) {
+    const int it = w >> 2, ih = (w >> 1) & 1, oh = w & 1;
+    const int lane = cx.tid & 63, j = lane & 15, g = lane >> 4;
+    f32x4 acc3 = {0.f, 0.f, 0.f, 0.f};
+    const float* hb = cx.h2s + (it * FT + 16 * ih + j) * P2 + 4 * g;
+    const float* w3row = cx.w3s + (16 * oh + j) * C::P3 + 4 * g;   // LDS: rows 4 banks apart
+#pragma unroll
+    for (int b = 0; b < H2 / 16; ++b) {
+      const f32x4 aw = *reinterpret_cast<const f32x4*>(w3row + 16 * b);
+      const f32x4 bx = *reinterpret_cast<const f32x4*>(hb + 16 * b);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) acc3 = mfma16(aw[t], bx[t], acc3);
+    }
+    const int64_t item = (int64_t)(tb + it) * FT + 16 * ih + j;
+    if (item < cx.n) {
+      const f32x4 bb = *reinterpret_cast<const f32x4*>(cx.b3 + 16 * oh + 4 * g);
+      f32x4 o;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) o[i] = bb[i] + acc3[i];
+      *reinterpret_cast<f32x4*>(cx.z_out + item * E + 16 * oh + 4 * g) = o;
+    }
+  }
+}
+
 // One pass over NP (compile-time) item tiles starting at tile tb.  No runtime branch depends on
 // the number of tiles, so the accumulators stay in AGPRs across the MFMA loops.
 // KS (NP = 2): ONE item tile whose two MKL k blocks run as the pass's two chains -- image rows
 // [0, FT) hold its k chunk c, rows [FT, 2 FT) chunk c + NC/2, with a second W1 fragment stream --
 // so a workgroup's odd last tile runs half the chunk iterations at two chains per wave instead of a
 // one-chain pass over all of them; y = (b1 + block 0) + block 1 as in every other pass.
-// next_ks: the pass after this one is a k-split pass (its first x chunk is staged in that layout).
+// next_tb / next_ks: the first tile of the pass after this one (-1: none) and whether that pass
+// stages its x image in the k-split layout (a k-split pass or a leftover-tile piece).
 template <int NP, int H1, int H2, bool KS = false>
-__device__ __forceinline__ void rq_fused_pass(FusedCtx<H1, H2>& cx, int tb, bool next_ks = false) {
+__device__ __forceinline__ void rq_fused_pass(FusedCtx<H1, H2>& cx, int tb, int next_tb, bool next_ks) {
 #pragma clang fp contract(off)
   using C = FusedCfg<H1, H2>;
-  constexpr int E = C::E, P1 = C::P1, P2 = C::P2, PI = C::PI;
+  constexpr int P1 = C::P1, PI = C::PI;
   static_assert(!KS || NP == 2, "k-split pass: two chains");
   constexpr int NR = KS ? 1 : NP;        // item tiles of the pass (L2, L3, z)
   const int w = cx.w, r = cx.r, h = cx.h;
   const int NC = KS ? cx.NC / 2 : cx.NC;   // chunk iterations
   const int kbo = cx.csplit * FXC;         // first k of the second MKL block
-  const int next_tb = tb + NR;
   // The later phases' operands (biases, W2/W3 fragments, their addresses) are loop-invariant
   // across passes; hiding the base pointers behind an empty asm keeps the compiler from hoisting
   // them out of the pass loop, where they would stay live (and take registers) through L1.
@@ -151,11 +257,12 @@ __device__ __forceinline__ void rq_fused_pass(FusedCtx<H1, H2>& cx, int tb, bool
   for (int i = 0; i < C::XV; ++i) {
     const int f = cx.tid + C::NTH * i, it = xrow(f), k4 = (f & 15) * 4;
     const int64_t a = (int64_t)tb * FT + (KS ? it % FT : it);
-    const int64_t b = (int64_t)next_tb * FT + (next_ks ? it % FT : it);
+    const int64_t b = next_tb < 0 ? cx.n : (int64_t)next_tb * FT + (next_ks ? it % FT : it);
     xsrc[i] = cx.x + (a < cx.n ? a : cx.n - 1) * cx.D0 + k4 + (KS && it >= FT ? kbo : 0);
     xnxt[i] = cx.x + (b < cx.n ? b : cx.n - 1) * cx.D0 + k4 + (next_ks && it >= FT ? kbo : 0);
     xok_cur[i] = a < cx.n;
     xok_nxt[i] = b < cx.n && (next_ks || (next_tb + it / FT) < cx.t_end);
+    if (b >= cx.n) xnxt[i] = cx.x + (cx.n - 1) * cx.D0 + k4;
   }
   auto group = [&](auto gsel, int c) {
     constexpr int g = decltype(gsel)::value;
@@ -295,115 +402,121 @@ __device__ __forceinline__ void rq_fused_pass(FusedCtx<H1, H2>& cx, int tb, bool
     }
   __syncthreads();
 
-  // ------------------------------------------------------------------ L2: W2 . h1^T
-  // waves 0-3: wave w, features [32w, 32w + 32) for all NR item tiles (NR accumulator chains per
-  // wave); waves 4-7 skip L2 (splitting it into one chain per wave over all 8 measured 483 vs 462
-  // us per C2 call, profiles/r02_ab_quant_ablation.txt)
-  if (w < 4) {
-    f32x16 acc2[NR];
-#pragma unroll
-    for (int it = 0; it < NR; ++it)
-#pragma unroll
-      for (int v = 0; v < 16; ++v) acc2[it][v] = 0.f;
-    const float* hb = cx.h1s + r * P1 + 16 * h;
-    const float* w2row = cx.W2 + (int64_t)(w * 32 + r) * H1 + 16 * h;
-    f32x4 aw2[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) aw2[j] = *reinterpret_cast<const f32x4*>(w2row + 4 * j);
-#pragma unroll 1
-    for (int g = 0; g < H1 / 32; ++g) {
-      const int gn = (g + 1 < H1 / 32) ? g + 1 : g;
-      f32x4 awn[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) awn[j] = *reinterpret_cast<const f32x4*>(w2row + gn * 32 + 4 * j);
-      f32x4 bx[NR][4];
-#pragma unroll
-      for (int it = 0; it < NR; ++it)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) bx[it][j] = *reinterpret_cast<const f32x4*>(hb + it * FT * P1 + g * 32 + 4 * j);
-#pragma unroll
-      for (int it = 0; it < NR; ++it)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-#pragma unroll
-          for (int s = 0; s < 4; ++s) acc2[it] = mfma32(aw2[j][s], bx[it][j][s], acc2[it]);
-      // same interleave as L1: item tile 0's h1 fragments first, then one load per MFMA
-      __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
-      }
-#pragma unroll
-      for (int i = 0; i < 4 * (NR - 1); ++i) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-      }
-      __builtin_amdgcn_sched_group_barrier(0x008, 16 * NR - 4 - 4 * (NR - 1), 0);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) aw2[j] = awn[j];
-    }
-#pragma unroll
-    for (int g4 = 0; g4 < 4; ++g4) {
-      const f32x4 bb = *reinterpret_cast<const f32x4*>(cx.b2 + w * 32 + 8 * g4 + 4 * h);
-#pragma unroll
-      for (int it = 0; it < NR; ++it) {
-        f32x4 o;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const float u = bb[i] + acc2[it][4 * g4 + i];
-          o[i] = u < 0.f ? 0.f : u;
-        }
-        // L3 layout: within each 16-feature block, feature 4t + g at 4g + t (a lane of k group g
-        // reads four consecutive 16x16x4 steps as one float4)
-        float* row = cx.h2s + (it * FT + r) * P2 + w * 32 + 16 * (g4 >> 1);
-        const int t = (2 * g4 + h) & 3;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) row[4 * i + t] = o[i];
-      }
-    }
-  }
-  __syncthreads();
-
-  // ------------------------------------------------------------------ L3: W3 . h2^T
-  // 16x16x4 tiles (16 outputs x 16 items), one per wave: item tile w >> 2, item half (w >> 1) & 1,
-  // output half w & 1; one k-ordered chain over k = 0..127 (32 MFMAs), z = b3 + chain, to HBM.
-  // W3 arrives packed for this form: feature 16b + 4t + g of a row at 16b + 4g + t.
-  if (w < 4 * NR) {
-    const int it = w >> 2, ih = (w >> 1) & 1, oh = w & 1;
-    const int lane = cx.tid & 63, j = lane & 15, g = lane >> 4;
-    f32x4 acc3 = {0.f, 0.f, 0.f, 0.f};
-    const float* hb = cx.h2s + (it * FT + 16 * ih + j) * P2 + 4 * g;
-    const float* w3row = cx.w3s + (16 * oh + j) * C::P3 + 4 * g;   // LDS: rows 4 banks apart
-#pragma unroll
-    for (int b = 0; b < H2 / 16; ++b) {
-      const f32x4 aw = *reinterpret_cast<const f32x4*>(w3row + 16 * b);
-      const f32x4 bx = *reinterpret_cast<const f32x4*>(hb + 16 * b);
-#pragma unroll
-      for (int t = 0; t < 4; ++t) acc3 = mfma16(aw[t], bx[t], acc3);
-    }
-    const int64_t item = (int64_t)(tb + it) * FT + 16 * ih + j;
-    if (item < cx.n) {
-      const f32x4 bb = *reinterpret_cast<const f32x4*>(cx.b3 + 16 * oh + 4 * g);
-      f32x4 o;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) o[i] = bb[i] + acc3[i];
-      *reinterpret_cast<f32x4*>(cx.z_out + item * E + 16 * oh + 4 * g) = o;
-    }
-  }
+  rq_l23<NR, H1, H2>(cx, tb);
   // no barrier: h2 is next written after the next pass's L1 barriers
 }
 
+// One leftover-tile PIECE: the first layer of features [128 fh, 128 fh + 128) of item tile tb,
+// relu(h1) written to h1g ([32 items][H1], natural order).  The tiles past q x G (q whole tiles per
+// workgroup) would otherwise run as a one-tile pass on a few workgroups while the others idle; split
+// in feature halves they run on twice as many workgroups at half the length each, and
+// rq_leftover_kernel finishes layers 2-3.  Wave w: feature group (w & 3) of the half, MKL k block
+// w >> 2 -- one chain each over the x image in the k-split layout (rows [0, FT): block 0's chunk c,
+// rows [FT, 2 FT): block 1's); the block-1 waves hand their sums to the block-0 waves through LDS,
+// which form y = (b1 + block 0) + block 1 exactly as every other pass.  The x image's chunk 0 is
+// already staged (k-split layout) by the pass before; chunk NC/2 - 1 prefetches nothing.
+template <int H1, int H2>
+__device__ __forceinline__ void rq_piece_pass(FusedCtx<H1, H2>& cx, int tb, int fh, float* __restrict__ h1g,
+                                              const float* __restrict__ W1) {
+#pragma clang fp contract(off)
+  using C = FusedCfg<H1, H2>;
+  constexpr int PI = C::PI;
+  const int w = cx.w, r = cx.r, h = cx.h, fg = w & 3, blk = w >> 2;
+  const int NC = cx.NC / 2, kbo = cx.csplit * FXC;
+  const int f0 = 128 * fh + 32 * fg;   // this wave's first feature
+  const float* w1row = W1 + (int64_t)(f0 + r) * cx.D0 + 16 * h + blk * kbo;
+  f32x4 awc[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) awc[j] = *reinterpret_cast<const f32x4*>(w1row + 4 * j);
+  const float* xsrc[C::XV];
+  bool xok[C::XV];
+#pragma unroll
+  for (int i = 0; i < C::XV; ++i) {
+    const int f = cx.tid + C::NTH * i, it = xrow(f), k4 = (f & 15) * 4;
+    const int64_t a = (int64_t)tb * FT + it % FT;
+    xsrc[i] = cx.x + (a < cx.n ? a : cx.n - 1) * cx.D0 + k4 + (it >= FT ? kbo : 0);
+    xok[i] = a < cx.n;
+  }
+  f32x16 acc;
+#pragma unroll
+  for (int v = 0; v < 16; ++v) acc[v] = 0.f;
+#pragma unroll 1
+  for (int c = 0; c < NC; ++c) {
+    const bool more = c + 1 < NC;
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+      const int gi = 2 * c + g;
+      const int gn = gi + 1 < 2 * NC ? gi + 1 : gi;
+      f32x4 awn[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) awn[j] = *reinterpret_cast<const f32x4*>(w1row + gn * 32 + 4 * j);
+      const float* xb = cx.xs + cx.buf * PI * FXP + (blk * FT + r) * FXP + 16 * h + g * 32;
+      f32x4 bx[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bx[j] = *reinterpret_cast<const f32x4*>(xb + 4 * j);
+      if (g == 0 && more) {
+#pragma unroll
+        for (int i = 0; i < C::XV; ++i) cx.xr[i] = *reinterpret_cast<const f32x4*>(xsrc[i] + (c + 1) * FXC);
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int s = 0; s < 4; ++s) acc = mfma32(awc[j][s], bx[j][s], acc);
+      if (g == 1 && more) {
+#pragma unroll
+        for (int i = 0; i < C::XV; ++i) {
+          const int f = cx.tid + C::NTH * i;
+          put_packed(cx.xs + (cx.buf ^ 1) * PI * FXP + xrow(f) * FXP, (f & 15) * 4,
+                     xok[i] ? cx.xr[i] : f32x4{0.f, 0.f, 0.f, 0.f});
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) awc[j] = awn[j];
+    }
+    __syncthreads();
+    cx.buf ^= 1;
+  }
+  // block 1's sums -> LDS (the h1 image is free here), then y = (b1 + block 0) + block 1, ReLU
+  float* hand = cx.h1s + (fg * 64 + (cx.tid & 63)) * 16;
+  if (blk == 1) {
+#pragma unroll
+    for (int v4 = 0; v4 < 4; ++v4)
+      *reinterpret_cast<f32x4*>(hand + 4 * v4) = f32x4{acc[4 * v4], acc[4 * v4 + 1], acc[4 * v4 + 2], acc[4 * v4 + 3]};
+  }
+  __syncthreads();
+  if (blk == 0) {
+    const int64_t item = (int64_t)tb * FT + r;
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      const f32x4 bb = *reinterpret_cast<const f32x4*>(cx.b1 + f0 + 8 * g4 + 4 * h);
+      const f32x4 a1 = *reinterpret_cast<const f32x4*>(hand + 4 * g4);
+      f32x4 o;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float part = bb[i] + acc[4 * g4 + i];
+        const float u = part + a1[i];
+        o[i] = u < 0.f ? 0.f : u;
+      }
+      if (item < cx.n) *reinterpret_cast<f32x4*>(h1g + (int64_t)r * H1 + f0 + 8 * g4 + 4 * h) = o;
+    }
+  }
+  __syncthreads();   // the hand-off image is free again
+}
+
+// Partition: q = tiles / grid whole tiles per workgroup (contiguous); the r = tiles % grid tiles
+// past q x grid run as 2 r feature-half pieces (rq_piece_pass), workgroup b taking pieces b, b + G.
 template <int H1, int H2>
 __global__ __launch_bounds__(64 * FWV, 1) void rq_encoder_kernel(
     const float* __restrict__ x, int64_t n, int D0, int csplit, const float* __restrict__ W1,
     const float* __restrict__ b1, const float* __restrict__ W2, const float* __restrict__ b2,
     const float* __restrict__ W3, const float* __restrict__ b3, float* __restrict__ z_out,
-    int tiles) {
+    int tiles, float* __restrict__ h1g) {
   using C = FusedCfg<H1, H2>;
   extern __shared__ __attribute__((aligned(16))) float sm[];
-  const int t_begin = (int)((int64_t)blockIdx.x * tiles / gridDim.x);
-  const int t_end = (int)((int64_t)(blockIdx.x + 1) * tiles / gridDim.x);
+  const int G = gridDim.x, q = tiles / G, b = blockIdx.x;
+  const int npieces = h1g ? 2 * (tiles - q * G) : 0;
+  const int t_begin = h1g ? b * q : (int)((int64_t)b * tiles / G);
+  const int t_end = h1g ? t_begin + q : (int)((int64_t)(b + 1) * tiles / G);
   if (t_begin >= t_end) return;
   FusedCtx<H1, H2> cx;
   cx.x = x; cx.n = n; cx.D0 = D0; cx.NC = D0 / FXC; cx.csplit = csplit; cx.t_end = t_end;
@@ -413,8 +526,8 @@ __global__ __launch_bounds__(64 * FWV, 1) void rq_encoder_kernel(
   cx.h2s = cx.h1s + C::PI * C::P1;         // [PI][P2]
   cx.w3s = cx.h2s + C::PI * C::P2;         // [32][P3] the packed W3, staged once
   for (int f = threadIdx.x; f < C::E * H2 / 4; f += C::NTH) {
-    const int row = f / (H2 / 4), q = f % (H2 / 4);
-    *reinterpret_cast<f32x4*>(cx.w3s + row * C::P3 + 4 * q) = *reinterpret_cast<const f32x4*>(W3 + row * H2 + 4 * q);
+    const int row = f / (H2 / 4), qq = f % (H2 / 4);
+    *reinterpret_cast<f32x4*>(cx.w3s + row * C::P3 + 4 * qq) = *reinterpret_cast<const f32x4*>(W3 + row * H2 + 4 * qq);
   }
   const int tid = threadIdx.x, lane = tid & 63;
   cx.tid = tid; cx.w = tid >> 6; cx.r = lane & 31; cx.h = lane >> 5;
@@ -423,16 +536,59 @@ __global__ __launch_bounds__(64 * FWV, 1) void rq_encoder_kernel(
   for (int j = 0; j < 4; ++j) cx.awc[j] = *reinterpret_cast<const f32x4*>(cx.w1row + 4 * j);
   cx.buf = 0;
   // an odd last tile runs as a k-split pass when MKL's block edge halves the chunks (in = 768)
-  const bool ks = 2 * csplit == cx.NC && ((t_end - t_begin) & 1);
+  const bool kso = 2 * csplit == cx.NC;
+  const bool ks = kso && ((t_end - t_begin) & 1);
+  const int piece0 = b < npieces ? b : -1;          // this workgroup's first piece
+  const int ptile = piece0 >= 0 ? q * G + (piece0 >> 1) : -1;
   cx.gload_x(t_begin, 0, ks && t_end - t_begin == 1);
   cx.swrite_x(0);
   __syncthreads();
   int tb = t_begin;
-  for (; tb + FP <= t_end; tb += FP) rq_fused_pass<FP, H1, H2>(cx, tb, ks && tb + FP + 1 == t_end);
-  if (tb < t_end) {   // FP == 2: at most one tile left
-    if (ks) rq_fused_pass<2, H1, H2, true>(cx, tb);
-    else rq_fused_pass<1, H1, H2>(cx, tb);
+  for (; tb + FP <= t_end; tb += FP) {
+    const bool last = tb + FP >= t_end;
+    rq_fused_pass<FP, H1, H2>(cx, tb, last ? ptile : tb + FP, last ? ptile >= 0 : ks && tb + FP + 1 == t_end);
   }
+  if (tb < t_end) {   // FP == 2: at most one tile left
+    if (ks) rq_fused_pass<2, H1, H2, true>(cx, tb, ptile, ptile >= 0);
+    else rq_fused_pass<1, H1, H2>(cx, tb, ptile, ptile >= 0);
+  }
+  for (int pc = piece0; pc >= 0 && pc < npieces; pc += G) {
+    const int t = q * G + (pc >> 1);
+    if (pc != piece0) {   // a second piece: stage its first chunk (k-split layout)
+      cx.gload_x(t, 0, true);
+      cx.swrite_x(cx.buf);
+      __syncthreads();
+    }
+    rq_piece_pass<H1, H2>(cx, t, pc & 1, h1g + (int64_t)(pc >> 1) * FT * H1, W1);
+  }
+}
+
+// Layers 2-3 of the leftover tiles (one 4-wave workgroup each) from the pieces' relu(h1).
+template <int H1, int H2>
+__global__ __launch_bounds__(256) void rq_leftover_kernel(const float* __restrict__ h1g, int64_t n, int t0,
+                                                          const float* __restrict__ W2, const float* __restrict__ b2,
+                                                          const float* __restrict__ W3, const float* __restrict__ b3,
+                                                          float* __restrict__ z_out) {
+  using C = FusedCfg<H1, H2>;
+  __shared__ __attribute__((aligned(16))) float h1s[FT * C::P1];
+  __shared__ __attribute__((aligned(16))) float h2s[FT * C::P2];
+  __shared__ __attribute__((aligned(16))) float w3s[C::E * C::P3];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const float* src = h1g + (int64_t)blockIdx.x * FT * H1;
+  for (int f = tid; f < FT * H1 / 4; f += 256) {   // relu(h1) -> the packed h1 image
+    const int row = f / (H1 / 4), k0 = (f % (H1 / 4)) * 4;
+    put_packed(h1s + row * C::P1, k0, *reinterpret_cast<const f32x4*>(src + row * H1 + k0));
+  }
+  for (int f = tid; f < C::E * H2 / 4; f += 256) {
+    const int row = f / (H2 / 4), qq = f % (H2 / 4);
+    *reinterpret_cast<f32x4*>(w3s + row * C::P3 + 4 * qq) = *reinterpret_cast<const f32x4*>(W3 + row * H2 + 4 * qq);
+  }
+  __syncthreads();
+  FusedCtx<H1, H2> cx;
+  cx.n = n; cx.W2 = W2; cx.b2 = b2; cx.W3 = W3; cx.b3 = b3; cx.z_out = z_out;
+  cx.h1s = h1s; cx.h2s = h2s; cx.w3s = w3s;
+  cx.tid = tid; cx.w = tid >> 6; cx.r = lane & 31; cx.h = lane >> 5;
+  rq_l23<1, H1, H2>(cx, t0 + blockIdx.x);
 }
 
 // Packed weight images of the three layers (one launch): W1 and W2 for the 32x32x2 chains (within
@@ -488,9 +644,10 @@ int gr_rq_encoder_pack_launch(int32_t n_linear, const int32_t* dims, const float
 }
 
 // packed: the image gr_rq_encoder_pack_launch wrote (`pack_is_ready`), or workspace for it.
+// scratch: >= n x 256 floats of workspace for the leftover pieces' h1 (null: no split).
 int gr_rq_encoder_fused_launch(const float* x, int64_t n, int32_t n_linear, const int32_t* dims,
                                const float* const* weights, const float* const* biases,
-                               float* z_out, float* pack, hipStream_t st, bool pack_is_ready) {
+                               float* z_out, float* pack, hipStream_t st, bool pack_is_ready, float* scratch) {
   using namespace gr;
   if (n_linear != 3 || dims[3] != 32 || dims[0] % FXC != 0 || !biases) return GR_ERR_UNSUPPORTED;
   if (!(dims[1] == 256 && dims[2] == 128)) return GR_ERR_UNSUPPORTED;
@@ -521,7 +678,14 @@ int gr_rq_encoder_fused_launch(const float* x, int64_t n, int32_t n_linear, cons
                                            hipFuncAttributeMaxDynamicSharedMemorySize,
                                            (int)(Cfg::LDS * sizeof(float))) == hipSuccess;
   if (!lds_ok) return fail(GR_ERR_HIP, "rq fused encoder: cannot raise the LDS limit");
+  // leftover-tile pieces when the MKL split halves the chunks (in = 768) and tiles % grid != 0
+  const int64_t left = tiles % grid;
+  float* h1g = (scratch && left && 2 * csplit * FXC == dims[0] && option("rq_pieces") != 0) ? scratch : nullptr;
   hipLaunchKernelGGL((rq_encoder_kernel<256, 128>), dim3((unsigned)grid), dim3(64 * FWV), Cfg::LDS * sizeof(float), st, x, n,
-                     dims[0], csplit, wp[0], biases[0], wp[1], biases[1], wp[2], biases[2], z_out, (int)tiles);
-  return check_launch("rq fused encoder");
+                     dims[0], csplit, wp[0], biases[0], wp[1], biases[1], wp[2], biases[2], z_out, (int)tiles, h1g);
+  int rc = check_launch("rq fused encoder");
+  if (rc || !h1g) return rc;
+  hipLaunchKernelGGL((rq_leftover_kernel<256, 128>), dim3((unsigned)left), dim3(256), 0, st, h1g, n,
+                     (int)(tiles - left), wp[1], biases[1], wp[2], biases[2], z_out);
+  return check_launch("rq fused encoder (leftover tiles)");
 }

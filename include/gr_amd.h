@@ -65,6 +65,9 @@ const char* gr_last_error(void);
  *                   1: always direct.  Identical results.
  *   "topk_sample"   1 (default): gr_score_topk_f32 prunes with a threshold from a strided sample
  *                   pass when the catalog is long enough; 0: one pass.  Identical results.
+ *   "lin_wres"      1 (default): gr_linear_f32 with k = 128, n % 128 == 0, no residual and
+ *                   m >= 96 x 256 runs a persistent kernel that keeps each wave's 32 columns of w in
+ *                   registers (the C5 block-0 in-projection); 0: the tiled kernel.  Identical results.
  * gr_set_option returns GR_ERR_ARG for an unknown name/value; gr_get_option returns -1 for an
  * unknown name. */
 int gr_set_option(const char* name, int64_t value);
