@@ -95,7 +95,18 @@ class SASRec(nn.Module):
         """``forward(log_seqs)[:, -1, :]`` (model.py:104) without materialising other positions."""
         return ops.sasrec_forward(self._binding(log_seqs), log_seqs, last_only=True)
 
+    # predict's logits layout: False (default) -- a [B, ld] buffer (rows 128-byte aligned, ld =
+    # roundup(item_num + 1, 32)) viewed as [B, item_num + 1], unit column stride, which every use in
+    # the reference (evaluate.py:27-32, train.py:45-50) takes as is; True -- a contiguous tensor like
+    # the reference's matmul result (.view() works), at the cost of the scoring kernel's unaligned
+    # store path (profiles/r03_ab_predict_ld.txt: 440 vs 394 us at B 2048, 146 vs 109 us at B 128).
+    contiguous_logits = False
+
     @torch.no_grad()
     def predict(self, log_seqs):
         """model.py:98-108: logits ``[B, item_num+1]`` = last hidden state x item table^T."""
-        return ops.sasrec_predict(self._binding(log_seqs), log_seqs)
+        out = None
+        if self.contiguous_logits:
+            out = torch.empty((log_seqs.shape[0], self.item_emb.weight.shape[0]), dtype=torch.float32,
+                              device=self.item_emb.weight.device)
+        return ops.sasrec_predict(self._binding(log_seqs), log_seqs, out=out)

@@ -93,6 +93,22 @@ def test_predict_returns_fresh_writable_tensor(dev):
     assert not torch.equal(a[:, 0], b[:, 0]) and torch.equal(a[:, 1:], b[:, 1:])
 
 
+def test_predict_contiguous_logits_option(dev):
+    """SASRec.contiguous_logits = True: predict returns a contiguous [B, N+1] tensor (the reference's
+    matmul layout: .view() works), bitwise the row-padded default's values."""
+    m, out, meta = build("sas_syn_c3", dev)
+    seqs = torch.from_numpy(out["seqs"]).to(dev)
+    a = m.predict(seqs)
+    try:
+        m.contiguous_logits = True
+        c = m.predict(seqs)
+    finally:
+        m.contiguous_logits = False
+    assert c.is_contiguous() and c.shape == a.shape
+    assert torch.equal(a, c)
+    assert c.view(-1).numel() == a.numel()
+
+
 @pytest.mark.parametrize("name", ["sas_csv_c1", "sas_syn_c3"])
 def test_predict_row_padded_layout(name, dev, sas_path):
     """predict() returns a [B, N+1] view whose rows are 32-float aligned (direct-store scoring); the
