@@ -66,6 +66,15 @@ static std::atomic<int64_t> g_lin_wres{1};
 // twice as many workgroups plus a layers-2-3 kernel; 0: a one-tile pass on r workgroups).  Bitwise
 // the same z; A/B timing.
 static std::atomic<int64_t> g_rq_pieces{1};
+// emb_proj (1 (default): the d = 128 forward's block 0 runs embed + LN_a0 + in-projection as one
+// persistent kernel; 0: embed_ln then gr_linear_f32) and emb_rows (32 (default) or 64 rows per tile
+// of that kernel).  Bitwise the same results; A/B timing.
+static std::atomic<int64_t> g_emb_proj{1};
+static std::atomic<int64_t> g_emb_rows{32};
+// rt_kv2 (1 (default): post_attn's next-block projection with nout / 32 a multiple of 8 runs one
+// column tile per wave over both row tiles (one weight stream, two chains); 0: one 32 x 32 tile
+// per task).  Bitwise the same; A/B timing.
+static std::atomic<int64_t> g_rt_kv2{1};
 
 int64_t option(const char* name) {
   if (!strcmp(name, "rq_fused")) return g_rq_fused.load();
@@ -87,6 +96,9 @@ int64_t option(const char* name) {
   if (!strcmp(name, "lin_w8")) return g_lin_w8.load();
   if (!strcmp(name, "lin_wres")) return g_lin_wres.load();
   if (!strcmp(name, "rq_pieces")) return g_rq_pieces.load();
+  if (!strcmp(name, "emb_proj")) return g_emb_proj.load();
+  if (!strcmp(name, "emb_rows")) return g_emb_rows.load();
+  if (!strcmp(name, "rt_kv2")) return g_rt_kv2.load();
   return -1;
 }
 }  // namespace gr
@@ -113,6 +125,9 @@ extern "C" int gr_set_option(const char* name, int64_t value) {
   if (!strcmp(name, "lin_w8") && (value == 0 || value == 1)) { gr::g_lin_w8 = value; return GR_OK; }
   if (!strcmp(name, "lin_wres") && (value == 0 || value == 1)) { gr::g_lin_wres = value; return GR_OK; }
   if (!strcmp(name, "rq_pieces") && (value == 0 || value == 1)) { gr::g_rq_pieces = value; return GR_OK; }
+  if (!strcmp(name, "emb_proj") && (value == 0 || value == 1)) { gr::g_emb_proj = value; return GR_OK; }
+  if (!strcmp(name, "emb_rows") && (value == 32 || value == 64)) { gr::g_emb_rows = value; return GR_OK; }
+  if (!strcmp(name, "rt_kv2") && (value == 0 || value == 1)) { gr::g_rt_kv2 = value; return GR_OK; }
   return gr::fail(GR_ERR_ARG, std::string("gr_set_option: unknown option or value: ") + name);
 }
 

@@ -316,10 +316,16 @@ static int run_forward_rowtile(const gr_sasrec_params* p, const int64_t* seqs, i
   // embed kernel measured slower: 218 us vs 37 + 133 at C5, its weight fragments come from L2
   // with one 16-B piece per row per lane); later blocks fold it into post_attn (198 us vs
   // 115 + 97 for the final block's K|V)
-  int rc = gr_embed_ln_launch(p, seqs, rows, n, nullptr, nullptr, 0, w.x, w.h, err, st);
-  if (rc) return rc;
+  // with 32-column slices of W_in resident in registers over a persistent tile range
+  // (embed_proj_kernel, option emb_proj) the two fold into one kernel
   proj(0, &wn, &bn, &nout);
-  rc = gr_linear_launch(w.h, rows, d, wn, nout, bn, nullptr, 0, GR_ACT_NONE, w.qkv, nout, st);
+  int rc = option("emb_proj") == 1 ? gr_embed_proj_launch(p, seqs, rows, n, wn, bn, nout, w.x, w.qkv, err, st)
+                                   : GR_ERR_UNSUPPORTED;
+  if (rc == GR_ERR_UNSUPPORTED) {
+    rc = gr_embed_ln_launch(p, seqs, rows, n, nullptr, nullptr, 0, w.x, w.h, err, st);
+    if (rc) return rc;
+    rc = gr_linear_launch(w.h, rows, d, wn, nout, bn, nullptr, 0, GR_ACT_NONE, w.qkv, nout, st);
+  }
   if (rc) return rc;
   const float scale = (float)std::sqrt(1.0 / (double)hd);
   for (int i = 0; i < nb; ++i) {

@@ -29,6 +29,7 @@ struct RowTileArgs {
   const float *wo, *bo, *ln_f_w, *ln_f_b, *w1, *b1, *w2, *b2, *ln_n_w, *ln_n_b;
   const float *wn, *bn;   // the next block's in-projection (rows of W_in / b_in), or null
   int mlp, nout;          // nout: 3d (Q|K|V) or 2d (K|V only, the final block of a tail forward)
+  int kv2;                // post_attn8: nout / 32 % 8 == 0 and option rt_kv2 (one column tile per wave)
   float eps;
 };
 
@@ -56,6 +57,8 @@ __device__ __forceinline__ void rt_gemm(f32x16 (&acc)[2], const float* A, int ap
       acc[0] = mfma32(x0[s], b[s], acc[0]);
       acc[1] = mfma32(x1[s], b[s], acc[1]);
     }
+    // keep the LDS reads of A at most 2 slices ahead (hoisted whole they take 128 VGPRs)
+    if (kc % 2 == 1) __builtin_amdgcn_sched_barrier(0);
   }
 }
 
@@ -118,6 +121,46 @@ __device__ __forceinline__ void rt_layernorm(float* img, const float* __restrict
 #pragma unroll
     for (int e = 0; e < 4; ++e) y[e] = (xv[e] - m) * rs * ww[e] + bb[e];
     if (rr < rows_left) *reinterpret_cast<f32x4*>(dst_global + (int64_t)rr * RT_D + c) = y;
+  }
+}
+
+// rt_layernorm's in-place form for one row (4 lanes per row, `part` = lane & 3, as there) with the
+// weight and bias read from LDS one float4 pair at a time (same arithmetic, bitwise the same rows):
+// for kernels that keep 64+ VGPRs of weights resident, where the 16 global loads rt_layernorm
+// issues together would not fit beside them.
+__device__ __forceinline__ void rt_layernorm_lds(float* img, const float* ws, const float* bs, float eps, int row,
+                                                 int part) {
+  float* x = img + row * RT_P + 32 * part;
+  f32x4 v[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) v[i] = *reinterpret_cast<const f32x4*>(x + 4 * i);
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) s += (v[i][0] + v[i][1]) + (v[i][2] + v[i][3]);
+  s += __shfl_xor(s, 1);
+  s += __shfl_xor(s, 2);
+  const float mean = s * (1.0f / RT_D);
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float d = v[i][e] - mean;
+      q = fmaf(d, d, q);
+    }
+  q += __shfl_xor(q, 1);
+  q += __shfl_xor(q, 2);
+  const float rstd = 1.0f / sqrtf(q * (1.0f / RT_D) + eps);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int c = 32 * part + 4 * i;
+    const f32x4 ww = *reinterpret_cast<const f32x4*>(ws + c);
+    const f32x4 bb = *reinterpret_cast<const f32x4*>(bs + c);
+    f32x4 y;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) y[e] = (v[i][e] - mean) * rstd * ww[e] + bb[e];
+    *reinterpret_cast<f32x4*>(x + 4 * i) = y;
+    __builtin_amdgcn_sched_barrier(0);
   }
 }
 
@@ -424,6 +467,31 @@ __global__ __launch_bounds__(512, 4) void post_attn8_kernel(const RowTileArgs a,
     rt_layernorm8(bufB, a.ln_n_w, a.ln_n_b, a.eps, nullptr, 0);
     __syncthreads();
     float* out = Hn + m0 * a.nout;
+    if (a.kv2) {   // the next block's in-projection, both row tiles per weight stream
+      for (int ct = w; ct < a.nout / 32; ct += 8) {
+        const int pc = 32 * ct + r;
+        f32x16 acc[2];
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+          for (int v = 0; v < 16; ++v) acc[rt][v] = 0.f;
+        rt_gemm<RT_D>(acc, bufB, RT_P, a.wn, pc, r, h);
+        const float bv = a.bn[pc];
+        // buffer stores, the row offset in soffset (32 global addresses would spill); rows past
+        // the end get an out-of-range voffset and are dropped
+        const auto rs = __builtin_amdgcn_make_buffer_rsrc(out, 0, 0x7fffffff, 0x00020000);
+        const int ld4 = a.nout * 4, loff = 4 * h * ld4 + pc * 4;
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+          for (int v = 0; v < 16; ++v) {
+            const int rr = 32 * rt + (v & 3) + 8 * (v >> 2);
+            const int off = left >= RT_BM || rr + 4 * h < left ? loff : 0x7fffffff;
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[rt][v] + bv), rs, off, rr * ld4, 0);
+          }
+      }
+      return;
+    }
     for (int t = w; t < 2 * (a.nout / 32); t += 8) {   // the next block's in-projection
       const int prt = t & 1, pc = 32 * (t >> 1) + r;
       f32x16 acc;
@@ -493,6 +561,162 @@ __global__ __launch_bounds__(256) void embed_ln_kernel(const int64_t* __restrict
   }
 }
 
+// Block 0 of the C5 forward in one persistent kernel: X = M[s] + P[t], H = LN_a0(X) and
+// QKV = H . W_in^T + b_in for NOUT = 32 NW columns (Q|K|V, or K|V only), per tile of BR = 32 RC rows.
+// NW waves; wave w keeps columns 32w..32w+31 of W_in in registers for the whole tile range (64
+// floats per lane: every column of the product lives in one workgroup, so the LayerNorm is taken
+// once per row and H never goes to HBM).  Three LDS images rotate: while tile t's MFMAs read one,
+// waves 0-3 normalise tile t+1's X in place in the next before their own MFMAs, and every wave
+// writes tile t+2's gathered X into the third -- one barrier per tile, the LayerNorm off the
+// critical path of 8 of the NW waves.  Gathers run two tiles ahead (ids three: the row addresses
+// depend on them).  Per element: embed_ln_kernel's X and LayerNorm (rt_layernorm's arithmetic,
+// weights from LDS), then linear_wres_kernel's k-ordered chain with the bias added last --
+// bitwise the two-kernel sequence it replaces.
+template <int NW, int RC>
+__global__ __launch_bounds__(64 * NW, 1) void embed_proj_kernel(const int64_t* __restrict__ seqs, int64_t M, int n,
+                                                                const float* __restrict__ item, int64_t item_rows,
+                                                                const float* __restrict__ pos,
+                                                                const float* __restrict__ lw,
+                                                                const float* __restrict__ lb, float eps,
+                                                                const float* __restrict__ wn,
+                                                                const float* __restrict__ bn, float* __restrict__ X,
+                                                                float* __restrict__ QKV, int32_t* err) {
+  constexpr int NT = 64 * NW, BR = 32 * RC, NOUT = 32 * NW;
+  constexpr int NV = BR * (RT_D / 4);        // float4 per tile
+  constexpr int GV = (NV + NT - 1) / NT;     // per thread
+  constexpr int LR = BR / 4;                 // LayerNorm rows per wave (waves 0-3, 4 lanes per row)
+  static_assert(NW >= 4, "the LayerNorm takes waves 0-3");
+  __shared__ __attribute__((aligned(16))) float img[3][BR * RT_P];
+  __shared__ __attribute__((aligned(16))) float lnw[RT_D], lnb[RT_D];
+  const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, h = lane >> 5;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  if (tid < RT_D) {
+    lnw[tid] = lw[tid];
+    lnb[tid] = lb[tid];
+  }
+  const int64_t tiles = (M + BR - 1) / BR;
+  const int64_t t0 = (int64_t)blockIdx.x * tiles / gridDim.x, t1 = (int64_t)(blockIdx.x + 1) * tiles / gridDim.x;
+  if (t0 >= t1) return;
+  const int col = 32 * wv + r;
+  f32x4 wf[RT_D / 8];   // W_in[col][8kc + 4h .. +3]
+#pragma unroll
+  for (int kc = 0; kc < RT_D / 8; ++kc)
+    wf[kc] = *reinterpret_cast<const f32x4*>(wn + (int64_t)col * RT_D + 8 * kc + 4 * h);
+  const float bv = bn[col];
+  const bool ln_lane = wv < 4 && lane < 4 * LR;
+  const int ln_row = wv * LR + (lane >> 2), ln_part = lane & 3;
+  int64_t idn[GV];
+  f32x4 e[GV], ps[GV];
+  auto live = [&](int i) { return NV % NT == 0 || tid + NT * i < NV; };
+  auto load_ids = [&](int64_t t) {
+    const int64_t m0 = t * BR, left = M - m0;
+#pragma unroll
+    for (int i = 0; i < GV; ++i)
+      if (live(i)) {
+        const int row = (tid + NT * i) >> 5;
+        idn[i] = seqs[m0 + (row < left ? row : left - 1)];
+      }
+  };
+  auto load_rows = [&](int64_t t) {   // reads idn (tile t's ids)
+    const int64_t m0 = t * BR, left = M - m0;
+    const int pb = (int)(m0 % n);     // position of the tile's first row
+#pragma unroll
+    for (int i = 0; i < GV; ++i)
+      if (live(i)) {
+        const int f = tid + NT * i, row = f >> 5, c = (f & 31) * 4;
+        int pp = pb + (row < left ? row : (int)left - 1);
+        while (pp >= n) pp -= n;
+        int64_t id = idn[i];
+        if (id < 0 || id >= item_rows) {   // flag only real rows (clamped duplicates re-read a real id)
+          if (row < left) set_err(err, 1);
+          id = 0;
+        }
+        e[i] = *reinterpret_cast<const f32x4*>(item + id * RT_D + c);
+        ps[i] = *reinterpret_cast<const f32x4*>(pos + (int64_t)pp * RT_D + c);
+      }
+  };
+  auto put = [&](int64_t t, float* im) {   // X to HBM, X to an LDS image
+    const int64_t m0 = t * BR, left = M - m0;
+#pragma unroll
+    for (int i = 0; i < GV; ++i)
+      if (live(i)) {
+        const int f = tid + NT * i, row = f >> 5, c = (f & 31) * 4;
+        const bool ok = row < left;
+        const f32x4 x = ok ? e[i] + ps[i] : f32x4{0.f, 0.f, 0.f, 0.f};
+        if (ok) *reinterpret_cast<f32x4*>(X + (m0 + row) * RT_D + c) = x;
+        *reinterpret_cast<f32x4*>(&im[row * RT_P + c]) = x;
+      }
+  };
+  load_ids(t0);
+  load_rows(t0);
+  put(t0, img[0]);
+  if (t0 + 1 < t1) {
+    load_ids(t0 + 1);
+    load_rows(t0 + 1);
+    put(t0 + 1, img[1]);
+    if (t0 + 2 < t1) load_ids(t0 + 2);
+  }
+  __syncthreads();
+  if (ln_lane) rt_layernorm_lds(img[0], lnw, lnb, eps, ln_row, ln_part);
+  __syncthreads();
+  int cur = 0;   // img[cur] = H(t); img[cur+1] = X(t+1); img[cur+2] <- X(t+2)
+  for (int64_t t = t0; t < t1; ++t) {
+    const int nx = cur == 2 ? 0 : cur + 1, nn = nx == 2 ? 0 : nx + 1;
+    if (t + 2 < t1) {
+      load_rows(t + 2);
+      if (t + 3 < t1) load_ids(t + 3);
+    }
+    if (ln_lane && t + 1 < t1) rt_layernorm_lds(img[nx], lnw, lnb, eps, ln_row, ln_part);
+    f32x16 acc[RC];
+#pragma unroll
+    for (int rc = 0; rc < RC; ++rc)
+#pragma unroll
+      for (int v = 0; v < 16; ++v) acc[rc][v] = 0.f;
+    const float* xrow = &img[cur][r * RT_P + 4 * h];
+#pragma unroll
+    for (int kc = 0; kc < RT_D / 8; ++kc) {
+      f32x4 a[RC];
+#pragma unroll
+      for (int rc = 0; rc < RC; ++rc) a[rc] = *reinterpret_cast<const f32x4*>(xrow + 32 * rc * RT_P + 8 * kc);
+#pragma unroll
+      for (int s2 = 0; s2 < 4; ++s2)
+#pragma unroll
+        for (int rc = 0; rc < RC; ++rc) acc[rc] = mfma32(a[rc][s2], wf[kc][s2], acc[rc]);
+      // at most 4 slices of A in flight: the scheduler would otherwise hoist all 16 LDS reads
+      // (128 VGPRs at RC = 2) above the chain and spill
+      if (kc % 4 == 3) __builtin_amdgcn_sched_barrier(0);
+    }
+    // buffer stores off a per-tile descriptor: rows past the end get an out-of-range offset and
+    // are dropped.  The per-lane terms are laundered through an empty asm each tile: hoisted out of
+    // the loop, the 16 RC row offsets would pin as many VGPRs next to the resident w and spill it.
+    const int64_t m0 = t * BR;
+    const int left = (int)((M - m0) < BR ? (M - m0) : BR);
+    const auto rs = __builtin_amdgcn_make_buffer_rsrc(QKV + m0 * NOUT, 0, 0x7fffffff, 0x00020000);
+    int lrow = 4 * h, loff = (4 * h * NOUT + col) * 4;
+    asm volatile("" : "+v"(lrow), "+v"(loff));
+    if (left == BR) {   // the row offset as the scalar soffset: no per-store VALU
+#pragma unroll
+      for (int rc = 0; rc < RC; ++rc)
+#pragma unroll
+        for (int v = 0; v < 16; ++v)
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[rc][v] + bv), rs, loff,
+                                                (32 * rc + (v & 3) + 8 * (v >> 2)) * NOUT * 4, 0);
+    } else {
+#pragma unroll
+      for (int rc = 0; rc < RC; ++rc)
+#pragma unroll
+        for (int v = 0; v < 16; ++v) {
+          const int rr = 32 * rc + (v & 3) + 8 * (v >> 2);
+          const int off = lrow + rr < left ? loff + rr * NOUT * 4 : 0x7fffffff;
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[rc][v] + bv), rs, off, 0, 0);
+        }
+    }
+    if (t + 2 < t1) put(t + 2, img[nn]);
+    __syncthreads();
+    cur = nx;
+  }
+}
+
 }  // namespace gr
 
 // Shapes: d == 128, mlp in {32, 64, 128}; anything else returns GR_ERR_UNSUPPORTED (the caller
@@ -513,6 +737,7 @@ int gr_post_attn_launch(const gr_sasrec_params* p, int blk, const float* ln_next
   a.w2 = p->ffn2_w[blk]; a.b2 = p->ffn2_b[blk];
   a.ln_n_w = ln_next_w; a.ln_n_b = ln_next_b;
   a.wn = wn; a.bn = bn; a.nout = nout;
+  a.kv2 = wn && (nout / 32) % 8 == 0 && option("rt_kv2") != 0;
   a.mlp = mlp; a.eps = p->eps;
   const float* ptrs[] = {a.wo, a.w1, a.w2, a.ln_f_w, a.ln_f_b, a.ln_n_w, a.ln_n_b, O, X, H};
   for (const float* q : ptrs)
@@ -547,4 +772,36 @@ int gr_embed_ln_launch(const gr_sasrec_params* p, const int64_t* seqs, int64_t M
   hipLaunchKernelGGL(embed_ln_kernel, dim3((unsigned)tiles), dim3(256), 0, st, seqs, M, n, p->item_emb, p->item_rows,
                      p->pos_emb, p->attn_ln_w[0], p->attn_ln_b[0], p->eps, wn, bn, nout, X, H, err);
   return check_launch("sasrec embed + layernorm");
+}
+
+// Block 0 fused: X, then QKV = LN_a0(X) . W^T + b ([M x nout], nout = 3d or 2d) by embed_proj_kernel
+// (d == 128 only; GR_ERR_UNSUPPORTED otherwise -- the caller keeps embed_ln + gr_linear).  One
+// workgroup per CU over contiguous ranges of 32 RC-row tiles (option emb_rows: 32 rows, or 64; C5
+// forward 403 vs 414 us: 3200 tiles over 256 CUs balance better than 1600).
+int gr_embed_proj_launch(const gr_sasrec_params* p, const int64_t* seqs, int64_t M, int32_t n, const float* wn,
+                         const float* bn, int nout, float* X, float* QKV, int32_t* err, hipStream_t st) {
+  using namespace gr;
+  if (p->d != RT_D || p->n_blocks < 1 || (nout != 3 * RT_D && nout != 2 * RT_D)) return GR_ERR_UNSUPPORTED;
+  if (!aligned16(p->attn_ln_w[0]) || !aligned16(p->attn_ln_b[0]) || !aligned16(wn) || !bn)
+    return GR_ERR_UNSUPPORTED;
+  if (M * nout >= (1LL << 40)) return GR_ERR_UNSUPPORTED;
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1) cus = 256;
+  }
+  const bool r64 = option("emb_rows") == 64;
+  const int64_t tiles = (M + (r64 ? 63 : 31)) / (r64 ? 64 : 32);
+  const unsigned g = (unsigned)(tiles < cus ? tiles : cus);
+#define GR_EMB_PROJ(NW, RC)                                                                              \
+  hipLaunchKernelGGL((embed_proj_kernel<NW, RC>), dim3(g), dim3(64 * NW), 0, st, seqs, M, n, p->item_emb, \
+                     p->item_rows, p->pos_emb, p->attn_ln_w[0], p->attn_ln_b[0], p->eps, wn, bn, X, QKV, err)
+  if (nout == 3 * RT_D) {
+    if (r64) GR_EMB_PROJ(12, 2); else GR_EMB_PROJ(12, 1);
+  } else {
+    if (r64) GR_EMB_PROJ(8, 2); else GR_EMB_PROJ(8, 1);
+  }
+#undef GR_EMB_PROJ
+  return check_launch("sasrec embed + layernorm + in-projection");
 }

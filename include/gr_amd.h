@@ -68,6 +68,13 @@ const char* gr_last_error(void);
  *   "lin_wres"      1 (default): gr_linear_f32 with k = 128, n % 128 == 0, no residual and
  *                   m >= 96 x 256 runs a persistent kernel that keeps each wave's 32 columns of w in
  *                   registers (the C5 block-0 in-projection); 0: the tiled kernel.  Identical results.
+ *   "emb_proj"      1 (default): the d = 128 forward's block 0 (embedding gather + LN_a0 +
+ *                   in-projection) runs as one persistent kernel with W_in in registers; 0: the
+ *                   embed_ln kernel then gr_linear_f32.  Identical results.
+ *   "emb_rows"      32 (default) or 64: rows per tile of that kernel.  Identical results.
+ *   "rt_kv2"        1 (default): the post-attention row tile's next-block projection, when its
+ *                   width is a multiple of 256, runs one column tile per wave over both row tiles;
+ *                   0: one 32 x 32 tile per task.  Identical results.
  * gr_set_option returns GR_ERR_ARG for an unknown name/value; gr_get_option returns -1 for an
  * unknown name. */
 int gr_set_option(const char* name, int64_t value);

@@ -188,7 +188,7 @@ def test_linear_vs_fp64(m_, k, n, act, res, dev):
 @pytest.mark.parametrize("m_,n,act", [(102_400, 384, "none"), (64 * 256 + 37, 128, "relu"), (64 * 300 - 1, 256, "none")])
 def test_linear_resident_w_equals_tiled(m_, n, act, dev):
     """k = 128, n % 128 == 0 (the C5 block-0 in-projection shape): the persistent kernel with w
-    slices resident in LDS (option lin_wres) is bitwise the tiled kernel, ragged m included."""
+    slices resident in registers (option lin_wres) is bitwise the tiled kernel, ragged m included."""
     from gr_amd import _lib, ops
     g = torch.Generator(device=dev).manual_seed(m_ + n)
     x = torch.randn(m_, 128, generator=g, device=dev)
@@ -202,6 +202,41 @@ def test_linear_resident_w_equals_tiled(m_, n, act, dev):
     finally:
         _lib.set_option("lin_wres", 1)
     assert torch.equal(tiled, res)
+
+
+@pytest.mark.parametrize("B,blocks", [(37, 2), (515, 2), (9, 1)])
+def test_embed_proj_equals_two_kernels(B, blocks, dev):
+    """d = 128 block 0 (option emb_proj): embedding gather + LN_a0 + in-projection as one persistent
+    kernel with W_in resident in registers, 64- and 32-row tiles, is bitwise the embed_ln +
+    gr_linear pair -- full forward and last-position predict (K|V-only projection when blocks = 1),
+    ragged row counts; out-of-range ids are still flagged."""
+    from gr_amd import _lib, ops, synth
+    n, items = 200, 5000
+    p = synth.sasrec_params(128, n, blocks, 1, 128, dev)
+    m = synth.sasrec_model(items, p, dev, seed=B + blocks)
+    seqs = synth.sequences(B, n, items, 7 + B, dev)
+    res = {}
+    try:
+        for opt, rows in ((0, 64), (1, 64), (1, 32)):
+            _lib.set_option("emb_proj", opt)
+            _lib.set_option("emb_rows", rows)
+            res[(opt, rows)] = (m.forward(seqs), m.predict(seqs))
+            bad = seqs.clone()
+            bad[B // 2, 5] = items + 3
+            old = ops.CHECK
+            ops.CHECK = True
+            try:
+                with pytest.raises(IndexError):
+                    m.predict(bad)
+            finally:
+                ops.CHECK = old
+    finally:
+        _lib.set_option("emb_proj", 1)
+        _lib.set_option("emb_rows", 32)
+    f0, p0 = res[(0, 64)]
+    for k, (f, pr) in res.items():
+        assert torch.equal(f, f0), k
+        assert torch.equal(pr, p0), k
 
 
 def test_score_matches_linear_and_rank_consistency(dev):
