@@ -384,11 +384,13 @@ def test_binding_cache_sees_weight_changes(dev):
 
 @pytest.mark.parametrize("rowtile", [1, 0], ids=["rowtile", "per_op"])
 @pytest.mark.parametrize("heads,mlp,n,blocks,B", [(1, 64, 200, 2, 6), (2, 32, 77, 3, 5), (4, 128, 33, 1, 4),
-                                                  (1, 64, 1, 2, 3), (1, 128, 65, 2, 70)])
+                                                  (1, 64, 1, 2, 3), (1, 128, 65, 2, 70), (1, 64, 208, 1, 3),
+                                                  (2, 64, 209, 2, 3)])
 def test_d128_layerwise_paths_vs_oracle(heads, mlp, n, blocks, B, rowtile, dev):
     """d = 128 (the C5 width): the row-tile fused forward (embed+LN, post-attention row tiles, the
     last-position tail) and the one-kernel-per-op forward, against the CPU oracle; forward (all
-    positions), last_hidden and predict."""
+    positions), last_hidden and predict; n = 208 / 209 with 16 lane groups of 13 keys at the
+    edge."""
     from gr_amd import _lib, synth
     from oracle import sasrec_oracle
     _lib.set_option("sas_rowtile", rowtile)
