@@ -160,20 +160,21 @@ def spinup(fn, seconds=None, world=1):
 
 def timed(fn, steps, warmup, world):
     """Spin-up, W untimed warmup steps, then exactly K steps between barrier+synchronize; returns
-    (max-over-ranks wall seconds, mean device ms per step from HIP events on the launch stream)."""
+    (max-over-ranks wall seconds, mean device ms per step from two HIP events on the launch stream
+    around the K steps -- no markers between steps, which would themselves open dispatch gaps)."""
     spinup(fn, world=world)
     for _ in range(warmup):
         fn()
     sync_all(world)
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
-    for s, e in ev:
-        s.record()
+    e0.record()
+    for _ in range(steps):
         fn()
-        e.record()
+    e1.record()
     sync_all(world)
     wall = time.perf_counter() - t0
-    dev_ms = sum(s.elapsed_time(e) for s, e in ev) / steps
+    dev_ms = e0.elapsed_time(e1) / steps
     if world > 1:
         t = torch.tensor([wall], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
