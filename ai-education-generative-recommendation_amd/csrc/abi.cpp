@@ -75,6 +75,10 @@ static std::atomic<int64_t> g_emb_rows{32};
 // column tile per wave over both row tiles (one weight stream, two chains); 0: one 32 x 32 tile
 // per task).  Bitwise the same; A/B timing.
 static std::atomic<int64_t> g_rt_kv2{1};
+// tail_h (1 (default): a last-position forward's final block runs the one-query tail on LN_a(X)
+// (sas_tail_h_kernel: q . K_j and p . V reassociated through W_k / W_v, no K|V projection of the
+// B n rows); 0: K|V projected for sas_tail_kernel).  Within the logits tolerance; A/B timing.
+static std::atomic<int64_t> g_tail_h{1};
 
 int64_t option(const char* name) {
   if (!strcmp(name, "rq_fused")) return g_rq_fused.load();
@@ -99,6 +103,7 @@ int64_t option(const char* name) {
   if (!strcmp(name, "emb_proj")) return g_emb_proj.load();
   if (!strcmp(name, "emb_rows")) return g_emb_rows.load();
   if (!strcmp(name, "rt_kv2")) return g_rt_kv2.load();
+  if (!strcmp(name, "tail_h")) return g_tail_h.load();
   return -1;
 }
 }  // namespace gr
@@ -128,6 +133,7 @@ extern "C" int gr_set_option(const char* name, int64_t value) {
   if (!strcmp(name, "emb_proj") && (value == 0 || value == 1)) { gr::g_emb_proj = value; return GR_OK; }
   if (!strcmp(name, "emb_rows") && (value == 32 || value == 64)) { gr::g_emb_rows = value; return GR_OK; }
   if (!strcmp(name, "rt_kv2") && (value == 0 || value == 1)) { gr::g_rt_kv2 = value; return GR_OK; }
+  if (!strcmp(name, "tail_h") && (value == 0 || value == 1)) { gr::g_tail_h = value; return GR_OK; }
   return gr::fail(GR_ERR_ARG, std::string("gr_set_option: unknown option or value: ") + name);
 }
 

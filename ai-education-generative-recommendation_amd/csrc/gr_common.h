@@ -153,6 +153,8 @@ int gr_embed_ln_launch(const gr_sasrec_params* p, const int64_t* seqs, int64_t M
 int gr_embed_proj_launch(const gr_sasrec_params* p, const int64_t* seqs, int64_t M, int32_t n, const float* wn,
                          const float* bn, int nout, float* X, float* QKV, int32_t* err, hipStream_t st);
 bool gr_sasrec_tail_ok(const gr_sasrec_params* p, int32_t n);
+int gr_sasrec_tail_h_launch(const gr_sasrec_params* p, int blk, const float* X, const float* Hs,
+                            int64_t B, int32_t n, float* out, hipStream_t st);
 // p[0 .. count) = value (32-bit words); a kernel, so it replays inside captured graphs (fill.hip).
 int gr_fill32_launch(void* p, uint32_t value, int64_t count, hipStream_t st);
 int gr_linear_exact_launch(const float* x, int64_t m, int32_t k, const float* w, int32_t n,

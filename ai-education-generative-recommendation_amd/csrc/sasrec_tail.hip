@@ -205,6 +205,158 @@ __global__ __launch_bounds__(ST_NT) void sas_tail_kernel(const SasTailArgs a, co
   for (int c = tid; c < d; c += ST_NT) out[b * d + c] = l1[c];
 }
 
+// The same final block without K or V: with one query per sequence, attention needs only the
+// LayerNorm output H of every position (functional.py:6578-6600 reassociated):
+//   q . K_j = q . (Wk H_j + bk) = (Wk_h^T q_h) . H_j + q_h . bk_h   -- the last term is the same for
+//                                                                    every key: softmax drops it
+//   sum_j p_j V_j = Wv_h (sum_j p_j H_j) + bv_h                      -- the p_j of a head sum to 1
+// so per sequence: q = Wq h + bq (scaled), q'_h = Wk_h^T q_h (a d-vector per head), scores q'_h . H_j,
+// softmax, u_h = sum_j p_j H_j, o_h = Wv_h u_h + bv_h, then out-proj, FFN and the last LayerNorm as
+// in sas_tail_kernel.  The final block's K|V projection over all B n rows (2 d^2 flop per token)
+// is never computed, and the kernel reads the n d-rows of H instead of the n 2d-rows of K|V.  fp32;
+// the reassociation rounds differently from the reference formulation, within the logits
+// tolerance (tests/test_sasrec_gpu.py).
+__global__ __launch_bounds__(ST_NT) void sas_tail_h_kernel(const SasTailArgs a, const float* __restrict__ X,
+                                                         const float* __restrict__ Hs, const float* __restrict__ wk,
+                                                         const float* __restrict__ wv, const float* __restrict__ bv,
+                                                         float* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) float xl[ST_MAX_D], hl[ST_MAX_D], q[ST_MAX_D], o[ST_MAX_D],
+      x1[ST_MAX_D], l1[ST_MAX_D], fh[ST_MAX_MLP], qk[ST_MAX_H * ST_MAX_D], u[ST_MAX_H * ST_MAX_D],
+      P[ST_MAX_H * ST_MAX_N], part[ST_NT * 4], red[2 * ST_MAX_H * ST_NW], stat[2];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t b = blockIdx.x;
+  const int d = a.d, n = a.n, H = a.heads, hd = d / H;
+  const int L = d >> 2, gpw = 64 / L, l = lane & (L - 1);
+  const int grp = wave * gpw + lane / L, ngrp = ST_NW * gpw;
+  const float* xr = X + (b * n + n - 1) * d;
+  const float* hb = Hs + b * n * d;         // row j: LN_a of position j (keys and values)
+  for (int c = tid; c < d; c += ST_NT) {
+    xl[c] = xr[c];
+    hl[c] = hb[(int64_t)(n - 1) * d + c];
+  }
+  __syncthreads();
+  st_gemv(a.wq, a.bq, hl, d, d, q);
+  __syncthreads();
+  for (int c = tid; c < d; c += ST_NT) q[c] *= a.scale;   // q * sqrt(1/hd) (functional.py:6578)
+  __syncthreads();
+  {   // q'_h[c] = sum_r Wk[h hd + r][c] q[h hd + r]: rows of Wk read coalesced across c, the r range
+      // split over RG thread groups (all 512 threads busy at H d = 128), partials summed in order
+    const int hdn = H * d, RG = hdn >= ST_NT ? 1 : ST_NT / hdn, rl = (hd + RG - 1) / RG;
+    for (int i = tid; i < hdn * RG; i += ST_NT) {
+      const int idx = i % hdn, rg = i / hdn, hh = idx / d, c = idx - hh * d;
+      const int r0 = rg * rl, r1 = r0 + rl < hd ? r0 + rl : hd;
+      const float* wc = wk + (int64_t)hh * hd * d + c;
+      const float* qh = q + hh * hd;
+      float acc = 0.f;
+#pragma unroll 8
+      for (int r = r0; r < r1; ++r) acc = fmaf(wc[(int64_t)r * d], qh[r], acc);
+      part[rg * hdn + idx] = acc;
+    }
+    __syncthreads();
+    for (int idx = tid; idx < hdn; idx += ST_NT) {
+      float t = part[idx];
+      for (int rg = 1; rg < RG; ++rg) t += part[rg * hdn + idx];
+      qk[idx] = t;
+    }
+  }
+  __syncthreads();
+  // scores: one lane group per key, lane l holds H_j[4l .. 4l+3]; every head dots the whole row
+  for (int j0 = grp; j0 < n; j0 += ST_U * ngrp) {
+    f32x4 h4[ST_U];
+#pragma unroll
+    for (int uu = 0; uu < ST_U; ++uu) {
+      const int j = j0 + uu * ngrp;
+      h4[uu] = j < n ? *reinterpret_cast<const f32x4*>(hb + (int64_t)j * d + 4 * l) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int uu = 0; uu < ST_U; ++uu) {
+      const int j = j0 + uu * ngrp;
+#pragma unroll
+      for (int hh = 0; hh < ST_MAX_H; ++hh) {
+        if (hh >= H) break;
+        const f32x4 q4 = *reinterpret_cast<const f32x4*>(qk + hh * d + 4 * l);
+        float sc = h4[uu][0] * q4[0];
+        sc = fmaf(h4[uu][1], q4[1], sc);
+        sc = fmaf(h4[uu][2], q4[2], sc);
+        sc = fmaf(h4[uu][3], q4[3], sc);
+        sc = seg_sum(sc, L);
+        if (j < n && l == 0) P[hh * n + j] = sc;
+      }
+    }
+  }
+  __syncthreads();
+  // softmax over keys per head (functional.py:6590): max, exp, sum
+  for (int hh = 0; hh < H; ++hh) {
+    float m = -INFINITY;
+    for (int j = tid; j < n; j += ST_NT) m = fmaxf(m, P[hh * n + j]);
+    for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off));
+    if (lane == 0) red[hh * ST_NW + wave] = m;
+  }
+  __syncthreads();
+  for (int hh = 0; hh < H; ++hh) {
+    float m = red[hh * ST_NW];
+    for (int w2 = 1; w2 < ST_NW; ++w2) m = fmaxf(m, red[hh * ST_NW + w2]);
+    float sm = 0.f;
+    for (int j = tid; j < n; j += ST_NT) {
+      const float e = __expf(P[hh * n + j] - m);
+      P[hh * n + j] = e;
+      sm += e;
+    }
+    for (int off = 32; off > 0; off >>= 1) sm += __shfl_xor(sm, off);
+    if (lane == 0) red[ST_MAX_H * ST_NW + hh * ST_NW + wave] = sm;
+  }
+  __syncthreads();
+  // u_h = sum_j p_j H_j, one head at a time through the group partials
+  for (int hh = 0; hh < H; ++hh) {
+    const float* sb = red + ST_MAX_H * ST_NW + hh * ST_NW;
+    float tot = sb[0];
+    for (int w2 = 1; w2 < ST_NW; ++w2) tot += sb[w2];
+    const float inv = 1.0f / tot;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int j0 = grp; j0 < n; j0 += ST_U * ngrp) {
+      f32x4 h4[ST_U];
+#pragma unroll
+      for (int uu = 0; uu < ST_U; ++uu) {
+        const int j = j0 + uu * ngrp;
+        h4[uu] = j < n ? *reinterpret_cast<const f32x4*>(hb + (int64_t)j * d + 4 * l) : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+      for (int uu = 0; uu < ST_U; ++uu) {
+        const int j = j0 + uu * ngrp;
+        const float pj = j < n ? P[hh * n + j] * inv : 0.f;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc[e] = fmaf(pj, h4[uu][e], acc[e]);
+      }
+    }
+    *reinterpret_cast<f32x4*>(part + grp * d + 4 * l) = acc;
+    __syncthreads();
+    for (int c = tid; c < d; c += ST_NT) {
+      float t = 0.f;
+      for (int g = 0; g < ngrp; ++g) t += part[g * d + c];
+      u[hh * d + c] = t;
+    }
+    __syncthreads();
+  }
+  for (int hh = 0; hh < H; ++hh)                                // o_h = Wv_h u_h + bv_h
+    st_gemv(wv + (int64_t)hh * hd * d, bv + hh * hd, u + hh * d, hd, d, o + hh * hd);
+  __syncthreads();
+  st_gemv(a.wo, a.bo, o, d, d, x1);                             // out_proj
+  __syncthreads();
+  for (int c = tid; c < d; c += ST_NT) x1[c] += xl[c];            // residual (model.py:84)
+  __syncthreads();
+  st_layernorm(x1, a.ln_f_w, a.ln_f_b, d, a.eps, l1, stat);
+  st_gemv(a.w1, a.b1, l1, a.mlp, d, fh);
+  __syncthreads();
+  for (int c = tid; c < a.mlp; c += ST_NT) fh[c] = fh[c] < 0.f ? 0.f : fh[c];
+  __syncthreads();
+  st_gemv(a.w2, a.b2, fh, d, a.mlp, o);                         // W2 f + b2 (o reused)
+  __syncthreads();
+  for (int c = tid; c < d; c += ST_NT) x1[c] += o[c];             // residual (model.py:94)
+  __syncthreads();
+  st_layernorm(x1, a.ln_w, a.ln_b, d, a.eps, l1, stat);         // last_layernorm (model.py:96)
+  for (int c = tid; c < d; c += ST_NT) out[b * d + c] = l1[c];
+}
+
 }  // namespace gr
 
 // Returns GR_ERR_UNSUPPORTED for shapes outside the kernel's limits (the caller keeps the
@@ -240,4 +392,31 @@ int gr_sasrec_tail_launch(const gr_sasrec_params* p, int blk, const float* X, co
   a.scale = (float)std::sqrt(1.0 / (double)(d / H));
   hipLaunchKernelGGL(sas_tail_kernel, dim3((unsigned)B), dim3(ST_NT), 0, st, a, X, KV, out);
   return check_launch("sasrec tail");
+}
+
+// The K/V-free form (sas_tail_h_kernel): Hs [B, n, d] = LN_a(X) of the final block (the LayerNorm
+// output the K|V projection would have read).  Same shape limits as gr_sasrec_tail_launch.
+int gr_sasrec_tail_h_launch(const gr_sasrec_params* p, int blk, const float* X, const float* Hs,
+                            int64_t B, int32_t n, float* out, hipStream_t st) {
+  using namespace gr;
+  const int d = p->d, H = p->n_heads;
+  if (!gr_sasrec_tail_ok(p, n) || B > 0x7fffffffLL) return GR_ERR_UNSUPPORTED;
+  SasTailArgs a;
+  a.ln_a_w = p->attn_ln_w[blk]; a.ln_a_b = p->attn_ln_b[blk];
+  a.wq = p->in_proj_w[blk];     a.bq = p->in_proj_b[blk];
+  a.wo = p->out_proj_w[blk];    a.bo = p->out_proj_b[blk];
+  a.ln_f_w = p->ffn_ln_w[blk];  a.ln_f_b = p->ffn_ln_b[blk];
+  a.w1 = p->ffn1_w[blk];        a.b1 = p->ffn1_b[blk];
+  a.w2 = p->ffn2_w[blk];        a.b2 = p->ffn2_b[blk];
+  a.ln_w = p->last_ln_w;        a.ln_b = p->last_ln_b;
+  const float* wk = p->in_proj_w[blk] + (int64_t)d * d;
+  const float* wv = p->in_proj_w[blk] + 2LL * d * d;
+  const float* bv = p->in_proj_b[blk] + 2 * d;
+  const float* ptrs[] = {a.wq, a.wo, a.w1, a.w2, wv, X, Hs};
+  for (const float* q : ptrs)
+    if (!aligned16(q)) return GR_ERR_UNSUPPORTED;
+  a.d = d; a.n = n; a.heads = H; a.mlp = p->mlp; a.eps = p->eps;
+  a.scale = (float)std::sqrt(1.0 / (double)(d / H));
+  hipLaunchKernelGGL(sas_tail_h_kernel, dim3((unsigned)B), dim3(ST_NT), 0, st, a, X, Hs, wk, wv, bv, out);
+  return check_launch("sasrec tail (H form)");
 }

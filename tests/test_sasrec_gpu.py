@@ -239,6 +239,35 @@ def test_embed_proj_equals_two_kernels(B, blocks, dev):
         assert torch.equal(pr, p0), k
 
 
+@pytest.mark.parametrize("d,heads,n,blocks,B", [(128, 1, 200, 2, 33), (128, 2, 77, 1, 9), (128, 4, 130, 3, 5),
+                                                (64, 2, 100, 2, 17), (32, 8, 90, 1, 6)])
+def test_tail_h_form_vs_kv_form_and_oracle(d, heads, n, blocks, B, dev):
+    """Option tail_h: the final block's one-query tail on LN_a(X) with q . K and p . V reassociated
+    through W_k / W_v (no K|V projection) against the K|V form and the CPU oracle: predict logits
+    within the row-scaled tolerance, last hidden states within 5e-5; row-tile (d 128) and per-op
+    (d 64 / 32, n > 64) paths, 1-8 heads."""
+    from gr_amd import _lib, synth
+    from oracle import sasrec_oracle
+    items = 600
+    p = synth.sasrec_params(d, n, blocks, heads, 2 * d if d < 128 else 64, dev)
+    m = synth.sasrec_model(items, p, dev, seed=d + heads + n)
+    seqs = synth.sequences(B, n, items, 5 + n, dev)
+    try:
+        _lib.set_option("tail_h", 0)
+        kv_h, kv_p = m.last_hidden(seqs).cpu(), m.predict(seqs).cpu()
+        _lib.set_option("tail_h", 1)
+        h_h, h_p = m.last_hidden(seqs).cpu(), m.predict(seqs).cpu()
+    finally:
+        _lib.set_option("tail_h", 1)
+    sd = {k: v.detach().cpu() for k, v in m.state_dict().items()}
+    ref_f = sasrec_oracle.forward(seqs.cpu(), sd, blocks, heads, 1e-8)
+    ref = sasrec_oracle.predict(seqs.cpu(), sd, blocks, heads, 1e-8)
+    assert (h_h - ref_f[:, -1, :]).abs().max().item() < 5e-5
+    assert (h_h - kv_h).abs().max().item() < 5e-5
+    for got in (h_p, kv_p):
+        assert ((got - ref).abs() / ref.abs().amax(1, keepdim=True)).max().item() <= TOL
+
+
 def test_score_matches_linear_and_rank_consistency(dev):
     """Fused-rank hard part 3: every logit sees the same fp32 fma chain, so the target's score
     recomputed on any tile equals its entry in the logits (strict '>' never counts the target)."""
