@@ -239,18 +239,25 @@ __global__ __launch_bounds__(ST_NT) void sas_tail_h_kernel(const SasTailArgs a, 
   __syncthreads();
   for (int c = tid; c < d; c += ST_NT) q[c] *= a.scale;   // q * sqrt(1/hd) (functional.py:6578)
   __syncthreads();
-  {   // q'_h[c] = sum_r Wk[h hd + r][c] q[h hd + r]: rows of Wk read coalesced across c, the r range
-      // split over RG thread groups (all 512 threads busy at H d = 128), partials summed in order
-    const int hdn = H * d, RG = hdn >= ST_NT ? 1 : ST_NT / hdn, rl = (hd + RG - 1) / RG;
-    for (int i = tid; i < hdn * RG; i += ST_NT) {
-      const int idx = i % hdn, rg = i / hdn, hh = idx / d, c = idx - hh * d;
+  {   // q'_h[c] = sum_r Wk[h hd + r][c] q[h hd + r]: each thread a float4 of columns over one of RG
+      // r ranges (rows of Wk read coalesced, all of a thread's rows in flight together), the RG
+      // partials summed in order
+    const int hdn = H * d, hdn4 = hdn >> 2, cq = d >> 2;
+    const int RG = hdn4 >= ST_NT ? 1 : ST_NT / hdn4, rl = (hd + RG - 1) / RG;
+    for (int i = tid; i < hdn4 * RG; i += ST_NT) {
+      const int idx4 = i % hdn4, rg = i / hdn4, hh = idx4 / cq, c4 = idx4 - hh * cq;
       const int r0 = rg * rl, r1 = r0 + rl < hd ? r0 + rl : hd;
-      const float* wc = wk + (int64_t)hh * hd * d + c;
+      const float* wc = wk + (int64_t)hh * hd * d + 4 * c4;
       const float* qh = q + hh * hd;
-      float acc = 0.f;
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll 8
-      for (int r = r0; r < r1; ++r) acc = fmaf(wc[(int64_t)r * d], qh[r], acc);
-      part[rg * hdn + idx] = acc;
+      for (int r = r0; r < r1; ++r) {
+        const f32x4 w4 = *reinterpret_cast<const f32x4*>(wc + (int64_t)r * d);
+        const float qr = qh[r];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc[e] = fmaf(w4[e], qr, acc[e]);
+      }
+      *reinterpret_cast<f32x4*>(part + rg * hdn + 4 * idx4) = acc;
     }
     __syncthreads();
     for (int idx = tid; idx < hdn; idx += ST_NT) {
@@ -412,7 +419,7 @@ int gr_sasrec_tail_h_launch(const gr_sasrec_params* p, int blk, const float* X, 
   const float* wk = p->in_proj_w[blk] + (int64_t)d * d;
   const float* wv = p->in_proj_w[blk] + 2LL * d * d;
   const float* bv = p->in_proj_b[blk] + 2 * d;
-  const float* ptrs[] = {a.wq, a.wo, a.w1, a.w2, wv, X, Hs};
+  const float* ptrs[] = {a.wq, a.wo, a.w1, a.w2, wk, wv, X, Hs};
   for (const float* q : ptrs)
     if (!aligned16(q)) return GR_ERR_UNSUPPORTED;
   a.d = d; a.n = n; a.heads = H; a.mlp = p->mlp; a.eps = p->eps;
