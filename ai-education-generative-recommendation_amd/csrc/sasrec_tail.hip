@@ -237,8 +237,6 @@ __global__ __launch_bounds__(ST_NT) void sas_tail_h_kernel(const SasTailArgs a, 
   __syncthreads();
   st_gemv(a.wq, a.bq, hl, d, d, q);
   __syncthreads();
-  for (int c = tid; c < d; c += ST_NT) q[c] *= a.scale;   // q * sqrt(1/hd) (functional.py:6578)
-  __syncthreads();
   {   // q'_h[c] = sum_r Wk[h hd + r][c] q[h hd + r]: each thread a float4 of columns over one of RG
       // r ranges (rows of Wk read coalesced, all of a thread's rows in flight together), the RG
       // partials summed in order
@@ -253,7 +251,7 @@ __global__ __launch_bounds__(ST_NT) void sas_tail_h_kernel(const SasTailArgs a, 
 #pragma unroll 8
       for (int r = r0; r < r1; ++r) {
         const f32x4 w4 = *reinterpret_cast<const f32x4*>(wc + (int64_t)r * d);
-        const float qr = qh[r];
+        const float qr = qh[r] * a.scale;   // q * sqrt(1/hd) (functional.py:6578)
 #pragma unroll
         for (int e = 0; e < 4; ++e) acc[e] = fmaf(w4[e], qr, acc[e]);
       }

@@ -58,15 +58,20 @@ def sas_flop_per_user(d, n, items, mlp=64, blocks=2):
     return blocks * per_block + 2 * d * (items + 1)
 
 
-def sas_exec_flop_per_user(d, n, items, mlp=64, blocks=2, causal=True):
+def sas_exec_flop_per_user(d, n, items, mlp=64, blocks=2, causal=True, tail_h=False, heads=1):
     """Flops the kernels execute per user: every block but the last in full,
     attention over the causal n(n+1)/2 query-key pairs (``causal``; the one-wave C3 kernel computes
-    the whole n x n tile, ``causal=False``); the last block's K|V projection for all n tokens and
-    everything else at position n-1 only (q, one query's attention, out-proj, FFN); scoring
+    the whole n x n tile, ``causal=False``); the last block at position n-1 only (q, one query's
+    attention, out-proj, FFN) plus, in the K|V form, the K|V projection of all n tokens -- the
+    H-form tail (``tail_h``, sas_tail_h_kernel) instead computes W_k^T q and W_v u (2 d^2 each)
+    and dots every head's d-vector with the n LayerNorm rows (4 n d per head); scoring
     2*d*(items+1) (``items`` = -1: forward only)."""
     pairs = n * (n + 1) // 2 if causal else n * n
     full = 2 * n * d * 3 * d + 4 * pairs * d + 2 * n * d * d + 4 * n * d * mlp
-    last = 2 * n * d * 2 * d + 2 * d * d + 4 * n * d + 2 * d * d + 4 * d * mlp
+    if tail_h:
+        last = 2 * d * d + 2 * d * d + 4 * n * d * heads + 2 * d * d + 2 * d * d + 4 * d * mlp
+    else:
+        last = 2 * n * d * 2 * d + 2 * d * d + 4 * n * d + 2 * d * d + 4 * d * mlp
     return (blocks - 1) * full + last + 2 * d * (items + 1)
 
 
@@ -437,8 +442,9 @@ def bench_sas_c5(a, world, rank, dev, time_it=True):
     topk_ms = kernel_ms(lambda: ops.score_topk(h, shard, 10, lo, thresholds=ts, mask_col0=(lo == 0)))
     fwd_ms = kernel_ms(lambda: model.last_hidden(lseqs))
     fl_ref = sas_flop_per_user(d, n, items)
-    fl_exe = sas_exec_flop_per_user(d, n, items, causal=True)
-    fwd_exe = sas_exec_flop_per_user(d, n, -1, causal=True)
+    th = gr_amd._lib.get_option("tail_h") != 0   # the C5 forward's final block: H form or K|V form
+    fl_exe = sas_exec_flop_per_user(d, n, items, causal=True, tail_h=th)
+    fwd_exe = sas_exec_flop_per_user(d, n, -1, causal=True, tail_h=th)
     res = {"metric": "seqs_scored/s", "value": B * steps / wall, "unit": "seqs/s", "scaling": "strong",
             "ms_per_step": wall / steps * 1e3, "steps": steps,
             "config": {"workload": "sas_c5: SASRec d 128, n 200, 2 blocks, 1M-item catalog, rank + top-10",
