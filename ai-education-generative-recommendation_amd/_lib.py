@@ -64,6 +64,9 @@ SIGNATURES = {
     "gr_rq_mlp_f32": (ctypes.c_int, [_vp, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
     "gr_mlp_exact_f32": (ctypes.c_int, [_vp, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _f32, _i32,
                                         _vp, _vp, _sz, _vp]),
+    "gr_mlp_exact_groups_f32": (ctypes.c_int, [_vp, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _f32,
+                                               _i32, _vp, _i64, _vp, _vp]),
+    "gr_mkl_plan": (_i32, [_i64, _i32, _i32, _c_int_p, _c_int_p]),
     "gr_rq_encode_sk_workspace_bytes": (_sz, [_i64, _i32, _i32, _vp]),
     "gr_rq_encode_sk_f32": (ctypes.c_int, [_vp, _i64, _i32, _i32, _vp, _vp, _vp, _i32, _vp, _i64,
                                            _vp, _vp, _sz, _vp]),

@@ -58,7 +58,7 @@ static std::atomic<int64_t> g_topk_impl{1};
 static std::atomic<int64_t> g_rt_w8{1};
 // lin_w8 (1 (default): gr_linear_f32's 128x128 / 128x64 tiles run 8 waves per workgroup; 0: 4)
 static std::atomic<int64_t> g_lin_w8{1};
-// lin_wres (1 (default): gr_linear_f32 with k = 128, n % 128 == 0, no residual and m >= 64 x 256
+// lin_wres (1 (default): gr_linear_f32 with k = 128, n % 128 == 0, no residual and m >= 96 x 256
 // runs the persistent kernel that keeps 32-column slices of w resident in registers; 0: the tiled
 // kernel).  Bitwise the same results; A/B timing.
 static std::atomic<int64_t> g_lin_wres{1};

@@ -113,13 +113,111 @@ __device__ __forceinline__ float aten_rowsq(At at, int e) {
   return f;
 }
 
-// k-block boundary of the reference's CPU nn.Linear (MKL sgemm) for inner size K (oracle/rq_exact.c
-// rqx_kblock): one block below 384, two blocks [0, kb), [kb, K) up to 768; -1 = not characterised.
-__host__ __device__ inline int mkl_kblock(int K) {
-  if (K < 384) return K;
-  if (K > 768) return -1;
-  return (((K + 1) / 2) + 3) & ~3;
+// Accumulation order of one reference CPU sgemm call (RQ-VAE/models/layers.py:23 nn.Linear,
+// vq.py:73 matmul; MKL 2024.2 in torch 2.10, 8 threads, AVX-512 -- oracle/rq_exact.c rqx_plan,
+// verified against torch by scripts/mkl_order_probe.py and tests/test_rq_exact_oracle.py).  It
+// depends on the CALL's row count M, inner size K and output count N:
+//   MKL_CHAIN   y = b; per k block of width kb: acc = 0, fma chain over k in order; y = y + acc
+//   MKL_GEMV16  (M = 1) s = x0 w0; 16-lane vector over k = 1.. with lane 0 starting at s, halving
+//               reduction; the (K-1) % 16 tail as a power-of-two-wide vector, lane 0 = s; y = s + b
+//   MKL_SMALL16 (2 <= M <= 15, see below) lane l accumulates k = l (mod 16) in order;
+//               g_i = ((a_i + a_i+4) + a_i+8) + a_i+12; y = ((g0 + g1) + (g2 + g3)) + b
+enum { MKL_CHAIN = 0, MKL_GEMV16 = 1, MKL_SMALL16 = 2 };
+struct MklPlan {
+  int kind;
+  int kb;   // MKL_CHAIN block width
+};
+
+__host__ __device__ inline MklPlan mkl_plan(int64_t M, int K, int N) {
+  int kb = K;
+  if (K == 384) kb = M >= 256 ? 384 : 192;
+  else if (K > 384 && K <= 768) kb = (((K + 1) / 2) + 3) & ~3;
+  else if (K > 768) kb = 384;
+  if (M == 1) return MklPlan{MKL_GEMV16, kb};
+  if (M >= 2 && M <= 15 && M <= K / 24 &&
+      (N % 256 == 0 || K % 256 == 0 || M <= 3 || M * (int64_t)N * K <= 256000))
+    return MklPlan{MKL_SMALL16, kb};
+  return MklPlan{MKL_CHAIN, kb};
 }
+
+// The envelope where the restated order was checked against torch on the fixture host; outside it
+// the kernels still compute in mkl_plan's order, but bitwise equality is not claimed (gr_mkl_plan).
+__host__ __device__ inline bool mkl_plan_pinned(int64_t M, int K, int N) {
+  const MklPlan p = mkl_plan(M, K, N);
+  if (p.kind == MKL_GEMV16) return K <= 2048 && (N % 32 == 0 || ((N == 8 || N == 16) && K <= 1024));
+  if (p.kind == MKL_SMALL16) return N >= 2 && K <= 4096;
+  if (K < 384) return M >= 16 || N % 8 == 0;
+  if (K == 384) return M >= 256;
+  if (K <= 768) return K % 128 == 0;
+  return false;
+}
+
+// b + x . w in plan p's order; xa(k), wa(k) return the operands (the quantizer's r . c: b = 0).
+template <typename XA, typename WA>
+__device__ __forceinline__ float mkl_dot(MklPlan p, XA xa, WA wa, int K, float b) {
+#pragma clang fp contract(off)
+  if (p.kind == MKL_CHAIN) {
+    float y = b;
+    for (int k0 = 0; k0 < K; k0 += p.kb) {
+      const int k1 = k0 + p.kb < K ? k0 + p.kb : K;
+      float acc = 0.f;
+      for (int k = k0; k < k1; ++k) acc = fmaf(xa(k), wa(k), acc);
+      y = y + acc;
+    }
+    return y;
+  }
+  float a[16];
+#pragma unroll
+  for (int l = 0; l < 16; ++l) a[l] = 0.f;
+  if (p.kind == MKL_SMALL16) {
+    int k0 = 0;
+    for (; k0 + 16 <= K; k0 += 16)
+#pragma unroll
+      for (int l = 0; l < 16; ++l) a[l] = fmaf(xa(k0 + l), wa(k0 + l), a[l]);
+#pragma unroll
+    for (int l = 0; l < 16; ++l)
+      if (k0 + l < K) a[l] = fmaf(xa(k0 + l), wa(k0 + l), a[l]);
+    float g[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) g[q] = ((a[q] + a[q + 4]) + a[q + 8]) + a[q + 12];
+    return ((g[0] + g[1]) + (g[2] + g[3])) + b;
+  }
+  // MKL_GEMV16
+  float s = fmaf(xa(0), wa(0), 0.f);
+  const int nmain = (K - 1) >> 4;
+  if (nmain > 0) {
+    a[0] = s;
+    for (int t = 0; t < nmain; ++t)
+#pragma unroll
+      for (int l = 0; l < 16; ++l) a[l] = fmaf(xa(1 + 16 * t + l), wa(1 + 16 * t + l), a[l]);
+#pragma unroll
+    for (int w = 8; w >= 1; w >>= 1)
+#pragma unroll
+      for (int l = 0; l < w; ++l) a[l] = a[l] + a[l + w];
+    s = a[0];
+  }
+  const int k1 = 1 + 16 * nmain, r = K - k1;
+  if (r > 0) {
+    int wd = 1;
+    while (wd < r) wd <<= 1;
+#pragma unroll
+    for (int l = 0; l < 16; ++l) a[l] = 0.f;
+    a[0] = s;
+#pragma unroll
+    for (int l = 0; l < 16; ++l)
+      if (l < r) a[l] = fmaf(xa(k1 + l), wa(k1 + l), a[l]);
+#pragma unroll
+    for (int w = 8; w >= 1; w >>= 1)
+      if (w < wd)
+#pragma unroll
+        for (int l = 0; l < w; ++l) a[l] = a[l] + a[l + w];
+    s = a[0];
+  }
+  return s + b;
+}
+
+// k-block width of a long call (>= 256 rows) for inner size K: mkl_plan's MKL_CHAIN width.
+__host__ __device__ inline int mkl_kblock(int K) { return mkl_plan(1 << 20, K, 256).kb; }
 
 // f32-input MFMA 16x16x4: an fma chain over its four k slots in ascending order (lane group
 // l >> 4 = k; profiles/r03_mfma_order.txt).  Lane l supplies A[i = l&15][k = l>>4] and
@@ -155,6 +253,12 @@ int gr_embed_proj_launch(const gr_sasrec_params* p, const int64_t* seqs, int64_t
 bool gr_sasrec_tail_ok(const gr_sasrec_params* p, int32_t n);
 int gr_sasrec_tail_h_launch(const gr_sasrec_params* p, int blk, const float* X, const float* Hs,
                             int64_t B, int32_t n, float* out, hipStream_t st);
+int gr_rq_rows_launch(const float* x, int64_t n, int64_t call_m, const int64_t* group_ptr, int64_t n_groups,
+                      int32_t n_linear, const int32_t* dims, const float* const* weights, const float* const* biases,
+                      const float* const* bn_mean, const float* const* bn_var, const float* const* bn_w,
+                      const float* const* bn_b, float bn_eps, int32_t act, int32_t L, const int32_t* K,
+                      const float* const* codebooks, float* z_out, int64_t* idx_out, float* best_out, float* gap_out,
+                      hipStream_t st);
 // p[0 .. count) = value (32-bit words); a kernel, so it replays inside captured graphs (fill.hip).
 int gr_fill32_launch(void* p, uint32_t value, int64_t count, hipStream_t st);
 int gr_linear_exact_launch(const float* x, int64_t m, int32_t k, const float* w, int32_t n,

@@ -16,9 +16,10 @@
 // reproduce the reference's CPU nn.Linear bit for bit (oracle/rq_exact.c): the LDS image holds each
 // 8-deep slice de-interleaved (even features in the lane-half-0 float4, odd ones in the half-1
 // float4), so MFMA step s feeds k = 8kc + 2s then 8kc + 2s + 1 -- one fma chain over k in order;
-// MKL's k blocking (mkl_kblock) restarts the chain at the block boundary, and the epilogue adds
-// y = bias; y += block 0; y += block 1.  Optional eval BatchNorm1d after the Linear in torch's CPU
-// formula (layers.py:25-26): a = w / sqrt(var + eps), y = fma(y, a, fma(-mean, a, b)).
+// MKL's k blocking (mkl_plan's MKL_CHAIN width kb, any even width) restarts the chain at every
+// block boundary: y = bias; y += block 0; y += block 1; ...  Optional eval BatchNorm1d after the
+// Linear in torch's CPU formula (layers.py:25-26): a = w / sqrt(var + eps), y = fma(y, a, fma(-mean,
+// a, b)).  Calls whose MKL order is not a chain (1-15 rows) run in rq_rows.hip.
 #include "gr_common.h"
 
 namespace gr {
@@ -104,8 +105,20 @@ __global__ __launch_bounds__(NT, NT / 128) void linear_f32_kernel(
     for (int b = 0; b < TN; ++b)
 #pragma unroll
       for (int v = 0; v < 16; ++v) acc[a][b][v] = 0.f;
-  f32x16 sv[EXACT ? TM : 1][EXACT ? TN : 1];   // EXACT: the first k block's chain
-  bool split = false;
+  // EXACT: y so far (bias, then + each finished k block's chain); ksplit = the block width kb
+  f32x16 sv[EXACT ? TM : 1][EXACT ? TN : 1];
+  int knext = EXACT ? ksplit : 0;   // next block boundary (k index)
+  if constexpr (EXACT) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int col = n0 + wn * (BN / WN) + j * 32 + r;
+      const float bv = (bias != nullptr && col < N) ? bias[col] : 0.f;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int v = 0; v < 16; ++v) sv[i][j][v] = bv;
+    }
+  }
 
   const int nk = (K + LIN_BK - 1) / LIN_BK;
   gload(0);
@@ -118,19 +131,6 @@ __global__ __launch_bounds__(NT, NT / 128) void linear_f32_kernel(
     const float* Bs = lds[cur] + (BM + wn * (BN / WN) + r) * LIN_PITCH + 4 * h;
 #pragma unroll
     for (int kc = 0; kc < LIN_BK / 8; ++kc) {
-      if constexpr (EXACT) {
-        if (kt * LIN_BK + kc * 8 == ksplit) {   // MKL's second k block: a fresh chain
-#pragma unroll
-          for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int j = 0; j < TN; ++j) {
-              sv[i][j] = acc[i][j];
-#pragma unroll
-              for (int v = 0; v < 16; ++v) acc[i][j][v] = 0.f;
-            }
-          split = true;
-        }
-      }
       f32x4 a[TM], b[TN];
 #pragma unroll
       for (int t = 0; t < TM; ++t)
@@ -139,11 +139,27 @@ __global__ __launch_bounds__(NT, NT / 128) void linear_f32_kernel(
       for (int t = 0; t < TN; ++t)
         b[t] = *reinterpret_cast<const f32x4*>(Bs + t * 32 * LIN_PITCH + kc * 8);
 #pragma unroll
-      for (int s = 0; s < 4; ++s)
+      for (int s = 0; s < 4; ++s) {
+        if constexpr (EXACT) {   // step s feeds k = 8kc + 2s, +1: a block edge starts a fresh chain
+          if (kt * LIN_BK + kc * 8 + 2 * s == knext) {
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+              for (int j = 0; j < TN; ++j) {
+#pragma unroll
+                for (int v = 0; v < 16; ++v) {
+                  sv[i][j][v] = sv[i][j][v] + acc[i][j][v];
+                  acc[i][j][v] = 0.f;
+                }
+              }
+            knext += ksplit;
+          }
+        }
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
           for (int j = 0; j < TN; ++j) acc[i][j] = mfma32(a[i][s], b[j][s], acc[i][j]);
+      }
     }
     if (kt + 1 < nk) swrite(cur ^ 1);
     __syncthreads();
@@ -173,10 +189,8 @@ __global__ __launch_bounds__(NT, NT / 128) void linear_f32_kernel(
         const int64_t row = m0 + wm * (BM / WM) + i * 32 + (v & 3) + 8 * (v >> 2) + 4 * h;
         if (cok && row < M) {
           float o = acc[i][j][v];
-          if constexpr (EXACT) {   // y = bias; y += block 0; y += block 1 (MKL); then BatchNorm
-            o = bias != nullptr ? bv : 0.f;
-            if (split) o = o + sv[i][j][v];
-            o = o + acc[i][j][v];
+          if constexpr (EXACT) {   // y = bias; y += block 0; y += block 1; ... (MKL); then BatchNorm
+            o = sv[i][j][v] + acc[i][j][v];
             if (bn.var != nullptr) {
               const float inv = 1.0f / sqrtf(bn.var[col] + bn.eps);
               const float a = bn.w != nullptr ? inv * bn.w[col] : inv;
@@ -379,13 +393,13 @@ int gr_linear_exact_launch(const float* x, int64_t m, int32_t k, const float* w,
   if (!x || !w || !y) return fail(GR_ERR_ARG, "gr_linear_exact: null pointer");
   if (k % 4 != 0 || !aligned16(x) || !aligned16(w))
     return fail(GR_ERR_UNSUPPORTED, "gr_linear_exact: k % 4 == 0 and 16-byte aligned x, w");
-  const int kb = mkl_kblock(k);
-  if (kb < 0 || (kb < k && kb % 8 != 0))
-    return fail(GR_ERR_UNSUPPORTED, "gr_linear_exact: in_features outside the characterised MKL k blocking");
+  const MklPlan pl = mkl_plan(m, k, n);
+  if (pl.kind != MKL_CHAIN || pl.kb % 2 != 0)
+    return fail(GR_ERR_UNSUPPORTED, "gr_linear_exact: MKL's order for this call is not a k-block chain");
   if ((bn_mean == nullptr) != (bn_var == nullptr)) return fail(GR_ERR_ARG, "gr_linear_exact: bn mean / var");
   const BnEval bn{bn_mean, bn_var, bn_w, bn_b, bn_eps};
-  const int ks = kb < k ? kb : -1;
-  // 4-wave 128 x 64 tiles: the second k block's chain doubles the accumulators (larger tiles spill)
+  const int ks = pl.kb < k ? pl.kb : (1 << 30);
+  // 4-wave 128 x 64 tiles: the running y beside the chain doubles the accumulators (larger tiles spill)
   if (n > 32)
     return launch_tile<128, 64, 2, 2, 256, true>(x, m, k, w, n, bias, nullptr, 0, act, y, n, stream, ks, bn);
   return launch_tile<128, 32, 4, 1, 256, true>(x, m, k, w, n, bias, nullptr, 0, act, y, n, stream, ks, bn);

@@ -342,7 +342,7 @@ static int launch_quantize(const float* z, int64_t n, int e, int L, const RQLeve
 }
 
 static int check_levels(int32_t e, int32_t L, const int32_t* K, const float* const* cbs) {
-  if (e < 1 || e > 64) return fail(GR_ERR_UNSUPPORTED, "rq: 1 <= e_dim <= 64");
+  if (e < 1 || e > 4096) return fail(GR_ERR_UNSUPPORTED, "rq: 1 <= e_dim <= 4096");
   if (L < 1 || L > GR_MAX_LEVELS) return fail(GR_ERR_UNSUPPORTED, "rq: 1 <= L <= 8 levels");
   if (!K || !cbs) return fail(GR_ERR_ARG, "rq: null K / codebooks");
   for (int l = 0; l < L; ++l) {
@@ -352,7 +352,33 @@ static int check_levels(int32_t e, int32_t L, const int32_t* K, const float* con
   return GR_OK;
 }
 
+// True when the MFMA quantizer reproduces MKL's order for a call of M rows: r . c as one chain.
+static bool quant_chain(int64_t M, int e, int L, const int32_t* K) {
+  if (e > 64) return false;
+  for (int l = 0; l < L; ++l) {
+    const MklPlan p = mkl_plan(M, e, K[l]);
+    if (p.kind != MKL_CHAIN || p.kb < e) return false;
+  }
+  return true;
+}
+
+// True when every Linear of a call of M rows is a k-block chain the MFMA exact kernels take.
+static bool mlp_chain(int64_t M, int32_t n_linear, const int32_t* dims) {
+  for (int i = 0; i < n_linear; ++i) {
+    const MklPlan p = mkl_plan(M, dims[i], dims[i + 1]);
+    if (p.kind != MKL_CHAIN || p.kb % 2 != 0 || dims[i] % 4 != 0) return false;
+  }
+  return true;
+}
+
 }  // namespace gr
+
+extern "C" int32_t gr_mkl_plan(int64_t M, int32_t K, int32_t N, int32_t* kind, int32_t* kb) {
+  const gr::MklPlan p = gr::mkl_plan(M, K, N);
+  if (kind) *kind = p.kind;
+  if (kb) *kb = p.kb;
+  return gr::mkl_plan_pinned(M, K, N) ? 1 : 0;
+}
 
 extern "C" int gr_rq_codebook_norms_f32(const float* codebook, int32_t K, int32_t e, float* cn_out,
                                         void* stream) {
@@ -373,6 +399,12 @@ extern "C" int gr_rq_quantize_f32(const float* z, int64_t n, int32_t e, int32_t 
   if (n < 0) return fail(GR_ERR_ARG, "gr_rq_quantize_f32: n < 0");
   if (n == 0) return GR_OK;
   if (!z || !idx_out || ((e == 16 || e == 32 || e == 64) && !aligned16(z))) return fail(GR_ERR_ARG, "gr_rq_quantize_f32: bad pointer");
+  if (!quant_chain(n, e, L, K)) {   // a one-row call (MKL's gemv order) or e > 64
+    const int32_t dims[1] = {e};
+    return gr_rq_rows_launch(z, n, n, nullptr, 0, 0, dims, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
+                             0.f, GR_ACT_NONE, L, K, codebooks, nullptr, idx_out, best_out, gap_out,
+                             reinterpret_cast<hipStream_t>(stream));
+  }
   RQLevels lv{};
   for (int l = 0; l < L; ++l) {
     lv.cb[l] = codebooks[l];
@@ -401,6 +433,9 @@ static int mlp_exact(const float* x, int64_t n, int32_t n_linear, const int32_t*
                      const float* const* bn_w, const float* const* bn_b, float bn_eps, int32_t act, float* z_out,
                      void* workspace, hipStream_t st, const float* packed = nullptr) {
   using namespace gr;
+  if (!mlp_chain(n, n_linear, dims))   // the reference's 1-15-row calls (or in_features % 4 != 0)
+    return gr_rq_rows_launch(x, n, n, nullptr, 0, n_linear, dims, weights, biases, bn_mean, bn_var, bn_w, bn_b,
+                             bn_eps, act, 0, nullptr, nullptr, z_out, nullptr, nullptr, nullptr, st);
   char* ws = reinterpret_cast<char*>(align_up(reinterpret_cast<uintptr_t>(workspace), 256));
   const size_t ab = act_bytes(n, n_linear, dims);
   float* buf[2] = {reinterpret_cast<float*>(ws), reinterpret_cast<float*>(ws + ab)};
@@ -468,6 +503,9 @@ extern "C" int gr_rq_encode_packed_f32(const float* x, int64_t n, int32_t n_line
     return fail(GR_ERR_WORKSPACE, "gr_rq_encode_f32: workspace too small (need " + std::to_string(need) + " bytes)");
   if (n == 0) return GR_OK;
   if (!x || !idx_out) return fail(GR_ERR_ARG, "gr_rq_encode_f32: null x / idx_out");
+  if (!mlp_chain(n, n_linear, dims) || !quant_chain(n, e, L, K))   // a 1-15-row call: MKL's small orders
+    return gr_rq_rows_launch(x, n, n, nullptr, 0, n_linear, dims, weights, biases, nullptr, nullptr, nullptr,
+                             nullptr, 0.f, GR_ACT_RELU, L, K, codebooks, z_out, idx_out, best_out, gap_out, st);
   float* zb = z_out;
   if (!zb) {   // z in the workspace, after the MLP's part
     char* ws = reinterpret_cast<char*>(align_up(reinterpret_cast<uintptr_t>(workspace), 256));
@@ -528,4 +566,26 @@ extern "C" int gr_mlp_exact_f32(const float* x, int64_t n, int32_t n_linear, con
   if (!x || !z_out) return fail(GR_ERR_ARG, "gr_mlp_exact_f32: null x / z_out");
   return mlp_exact(x, n, n_linear, dims, weights, biases, bn_mean, bn_var, bn_w, bn_b, bn_eps, act, z_out,
                    workspace, st);
+}
+
+// MLPLayers.forward for consecutive row groups, each one reference call (its own MKL order): the
+// encoder half of RQVAE.get_indices(group, use_sk=True) per collision group (RQ-VAE/infer.py:116-127).
+extern "C" int gr_mlp_exact_groups_f32(const float* x, int64_t n, int32_t n_linear, const int32_t* dims,
+                                       const float* const* weights, const float* const* biases,
+                                       const float* const* bn_mean, const float* const* bn_var,
+                                       const float* const* bn_w, const float* const* bn_b, float bn_eps,
+                                       int32_t act, const int64_t* group_ptr, int64_t n_groups, float* z_out,
+                                       void* stream) {
+  using namespace gr;
+  clear_error();
+  if (n_linear < 1 || n_linear > GR_MAX_LINEAR || !dims || !weights || n < 0 || n_groups < 0)
+    return fail(GR_ERR_ARG, "gr_mlp_exact_groups_f32: bad encoder description");
+  if (act != GR_ACT_RELU && act != GR_ACT_NONE && act != GR_ACT_LEAKYRELU)
+    return fail(GR_ERR_UNSUPPORTED, "gr_mlp_exact_groups_f32: act must be relu / leakyrelu / none");
+  if ((bn_mean == nullptr) != (bn_var == nullptr)) return fail(GR_ERR_ARG, "gr_mlp_exact_groups_f32: bn mean / var");
+  if (n == 0) return GR_OK;
+  if (!x || !z_out || !group_ptr || n_groups < 1) return fail(GR_ERR_ARG, "gr_mlp_exact_groups_f32: null pointer");
+  return gr_rq_rows_launch(x, n, n, group_ptr, n_groups, n_linear, dims, weights, biases, bn_mean, bn_var, bn_w, bn_b,
+                           bn_eps, act, 0, nullptr, nullptr, z_out, nullptr, nullptr, nullptr,
+                           reinterpret_cast<hipStream_t>(stream));
 }

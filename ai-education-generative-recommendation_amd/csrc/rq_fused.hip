@@ -651,8 +651,12 @@ int gr_rq_encoder_fused_launch(const float* x, int64_t n, int32_t n_linear, cons
   using namespace gr;
   if (n_linear != 3 || dims[3] != 32 || dims[0] % FXC != 0 || !biases) return GR_ERR_UNSUPPORTED;
   if (!(dims[1] == 256 && dims[2] == 128)) return GR_ERR_UNSUPPORTED;
-  const int kb = mkl_kblock(dims[0]);
-  if (kb < 0 || (kb < dims[0] && kb % FXC != 0)) return GR_ERR_UNSUPPORTED;   // block edge off a chunk
+  // MKL's order of this call (n rows): a k-block chain per layer, at most two blocks in layer 1
+  const MklPlan p1 = mkl_plan(n, dims[0], 256);
+  if (p1.kind != MKL_CHAIN || mkl_plan(n, 256, 128).kind != MKL_CHAIN || mkl_plan(n, 128, 32).kind != MKL_CHAIN)
+    return GR_ERR_UNSUPPORTED;
+  const int kb = p1.kb;
+  if (2 * kb < dims[0] || (kb < dims[0] && kb % FXC != 0)) return GR_ERR_UNSUPPORTED;   // block edge off a chunk
   for (int i = 0; i < 3; ++i)
     if (!weights[i] || !biases[i] || !aligned16(biases[i])) return GR_ERR_UNSUPPORTED;
   if (!aligned16(x) || !aligned16(z_out) || !pack || !aligned16(pack)) return GR_ERR_UNSUPPORTED;

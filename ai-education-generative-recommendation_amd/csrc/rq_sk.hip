@@ -98,6 +98,7 @@ __global__ __launch_bounds__(SK_T) void rq_sk_kernel(const float* __restrict__ z
   for (int l = 0; l < L; ++l) {
     const float* C = lv.cb[l];
     const int K = lv.K[l];
+    const MklPlan qp = mkl_plan(B, e, K);   // the group is one reference call of B rows
     // [B, K] row-major (row pitch P = K; an odd LDS pitch against bank conflicts in the row pass
     // measured slower at 64 x 8, profiles/r02_ab_sk.txt)
     const bool in_lds = (int64_t)B * K <= lds_elems;
@@ -121,10 +122,10 @@ __global__ __launch_bounds__(SK_T) void rq_sk_kernel(const float* __restrict__ z
         const int b = i / K, k = i % K;
         const float* rb = R + (int64_t)b * e;
         const float* ck = C + (int64_t)k * e;
-        // |r|^2 in ATen's row-sum order, r.c as MKL's one fma chain over k (oracle/rq_exact.c)
+        // |r|^2 in ATen's row-sum order, r.c in MKL's order for this group's call (mkl_plan:
+        // one fma chain from 2 rows on at e < 48; oracle/rq_exact.c)
         const float rn = aten_rowsq([&](int f) { return rb[f]; }, e);
-        float dot = 0.f;
-        for (int j = 0; j < e; ++j) dot = fmaf(rb[j], ck[j], dot);
+        const float dot = mkl_dot(qp, [&](int f) { return rb[f]; }, [&](int f) { return ck[f]; }, e, 0.f);
         const float d = (rn + cn[k]) - 2.0f * dot;
         Q[b * P + k] = (double)d;
         mx = fmaxf(mx, d);

@@ -1,7 +1,9 @@
 """Semantic-ID emission of RQ-VAE/infer.py:44-184 on the gfx950 kernels.
 
-1. codes of every item with ``get_indices(use_sk=False)`` — one launch over the whole catalog (the
-   GPU path is batch-invariant, so the reference's batch-64 DataLoader loop gives the same IDs);
+1. codes of every item with ``get_indices(use_sk=False)`` in the reference's batch-64 DataLoader
+   call pattern (``RQVAE.get_indices_batched``): MKL's CPU order depends on a call's row count, and
+   a tail batch of 1-15 rows (707 items: 3) takes its small-call order, so the tail is its own call;
+   the full batches share one launch;
 2. collision rounds (infer.py:108-130): every level but the last gets ``sk_epsilon = 0`` (the
    reference mutates the model the same way), then up to 30 times: group the items that share a
    code (first-appearance order, infer.py:29-41) and re-encode each group with ``use_sk=True`` —
@@ -41,12 +43,13 @@ def dedup_codes(codes):
 
 
 @torch.no_grad()
-def generate_codes(model, embeddings, device, max_rounds=30, log=None):
+def generate_codes(model, embeddings, device, max_rounds=30, log=None, batch_size=64):
     """Steps 1-3 for ``embeddings`` [N, in_dim] (numpy or tensor).  Returns (codes [N, L] after the
-    collision rounds, codes_array [N, L+1] with the dedup digit, stats)."""
+    collision rounds, codes_array [N, L+1] with the dedup digit, stats).  ``batch_size``: the
+    reference DataLoader's (infer.py:85)."""
     x = torch.as_tensor(np.asarray(embeddings, dtype=np.float32) if not torch.is_tensor(embeddings)
                         else embeddings, dtype=torch.float32).to(device)
-    codes = model.get_indices(x, use_sk=False).cpu().numpy()
+    codes = model.get_indices_batched(x, batch_size).cpu().numpy()
     for vq in model.rq.vq_layers[:-1]:                        # infer.py:109-110
         vq.sk_epsilon = 0.0
     rounds = 0

@@ -242,17 +242,24 @@ class RqBinding:
         self.w_arr, self.b_arr, self.c_arr = L.ptr_array(self.ws), L.ptr_array(self.bs), L.ptr_array(self.cbs)
         self.device = self.ws[0].device
         self._ws_bytes = {}
-        # the fused encoder's packed weight image, re-packed only when a weight changed (in-place
-        # updates bump the shared version counter of the detached views)
+        # the fused encoder's packed weight image (frozen weights only, see packed_ptr)
         nf = L.lib().gr_rq_encoder_pack_floats(len(self.ws), self.dims_c)
         self.packed = torch.empty(nf, dtype=torch.float32, device=self.device) if nf else None
         self._pack_key = None
 
+    # Re-use one packed encoder image across calls.  Off by default: an update that bumps no
+    # version counter (a replayed training graph's optimizer step, a write through ``.data``)
+    # would leave the image stale, so every call packs the current weights into its workspace
+    # (one extra launch).  ``RQVAE.freeze_encoder()`` turns it on for serving with fixed weights;
+    # the image is then re-packed whenever a weight's version or the graph-replay epoch changes.
+    frozen = False
+
     def packed_ptr(self):
-        """Device pointer of the up-to-date packed encoder image (None: not the fused shape)."""
-        if self.packed is None:
+        """Device pointer of the up-to-date packed encoder image; None: pack per call (the default,
+        or not the fused encoder shape)."""
+        if self.packed is None or not self.frozen:
             return None
-        key = tuple(w._version for w in self.ws)
+        key = tuple(w._version for w in self.ws) + (_WEIGHT_EPOCH[0],)
         if key != self._pack_key:
             with torch.cuda.device(self.device):
                 L.check(L.lib().gr_rq_encoder_pack_f32(len(self.ws), self.dims_c, self.w_arr, L.ptr(self.packed),
@@ -269,6 +276,24 @@ class RqBinding:
             if len(self._ws_bytes) < 64:
                 self._ws_bytes[n] = nb
         return nb
+
+
+# Bumped by every replay of a captured training step (its optimizer updates parameters in place
+# without touching their version counters), so cached weight images re-pack after it.
+_WEIGHT_EPOCH = [0]
+
+
+def weights_changed():
+    """Tell the cached kernel bindings that parameters changed behind torch's version counters."""
+    _WEIGHT_EPOCH[0] += 1
+
+
+def mkl_plan(m, k, n):
+    """MKL's accumulation order for one reference CPU sgemm call of ``m`` rows, inner size ``k``,
+    ``n`` outputs (``gr_mkl_plan``): (kind, block width, pinned), kind in chain / gemv16 / small16."""
+    kind, kb = ctypes.c_int32(0), ctypes.c_int32(0)
+    pinned = L.lib().gr_mkl_plan(int(m), int(k), int(n), ctypes.byref(kind), ctypes.byref(kb))
+    return ("chain", "gemv16", "small16")[kind.value], kb.value, bool(pinned)
 
 
 def rq_binding(owner, weights_fn):
@@ -327,12 +352,14 @@ def rq_encode(x, weights=None, biases=None, codebooks=None, with_gap=False, with
 _EXACT_ACTS = {"relu": 1, "none": 0, None: 0, "leakyrelu": 4}
 
 
-def rq_mlp(x, weights, biases, bn=None, act="relu"):
+def rq_mlp(x, weights, biases, bn=None, act="relu", group_sizes=None):
     """MLPLayers.forward (RQ-VAE/models/layers.py:18-43, eval): the encoder output ``z`` alone, in
     the reference's CPU order bit for bit (``gr_mlp_exact_f32``: the fused kernel for in -> 256 ->
-    128 -> 32 ReLU MLPs, exact layer-wise launches otherwise).  ``bn``: None, or (means, vars,
-    weights, biases, eps) of the eval BatchNorm1d after every Linear but the last (weights /
-    biases entries may be None: affine off); ``act``: relu / leakyrelu / none."""
+    128 -> 32 ReLU MLPs, exact layer-wise launches otherwise, the per-row kernel for 1-15-row
+    calls).  ``bn``: None, or (means, vars, weights, biases, eps) of the eval BatchNorm1d after every
+    Linear but the last (weights / biases entries may be None: affine off); ``act``: relu /
+    leakyrelu / none.  ``group_sizes``: consecutive row groups, each ONE reference call (MKL's order
+    depends on the call's row count; ``gr_mlp_exact_groups_f32``)."""
     L.require_gpu(x, *weights)
     x2 = L.as_f32(x)
     n = x2.shape[0]
@@ -362,6 +389,16 @@ def rq_mlp(x, weights, biases, bn=None, act="relu"):
             keep.append(ts)
             bn_arrs[j] = L.ptr_array(ts)
     with torch.cuda.device(dev):
+        if group_sizes is not None:
+            sizes = [int(g) for g in group_sizes]
+            if sum(sizes) != n or any(g < 1 for g in sizes):
+                raise RuntimeError("rq_mlp: group sizes must be positive and sum to the batch")
+            ptr = _group_ptr(sizes, dev)
+            L.check(lib.gr_mlp_exact_groups_f32(L.ptr(x2), n, len(ws), dims_c, L.ptr_array(ws),
+                                                L.ptr_array(bs) if bs is not None else None, *bn_arrs, float(eps),
+                                                _EXACT_ACTS[act], L.ptr(ptr), len(sizes), L.ptr(z),
+                                                L.stream_of(dev)), "gr_mlp_exact_groups_f32")
+            return z
         L.check(lib.gr_mlp_exact_f32(L.ptr(x2), n, len(ws), dims_c, L.ptr_array(ws),
                                      L.ptr_array(bs) if bs is not None else None, *bn_arrs, float(eps),
                                      _EXACT_ACTS[act], L.ptr(z), L.ptr(wsp), nbytes, L.stream_of(dev)),
@@ -374,7 +411,8 @@ def rq_encode_sk(x, weights, biases, codebooks, sk_eps, sk_iters, group_sizes=No
     independent row groups in ONE launch: ``group_sizes`` partitions the rows of ``x`` into
     consecutive groups, each one reference call (default: the whole batch is one group)."""
     L.require_gpu(x, *weights, *codebooks)
-    return rq_quantize_sk(rq_mlp(x, weights, biases), codebooks, sk_eps, sk_iters, group_sizes)
+    return rq_quantize_sk(rq_mlp(x, weights, biases, group_sizes=group_sizes), codebooks, sk_eps, sk_iters,
+                          group_sizes)
 
 
 def rq_encode_z(z, codebooks, with_gap=False):
@@ -902,6 +940,7 @@ class SasTrainGraph:
             out = tuple(x.detach() for x in self._body())
         else:
             self.graph.replay()
+            weights_changed()
             out = self.out
         if self._check:   # a row whose negative population may be short: the reference raises
             check_errors(self.inputs.device)
@@ -1003,6 +1042,7 @@ class RqTrainGraph:
         if self.graph is None:
             return tuple(x.detach() for x in self._body())
         self.graph.replay()
+        weights_changed()   # the captured AdamW step moved the weights without a version bump
         return self.out
 
     def _body(self):

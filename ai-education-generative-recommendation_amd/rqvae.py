@@ -150,7 +150,10 @@ class MLPLayers(nn.Module):
         return ([b.running_mean for b in bns], [b.running_var for b in bns], [d(b.weight) for b in bns],
                 [d(b.bias) for b in bns], float(bns[0].eps))
 
-    def forward(self, x):
+    def forward(self, x, group_sizes=None):
+        """Eval forward in the reference's CPU order for ONE call of ``len(x)`` rows (MKL's order
+        depends on the call's row count), or, with ``group_sizes``, for consecutive row groups
+        that are one reference call each (the collision re-encode of RQ-VAE/infer.py:116-127)."""
         if self.training and (self.dropout > 0 or self.use_bn):
             raise RuntimeError("gr_amd MLPLayers runs the eval-mode encoder: call .eval() (dropout / "
                                "BatchNorm batch statistics are train-mode only)")
@@ -159,7 +162,7 @@ class MLPLayers(nn.Module):
         lin = self.linears()
         return ops.rq_mlp(x, [m.weight.detach() for m in lin],
                           [m.bias.detach() if m.bias is not None else torch.zeros(m.out_features, device=x.device)
-                           for m in lin], bn=self.bn_params(), act=self.act or "none")
+                           for m in lin], bn=self.bn_params(), act=self.act or "none", group_sizes=group_sizes)
 
 
 class VectorQuantizer(nn.Module):
@@ -353,7 +356,52 @@ class RQVAE(nn.Module):
         if self.bn:
             ws, bs = self.encoder.folded()
             return ops.RqBinding(ws, bs, self.rq.codebooks())
-        return ops.rq_binding(self, self._encode_params)
+        b = ops.rq_binding(self, self._encode_params)
+        b.frozen = self.__dict__.get("_gr_frozen", False)
+        return b
+
+    def freeze_encoder(self, frozen=True):
+        """Serving with fixed weights: keep the fused encoder's packed weight image across
+        get_indices calls (re-packed when a weight's version counter or ops.weights_changed()
+        moves) instead of packing it per call.  Writes that bypass both (``param.data[...] = ``)
+        must call ops.weights_changed()."""
+        self.__dict__["_gr_frozen"] = bool(frozen)
+        return self
+
+    def call_plans(self, n):
+        """MKL's order for a reference call of ``n`` rows: [(kind, kb, pinned)] per encoder Linear,
+        then per quantizer level (ops.mkl_plan)."""
+        dims = self.encode_layer_dims
+        plans = [ops.mkl_plan(n, k, o) for k, o in zip(dims[:-1], dims[1:])]
+        return plans + [ops.mkl_plan(n, self.e_dim, q.n_e) for q in self.rq.vq_layers]
+
+    def parity_pinned(self, n):
+        """True when every sgemm order of a get_indices call of ``n`` rows is in the envelope
+        checked bit for bit against the reference's CPU run (gr_mkl_plan)."""
+        return all(p[2] for p in self.call_plans(n))
+
+    @torch.no_grad()
+    def get_indices_batched(self, xs, batch_size=64):
+        """``torch.cat([get_indices(xs[i:i + batch_size]) for i in range(0, len(xs), batch_size)])``
+        -- the reference's DataLoader loop (RQ-VAE/infer.py:84-95, generate_code.py:78-88) -- in at
+        most two launches when the full batches share one MKL order with a single call over them
+        (true for the reference's widths): the full batches together, then the short tail batch
+        as its own call (1-15 rows take MKL's small-call orders)."""
+        n = xs.shape[0]
+        tail = n % batch_size
+        main = n - tail
+        parts = []
+        if main:
+            order = lambda m: [p[:2] for p in self.call_plans(m)]   # noqa: E731
+            if main == batch_size or order(batch_size) == order(main):
+                parts.append(self.get_indices(xs[:main]))
+            else:
+                parts += [self.get_indices(xs[i:i + batch_size]) for i in range(0, main, batch_size)]
+        if tail:
+            parts.append(self.get_indices(xs[main:]))
+        if not parts:
+            return torch.empty((0, len(self.rq.vq_layers)), dtype=torch.int64, device=xs.device)
+        return torch.cat(parts) if len(parts) > 1 else parts[0]
 
     def _encode_params(self):
         lin = self.encoder.linears()
@@ -367,8 +415,8 @@ class RQVAE(nn.Module):
         """``torch.cat([get_indices(g, use_sk=True) for g in groups])`` for consecutive row groups
         of ``xs`` in one launch — the per-group loop of RQ-VAE/infer.py:116-127."""
         self._check_encode(xs, True)
-        return ops.rq_quantize_sk(self.encoder(xs), self.rq.codebooks(), self.sk_eps(), self.rq.sk_iters,
-                                  group_sizes)
+        return ops.rq_quantize_sk(self.encoder(xs, group_sizes=group_sizes), self.rq.codebooks(), self.sk_eps(),
+                                  self.rq.sk_iters, group_sizes)
 
     @torch.no_grad()
     def get_indices_certified(self, xs):

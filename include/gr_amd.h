@@ -75,6 +75,16 @@ const char* gr_last_error(void);
  *   "rt_kv2"        1 (default): the post-attention row tile's next-block projection, when its
  *                   width is a multiple of 256, runs one column tile per wave over both row tiles;
  *                   0: one 32 x 32 tile per task.  Identical results.
+ *   "rq_pieces"     1 (default): the fused encoder's item tiles past q x grid (q whole tiles per
+ *                   workgroup) run as feature-half pieces on twice as many workgroups plus a layers
+ *                   2-3 kernel; 0: a one-tile pass on the first workgroups.  Identical results.
+ *   "tail_h"        1 (default): a last-position SASRec forward (predict) runs its final block as
+ *                   the one-query tail on LN_a(X): q . K_j = (W_k^T q) . H_j (+ a term constant
+ *                   over j that cancels in the softmax) and p . V = W_v (p . H) + b_v, so K|V of
+ *                   the B n rows are never projected.  NOT bitwise: the reassociated sums round
+ *                   differently (logits within the 1e-5 row-scaled tolerance, tests/
+ *                   test_sasrec_gpu.py::test_tail_h_form_vs_kv_form_and_oracle); 0: K|V projected
+ *                   and the reference's association order.
  * gr_set_option returns GR_ERR_ARG for an unknown name/value; gr_get_option returns -1 for an
  * unknown name. */
 int gr_set_option(const char* name, int64_t value);
@@ -109,8 +119,8 @@ int gr_rq_codebook_norms_f32(const float* codebook, int32_t K, int32_t e, float*
  * idx_out[n, L] int64 row-major (the stacked `indices` of rq.py:54).
  * best_out[n, L], gap_out[n, L] (optional, may be NULL): the best fp32 distance and the gap to the
  * second best per level.
- * Supports 1 <= e <= 64, 1 <= L <= GR_MAX_LEVELS, any K >= 1; z and the codebooks must be 16-byte
- * aligned when e is 16, 32 or 64. */
+ * Supports 1 <= e <= 4096 (e > 64 and one-row calls on the per-row kernel), 1 <= L <= GR_MAX_LEVELS,
+ * any K >= 1; z and the codebooks must be 16-byte aligned when e is 16, 32 or 64. */
 int gr_rq_quantize_f32(const float* z, int64_t n, int32_t e, int32_t L, const int32_t* K,
                        const float* const* codebooks, const float* const* code_norms,
                        int64_t* idx_out, float* best_out, float* gap_out, void* stream);
@@ -122,10 +132,10 @@ size_t gr_rq_encode_workspace_bytes(int64_t n, int32_t n_linear, const int32_t* 
 
 /* RQVAE.get_indices(xs, use_sk=False) (RQ-VAE/models/rqvae.py:67-71): encoder MLP
  * (layers.py:42-43; ReLU after every Linear but the last) followed by gr_rq_quantize_f32.
- * The encoder reproduces the reference's CPU nn.Linear bit for bit (MKL's k blocking: one fma chain
- * per block, y = bias; y += block 0; y += block 1) for every in_features <= 768 (multiples of 4; a
- * two-block layer needs its block edge on a multiple of 8); other widths are refused
- * (GR_ERR_UNSUPPORTED). 
+ * The encoder and the quantizer's r . c reproduce the reference's CPU sgemm order for a call of n
+ * rows (gr_mkl_plan: k-block chains of >= 16-row calls on the MFMA kernels, the one-row and 2-15-row
+ * 16-lane orders on a per-row kernel; widths whose order is not pinned, in_features % 4 != 0 and
+ * e_dim > 64 also run there); any width is accepted. 
  * weights/biases: host arrays (n_linear) of device pointers; codebooks, K: host arrays (L).
  * best_out, gap_out: as gr_rq_quantize_f32 (optional).
  * z_out (optional, may be NULL): the encoder output [n, e]. */
@@ -171,6 +181,27 @@ int gr_mlp_exact_f32(const float* x, int64_t n, int32_t n_linear, const int32_t*
                      const float* const* bn_w, const float* const* bn_b, float bn_eps,
                      int32_t act, float* z_out, void* workspace, size_t workspace_bytes,
                      void* stream);
+
+/* MLPLayers.forward (eval) for consecutive row groups, each ONE reference call with its own MKL
+ * accumulation order (the call's row count selects it, see gr_mkl_plan): the encoder half of
+ * RQVAE.get_indices(group, use_sk=True) per collision group (RQ-VAE/infer.py:116-127).  group_ptr:
+ * device int64 [n_groups + 1] offsets as gr_rq_encode_sk_f32.  Other arguments as gr_mlp_exact_f32
+ * (no workspace). */
+int gr_mlp_exact_groups_f32(const float* x, int64_t n, int32_t n_linear, const int32_t* dims,
+                            const float* const* weights, const float* const* biases,
+                            const float* const* bn_mean, const float* const* bn_var,
+                            const float* const* bn_w, const float* const* bn_b, float bn_eps,
+                            int32_t act, const int64_t* group_ptr, int64_t n_groups, float* z_out,
+                            void* stream);
+
+/* The accumulation order the reference's CPU sgemm (torch 2.10 / MKL 2024.2, 8 threads, AVX-512:
+ * the golden-fixture host) uses for ONE call of M rows, inner size K, N outputs -- nn.Linear
+ * (RQ-VAE/models/layers.py:23) and the quantizer's matmul (vq.py:73, K = e_dim, N = codebook size):
+ *   *kind 0 = k-block chain of width *kb, 1 = one-row 16-lane gemv, 2 = 2-15-row 16-lane small
+ * kernel (oracle/rq_exact.c rqx_plan).  Every gr_rq_* / gr_mlp_* entry point computes each call in
+ * this order.  Returns 1 when (M, K, N) lies in the envelope checked bit for bit against torch on
+ * that host, 0 outside it (the order is then mkl_plan's best restatement, parity unpinned). */
+int32_t gr_mkl_plan(int64_t M, int32_t K, int32_t N, int32_t* kind, int32_t* kb);
 
 /* MLPLayers.forward in train mode (RQ-VAE/models/layers.py:18-43, [Dropout -> Linear -> ReLU] x
  * (n_linear - 1), then Dropout -> Linear; RQVAE.forward under RQ-VAE/train.py:113).  Dropout p_drop

@@ -32,7 +32,7 @@ def lib():
             build()
         _lib = ctypes.CDLL(LIB)
         _lib.rqx_kblock.restype = ctypes.c_int
-        for f in ("rqx_encode", "rqx_quantize", "rqx_linear", "rqx_mlp"):
+        for f in ("rqx_encode_m", "rqx_quantize_m", "rqx_linear", "rqx_mlp_m", "rqx_plan", "rqx_plan_pinned"):
             getattr(_lib, f).restype = ctypes.c_int
     return _lib
 
@@ -59,14 +59,26 @@ def kblock(k):
     return lib().rqx_kblock(int(k))
 
 
+PLAN_KINDS = {0: "chain", 1: "gemv16", 2: "small16"}
+
+
+def plan(m, k, n):
+    """MKL's accumulation order for a call of ``m`` rows, inner size ``k``, ``n`` outputs:
+    (kind, block width, pinned) -- see rq_exact.c rqx_plan / rqx_plan_pinned."""
+    kb = ctypes.c_int(0)
+    kind = lib().rqx_plan(ctypes.c_int64(int(m)), int(k), int(n), ctypes.byref(kb))
+    return PLAN_KINDS[kind], kb.value, bool(lib().rqx_plan_pinned(ctypes.c_int64(int(m)), int(k), int(n)))
+
+
 def linear(x, w, b=None, act="none"):
+    """One reference ``F.linear`` call on the rows of ``x`` (the order depends on their count)."""
     x, w = _f(x), _f(w)
     b = None if b is None else _f(b)
     y = np.empty((x.shape[0], w.shape[0]), np.float32)
     rc = lib().rqx_linear(_p(x), ctypes.c_int64(x.shape[0]), x.shape[1], _p(w), w.shape[0],
                           None if b is None else _p(b), {"none": 0, "relu": 1, "leakyrelu": 2}[act], _p(y))
     if rc:
-        raise ValueError(f"rq_exact.linear: K={x.shape[1]} outside the characterised MKL blocking rule")
+        raise ValueError("rq_exact.linear: bad arguments")
     return y
 
 
@@ -77,9 +89,10 @@ def rowsq(x):
     return out
 
 
-def encode(x, weights, biases, codebooks, with_detail=False, threads=None):
+def encode(x, weights, biases, codebooks, with_detail=False, threads=None, call_m=None):
     """get_indices(x) with encoder ``weights``/``biases`` ([out, in] / [out]) and ``codebooks``
-    ([K, e] per level) -> idx [n, L] int64 (and z, best distance, best/second gap with detail)."""
+    ([K, e] per level) -> idx [n, L] int64 (and z, best distance, best/second gap with detail).
+    All rows are ONE reference call of ``call_m`` rows (default: n) -- MKL's order depends on it."""
     x = _f(x)
     ws = [_f(w) for w in weights]
     bs = [_f(b) for b in biases]
@@ -92,16 +105,16 @@ def encode(x, weights, biases, codebooks, with_detail=False, threads=None):
     z = np.empty((n, e), np.float32) if with_detail else None
     best = np.empty((n, L), np.float32) if with_detail else None
     gap = np.empty((n, L), np.float32) if with_detail else None
-    rc = lib().rqx_encode(_p(x), ctypes.c_int64(n), len(ws), dims, _ptrs(ws), _ptrs(bs), L, K, _ptrs(cbs),
-                          idx.ctypes.data_as(_i64p), None if z is None else _p(z),
-                          None if best is None else _p(best), None if gap is None else _p(gap),
-                          _threads(threads))
+    rc = lib().rqx_encode_m(_p(x), ctypes.c_int64(n), len(ws), dims, _ptrs(ws), _ptrs(bs), L, K, _ptrs(cbs),
+                            idx.ctypes.data_as(_i64p), None if z is None else _p(z),
+                            None if best is None else _p(best), None if gap is None else _p(gap),
+                            _threads(threads), ctypes.c_int64(call_m or n))
     if rc:
-        raise ValueError("rq_exact.encode: an encoder K outside the characterised MKL blocking rule")
+        raise ValueError("rq_exact.encode: bad arguments")
     return (idx, z, best, gap) if with_detail else idx
 
 
-def quantize(z, codebooks, with_detail=False, threads=None):
+def quantize(z, codebooks, with_detail=False, threads=None, call_m=None):
     z = _f(z)
     cbs = [_f(c) for c in codebooks]
     n, L = z.shape[0], len(cbs)
@@ -109,12 +122,13 @@ def quantize(z, codebooks, with_detail=False, threads=None):
     idx = np.empty((n, L), np.int64)
     best = np.empty((n, L), np.float32) if with_detail else None
     gap = np.empty((n, L), np.float32) if with_detail else None
-    lib().rqx_quantize(_p(z), ctypes.c_int64(n), z.shape[1], L, K, _ptrs(cbs), idx.ctypes.data_as(_i64p),
-                       None if best is None else _p(best), None if gap is None else _p(gap), _threads(threads))
+    lib().rqx_quantize_m(_p(z), ctypes.c_int64(n), z.shape[1], L, K, _ptrs(cbs), idx.ctypes.data_as(_i64p),
+                         None if best is None else _p(best), None if gap is None else _p(gap), _threads(threads),
+                         ctypes.c_int64(call_m or n))
     return (idx, best, gap) if with_detail else idx
 
 
-def mlp(x, weights, biases, bn=None, act="relu", threads=None):
+def mlp(x, weights, biases, bn=None, act="relu", threads=None, call_m=None):
     """MLPLayers.forward (eval) in the reference's CPU order: ``bn`` = None or (means, vars, weights,
     biases, eps) of the BatchNorm1d after every Linear but the last; act relu / leakyrelu / none."""
     x = _f(x)
@@ -134,8 +148,17 @@ def mlp(x, weights, biases, bn=None, act="relu", threads=None):
             ts = [_f(t) for t in grp]
             keep.append(ts)
             arrs[j] = _ptrs(ts)
-    rc = lib().rqx_mlp(_p(x), ctypes.c_int64(n), len(ws), dims, _ptrs(ws), _ptrs(bs), *arrs,
-                       ctypes.c_float(eps), {"none": 0, "relu": 1, "leakyrelu": 2}[act], _p(z), _threads(threads))
+    rc = lib().rqx_mlp_m(_p(x), ctypes.c_int64(n), len(ws), dims, _ptrs(ws), _ptrs(bs), *arrs,
+                         ctypes.c_float(eps), {"none": 0, "relu": 1, "leakyrelu": 2}[act], _p(z), _threads(threads),
+                         ctypes.c_int64(call_m or n))
     if rc:
-        raise ValueError("rq_exact.mlp: an encoder K outside the characterised MKL blocking rule")
+        raise ValueError("rq_exact.mlp: bad arguments")
     return z
+
+
+def encode_batches(x, weights, biases, codebooks, bs=64, threads=None):
+    """The reference's DataLoader loop (RQ-VAE/infer.py:84-95, generate_code.py:78-88): one
+    get_indices call per ``bs`` rows, the tail call with its own (short) row count."""
+    x = _f(x)
+    parts = [encode(x[i:i + bs], weights, biases, codebooks, threads=threads) for i in range(0, x.shape[0], bs)]
+    return np.concatenate(parts) if parts else np.zeros((0, len(codebooks)), np.int64)
