@@ -5,6 +5,10 @@
     python bench.py [--gpus N --steps K --warmup W]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
 
+``python bench.py --gpus N`` (N > 1) outside torch.distributed.run launches its N ranks itself: the
+parent imports neither torch nor gr_amd, runs ``torch.distributed.run`` as a child process (one rank
+per GPU, rendezvous on 127.0.0.1), relays rank 0's JSON line and exits with the children's status.
+
 Primary line (``value``): RQ-VAE encode at config C2 = 3x256 codebooks, in 768 -> [256,128] -> e 32,
 100k synthetic items per rank per step (``RQVAE.get_indices`` on device-resident inputs).  Items
 shard across ranks with no collective ("scaling": "weak").  The same JSON line carries:
@@ -22,12 +26,41 @@ times the CPU oracle (oracle/) on a bounded sample of the same workloads ("cpu_b
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
-import numpy as np
-import torch
-import torch.distributed as dist
+
+def _self_launch():
+    """``--gpus N`` (N > 1) outside torch.distributed.run: start the N ranks as a child
+    ``python -m torch.distributed.run`` and return its exit status (None: run in this process).
+    Nothing here touches the GPU (no torch import), so the parent never holds a device context."""
+    if "WORLD_SIZE" in os.environ or "LOCAL_RANK" in os.environ:
+        return None
+    ap = argparse.ArgumentParser(add_help=False)
+    ap.add_argument("--gpus", type=int, default=1)
+    known, _ = ap.parse_known_args()
+    if known.gpus <= 1:
+        return None
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:   # a free rendezvous port
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")   # dmabuf IPC: RCCL across processes
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={known.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.run(cmd, env=env).returncode
+
+
+if __name__ == "__main__":
+    _rc = _self_launch()
+    if _rc is not None:
+        sys.exit(_rc)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
@@ -75,11 +108,16 @@ def sas_exec_flop_per_user(d, n, items, mlp=64, blocks=2, causal=True, tail_h=Fa
     return (blocks - 1) * full + last + 2 * d * (items + 1)
 
 
+# device of the bench's own small collectives: "cuda" (RCCL, or gloo on device tensors in the
+# rehearsal mode); "cpu" for the launcher self-test (GR_BENCH_DEVICE=cpu, no GPU needed)
+COLL_DEV = "cuda"
+
+
 def per_rank(x, world):
     """``x`` (this rank's float) from every rank, in rank order (a collective at world > 1)."""
     if world <= 1 or not dist.is_initialized():
         return [x]
-    t = torch.zeros(world, dtype=torch.float64, device="cuda")
+    t = torch.zeros(world, dtype=torch.float64, device=COLL_DEV)
     t[dist.get_rank()] = x
     dist.all_reduce(t)
     return t.tolist()
@@ -98,7 +136,7 @@ def result_checksum(res, world):
     mine = int(dg, 16) & ((1 << 62) - 1)
     allr = [mine]
     if world > 1 and dist.is_initialized():
-        t = torch.zeros(world, dtype=torch.int64, device="cuda")
+        t = torch.zeros(world, dtype=torch.int64, device=COLL_DEV)
         t[dist.get_rank()] = mine
         dist.all_reduce(t)
         allr = t.tolist()
@@ -875,6 +913,37 @@ LEGS = ["c2", "calls", "sasrec", "c4", "c5", "shard", "train", "train_step", "rq
 OPT_LEGS = []   # run only when named in --legs
 
 
+def selftest(a, world, rank):
+    """GR_BENCH_DEVICE=cpu: the multi-rank plumbing of this bench on CPU ranks over gloo -- the
+    process group, max-over-ranks timing, per-rank reporting and the C5 result checksum agreement
+    -- with a deterministic stand-in for the merged C5 result (no GPU, no kernels)."""
+    global COLL_DEV
+    COLL_DEV = "cpu"
+    if world > 1:
+        dist.init_process_group("gloo")
+    g = torch.Generator().manual_seed(0)   # the same "merged" result on every rank, as after C5's exchange
+    ranks = torch.randint(1, 1000, (512,), generator=g)
+    vals = torch.randn(512, 10, generator=g)
+    ids = torch.randint(1, 10**6, (512, 10), generator=g)
+    t0 = time.perf_counter()
+    x = torch.randn(256, 256, generator=g)
+    for _ in range(a.steps):
+        x = torch.tanh(x @ x.t() / 256)
+    wall = time.perf_counter() - t0
+    walls = per_rank(wall, world)
+    line = {"metric": METRIC, "value": None, "unit": "items/s", "n_gpus": world, "steps": a.steps,
+            "note": "launcher self-test (GR_BENCH_DEVICE=cpu): no GPU work was measured",
+            "selftest": {"wall_s_per_rank": walls, "max_wall_s": max(walls),
+                         "result_checksum": result_checksum((ranks, vals, ids), world)}}
+    line["dist"] = ({"backend": str(dist.get_backend()), "world_size": dist.get_world_size()}
+                    if dist.is_initialized() else {"backend": None, "world_size": 1})
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if dist.is_initialized():
+        dist.barrier()
+        dist.destroy_process_group()
+
+
 def main():
     a = parse()
     global SPINUP_S
@@ -886,7 +955,9 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if a.gpus != world and world == 1 and a.gpus > 1:
-        sys.exit("bench.py: --gpus N>1 must be launched with torch.distributed.run (one rank per GPU)")
+        sys.exit("bench.py: --gpus N>1 without WORLD_SIZE: run it as a script (it launches its ranks)")
+    if os.environ.get("GR_BENCH_DEVICE") == "cpu":   # launcher / process-group self-test, no GPU
+        return selftest(a, world, rank)
     # GR_BENCH_BACKEND=gloo is a rehearsal mode only (several ranks sharing one GPU to exercise the
     # multi-rank code paths on a one-GPU box); real runs use RCCL ("nccl"), one GPU per rank.
     backend = os.environ.get("GR_BENCH_BACKEND", "nccl")
