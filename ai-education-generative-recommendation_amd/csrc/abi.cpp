@@ -116,7 +116,7 @@ extern "C" int gr_set_option(const char* name, int64_t value) {
   if (!strcmp(name, "topk_sample") && (value == 0 || value == 1)) { gr::g_topk_sample = value; return GR_OK; }
   if (!strcmp(name, "score_flags") && (value == 0 || value == 1)) { gr::g_score_flags = value; return GR_OK; }
   if (!strcmp(name, "score_ubmajor") && (value == 0 || value == 1)) { gr::g_score_ubmajor = value; return GR_OK; }
-  if (!strcmp(name, "score_impl") && value >= 0 && value <= 2) { gr::g_score_impl = value; return GR_OK; }
+  if (!strcmp(name, "score_impl") && value >= 0 && value <= 4) { gr::g_score_impl = value; return GR_OK; }
   if (!strcmp(name, "topk_wg_per_cu") && value >= 0 && value <= 4) { gr::g_topk_wg_per_cu = value; return GR_OK; }
   if (!strcmp(name, "attn_pair") && (value == 0 || value == 1)) { gr::g_attn_pair = value; return GR_OK; }
   if (!strcmp(name, "sas_rowtile") && (value == 0 || value == 1)) { gr::g_sas_rowtile = value; return GR_OK; }

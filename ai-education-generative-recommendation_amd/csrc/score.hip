@@ -343,7 +343,7 @@ __global__ __launch_bounds__(64 * (ScCW<D, FLAGS>::value + ScSW<D, FLAGS>::value
 // 32 consecutive logits (two 128-B segments, unaligned when the row stride is odd: the next
 // chunk's stores complete the lines in L2).  Two workgroups per CU, so one wave's MFMAs run while
 // another's stores drain.
-template <int D>
+template <int D, bool NTS = true>
 __global__ __launch_bounds__(256, 2) void score_direct_kernel(const float* __restrict__ h, int64_t B,
                                                             const float* __restrict__ table, int64_t rows,
                                                             float* __restrict__ out, int64_t ld,
@@ -409,7 +409,10 @@ __global__ __launch_bounds__(256, 2) void score_direct_kernel(const float* __res
     const int rl = 32 * ut + (v & 3) + 8 * (v >> 2) + 4 * hh;
     const int64_t col = pk * SC_CHUNK + r;
     float* op = obase + pk * SC_CHUNK + (int64_t)rl * ld;
-    if (full_rows && pk * SC_CHUNK + SC_CHUNK <= rows) __builtin_nontemporal_store(prev[ut][v], op);
+    if (full_rows && pk * SC_CHUNK + SC_CHUNK <= rows) {
+      if (NTS) __builtin_nontemporal_store(prev[ut][v], op);
+      else *op = prev[ut][v];   // unaligned rows: let L2 merge the two halves of each straddled line
+    }
     else if (u0 + rl < B && col < rows) *op = prev[ut][v];
   };
   constexpr int STEPS = KG * 16;             // (g, q, s) steps of a chunk, 2 MFMAs each
@@ -454,6 +457,169 @@ __global__ __launch_bounds__(256, 2) void score_direct_kernel(const float* __res
   for (int t = 0; t < 32; ++t) store_one(t);
 }
 
+// Direct stores into rows that do not start on a 128-byte line (the reference's own contiguous
+// [B, N+1] logits: row stride N + 1).  Register v of a half-wave holds 32 consecutive logits of one
+// row (columns 32k + r of chunk k), which straddle two lines of that row, so storing it as is writes
+// every line in two pieces (measured 593 vs 393 us per C3 predict at B 2048: the halves of a line
+// are not merged before they reach HBM).  Instead the lanes are rotated by the row's line offset o
+// (ds_bpermute: the LDS crossbar, no LDS memory): rot_k[p] = chunk_k[(p - o) mod 32].  Line A_k of
+// the row (the one holding column 32k at position o) is then
+//     lanes p < o: rot_{k-1}[p]  (columns 32k - o + p of chunk k - 1),  lanes p >= o: rot_k[p],
+// one whole aligned 128-byte line per half-wave store.  The rotated chunk is kept for the next line;
+// a slice's first line, the line after its last chunk and the lines at a row's end are written with
+// per-lane masks (column in [32 c_begin, min(32 c_end, rows)), row < B), so every logit is written
+// exactly once.  Rotation addresses and store offsets are per (lane, register) constants of the
+// workgroup, computed once.  Same fma chains as score_direct_kernel: bitwise the same logits.
+template <int D, bool PREOFF>
+__global__ __launch_bounds__(256, 2) void score_rot_kernel(const float* __restrict__ h, int64_t B,
+                                                         const float* __restrict__ table, int64_t rows,
+                                                         float* __restrict__ out, int64_t ld,
+                                                         int ublocks, int slices, int slice_major) {
+  constexpr int KG = D / 32;
+  constexpr int P = D + 4;
+  constexpr int LV = SC_CHUNK * D / 4 / 256;
+  __shared__ __attribute__((aligned(16))) float tab[2][SC_CHUNK * P];
+  const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, hh = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wgid = xcd_remap(blockIdx.x, gridDim.x);
+  const int ub = slice_major ? wgid % ublocks : wgid / slices;
+  const int sl = slice_major ? wgid / ublocks : wgid % slices;
+  const int64_t chunks = (rows + SC_CHUNK - 1) / SC_CHUNK;
+  const int64_t c_begin = chunks * sl / slices, c_end = chunks * (sl + 1) / slices;
+  if (c_begin >= c_end) return;
+  const int64_t u0 = (int64_t)ub * 256 + wave * 64;
+  f32x4 hf[2][KG][4];
+#pragma unroll
+  for (int ut = 0; ut < 2; ++ut) {
+    const int64_t u = u0 + ut * 32 + r;
+    const int64_t uc = u < B ? u : B - 1;
+#pragma unroll
+    for (int g = 0; g < KG; ++g)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const f32x4 v = *reinterpret_cast<const f32x4*>(h + uc * D + 32 * g + 8 * q + 4 * hh);
+        hf[ut][g][q] = u < B ? v : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+  }
+  const bool full_rows = u0 + 64 <= B;
+  // per register v: row rl(v) of user tile 0 (tile 1's row rl + 32 has the same line offset o,
+  // 32 ld = 0 mod 32, and its store offset is 32 ld floats further: a scalar)
+  const uint32_t pw = (uint32_t)((reinterpret_cast<uintptr_t>(out) >> 2) & 31u);
+  int rot_addr[16];   // ds_bpermute byte address: lane 32 hh + ((r - o) & 31)
+  int voff[PREOFF ? 16 : 1];   // byte offset of lane r's element of line A_0, from 32 floats before row u0
+  const int64_t ldm = ld & 31;
+#pragma unroll
+  for (int v = 0; v < 16; ++v) {
+    const int rl = (v & 3) + 8 * (v >> 2) + 4 * hh;
+    const int o = (int)((pw + (uint32_t)(((u0 + rl) & 31) * ldm)) & 31u);
+    rot_addr[v] = (32 * hh + ((r - o) & 31)) * 4;
+    if (PREOFF) voff[v] = (int)(((int64_t)rl * ld + 32 - o + r) * 4);
+  }
+  // without PREOFF: voff = b_v ld 4 (scalar) + lane_c + rot_addr - 128 [p < o], where
+  // lane_c = 16 hh ld - 128 hh + 128 (the rotation's lane half and the + 32 base shift)
+  const int lane_c = (int)(16 * hh * ld) - 128 * hh + 128;
+  const int ut_off = (int)(32 * ld * 4);
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc(out + u0 * ld - 32, 0, -1, 0x00020000);
+  f32x4 st[LV];
+  auto gload = [&](int64_t c) {
+#pragma unroll
+    for (int i = 0; i < LV; ++i) {
+      const int f = tid + 256 * i, row = f / (D / 4), col = (f % (D / 4)) * 4;
+      int64_t item = c * SC_CHUNK + row;
+      item = item < rows ? item : rows - 1;
+      st[i] = *reinterpret_cast<const f32x4*>(table + item * D + col);
+    }
+  };
+  auto swrite = [&](int b) {
+#pragma unroll
+    for (int i = 0; i < LV; ++i) {
+      const int f = tid + 256 * i, row = f / (D / 4), col = (f % (D / 4)) * 4;
+      *reinterpret_cast<f32x4*>(&tab[b][row * P + col]) = st[i];
+    }
+  };
+  gload(c_begin);
+  swrite(0);
+  if (c_begin + 1 < c_end) gload(c_begin + 1);
+  __syncthreads();
+  const int64_t col_lo = c_begin * SC_CHUNK, col_hi = c_end * SC_CHUNK < rows ? c_end * SC_CHUNK : rows;
+  const int rows_left = (int)(B - u0 < 64 ? B - u0 : 64);
+  // rotated chunks k - 2 (r2) and k - 1 (r1); line A_{k-1} = lanes p < o from r2, p >= o from r1
+  f32x16 r1[2], r2[2];
+  // one register t (user tile t >> 4, register t & 15) of line A_L
+  auto store_reg = [&](int64_t L, int t, bool interior) {
+    const int ut = t >> 4, v = t & 15;
+    const bool lo = rot_addr[v] > (32 * hh + r) * 4;   // p < o
+    const float val = lo ? r2[ut][v] : r1[ut][v];
+    const int bv = (v & 3) + 8 * (v >> 2);
+    const int vo = PREOFF ? voff[v] : lane_c + rot_addr[v] - (lo ? 128 : 0);
+    const int so = (int)(L * SC_CHUNK * 4) + ut * ut_off + (PREOFF ? 0 : (int)(bv * ld * 4));
+    if (interior) {
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(val), rs, vo, so, 0);
+    } else {
+      // column of this lane's element relative to 32 L: r - o = q - 32 [p < o]; all 32-bit
+      const int colrel = ((rot_addr[v] >> 2) - 32 * hh) - (lo ? 32 : 0);
+      const int lo_s = (int)(col_lo - L * SC_CHUNK), hi_s = (int)(col_hi - L * SC_CHUNK);
+      if (colrel >= lo_s && colrel < hi_s && bv + 4 * hh < rows_left - 32 * ut)
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(val), rs, vo, so, 0);
+    }
+  };
+  auto line_interior = [&](int64_t L) { return full_rows && L > c_begin && (L + 1) * SC_CHUNK <= rows; };
+  constexpr int STEPS = KG * 16;                          // (g, q, s) steps of a chunk, 2 MFMAs each
+  constexpr int PER = 32 / STEPS > 0 ? 32 / STEPS : 1;    // stores per step
+  constexpr int EVERY = STEPS / 32 > 0 ? STEPS / 32 : 1;  // steps per store
+#pragma unroll 1
+  for (int64_t k = c_begin; k < c_end; ++k) {
+    const int kb = (int)((k - c_begin) & 1);
+    // line A_{k-1}'s stores ride between this chunk's MFMAs when it is an interior line
+    const bool inter = k > c_begin && line_interior(k - 1);
+    f32x16 acc[2];
+#pragma unroll
+    for (int ut = 0; ut < 2; ++ut)
+#pragma unroll
+      for (int v = 0; v < 16; ++v) acc[ut][v] = 0.f;
+    const float* tb = &tab[kb][r * P + 4 * hh];
+#pragma unroll
+    for (int g = 0; g < KG; ++g)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const f32x4 bt = *reinterpret_cast<const f32x4*>(tb + 32 * g + 8 * q);
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) {
+          const int step = (g * 4 + q) * 4 + s4;
+#pragma unroll
+          for (int ut = 0; ut < 2; ++ut) acc[ut] = mfma32(hf[ut][g][q][s4], bt[s4], acc[ut]);
+          if (inter && step % EVERY == 0) {
+#pragma unroll
+            for (int e = 0; e < PER; ++e) store_reg(k - 1, (step / EVERY) * PER + e, true);
+          }
+        }
+      }
+    if (k > c_begin && !inter) {
+#pragma unroll
+      for (int t = 0; t < 32; ++t) store_reg(k - 1, t, false);
+    }
+    if (k + 1 < c_end) {
+      swrite(kb ^ 1);
+      if (k + 2 < c_end) gload(k + 2);
+    }
+#pragma unroll
+    for (int ut = 0; ut < 2; ++ut) {
+      r2[ut] = r1[ut];
+#pragma unroll
+      for (int v = 0; v < 16; ++v)
+        r1[ut][v] = __int_as_float(__builtin_amdgcn_ds_bpermute(rot_addr[v], __float_as_int(acc[ut][v])));
+    }
+    __syncthreads();
+  }
+  // line A_{c_end - 1}, then the line after the last chunk (its lanes p < o)
+#pragma unroll
+  for (int t = 0; t < 32; ++t) store_reg(c_end - 1, t, false);
+#pragma unroll
+  for (int ut = 0; ut < 2; ++ut) r2[ut] = r1[ut];
+#pragma unroll
+  for (int t = 0; t < 32; ++t) store_reg(c_end, t, false);
+}
+
 }  // namespace gr
 
 // Returns GR_ERR_UNSUPPORTED when d is not one the kernel is built for (caller falls back).
@@ -486,8 +652,40 @@ int gr_score_launch(const float* h, int64_t B, int32_t d, const float* table, in
   // Direct accumulator stores when every logits row starts on a 128-byte line (row stride a
   // multiple of 32 floats, 128-B aligned base): 265 us vs the ring's 296 at C3 shapes.  The
   // reference's own layout (stride N+1, odd) straddles lines and keeps the ring (456 vs 296 us).
-  const int64_t impl = option("score_impl");
+  int64_t impl = option("score_impl");
   const bool lines_aligned = ld % 32 == 0 && (reinterpret_cast<uintptr_t>(logits) & 127) == 0;
+  // Rows off the 128-byte grid (the reference's contiguous [B, N+1] logits, d <= 64): up to ~160 MB of
+  // logits the halves of every straddled line meet in the 256 MB Infinity Cache, so the direct
+  // kernel's plain stores cost nothing (C3 B 512: 136 vs 135 us padded); beyond it they reach HBM as
+  // partial lines (B 2048: 593 vs 393 us) and the rotated whole-line kernel runs (412 us;
+  // profiles/r04/ab_predict_contiguous.txt).
+  const bool fits_mall = (double)B * (double)ld * 4.0 <= 160e6;
+  if (!lines_aligned && d <= 64 && impl == 2 && fits_mall) impl = 3;
+  if (!lines_aligned && d <= 64 && (impl == 2 || impl == 4)) {   // rotated whole-line stores
+    int64_t sl2 = (2 * cus + ublocks - 1) / ublocks;
+    if (sl2 > chunks) sl2 = chunks;
+    if (sl2 < 1) sl2 = 1;
+    const dim3 g2((unsigned)(ublocks * sl2));
+    const int smaj = option("score_slice_major") != 0 ? 1 : 0;
+    const bool pre = impl == 2;   // store offsets precomputed per register (4: on the fly; A/B)
+    auto k = d == 32 ? (pre ? score_rot_kernel<32, true> : score_rot_kernel<32, false>)
+                     : (pre ? score_rot_kernel<64, true> : score_rot_kernel<64, false>);
+    hipLaunchKernelGGL(k, g2, dim3(256), 0, st, h, B, table, rows, logits, ld, (int)ublocks, (int)sl2, smaj);
+    return check_launch("gr_score_f32 (rotated lines)");
+  }
+  if (impl == 3) {   // direct stores through L2 (no streaming hint), any row alignment
+    int64_t sl2 = (2 * cus + ublocks - 1) / ublocks;
+    if (sl2 > chunks) sl2 = chunks;
+    if (sl2 < 1) sl2 = 1;
+    const dim3 g2((unsigned)(ublocks * sl2));
+    const int smaj = option("score_slice_major") != 0 ? 1 : 0;
+    switch (d) {
+      case 32: hipLaunchKernelGGL((score_direct_kernel<32, false>), g2, dim3(256), 0, st, h, B, table, rows, logits, ld, (int)ublocks, (int)sl2, smaj); break;
+      case 64: hipLaunchKernelGGL((score_direct_kernel<64, false>), g2, dim3(256), 0, st, h, B, table, rows, logits, ld, (int)ublocks, (int)sl2, smaj); break;
+      default: hipLaunchKernelGGL((score_direct_kernel<128, false>), g2, dim3(256), 0, st, h, B, table, rows, logits, ld, (int)ublocks, (int)sl2, smaj); break;
+    }
+    return check_launch("gr_score_f32 (direct, cached stores)");
+  }
   if (impl == 1 || (impl == 2 && lines_aligned)) {
     int64_t sl2 = (2 * cus + ublocks - 1) / ublocks;
     if (sl2 > chunks) sl2 = chunks;

@@ -95,16 +95,18 @@ class SASRec(nn.Module):
         """``forward(log_seqs)[:, -1, :]`` (model.py:104) without materialising other positions."""
         return ops.sasrec_forward(self._binding(log_seqs), log_seqs, last_only=True)
 
-    # predict's logits layout: False (default) -- a [B, ld] buffer (rows 128-byte aligned, ld =
-    # roundup(item_num + 1, 32)) viewed as [B, item_num + 1], unit column stride, which every use in
-    # the reference (evaluate.py:27-32, train.py:45-50) takes as is; True -- a contiguous tensor like
-    # the reference's matmul result (.view() works), at the cost of the scoring kernel's unaligned
-    # store path (profiles/r03_ab_predict_ld.txt: 440 vs 394 us at B 2048, 146 vs 109 us at B 128).
-    contiguous_logits = False
+    # predict's logits layout: True (default) -- a contiguous [B, item_num + 1] tensor like the
+    # reference's matmul result (model.py:107; .view() works).  Its rows start anywhere in a 128-byte
+    # line; the scoring kernel stores whole lines anyway (lanes rotated by each row's line offset,
+    # score.hip score_rot_kernel): 412 vs 393 us per C3 call at B 2048, equal at B <= 512
+    # (profiles/r04/ab_predict_contiguous.txt).  False -- a [B, ld] buffer (ld = roundup(item_num +
+    # 1, 32)) viewed as [B, item_num + 1]: unit column stride, not contiguous.
+    contiguous_logits = True
 
     @torch.no_grad()
     def predict(self, log_seqs):
-        """model.py:98-108: logits ``[B, item_num+1]`` = last hidden state x item table^T."""
+        """model.py:98-108: logits ``[B, item_num+1]`` = last hidden state x item table^T, a fresh
+        writable contiguous tensor (evaluate.py:27 writes column 0 in place)."""
         out = None
         if self.contiguous_logits:
             out = torch.empty((log_seqs.shape[0], self.item_emb.weight.shape[0]), dtype=torch.float32,

@@ -397,10 +397,11 @@ def bench_sas_c3(a, world, rank, dev):
     p = synth.sasrec_params(d, n, 2, 1, 64, dev)
     model = synth.sasrec_model(items, p, dev)
     seqs = synth.sequences(a.sas_batch, n, items, 2000 + rank, dev)
-    # timed through the drop-in surface: model.predict(seqs) allocates its fresh [B, N+1] logits
-    # (rows 128-B aligned, ops.logits_buffer) every call, as the reference's evaluate.py:26 sees it
+    # timed through the drop-in surface: model.predict(seqs) allocates its fresh contiguous [B, N+1]
+    # logits every call (the reference's matmul layout, model.py:107), as evaluate.py:26 sees it
+    assert model.contiguous_logits
     wall, dev_ms = timed(lambda: model.predict(seqs), a.steps, a.warmup, world)
-    out = ops.logits_buffer(a.sas_batch, items + 1, dev)
+    out = torch.empty((a.sas_batch, items + 1), dtype=torch.float32, device=dev)   # predict's layout
     h = model.last_hidden(seqs)
     table = model.item_emb.weight.detach()
     score_ms = kernel_ms(lambda: ops.score(h, table, out=out))
@@ -415,7 +416,8 @@ def bench_sas_c3(a, world, rank, dev):
            "config": {"workload": "sas_c3: SASRec predict, 2 blocks, d 64, n 50, H 1, mlp 64, "
                                   "100k-item full-catalog logits written", "users_per_rank_per_step": a.sas_batch,
                       "parallelism": f"user-sharded x{world}, no collective"},
-           "roofline": roofline("score_direct_kernel<64>", 2 * d * (items + 1) * a.sas_batch, score_ms, "sasrec"),
+           "roofline": roofline("score_rot_kernel<64" if a.sas_batch * (items + 1) * 4 > 160e6 else "score_direct_kernel<64",
+                                2 * d * (items + 1) * a.sas_batch, score_ms, "sasrec"),
            "call": {"device_ms": dev_ms, "device_ms_per_rank": per_rank(dev_ms, world), "flop_per_user": fl,
                     "frac_of_fp32_peak": fl * a.sas_batch / (dev_ms * 1e-3) / 1e12 / FP32_PEAK_TFLOPS,
                     "flop_per_user_executed": fl_exe,

@@ -17,6 +17,7 @@ from gr_amd import ops, synth  # noqa: E402
 ap = argparse.ArgumentParser()
 ap.add_argument("--B", default="2048,128")
 ap.add_argument("--items", type=int, default=100_000)
+ap.add_argument("--impls", default="2,3", help="score_impl values to time (gr_amd.h)")
 a = ap.parse_args()
 dev = torch.device("cuda:0")
 p = synth.sasrec_params(64, 50, 2, 1, 64, dev)
@@ -46,7 +47,15 @@ for B in [int(v) for v in a.B.split(",")]:
     ops.sasrec_predict(b, seqs, out=cont)
     torch.cuda.synchronize()
     same = torch.equal(pad, cont)
-    for name, out in (("padded ld", pad), ("contiguous", cont), ("padded ld", pad), ("contiguous", cont)):
-        us = timeit(lambda: ops.sasrec_predict(b, seqs, out=out))
-        print(f"B={B:5d} {name:10s} ld={out.stride(0):6d}: {us:8.1f} us/call ({B / us:6.3f} M seqs/s)  "
-              f"bitwise equal: {same}", flush=True)
+    from gr_amd import _lib
+    ref = pad.clone()
+    for rep in range(2):
+        for impl in [int(v) for v in a.impls.split(",")]:
+            _lib.set_option("score_impl", impl)
+            for name, out in (("padded ld", pad), ("contiguous", cont)):
+                out.fill_(float("nan"))
+                us = timeit(lambda: ops.sasrec_predict(b, seqs, out=out))
+                eq = torch.equal(out, ref)
+                print(f"B={B:5d} score_impl={impl} {name:10s} ld={out.stride(0):6d}: {us:8.1f} us/call "
+                      f"({B / us:6.3f} M seqs/s)  bitwise equal to padded: {eq}", flush=True)
+    _lib.set_option("score_impl", 2)

@@ -93,28 +93,52 @@ def test_predict_returns_fresh_writable_tensor(dev):
     assert not torch.equal(a[:, 0], b[:, 0]) and torch.equal(a[:, 1:], b[:, 1:])
 
 
-def test_predict_contiguous_logits_option(dev):
-    """SASRec.contiguous_logits = True: predict returns a contiguous [B, N+1] tensor (the reference's
-    matmul layout: .view() works), bitwise the row-padded default's values."""
+def test_predict_contiguous_by_default(dev):
+    """predict returns a contiguous [B, N+1] tensor by default (the reference's matmul layout,
+    model.py:107: .view() works), bitwise the row-padded option's values."""
     m, out, meta = build("sas_syn_c3", dev)
     seqs = torch.from_numpy(out["seqs"]).to(dev)
-    a = m.predict(seqs)
+    c = m.predict(seqs)
     try:
-        m.contiguous_logits = True
-        c = m.predict(seqs)
-    finally:
         m.contiguous_logits = False
-    assert c.is_contiguous() and c.shape == a.shape
+        a = m.predict(seqs)
+    finally:
+        m.contiguous_logits = True
+    assert c.is_contiguous() and c.shape == a.shape and not a.is_contiguous()
     assert torch.equal(a, c)
     assert c.view(-1).numel() == a.numel()
 
 
+@pytest.mark.parametrize("B,rows,pad,off", [(2048, 100001, 0, 0), (700, 60001, 0, 0), (300, 100001, 0, 0),
+                                            (1000, 50001, 5, 3), (1500, 40000, 7, 1), (129, 100001, 0, 0)])
+def test_score_unaligned_rows_bitwise(dev, B, rows, pad, off):
+    """Logits rows off the 128-byte grid: the rotated whole-line kernel (> 160 MB of logits) and the
+    direct kernel (smaller) against the aligned layout, bit for bit, including a row stride that is
+    not rows (pad), a base that is not line-aligned (off), partial user blocks and a partial last
+    chunk; every element written exactly once (NaN-filled canvas, guard columns untouched)."""
+    from gr_amd import ops
+    g = torch.Generator(device=dev).manual_seed(B + rows)
+    h = torch.randn(B, 64, device=dev, generator=g)
+    table = torch.randn(rows, 64, device=dev, generator=g)
+    ref = ops.logits_buffer(B, rows, dev)
+    ops.score(h, table, out=ref)
+    canvas = torch.full((B, rows + pad + off), float("nan"), device=dev)
+    view = canvas[:, off:off + rows]
+    ops.score(h, table, out=view)
+    torch.cuda.synchronize()
+    assert torch.equal(view, ref)
+    if pad + off:
+        assert torch.isnan(canvas[:, :off]).all() and torch.isnan(canvas[:, off + rows:]).all()
+
+
 @pytest.mark.parametrize("name", ["sas_csv_c1", "sas_syn_c3"])
 def test_predict_row_padded_layout(name, dev, sas_path):
-    """predict() returns a [B, N+1] view whose rows are 32-float aligned (direct-store scoring); the
-    values are bitwise those written into a packed buffer, and evaluate.py:27-32 runs on the view."""
+    """contiguous_logits = False: predict() returns a [B, N+1] view whose rows are 32-float aligned
+    (direct-store scoring); the values are bitwise those written into a packed buffer, and
+    evaluate.py:27-32 runs on the view."""
     from gr_amd import ops
     m, out, meta = build(name, dev)
+    m.contiguous_logits = False
     seqs = torch.from_numpy(out["seqs"]).to(dev)
     targets = torch.from_numpy(out["targets"]).to(dev)
     a = m.predict(seqs)
