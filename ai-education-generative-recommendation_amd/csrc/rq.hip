@@ -189,15 +189,25 @@ __global__ __launch_bounds__(RQ_W * 64) void rq_quantize_kernel(
             f32x16 acc;
 #pragma unroll
             for (int v = 0; v < 16; ++v) acc[v] = 0.f;
+#ifndef GR_QDIAG
+#define GR_QDIAG 0   // diagnostic builds only (scripts/build_variant.sh): 1 no argmin, 2 no MFMA
+#endif
 #pragma unroll
             for (int j = 0; j < HQ; ++j)
 #pragma unroll
-              for (int s = 0; s < 4; ++s) acc = mfma32(a[j][s], res[i][j][s], acc);
+              for (int s = 0; s < 4; ++s) {
+                if (GR_QDIAG == 2) acc[4 * j + s] += a[j][s] * res[i][j][s];
+                else acc = mfma32(a[j][s], res[i][j][s], acc);
+              }
 #pragma unroll
             for (int v = 0; v < 16; ++v) {
               const int cd = c0 + ct * 32 + (v & 3) + 8 * (v >> 2) + 4 * h;
               // (|r|^2 + |c|^2) - 2 r.c: 2 r.c is exact, so one fma rounds the same value
               const float dd = fmaf(-2.f, acc[v], rn[i] + cnv[v]);
+              if (GR_QDIAG == 1) {
+                best[i] = fminf(best[i], acc[v]);
+                continue;
+              }
               const bool lt = dd < best[i];
               if (SECOND) second[i] = lt ? best[i] : fminf(second[i], dd);
               bi[i] = lt ? cd : bi[i];
