@@ -32,6 +32,10 @@
 #include "gr_common.h"
 #include "rq_quant.h"
 
+#ifndef GR_QDIAG
+#define GR_QDIAG 0   // diagnostic builds only (scripts/build_variant.sh): 1 no argmin, 2 no MFMA,
+#endif               // 3 no codebook norms, 4 no residual norms (wrong IDs in all of them)
+
 namespace gr {
 
 struct RQLevels {
@@ -77,7 +81,7 @@ __device__ __forceinline__ void stage_codes(const float* __restrict__ cb, int e,
 #pragma unroll
           for (int i = 0; i < 4; ++i) v[8 * (q % HQ) + 2 * i + q / HQ] = t[i];
         }
-        s = aten_rowsq([&](int f) { return v[f]; }, EP);
+        s = GR_QDIAG == 3 ? 0.f : aten_rowsq([&](int f) { return v[f]; }, EP);
       } else {
         s = aten_rowsq([&](int f) { return cbs[feat_off<EP>(c, f)]; }, e);
       }
@@ -156,7 +160,7 @@ __global__ __launch_bounds__(RQ_W * 64) void rq_quantize_kernel(
     int bi[RQ_MAXT];
 #pragma unroll
     for (int i = 0; i < RQ_MAXT; ++i) {
-      rn[i] = rn_exact<EP>(res[i], e, h);
+      rn[i] = GR_QDIAG == 4 ? 0.f : rn_exact<EP>(res[i], e, h);
       best[i] = __builtin_inff();
       second[i] = __builtin_inff();
       bi[i] = 0x7fffffff;
@@ -189,9 +193,6 @@ __global__ __launch_bounds__(RQ_W * 64) void rq_quantize_kernel(
             f32x16 acc;
 #pragma unroll
             for (int v = 0; v < 16; ++v) acc[v] = 0.f;
-#ifndef GR_QDIAG
-#define GR_QDIAG 0   // diagnostic builds only (scripts/build_variant.sh): 1 no argmin, 2 no MFMA
-#endif
 #pragma unroll
             for (int j = 0; j < HQ; ++j)
 #pragma unroll
