@@ -79,6 +79,10 @@ static std::atomic<int64_t> g_rt_kv2{1};
 // (sas_tail_h_kernel: q . K_j and p . V reassociated through W_k / W_v, no K|V projection of the
 // B n rows); 0: K|V projected for sas_tail_kernel).  Within the logits tolerance; A/B timing.
 static std::atomic<int64_t> g_tail_h{1};
+// attn_wave (0 (default): the 4-wave workgroup attention kernel; 1: at hd 64 / 128 one wave per
+// (sequence, head, query tile) walking its own key tiles, attn.hip attn_wave_kernel; 2: its
+// two-waves-per-SIMD form at hd 128).  Bitwise the same output; A/B timing.
+static std::atomic<int64_t> g_attn_wave{0};
 
 int64_t option(const char* name) {
   if (!strcmp(name, "rq_fused")) return g_rq_fused.load();
@@ -104,6 +108,7 @@ int64_t option(const char* name) {
   if (!strcmp(name, "emb_rows")) return g_emb_rows.load();
   if (!strcmp(name, "rt_kv2")) return g_rt_kv2.load();
   if (!strcmp(name, "tail_h")) return g_tail_h.load();
+  if (!strcmp(name, "attn_wave")) return g_attn_wave.load();
   return -1;
 }
 }  // namespace gr
@@ -134,6 +139,7 @@ extern "C" int gr_set_option(const char* name, int64_t value) {
   if (!strcmp(name, "emb_rows") && (value == 32 || value == 64)) { gr::g_emb_rows = value; return GR_OK; }
   if (!strcmp(name, "rt_kv2") && (value == 0 || value == 1)) { gr::g_rt_kv2 = value; return GR_OK; }
   if (!strcmp(name, "tail_h") && (value == 0 || value == 1)) { gr::g_tail_h = value; return GR_OK; }
+  if (!strcmp(name, "attn_wave") && value >= 0 && value <= 2) { gr::g_attn_wave = value; return GR_OK; }
   return gr::fail(GR_ERR_ARG, std::string("gr_set_option: unknown option or value: ") + name);
 }
 

@@ -388,6 +388,259 @@ __global__ __launch_bounds__(256, 1) void attn_pair_kernel(const float* __restri
   }
 }
 
+// One wave per (sequence, head, query tile), no lockstep (option attn_wave, the default): the
+// workgroup kernel above walks its 4 waves' key tiles together over shared K/V tiles, so at n = 200
+// (T = 7 query tiles) a workgroup runs 7 + 3 key-tile iterations for 28 (query, key) tile steps
+// and a SIMD idles ~30 % of them.  Here each wave walks exactly its own
+// qt + 1 key tiles, reading K and V straight from global (L2) into registers as the MFMA operands
+// -- K fragments kf[it][g] = K[key 32 kt + r][32 it + 8 g + 4 h .. +3] (the A operand), V values
+// vf[ft][s] = V[key 32 kt + (s&3) + 8 (s>>2) + 4 h][32 ft + r] -- with the next tile's K issued
+// right after this tile's S = K Q^T MFMAs and its V after the O += V P^T MFMAs (each hidden
+// behind the other half of the step).  One wave per SIMD (~300 VGPRs of operands and
+// accumulators); the hardware deals the waves out, longest query tiles first, and every query tile
+// of one (sequence, head) goes to the same XCD so its K / V stay in that XCD's L2.  Per row the
+// instruction sequence is attn_mfma_kernel<HD, *, true>'s (same S chain over (it, g, s4), the same
+// lazy softmax, the same O chain over (ft, s)): bitwise the same output.
+template <int HD>
+__global__ __launch_bounds__(64) void attn_wave_kernel(const float* __restrict__ qkv, float* __restrict__ out,
+                                                      int n, int H, float scale, int nbh, int qt_lo) {
+  constexpr int FT = HD / 32;
+  const int lane = threadIdx.x, r = lane & 31, h = lane >> 5;
+  const int T = (n + 31) / 32, nt = T - qt_lo;
+  // work item of this wave: XCD x = blockIdx % 8 owns the (sequence, head) pairs bh = x (mod 8);
+  // within it, pair-major with the query tiles in descending order
+  const int x = blockIdx.x & 7, k = blockIdx.x >> 3;
+  const int mx = (nbh - x + 7) / 8;   // pairs on this XCD
+  if (k >= mx * nt) return;
+  const int bh = x + 8 * (k / nt), qt = T - 1 - k % nt;
+  const int b = bh / H, hh = bh % H;
+  const int d = H * HD;
+  const int64_t rs = 3LL * d;
+  const float* base = qkv + (int64_t)b * n * rs + hh * HD;
+  const float* Qb = base;
+  const float* Kb = base + d;
+  const float* Vb = base + 2 * d;
+  const int qi = qt * 32 + r;
+  const int qc = qi < n ? qi : n - 1;
+  f32x4 qf[FT][4];
+#pragma unroll
+  for (int it = 0; it < FT; ++it)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const f32x4 v = *reinterpret_cast<const f32x4*>(Qb + (int64_t)qc * rs + 32 * it + 8 * g + 4 * h);
+      qf[it][g] = v * scale;   // q * sqrt(1/hd) (functional.py:6578)
+    }
+  f32x16 O[FT];
+#pragma unroll
+  for (int ft = 0; ft < FT; ++ft)
+#pragma unroll
+    for (int v = 0; v < 16; ++v) O[ft][v] = 0.f;
+  float m = -INFINITY, l = 0.f;
+  f32x4 kf[FT][4];
+  float vf[FT][16];
+  auto load_k = [&](int kt) {
+    int key = kt * 32 + r;
+    key = key < n ? key : n - 1;
+    const float* kr = Kb + (int64_t)key * rs + 4 * h;
+#pragma unroll
+    for (int it = 0; it < FT; ++it)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) kf[it][g] = *reinterpret_cast<const f32x4*>(kr + 32 * it + 8 * g);
+  };
+  auto load_v = [&](int kt) {
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      int key = kt * 32 + (s & 3) + 8 * (s >> 2) + 4 * h;
+      key = key < n ? key : n - 1;   // keys past n: P = 0 against a clamped (finite) row
+      const float* vr = Vb + (int64_t)key * rs + r;
+#pragma unroll
+      for (int ft = 0; ft < FT; ++ft) vf[ft][s] = vr[32 * ft];
+    }
+  };
+  load_k(0);
+  load_v(0);
+  for (int kt = 0; kt <= qt; ++kt) {
+    f32x16 S;
+#pragma unroll
+    for (int v = 0; v < 16; ++v) S[v] = 0.f;
+#pragma unroll
+    for (int it = 0; it < FT; ++it)
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) S = mfma32(kf[it][g][s4], qf[it][g][s4], S);
+    if (kt < qt) load_k(kt + 1);   // the K operands are read at issue: their registers refill now
+    // causal / padding mask on the diagonal tile and the last key tile (attn_mfma_kernel, LAZY)
+    float tmax = -INFINITY;
+    if (kt == qt || kt * 32 + 32 > n) {
+#pragma unroll
+      for (int v = 0; v < 16; ++v) {
+        const int key = kt * 32 + (v & 3) + 8 * (v >> 2) + 4 * h;
+        if (key > qi || key >= n) S[v] = -INFINITY;
+        tmax = fmaxf(tmax, S[v]);
+      }
+    } else {
+#pragma unroll
+      for (int v = 0; v < 16; ++v) tmax = fmaxf(tmax, S[v]);
+    }
+    tmax = fmaxf(tmax, __shfl_xor(tmax, 32));
+    const bool up = tmax > m + AT_LAZY;   // lazy rescaling (attn_mfma_kernel)
+    if (__any(up)) {
+      const float mn = up ? tmax : m;
+      const float alpha = __expf(m - mn);
+      l *= alpha;
+      m = mn;
+#pragma unroll
+      for (int ft = 0; ft < FT; ++ft) O[ft] *= alpha;
+    }
+    float ts = 0.f;
+#pragma unroll
+    for (int v = 0; v < 16; ++v) {
+      const float e = __expf(S[v] - m);
+      S[v] = e;
+      ts += e;
+    }
+    ts += __shfl_xor(ts, 32);
+    l += ts;
+#pragma unroll
+    for (int ft = 0; ft < FT; ++ft)
+#pragma unroll
+      for (int s = 0; s < 16; ++s) O[ft] = mfma32(vf[ft][s], S[s], O[ft]);
+    if (kt < qt) load_v(kt + 1);
+  }
+  if (qi < n) {
+    const float inv = 1.0f / l;
+    float* orow = out + ((int64_t)b * n + qi) * d + hh * HD;
+#pragma unroll
+    for (int ft = 0; ft < FT; ++ft)
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        *reinterpret_cast<f32x4*>(orow + 32 * ft + 8 * g + 4 * h) =
+            f32x4{O[ft][4 * g], O[ft][4 * g + 1], O[ft][4 * g + 2], O[ft][4 * g + 3]} * inv;
+  }
+}
+
+// attn_wave=2: the same walk at TWO waves per SIMD (<= 256 registers): K is streamed in 32-feature
+// quarters and V in 32-feature slices, each one step ahead in a two-slot ring (K quarter it + 1,
+// or the next key tile's first quarter, is issued before quarter it's 16 MFMAs; likewise V), so
+// only 64 operand registers are live instead of 128; the second wave on the SIMD covers what one
+// 16-MFMA step does not hide.  Same per-row instruction sequence: bitwise attn_wave_kernel.
+template <int HD>
+__global__ __launch_bounds__(64, 2) void attn_wave2_kernel(const float* __restrict__ qkv, float* __restrict__ out,
+                                                          int n, int H, float scale, int nbh, int qt_lo) {
+  constexpr int FT = HD / 32;
+  const int lane = threadIdx.x, r = lane & 31, h = lane >> 5;
+  const int T = (n + 31) / 32, nt = T - qt_lo;
+  const int x = blockIdx.x & 7, k = blockIdx.x >> 3;
+  const int mx = (nbh - x + 7) / 8;
+  if (k >= mx * nt) return;
+  const int bh = x + 8 * (k / nt), qt = T - 1 - k % nt;
+  const int b = bh / H, hh = bh % H;
+  const int d = H * HD;
+  const int64_t rs = 3LL * d;
+  const float* base = qkv + (int64_t)b * n * rs + hh * HD;
+  const float* Qb = base;
+  const float* Kb = base + d + 4 * h;
+  const float* Vb = base + 2 * d + r;
+  const int qi = qt * 32 + r;
+  const int qc = qi < n ? qi : n - 1;
+  f32x4 qf[FT][4];
+#pragma unroll
+  for (int it = 0; it < FT; ++it)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const f32x4 v = *reinterpret_cast<const f32x4*>(Qb + (int64_t)qc * rs + 32 * it + 8 * g + 4 * h);
+      qf[it][g] = v * scale;
+    }
+  f32x16 O[FT];
+#pragma unroll
+  for (int ft = 0; ft < FT; ++ft)
+#pragma unroll
+    for (int v = 0; v < 16; ++v) O[ft][v] = 0.f;
+  float m = -INFINITY, l = 0.f;
+  f32x4 kq[2][4];
+  float vq[2][16];
+  auto load_k = [&](int kt, int it, int slot) {
+    int key = kt * 32 + r;
+    key = key < n ? key : n - 1;
+    const float* kr = Kb + (int64_t)key * rs + 32 * it;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) kq[slot][g] = *reinterpret_cast<const f32x4*>(kr + 8 * g);
+  };
+  auto load_v = [&](int kt, int ft, int slot) {
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      int key = kt * 32 + (s & 3) + 8 * (s >> 2) + 4 * h;
+      key = key < n ? key : n - 1;
+      vq[slot][s] = Vb[(int64_t)key * rs + 32 * ft];
+    }
+  };
+  load_k(0, 0, 0);
+  load_v(0, 0, 0);
+  for (int kt = 0; kt <= qt; ++kt) {
+    f32x16 S;
+#pragma unroll
+    for (int v = 0; v < 16; ++v) S[v] = 0.f;
+#pragma unroll
+    for (int it = 0; it < FT; ++it) {
+      if (it + 1 < FT) load_k(kt, it + 1, (it + 1) & 1);
+      else if (kt < qt) load_k(kt + 1, 0, (it + 1) & 1);
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) S = mfma32(kq[it & 1][g][s4], qf[it][g][s4], S);
+    }
+    float tmax = -INFINITY;
+    if (kt == qt || kt * 32 + 32 > n) {
+#pragma unroll
+      for (int v = 0; v < 16; ++v) {
+        const int key = kt * 32 + (v & 3) + 8 * (v >> 2) + 4 * h;
+        if (key > qi || key >= n) S[v] = -INFINITY;
+        tmax = fmaxf(tmax, S[v]);
+      }
+    } else {
+#pragma unroll
+      for (int v = 0; v < 16; ++v) tmax = fmaxf(tmax, S[v]);
+    }
+    tmax = fmaxf(tmax, __shfl_xor(tmax, 32));
+    const bool up = tmax > m + AT_LAZY;
+    if (__any(up)) {
+      const float mn = up ? tmax : m;
+      const float alpha = __expf(m - mn);
+      l *= alpha;
+      m = mn;
+#pragma unroll
+      for (int ft = 0; ft < FT; ++ft) O[ft] *= alpha;
+    }
+    float ts = 0.f;
+#pragma unroll
+    for (int v = 0; v < 16; ++v) {
+      const float e = __expf(S[v] - m);
+      S[v] = e;
+      ts += e;
+    }
+    ts += __shfl_xor(ts, 32);
+    l += ts;
+#pragma unroll
+    for (int ft = 0; ft < FT; ++ft) {
+      if (ft + 1 < FT) load_v(kt, ft + 1, (ft + 1) & 1);
+      else if (kt < qt) load_v(kt + 1, 0, (ft + 1) & 1);
+#pragma unroll
+      for (int s = 0; s < 16; ++s) O[ft] = mfma32(vq[ft & 1][s], S[s], O[ft]);
+    }
+  }
+  if (qi < n) {
+    const float inv = 1.0f / l;
+    float* orow = out + ((int64_t)b * n + qi) * d + hh * HD;
+#pragma unroll
+    for (int ft = 0; ft < FT; ++ft)
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        *reinterpret_cast<f32x4*>(orow + 32 * ft + 8 * g + 4 * h) =
+            f32x4{O[ft][4 * g], O[ft][4 * g + 1], O[ft][4 * g + 2], O[ft][4 * g + 3]} * inv;
+  }
+}
+
 }  // namespace gr
 
 // Returns GR_ERR_UNSUPPORTED (message untouched) for head widths the kernel is not built for.
@@ -401,6 +654,23 @@ int gr_attn_mfma_launch(const float* qkv, float* out, int64_t B, int n, int H, i
   if (B * H > 0x7fffffffLL) return GR_ERR_UNSUPPORTED;
   const int qt_lo = last_tile_only ? (n - 1) / 32 : 0;
   const dim3 g((unsigned)(B * H)), blk(256);
+  if ((hd == 64 || hd == 128) && option("attn_wave") != 0 && option("attn_lazy") != 0) {
+    const int64_t nbh = B * H, nt = (n + 31) / 32 - qt_lo;
+    const int64_t waves = 8 * ((nbh + 7) / 8) * nt;
+    if (waves <= 0x7fffffffLL) {
+      const bool two = option("attn_wave") == 2;
+      if (hd == 64)
+        hipLaunchKernelGGL(attn_wave_kernel<64>, dim3((unsigned)waves), dim3(64), 0, st, qkv, out, n, H, scale,
+                           (int)nbh, qt_lo);
+      else if (two)
+        hipLaunchKernelGGL(attn_wave2_kernel<128>, dim3((unsigned)waves), dim3(64), 0, st, qkv, out, n, H, scale,
+                           (int)nbh, qt_lo);
+      else
+        hipLaunchKernelGGL(attn_wave_kernel<128>, dim3((unsigned)waves), dim3(64), 0, st, qkv, out, n, H, scale,
+                           (int)nbh, qt_lo);
+      return check_launch("sasrec attention (one wave per query tile)");
+    }
+  }
   if (!last_tile_only && option("attn_pair") != 0) {
     switch (hd) {
       case 32: hipLaunchKernelGGL(attn_pair_kernel<32>, g, blk, 0, st, qkv, out, n, H, scale); break;

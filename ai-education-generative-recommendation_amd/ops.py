@@ -247,12 +247,13 @@ class RqBinding:
         self.packed = torch.empty(nf, dtype=torch.float32, device=self.device) if nf else None
         self._pack_key = None
 
-    # Re-use one packed encoder image across calls.  Off by default: an update that bumps no
-    # version counter (a replayed training graph's optimizer step, a write through ``.data``)
-    # would leave the image stale, so every call packs the current weights into its workspace
-    # (one extra launch).  ``RQVAE.freeze_encoder()`` turns it on for serving with fixed weights;
-    # the image is then re-packed whenever a weight's version or the graph-replay epoch changes.
-    frozen = False
+    # Re-use one packed encoder image across calls, re-packed whenever a weight's version counter
+    # (load_state_dict, optimizer steps, any in-place op) or the graph-replay epoch moves (a
+    # replayed training graph updates the weights without a version bump: ops.weights_changed).
+    # A write that bypasses both (``param.data[...] = ...``) must call weights_changed(), or the
+    # owner runs with ``RQVAE.freeze_encoder(False)``: every call then packs the current weights
+    # into its workspace (one extra launch, 4 us per C2 call, profiles/r04/ab_rq_pack.txt).
+    frozen = True
 
     def packed_ptr(self):
         """Device pointer of the up-to-date packed encoder image; None: pack per call (the default,

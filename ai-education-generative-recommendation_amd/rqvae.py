@@ -357,14 +357,15 @@ class RQVAE(nn.Module):
             ws, bs = self.encoder.folded()
             return ops.RqBinding(ws, bs, self.rq.codebooks())
         b = ops.rq_binding(self, self._encode_params)
-        b.frozen = self.__dict__.get("_gr_frozen", False)
+        b.frozen = self.__dict__.get("_gr_frozen", True)
         return b
 
     def freeze_encoder(self, frozen=True):
-        """Serving with fixed weights: keep the fused encoder's packed weight image across
-        get_indices calls (re-packed when a weight's version counter or ops.weights_changed()
-        moves) instead of packing it per call.  Writes that bypass both (``param.data[...] = ``)
-        must call ops.weights_changed()."""
+        """True (default): keep the fused encoder's packed weight image across get_indices calls,
+        re-packed when a weight's version counter or the graph-replay epoch moves
+        (ops.weights_changed(); every training-graph replay bumps it).  False: pack the current
+        weights on every call -- for callers that write weights through ``.data`` without calling
+        ops.weights_changed()."""
         self.__dict__["_gr_frozen"] = bool(frozen)
         return self
 

@@ -167,8 +167,9 @@ def test_wider_envelope_vs_oracle(dev, in_dim, e_dim, parity_log):
 
 def test_frozen_pack_sees_graph_replayed_updates(dev):
     """ADVICE r3 (high): a captured AdamW step changes the encoder weights without a version bump;
-    get_indices must encode with the new weights (per-call pack by default; the frozen cache
-    re-packs on the replay epoch)."""
+    get_indices must encode with the new weights (the cached image, the default, re-packs on the
+    replay epoch; freeze_encoder(False) packs per call).  Also a write through .data followed by
+    ops.weights_changed()."""
     from gr_amd import RQVAE, ops
     torch.manual_seed(0)
     m = RQVAE(in_dim=768, num_emb_list=[256] * 3, e_dim=32, layers=[256, 128], dropout_prob=0.0,
@@ -189,3 +190,11 @@ def test_frozen_pack_sees_graph_replayed_updates(dev):
         ref = ops.rq_encode(xt, [l.weight.detach().clone() for l in lin], [l.bias.detach().clone() for l in lin],
                             [c.clone() for c in m.rq.codebooks()])
         assert torch.equal(m.get_indices(xt), ref), f"frozen={frozen}"
+    m.freeze_encoder(True)
+    m.get_indices(xt)
+    lin = m.encoder.linears()
+    lin[0].weight.data.mul_(0.5)    # bypasses the version counter the autograd tensor carries
+    ops.weights_changed()
+    ref = ops.rq_encode(xt, [l.weight.detach().clone() for l in lin], [l.bias.detach().clone() for l in lin],
+                        [c.clone() for c in m.rq.codebooks()])
+    assert torch.equal(m.get_indices(xt), ref)

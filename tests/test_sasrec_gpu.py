@@ -292,6 +292,31 @@ def test_tail_h_form_vs_kv_form_and_oracle(d, heads, n, blocks, B, dev):
         assert ((got - ref).abs() / ref.abs().amax(1, keepdim=True)).max().item() <= TOL
 
 
+@pytest.mark.parametrize("d,heads,n,blocks,B", [(128, 1, 200, 2, 37), (128, 2, 130, 2, 9), (64, 1, 100, 2, 17),
+                                                (64, 2, 77, 1, 5), (128, 1, 33, 1, 3)])
+def test_attn_wave_equals_workgroup_kernel(d, heads, n, blocks, B, dev):
+    """Option attn_wave: the one-wave-per-query-tile attention (attn.hip attn_wave_kernel; 2: the
+    two-waves-per-SIMD form attn_wave2_kernel) against the 4-wave workgroup kernel -- the same
+    per-row instruction sequence, so hidden states and logits are bitwise equal (hd 128 / 64)."""
+    from gr_amd import _lib, synth
+    items = 500
+    p = synth.sasrec_params(d, n, blocks, heads, 64, dev)
+    m = synth.sasrec_model(items, p, dev, seed=d + n)
+    seqs = synth.sequences(B, n, items, 3 + n, dev)
+    res = {}
+    try:
+        _lib.set_option("sas_fused", 0)
+        for opt in (0, 1, 2):
+            _lib.set_option("attn_wave", opt)
+            res[opt] = (m.forward(seqs).cpu(), m.predict(seqs).cpu())
+    finally:
+        _lib.set_option("attn_wave", 0)
+        _lib.set_option("sas_fused", 1)
+    for opt in (1, 2):
+        assert torch.equal(res[0][0], res[opt][0]), opt
+        assert torch.equal(res[0][1], res[opt][1]), opt
+
+
 def test_score_matches_linear_and_rank_consistency(dev):
     """Fused-rank hard part 3: every logit sees the same fp32 fma chain, so the target's score
     recomputed on any tile equals its entry in the logits (strict '>' never counts the target)."""
