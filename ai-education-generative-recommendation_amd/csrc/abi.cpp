@@ -75,14 +75,16 @@ static std::atomic<int64_t> g_emb_rows{32};
 // column tile per wave over both row tiles (one weight stream, two chains); 0: one 32 x 32 tile
 // per task).  Bitwise the same; A/B timing.
 static std::atomic<int64_t> g_rt_kv2{1};
-// tail_h (1 (default): a last-position forward's final block runs the one-query tail on LN_a(X)
-// (sas_tail_h_kernel: q . K_j and p . V reassociated through W_k / W_v, no K|V projection of the
-// B n rows); 0: K|V projected for sas_tail_kernel).  Within the logits tolerance; A/B timing.
-static std::atomic<int64_t> g_tail_h{1};
-// attn_wave (0 (default): the 4-wave workgroup attention kernel; 1: at hd 64 / 128 one wave per
-// (sequence, head, query tile) walking its own key tiles, attn.hip attn_wave_kernel; 2: its
-// two-waves-per-SIMD form at hd 128).  Bitwise the same output; A/B timing.
-static std::atomic<int64_t> g_attn_wave{0};
+// tail_h (a last-position forward's final block: 2 (default): the one-query tail on LN_a(X) in one
+// pass over its rows with an online softmax per lane group and the GEMV weights loaded a phase
+// ahead (sas_tail_h2_kernel, 48 -> 39 us per C5 call); 1: the two-pass form sas_tail_h_kernel (q . K_j
+// and p . V reassociated through W_k / W_v, no K|V projection of the B n rows); 0: K|V projected for
+// sas_tail_kernel).  Within the logits tolerance; A/B timing.
+static std::atomic<int64_t> g_tail_h{2};
+// attn_wave (0: the 4-wave workgroup attention kernel; 1: at hd 64 / 128 one wave per (sequence,
+// head, query tile) walking its own key tiles, attn.hip attn_wave_kernel; 2: its two-waves-per-SIMD
+// form at hd 128; 3 (default): 1 when B * heads < 512, else 0).  Bitwise the same output.
+static std::atomic<int64_t> g_attn_wave{3};
 
 int64_t option(const char* name) {
   if (!strcmp(name, "rq_fused")) return g_rq_fused.load();
@@ -138,8 +140,8 @@ extern "C" int gr_set_option(const char* name, int64_t value) {
   if (!strcmp(name, "emb_proj") && (value == 0 || value == 1)) { gr::g_emb_proj = value; return GR_OK; }
   if (!strcmp(name, "emb_rows") && (value == 32 || value == 64)) { gr::g_emb_rows = value; return GR_OK; }
   if (!strcmp(name, "rt_kv2") && (value == 0 || value == 1)) { gr::g_rt_kv2 = value; return GR_OK; }
-  if (!strcmp(name, "tail_h") && (value == 0 || value == 1)) { gr::g_tail_h = value; return GR_OK; }
-  if (!strcmp(name, "attn_wave") && value >= 0 && value <= 2) { gr::g_attn_wave = value; return GR_OK; }
+  if (!strcmp(name, "tail_h") && value >= 0 && value <= 2) { gr::g_tail_h = value; return GR_OK; }
+  if (!strcmp(name, "attn_wave") && value >= 0 && value <= 3) { gr::g_attn_wave = value; return GR_OK; }
   return gr::fail(GR_ERR_ARG, std::string("gr_set_option: unknown option or value: ") + name);
 }
 

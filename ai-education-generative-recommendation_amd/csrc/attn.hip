@@ -654,7 +654,13 @@ int gr_attn_mfma_launch(const float* qkv, float* out, int64_t B, int n, int H, i
   if (B * H > 0x7fffffffLL) return GR_ERR_UNSUPPORTED;
   const int qt_lo = last_tile_only ? (n - 1) / 32 : 0;
   const dim3 g((unsigned)(B * H)), blk(256);
-  if ((hd == 64 || hd == 128) && option("attn_wave") != 0 && option("attn_lazy") != 0) {
+  // attn_wave 3 (auto): the per-wave kernels when the workgroup kernel would not put two
+  // (sequence, head) workgroups on every CU (B H < 512: forward(seqs[:64]) 204 -> 163 us); at C5
+  // (B H = 512) the workgroup kernel measured 107 vs 111 (attn_wave_kernel) and 138 us
+  // (attn_wave2_kernel), profiles/r04/ab_attn_wave.txt
+  const int64_t aw = option("attn_wave");
+  const bool wave = aw == 3 ? B * H < 512 : aw != 0;
+  if ((hd == 64 || hd == 128) && wave && option("attn_lazy") != 0) {
     const int64_t nbh = B * H, nt = (n + 31) / 32 - qt_lo;
     const int64_t waves = 8 * ((nbh + 7) / 8) * nt;
     if (waves <= 0x7fffffffLL) {

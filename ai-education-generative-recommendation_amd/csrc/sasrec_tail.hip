@@ -17,6 +17,11 @@
 
 #include "gr_common.h"
 
+#ifndef GR_TDIAG
+#define GR_TDIAG 0   // diagnostic builds only (scripts/build_variant.sh): 1 no H passes (scores / u),
+                     // 2 no GEMVs, 3 no W_k^T q phase -- wrong results, phase costs of sas_tail_h_kernel
+#endif
+
 namespace gr {
 
 struct SasTailArgs {
@@ -42,6 +47,7 @@ __device__ __forceinline__ float seg_sum(float v, int L) {
 // per workgroup, every phase a dependent step).
 __device__ __forceinline__ void st_gemv(const float* __restrict__ W, const float* __restrict__ bias,
                                         const float* v, int rows, int k, float* out) {
+  if (GR_TDIAG == 2) return;
   const int L = k >> 2, gpw = 64 / L;
   const int lane = threadIdx.x & 63, l = lane & (L - 1);
   const int grp = (threadIdx.x >> 6) * gpw + lane / L, ngrp = ST_NW * gpw;
@@ -242,7 +248,7 @@ __global__ __launch_bounds__(ST_NT) void sas_tail_h_kernel(const SasTailArgs a, 
       // partials summed in order
     const int hdn = H * d, hdn4 = hdn >> 2, cq = d >> 2;
     const int RG = hdn4 >= ST_NT ? 1 : ST_NT / hdn4, rl = (hd + RG - 1) / RG;
-    for (int i = tid; i < hdn4 * RG; i += ST_NT) {
+    for (int i = tid; i < (GR_TDIAG == 3 ? 0 : hdn4 * RG); i += ST_NT) {
       const int idx4 = i % hdn4, rg = i / hdn4, hh = idx4 / cq, c4 = idx4 - hh * cq;
       const int r0 = rg * rl, r1 = r0 + rl < hd ? r0 + rl : hd;
       const float* wc = wk + (int64_t)hh * hd * d + 4 * c4;
@@ -266,7 +272,7 @@ __global__ __launch_bounds__(ST_NT) void sas_tail_h_kernel(const SasTailArgs a, 
   }
   __syncthreads();
   // scores: one lane group per key, lane l holds H_j[4l .. 4l+3]; every head dots the whole row
-  for (int j0 = grp; j0 < n; j0 += ST_U * ngrp) {
+  for (int j0 = grp; j0 < (GR_TDIAG == 1 ? 0 : n); j0 += ST_U * ngrp) {
     f32x4 h4[ST_U];
 #pragma unroll
     for (int uu = 0; uu < ST_U; ++uu) {
@@ -318,7 +324,7 @@ __global__ __launch_bounds__(ST_NT) void sas_tail_h_kernel(const SasTailArgs a, 
     for (int w2 = 1; w2 < ST_NW; ++w2) tot += sb[w2];
     const float inv = 1.0f / tot;
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-    for (int j0 = grp; j0 < n; j0 += ST_U * ngrp) {
+    for (int j0 = grp; j0 < (GR_TDIAG == 1 ? 0 : n); j0 += ST_U * ngrp) {
       f32x4 h4[ST_U];
 #pragma unroll
       for (int uu = 0; uu < ST_U; ++uu) {
@@ -359,6 +365,223 @@ __global__ __launch_bounds__(ST_NT) void sas_tail_h_kernel(const SasTailArgs a, 
   for (int c = tid; c < d; c += ST_NT) x1[c] += o[c];             // residual (model.py:94)
   __syncthreads();
   st_layernorm(x1, a.ln_w, a.ln_b, d, a.eps, l1, stat);         // last_layernorm (model.py:96)
+  for (int c = tid; c < d; c += ST_NT) out[b * d + c] = l1[c];
+}
+
+// A GEMV's first row chunk (rows grp + u ngrp, u < ST_U: every row when rows <= ST_U ngrp) and its
+// biases, loaded ahead of the vector it multiplies (tail_h=2): the kernel is a chain of dependent
+// phases, and each L2 round trip of the weights now overlaps the phase before.  The biases travel
+// with the rows, so no later load waits behind a prefetch in the in-order load counter.
+struct GemvRows {
+  f32x4 a[ST_U];
+  float bias[ST_U];
+};
+
+__device__ __forceinline__ void st_gemv_issue(const float* __restrict__ W, const float* __restrict__ bias, int rows,
+                                              int k, GemvRows& g) {
+  const int L = k >> 2, gpw = 64 / L;
+  const int lane = threadIdx.x & 63, l = lane & (L - 1);
+  const int grp = (threadIdx.x >> 6) * gpw + lane / L, ngrp = ST_NW * gpw;
+#pragma unroll
+  for (int u = 0; u < ST_U; ++u) {
+    const int o = grp + u * ngrp;
+    g.a[u] = o < rows ? *reinterpret_cast<const f32x4*>(W + (int64_t)o * k + 4 * l) : f32x4{0.f, 0.f, 0.f, 0.f};
+    g.bias[u] = o < rows ? bias[o] : 0.f;
+  }
+}
+
+// st_gemv with the first chunk from st_gemv_issue (same fma order: bitwise st_gemv's result)
+__device__ __forceinline__ void st_gemv_finish(const float* __restrict__ W, const float* __restrict__ bias,
+                                               const float* v, int rows, int k, float* out, const GemvRows& g) {
+  if (GR_TDIAG == 2) return;
+  const int L = k >> 2, gpw = 64 / L;
+  const int lane = threadIdx.x & 63, l = lane & (L - 1);
+  const int grp = (threadIdx.x >> 6) * gpw + lane / L, ngrp = ST_NW * gpw;
+  const f32x4 x = *reinterpret_cast<const f32x4*>(v + 4 * l);
+#pragma unroll
+  for (int u = 0; u < ST_U; ++u) {
+    const int o = grp + u * ngrp;
+    float acc = g.a[u][0] * x[0];
+    acc = fmaf(g.a[u][1], x[1], acc);
+    acc = fmaf(g.a[u][2], x[2], acc);
+    acc = fmaf(g.a[u][3], x[3], acc);
+    acc = seg_sum(acc, L);
+    if (l == 0 && o < rows) out[o] = acc + g.bias[u];
+  }
+  for (int o0 = grp + ST_U * ngrp; o0 < rows; o0 += ST_U * ngrp) {
+    f32x4 a[ST_U];
+#pragma unroll
+    for (int u = 0; u < ST_U; ++u) {
+      const int o = o0 + u * ngrp;
+      a[u] = o < rows ? *reinterpret_cast<const f32x4*>(W + (int64_t)o * k + 4 * l) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int u = 0; u < ST_U; ++u) {
+      const int o = o0 + u * ngrp;
+      float acc = a[u][0] * x[0];
+      acc = fmaf(a[u][1], x[1], acc);
+      acc = fmaf(a[u][2], x[2], acc);
+      acc = fmaf(a[u][3], x[3], acc);
+      acc = seg_sum(acc, L);
+      if (l == 0 && o < rows) out[o] = acc + bias[o];
+    }
+  }
+}
+
+// tail_h=2 (default): sas_tail_h_kernel's block with (1) ONE pass over the H rows -- each lane
+// group keeps an online softmax (running max m, sum l, and u = sum_j e^(s_j - m) H_j) over its keys,
+// and the groups' states are merged in group order (the old form read H twice: scores, then u);
+// (2) every GEMV's weights and biases loaded one or two phases ahead (GemvRows), and the LayerNorm
+// weights staged in LDS at the start; <= 128 VGPRs, so two workgroups (sequences) share a CU.  Same math; the softmax's fp32 rounding differs from the
+// two-pass form (within the logits tolerance, tests/test_sasrec_gpu.py::test_tail_h_form_*).
+// HM = the number of heads (a power of two <= 8).
+template <int HM>
+__global__ __launch_bounds__(ST_NT, 2) void sas_tail_h2_kernel(const SasTailArgs a, const float* __restrict__ X,
+                                                          const float* __restrict__ Hs, const float* __restrict__ wk,
+                                                          const float* __restrict__ wv, const float* __restrict__ bv,
+                                                          float* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) float xl[ST_MAX_D], hl[ST_MAX_D], q[ST_MAX_D], o[ST_MAX_D],
+      x1[ST_MAX_D], l1[ST_MAX_D], fh[ST_MAX_MLP], qk[HM * ST_MAX_D], u[HM * ST_MAX_D], part[ST_NT * 4],
+      gms[ST_NT], gls[ST_NT], lnw[4 * ST_MAX_D], stat[2];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t b = blockIdx.x;
+  const int d = a.d, n = a.n, hd = d / HM;
+  const int L = d >> 2, gpw = 64 / L, l = lane & (L - 1);
+  const int grp = wave * gpw + lane / L, ngrp = ST_NW * gpw;
+  const float* xr = X + (b * n + n - 1) * d;
+  const float* hb = Hs + b * n * d;
+  GemvRows g0, g1;
+  st_gemv_issue(a.wq, a.bq, d, d, g0);
+  // W_k^T q operands: thread i takes a float4 of columns over rows [r0, r1) of one head (one i per
+  // thread: H d / 4 is a power of two <= ST_NT), the first 8 rows loaded now
+  const int hdn = HM * d, hdn4 = hdn >> 2, cq = d >> 2;
+  const int RG = hdn4 >= ST_NT ? 1 : ST_NT / hdn4, rl = (hd + RG - 1) / RG;
+  const int idx4 = tid % hdn4, rg = tid / hdn4, kh = idx4 / cq, c4 = idx4 - kh * cq;
+  const int r0 = rg * rl, r1 = r0 + rl < hd ? r0 + rl : hd;
+  const float* wc = wk + (int64_t)kh * hd * d + 4 * c4;
+  f32x4 wkp[8];
+#pragma unroll
+  for (int t = 0; t < 8; ++t)
+    wkp[t] = r0 + t < r1 ? *reinterpret_cast<const f32x4*>(wc + (int64_t)(r0 + t) * d) : f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int c = tid; c < d; c += ST_NT) {
+    xl[c] = xr[c];
+    hl[c] = hb[(int64_t)(n - 1) * d + c];
+    lnw[c] = a.ln_f_w[c];
+    lnw[d + c] = a.ln_f_b[c];
+    lnw[2 * d + c] = a.ln_w[c];
+    lnw[3 * d + c] = a.ln_b[c];
+  }
+  __syncthreads();
+  st_gemv_finish(a.wq, a.bq, hl, d, d, q, g0);
+  st_gemv_issue(wv, bv, hd, d, g0);                 // head 0's W_v rows, used after the H pass
+  __syncthreads();
+  if (GR_TDIAG != 3) {   // q'_h = W_k,h^T q_h (sas_tail_h_kernel's order)
+    const float* qh = q + kh * hd;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      if (r0 + t >= r1) break;
+      const float qr = qh[r0 + t] * a.scale;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc[e] = fmaf(wkp[t][e], qr, acc[e]);
+    }
+    for (int r = r0 + 8; r < r1; ++r) {
+      const f32x4 w4 = *reinterpret_cast<const f32x4*>(wc + (int64_t)r * d);
+      const float qr = qh[r] * a.scale;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc[e] = fmaf(w4[e], qr, acc[e]);
+    }
+    *reinterpret_cast<f32x4*>(part + rg * hdn + 4 * idx4) = acc;
+    __syncthreads();
+    for (int idx = tid; idx < hdn; idx += ST_NT) {
+      float t = part[idx];
+      for (int r2 = 1; r2 < RG; ++r2) t += part[r2 * hdn + idx];
+      qk[idx] = t;
+    }
+  }
+  __syncthreads();
+  // one pass over H: lane group grp takes keys grp, grp + ngrp, ...; per head an online softmax
+  float m[HM], ls[HM];
+  f32x4 uh[HM];
+#pragma unroll
+  for (int hh = 0; hh < HM; ++hh) {
+    m[hh] = -INFINITY;
+    ls[hh] = 0.f;
+    uh[hh] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  for (int j0 = grp; j0 < (GR_TDIAG == 1 ? 0 : n); j0 += ST_U * ngrp) {
+    f32x4 h4[ST_U];
+#pragma unroll
+    for (int uu = 0; uu < ST_U; ++uu) {
+      const int j = j0 + uu * ngrp;
+      h4[uu] = j < n ? *reinterpret_cast<const f32x4*>(hb + (int64_t)j * d + 4 * l) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int hh = 0; hh < HM; ++hh) {
+      const f32x4 q4 = *reinterpret_cast<const f32x4*>(qk + hh * d + 4 * l);
+      float sc[ST_U];
+#pragma unroll
+      for (int uu = 0; uu < ST_U; ++uu) {
+        float t = h4[uu][0] * q4[0];
+        t = fmaf(h4[uu][1], q4[1], t);
+        t = fmaf(h4[uu][2], q4[2], t);
+        t = fmaf(h4[uu][3], q4[3], t);
+        sc[uu] = seg_sum(t, L);
+      }
+#pragma unroll
+      for (int uu = 0; uu < ST_U; ++uu) {
+        if (j0 + uu * ngrp >= n) break;
+        const float mn = fmaxf(m[hh], sc[uu]);
+        const float al = __expf(m[hh] - mn), e = __expf(sc[uu] - mn);
+        ls[hh] = fmaf(ls[hh], al, e);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) uh[hh][c] = fmaf(uh[hh][c], al, e * h4[uu][c]);
+        m[hh] = mn;
+      }
+    }
+  }
+  // merge the groups' states in group order: u_h = sum_g e^(m_g - M) u_g / sum_g e^(m_g - M) l_g
+#pragma unroll
+  for (int hh = 0; hh < HM; ++hh) {
+    if (l == 0) {
+      gms[grp] = m[hh];
+      gls[grp] = ls[hh];
+    }
+    *reinterpret_cast<f32x4*>(part + grp * d + 4 * l) = uh[hh];
+    __syncthreads();
+    float M = -INFINITY;
+    for (int g2 = 0; g2 < ngrp; ++g2) M = fmaxf(M, gms[g2]);
+    float tot = 0.f;
+    for (int g2 = 0; g2 < ngrp; ++g2) tot += gls[g2] * __expf(gms[g2] - M);
+    const float inv = 1.0f / tot;
+    for (int c = tid; c < d; c += ST_NT) {
+      float t = 0.f;
+      for (int g2 = 0; g2 < ngrp; ++g2) t += part[g2 * d + c] * __expf(gms[g2] - M);
+      u[hh * d + c] = t * inv;
+    }
+    __syncthreads();
+  }
+  st_gemv_finish(wv, bv, u, hd, d, o, g0);                      // o_0 = Wv_0 u_0 + bv_0
+  for (int hh = 1; hh < HM; ++hh)
+    st_gemv(wv + (int64_t)hh * hd * d, bv + hh * hd, u + hh * d, hd, d, o + hh * hd);
+  st_gemv_issue(a.wo, a.bo, d, d, g0);
+  st_gemv_issue(a.w1, a.b1, a.mlp, d, g1);                      // FFN1 rows, used after the LayerNorm
+  __syncthreads();
+  st_gemv_finish(a.wo, a.bo, o, d, d, x1, g0);                  // out_proj
+  st_gemv_issue(a.w2, a.b2, d, a.mlp, g0);
+  __syncthreads();
+  for (int c = tid; c < d; c += ST_NT) x1[c] += xl[c];            // residual (model.py:84)
+  __syncthreads();
+  st_layernorm(x1, lnw, lnw + d, d, a.eps, l1, stat);
+  st_gemv_finish(a.w1, a.b1, l1, a.mlp, d, fh, g1);
+  __syncthreads();
+  for (int c = tid; c < a.mlp; c += ST_NT) fh[c] = fh[c] < 0.f ? 0.f : fh[c];
+  __syncthreads();
+  st_gemv_finish(a.w2, a.b2, fh, d, a.mlp, o, g0);              // W2 f + b2 (o reused)
+  __syncthreads();
+  for (int c = tid; c < d; c += ST_NT) x1[c] += o[c];             // residual (model.py:94)
+  __syncthreads();
+  st_layernorm(x1, lnw + 2 * d, lnw + 3 * d, d, a.eps, l1, stat);  // last_layernorm (model.py:96)
   for (int c = tid; c < d; c += ST_NT) out[b * d + c] = l1[c];
 }
 
@@ -422,6 +645,15 @@ int gr_sasrec_tail_h_launch(const gr_sasrec_params* p, int blk, const float* X, 
     if (!aligned16(q)) return GR_ERR_UNSUPPORTED;
   a.d = d; a.n = n; a.heads = H; a.mlp = p->mlp; a.eps = p->eps;
   a.scale = (float)std::sqrt(1.0 / (double)(d / H));
+  if (option("tail_h") == 2) {
+    switch (H) {
+      case 1: hipLaunchKernelGGL(sas_tail_h2_kernel<1>, dim3((unsigned)B), dim3(ST_NT), 0, st, a, X, Hs, wk, wv, bv, out); break;
+      case 2: hipLaunchKernelGGL(sas_tail_h2_kernel<2>, dim3((unsigned)B), dim3(ST_NT), 0, st, a, X, Hs, wk, wv, bv, out); break;
+      case 4: hipLaunchKernelGGL(sas_tail_h2_kernel<4>, dim3((unsigned)B), dim3(ST_NT), 0, st, a, X, Hs, wk, wv, bv, out); break;
+      default: hipLaunchKernelGGL(sas_tail_h2_kernel<8>, dim3((unsigned)B), dim3(ST_NT), 0, st, a, X, Hs, wk, wv, bv, out); break;
+    }
+    return check_launch("sasrec tail (H form, one pass)");
+  }
   hipLaunchKernelGGL(sas_tail_h_kernel, dim3((unsigned)B), dim3(ST_NT), 0, st, a, X, Hs, wk, wv, bv, out);
   return check_launch("sasrec tail (H form)");
 }

@@ -17,6 +17,9 @@ ap.add_argument("--what", default="c5fwd,c2")
 ap.add_argument("--calls", type=int, default=5)
 ap.add_argument("--opt", default="", help="gr_set_option settings, e.g. lin_wres=0,attn_lazy=1")
 a = ap.parse_args()
+if os.environ.get("GR_DIAG_LIB"):   # diagnostic build (build.py --abl MACRO): results may be wrong
+    from gr_amd import _lib
+    _lib.LIB_PATH = os.path.join(os.path.dirname(_lib.LIB_PATH), os.environ["GR_DIAG_LIB"])
 if a.opt:
     from gr_amd import _lib
     for kv in a.opt.split(","):

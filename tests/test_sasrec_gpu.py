@@ -267,7 +267,8 @@ def test_embed_proj_equals_two_kernels(B, blocks, dev):
                                                 (64, 2, 100, 2, 17), (32, 8, 90, 1, 6)])
 def test_tail_h_form_vs_kv_form_and_oracle(d, heads, n, blocks, B, dev):
     """Option tail_h: the final block's one-query tail on LN_a(X) with q . K and p . V reassociated
-    through W_k / W_v (no K|V projection) against the K|V form and the CPU oracle: predict logits
+    through W_k / W_v (no K|V projection; 1: two passes over H, 2: one pass with an online softmax
+    per lane group) against the K|V form and the CPU oracle: predict logits
     within the row-scaled tolerance, last hidden states within 5e-5; row-tile (d 128) and per-op
     (d 64 / 32, n > 64) paths, 1-8 heads."""
     from gr_amd import _lib, synth
@@ -276,20 +277,24 @@ def test_tail_h_form_vs_kv_form_and_oracle(d, heads, n, blocks, B, dev):
     p = synth.sasrec_params(d, n, blocks, heads, 2 * d if d < 128 else 64, dev)
     m = synth.sasrec_model(items, p, dev, seed=d + heads + n)
     seqs = synth.sequences(B, n, items, 5 + n, dev)
+    default = _lib.get_option("tail_h")
+    res = {}
     try:
-        _lib.set_option("tail_h", 0)
-        kv_h, kv_p = m.last_hidden(seqs).cpu(), m.predict(seqs).cpu()
-        _lib.set_option("tail_h", 1)
-        h_h, h_p = m.last_hidden(seqs).cpu(), m.predict(seqs).cpu()
+        for opt in (0, 1, 2):
+            _lib.set_option("tail_h", opt)
+            res[opt] = (m.last_hidden(seqs).cpu(), m.predict(seqs).cpu())
     finally:
-        _lib.set_option("tail_h", 1)
+        _lib.set_option("tail_h", default)
     sd = {k: v.detach().cpu() for k, v in m.state_dict().items()}
     ref_f = sasrec_oracle.forward(seqs.cpu(), sd, blocks, heads, 1e-8)
     ref = sasrec_oracle.predict(seqs.cpu(), sd, blocks, heads, 1e-8)
-    assert (h_h - ref_f[:, -1, :]).abs().max().item() < 5e-5
-    assert (h_h - kv_h).abs().max().item() < 5e-5
-    for got in (h_p, kv_p):
-        assert ((got - ref).abs() / ref.abs().amax(1, keepdim=True)).max().item() <= TOL
+    kv_h = res[0][0]
+    for opt in (1, 2):   # the two-pass and the one-pass (online softmax) H forms
+        h_h = res[opt][0]
+        assert (h_h - ref_f[:, -1, :]).abs().max().item() < 5e-5, opt
+        assert (h_h - kv_h).abs().max().item() < 5e-5, opt
+    for opt, (_, got) in res.items():
+        assert ((got - ref).abs() / ref.abs().amax(1, keepdim=True)).max().item() <= TOL, opt
 
 
 @pytest.mark.parametrize("d,heads,n,blocks,B", [(128, 1, 200, 2, 37), (128, 2, 130, 2, 9), (64, 1, 100, 2, 17),
@@ -310,7 +315,7 @@ def test_attn_wave_equals_workgroup_kernel(d, heads, n, blocks, B, dev):
             _lib.set_option("attn_wave", opt)
             res[opt] = (m.forward(seqs).cpu(), m.predict(seqs).cpu())
     finally:
-        _lib.set_option("attn_wave", 0)
+        _lib.set_option("attn_wave", 3)
         _lib.set_option("sas_fused", 1)
     for opt in (1, 2):
         assert torch.equal(res[0][0], res[opt][0]), opt
