@@ -81,10 +81,12 @@ static std::atomic<int64_t> g_rt_kv2{1};
 // and p . V reassociated through W_k / W_v, no K|V projection of the B n rows); 0: K|V projected for
 // sas_tail_kernel).  Within the logits tolerance; A/B timing.
 static std::atomic<int64_t> g_tail_h{2};
-// attn_wave (0: the 4-wave workgroup attention kernel; 1: at hd 64 / 128 one wave per (sequence,
-// head, query tile) walking its own key tiles, attn.hip attn_wave_kernel; 2: its two-waves-per-SIMD
-// form at hd 128; 3 (default): 1 when B * heads < 512, else 0).  Bitwise the same output.
-static std::atomic<int64_t> g_attn_wave{3};
+// attn_wave (1 (default): causal attention at hd 64 / 128 with one wave per (sequence, head, query
+// tile) walking its own key tiles, longest tiles first (attn.hip attn_wave_kernel<HD, false>); 4:
+// the same with the next tile's K Q^T chain issued before this tile's softmax;
+// 2: the two-waves-per-SIMD form at hd 128; 0: the 4-wave workgroup kernel; 3: 1 when B * heads <
+// 512, else 0).  Bitwise the same output.
+static std::atomic<int64_t> g_attn_wave{1};
 
 int64_t option(const char* name) {
   if (!strcmp(name, "rq_fused")) return g_rq_fused.load();
@@ -141,7 +143,7 @@ extern "C" int gr_set_option(const char* name, int64_t value) {
   if (!strcmp(name, "emb_rows") && (value == 32 || value == 64)) { gr::g_emb_rows = value; return GR_OK; }
   if (!strcmp(name, "rt_kv2") && (value == 0 || value == 1)) { gr::g_rt_kv2 = value; return GR_OK; }
   if (!strcmp(name, "tail_h") && value >= 0 && value <= 2) { gr::g_tail_h = value; return GR_OK; }
-  if (!strcmp(name, "attn_wave") && value >= 0 && value <= 3) { gr::g_attn_wave = value; return GR_OK; }
+  if (!strcmp(name, "attn_wave") && value >= 0 && value <= 4) { gr::g_attn_wave = value; return GR_OK; }
   return gr::fail(GR_ERR_ARG, std::string("gr_set_option: unknown option or value: ") + name);
 }
 

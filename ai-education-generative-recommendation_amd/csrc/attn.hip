@@ -23,6 +23,11 @@
 
 #include "gr_common.h"
 
+#ifndef GR_ADIAG
+#define GR_ADIAG 0   // diagnostic builds only (scripts/build_variant.sh), attn_wave_kernel: 1 no K/V
+                     // loads inside the key loop, 2 also no softmax (MFMA chains only) -- wrong results
+#endif
+
 namespace gr {
 
 constexpr int AT_KT = 32;   // keys per tile
@@ -397,11 +402,11 @@ __global__ __launch_bounds__(256, 1) void attn_pair_kernel(const float* __restri
 // vf[ft][s] = V[key 32 kt + (s&3) + 8 (s>>2) + 4 h][32 ft + r] -- with the next tile's K issued
 // right after this tile's S = K Q^T MFMAs and its V after the O += V P^T MFMAs (each hidden
 // behind the other half of the step).  One wave per SIMD (~300 VGPRs of operands and
-// accumulators); the hardware deals the waves out, longest query tiles first, and every query tile
-// of one (sequence, head) goes to the same XCD so its K / V stay in that XCD's L2.  Per row the
+// accumulators); the hardware deals the waves out longest query tiles first, and every query tile
+// of one (sequence, head) goes to the same XCD (its K / V in that XCD's L2 / the Infinity Cache).  Per row the
 // instruction sequence is attn_mfma_kernel<HD, *, true>'s (same S chain over (it, g, s4), the same
 // lazy softmax, the same O chain over (ft, s)): bitwise the same output.
-template <int HD>
+template <int HD, bool PIPE>
 __global__ __launch_bounds__(64) void attn_wave_kernel(const float* __restrict__ qkv, float* __restrict__ out,
                                                       int n, int H, float scale, int nbh, int qt_lo) {
   constexpr int FT = HD / 32;
@@ -412,7 +417,10 @@ __global__ __launch_bounds__(64) void attn_wave_kernel(const float* __restrict__
   const int x = blockIdx.x & 7, k = blockIdx.x >> 3;
   const int mx = (nbh - x + 7) / 8;   // pairs on this XCD
   if (k >= mx * nt) return;
-  const int bh = x + 8 * (k / nt), qt = T - 1 - k % nt;
+  // longest first: every pair's last query tile, then every pair's second-to-last, ...  (a greedy
+  // dispatcher then finishes in ~ the average per-SIMD work; pair-major order measured 18 tile steps
+  // per SIMD against the average 14 at C5)
+  const int bh = x + 8 * (k % mx), qt = T - 1 - k / mx;
   const int b = bh / H, hh = bh % H;
   const int d = H * HD;
   const int64_t rs = 3LL * d;
@@ -457,9 +465,7 @@ __global__ __launch_bounds__(64) void attn_wave_kernel(const float* __restrict__
       for (int ft = 0; ft < FT; ++ft) vf[ft][s] = vr[32 * ft];
     }
   };
-  load_k(0);
-  load_v(0);
-  for (int kt = 0; kt <= qt; ++kt) {
+  auto s_chain = [&]() {
     f32x16 S;
 #pragma unroll
     for (int v = 0; v < 16; ++v) S[v] = 0.f;
@@ -469,44 +475,74 @@ __global__ __launch_bounds__(64) void attn_wave_kernel(const float* __restrict__
       for (int g = 0; g < 4; ++g)
 #pragma unroll
         for (int s4 = 0; s4 < 4; ++s4) S = mfma32(kf[it][g][s4], qf[it][g][s4], S);
-    if (kt < qt) load_k(kt + 1);   // the K operands are read at issue: their registers refill now
-    // causal / padding mask on the diagonal tile and the last key tile (attn_mfma_kernel, LAZY)
-    float tmax = -INFINITY;
-    if (kt == qt || kt * 32 + 32 > n) {
+    return S;
+  };
+  // softmax of key tile kt (S -> P in place) and O += V^T P^T
+  auto softmax_pv = [&](f32x16& S, int kt) {
+    if (GR_ADIAG != 2) {
+      // causal / padding mask on the diagonal tile and the last key tile (attn_mfma_kernel, LAZY)
+      float tmax = -INFINITY;
+      if (kt == qt || kt * 32 + 32 > n) {
+#pragma unroll
+        for (int v = 0; v < 16; ++v) {
+          const int key = kt * 32 + (v & 3) + 8 * (v >> 2) + 4 * h;
+          if (key > qi || key >= n) S[v] = -INFINITY;
+          tmax = fmaxf(tmax, S[v]);
+        }
+      } else {
+#pragma unroll
+        for (int v = 0; v < 16; ++v) tmax = fmaxf(tmax, S[v]);
+      }
+      tmax = fmaxf(tmax, __shfl_xor(tmax, 32));
+      const bool up = tmax > m + AT_LAZY;   // lazy rescaling (attn_mfma_kernel)
+      if (__any(up)) {
+        const float mn = up ? tmax : m;
+        const float alpha = __expf(m - mn);
+        l *= alpha;
+        m = mn;
+#pragma unroll
+        for (int ft = 0; ft < FT; ++ft) O[ft] *= alpha;
+      }
+      float ts = 0.f;
 #pragma unroll
       for (int v = 0; v < 16; ++v) {
-        const int key = kt * 32 + (v & 3) + 8 * (v >> 2) + 4 * h;
-        if (key > qi || key >= n) S[v] = -INFINITY;
-        tmax = fmaxf(tmax, S[v]);
+        const float e = __expf(S[v] - m);
+        S[v] = e;
+        ts += e;
       }
-    } else {
-#pragma unroll
-      for (int v = 0; v < 16; ++v) tmax = fmaxf(tmax, S[v]);
+      ts += __shfl_xor(ts, 32);
+      l += ts;
     }
-    tmax = fmaxf(tmax, __shfl_xor(tmax, 32));
-    const bool up = tmax > m + AT_LAZY;   // lazy rescaling (attn_mfma_kernel)
-    if (__any(up)) {
-      const float mn = up ? tmax : m;
-      const float alpha = __expf(m - mn);
-      l *= alpha;
-      m = mn;
-#pragma unroll
-      for (int ft = 0; ft < FT; ++ft) O[ft] *= alpha;
-    }
-    float ts = 0.f;
-#pragma unroll
-    for (int v = 0; v < 16; ++v) {
-      const float e = __expf(S[v] - m);
-      S[v] = e;
-      ts += e;
-    }
-    ts += __shfl_xor(ts, 32);
-    l += ts;
 #pragma unroll
     for (int ft = 0; ft < FT; ++ft)
 #pragma unroll
       for (int s = 0; s < 16; ++s) O[ft] = mfma32(vf[ft][s], S[s], O[ft]);
-    if (kt < qt) load_v(kt + 1);
+  };
+  load_k(0);
+  load_v(0);
+  if (PIPE) {
+    // PIPE (attn_wave=4): tile kt + 1's S = K Q^T chain issued before tile kt's softmax, so the
+    // matrix pipe has work while the softmax runs (per row the same operations).  Measured 106 vs
+    // 103 us per C5 call without it (profiles/r04/ab_attn_wave.txt): not the default
+    f32x16 Sc = s_chain();
+    if (GR_ADIAG == 0 && 0 < qt) load_k(1);
+    for (int kt = 0; kt <= qt; ++kt) {
+      f32x16 Sn;
+      if (kt < qt) {
+        Sn = s_chain();
+        if (GR_ADIAG == 0 && kt + 1 < qt) load_k(kt + 2);
+      }
+      softmax_pv(Sc, kt);
+      if (GR_ADIAG == 0 && kt < qt) load_v(kt + 1);
+      Sc = Sn;
+    }
+  } else {
+    for (int kt = 0; kt <= qt; ++kt) {
+      f32x16 S = s_chain();
+      if (GR_ADIAG == 0 && kt < qt) load_k(kt + 1);   // the K operands are read at issue: their registers refill now
+      softmax_pv(S, kt);
+      if (GR_ADIAG == 0 && kt < qt) load_v(kt + 1);
+    }
   }
   if (qi < n) {
     const float inv = 1.0f / l;
@@ -534,7 +570,7 @@ __global__ __launch_bounds__(64, 2) void attn_wave2_kernel(const float* __restri
   const int x = blockIdx.x & 7, k = blockIdx.x >> 3;
   const int mx = (nbh - x + 7) / 8;
   if (k >= mx * nt) return;
-  const int bh = x + 8 * (k / nt), qt = T - 1 - k % nt;
+  const int bh = x + 8 * (k % mx), qt = T - 1 - k / mx;   // longest first (attn_wave_kernel)
   const int b = bh / H, hh = bh % H;
   const int d = H * HD;
   const int64_t rs = 3LL * d;
@@ -659,21 +695,22 @@ int gr_attn_mfma_launch(const float* qkv, float* out, int64_t B, int n, int H, i
   // (B H = 512) the workgroup kernel measured 107 vs 111 (attn_wave_kernel) and 138 us
   // (attn_wave2_kernel), profiles/r04/ab_attn_wave.txt
   const int64_t aw = option("attn_wave");
-  const bool wave = aw == 3 ? B * H < 512 : aw != 0;
+  const bool wave = aw == 3 ? B * H < 512 : aw != 0;   // 3: the pre-longest-first rule, kept for A/B
   if ((hd == 64 || hd == 128) && wave && option("attn_lazy") != 0) {
     const int64_t nbh = B * H, nt = (n + 31) / 32 - qt_lo;
     const int64_t waves = 8 * ((nbh + 7) / 8) * nt;
     if (waves <= 0x7fffffffLL) {
-      const bool two = option("attn_wave") == 2;
-      if (hd == 64)
-        hipLaunchKernelGGL(attn_wave_kernel<64>, dim3((unsigned)waves), dim3(64), 0, st, qkv, out, n, H, scale,
-                           (int)nbh, qt_lo);
-      else if (two)
-        hipLaunchKernelGGL(attn_wave2_kernel<128>, dim3((unsigned)waves), dim3(64), 0, st, qkv, out, n, H, scale,
-                           (int)nbh, qt_lo);
+      const dim3 gw((unsigned)waves), bw(64);
+      if (aw == 2 && hd == 128)
+        hipLaunchKernelGGL(attn_wave2_kernel<128>, gw, bw, 0, st, qkv, out, n, H, scale, (int)nbh, qt_lo);
+      else if (aw == 4 && hd == 128)
+        hipLaunchKernelGGL((attn_wave_kernel<128, true>), gw, bw, 0, st, qkv, out, n, H, scale, (int)nbh, qt_lo);
+      else if (aw == 4)
+        hipLaunchKernelGGL((attn_wave_kernel<64, true>), gw, bw, 0, st, qkv, out, n, H, scale, (int)nbh, qt_lo);
+      else if (hd == 128)
+        hipLaunchKernelGGL((attn_wave_kernel<128, false>), gw, bw, 0, st, qkv, out, n, H, scale, (int)nbh, qt_lo);
       else
-        hipLaunchKernelGGL(attn_wave_kernel<128>, dim3((unsigned)waves), dim3(64), 0, st, qkv, out, n, H, scale,
-                           (int)nbh, qt_lo);
+        hipLaunchKernelGGL((attn_wave_kernel<64, false>), gw, bw, 0, st, qkv, out, n, H, scale, (int)nbh, qt_lo);
       return check_launch("sasrec attention (one wave per query tile)");
     }
   }
