@@ -1,5 +1,6 @@
 """A short, fixed workload for rocprofv3 PMC passes: a few calls of the C5 forward
-(model.last_hidden, d 128, n 200, B 512) and/or the C2 encode (get_indices, 100k items).
+(model.last_hidden, d 128, n 200, B 512), one C5 catalog shard's score_topk (shard) and/or the C2
+encode (get_indices, 100k items).
 
     rocprofv3 --pmc ... -d OUT -- python3 scripts/prof_kernels.py --what c5fwd,c2 --calls 5
 """
@@ -32,6 +33,14 @@ if "c5fwd" in what:
     m, ls = synth.sasrec_rank_model(1_000_000, synth.sasrec_params(128, 200, 2, 1, 64, dev), seqs, dev, seed=5)
     for _ in range(a.calls):
         m.last_hidden(ls)
+    torch.cuda.synchronize()
+if "shard" in what:   # one C5 catalog shard (125,000 rows) against 512 users: gr_score_topk_f32
+    from gr_amd import ops
+    h = torch.randn(512, 128, device=dev)
+    shard = torch.randn(125_000, 128, device=dev)
+    ts = torch.zeros(512, device=dev)
+    for _ in range(a.calls):
+        ops.score_topk(h, shard, 10, 0, thresholds=ts, mask_col0=True)
     torch.cuda.synchronize()
 if "c2" in what:
     rq = synth.rqvae_model(3, 256, dev)
