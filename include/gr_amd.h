@@ -60,9 +60,11 @@ const char* gr_last_error(void);
  *                   store waves through LDS words; 0: one barrier per chunk.  Identical results.
  *   "score_ubmajor" 1 (default): one XCD's workgroups share a user block; 0: a catalog slice.
  *   "score_impl"    2 (default): the compute waves store their accumulators directly when every
- *                   logits row starts on a 128-byte line (row stride % 32 == 0, aligned base),
- *                   else compute / store wave specialisation with an LDS ring; 0: always the ring;
- *                   1: always direct.  Identical results.
+ *                   logits row starts on a 128-byte line (row stride % 32 == 0, aligned base);
+ *                   otherwise (d <= 64) plain direct stores when the logits fit the 160 MB
+ *                   Infinity Cache, else the lane-rotated whole-line kernel (score_rot_kernel);
+ *                   0: compute / store wave specialisation with an LDS ring; 1: always direct;
+ *                   3: direct, plain stores; 4: the rotated kernel.  Identical results.
  *   "topk_sample"   1 (default): gr_score_topk_f32 prunes with a threshold from a strided sample
  *                   pass when the catalog is long enough; 0: one pass.  Identical results.
  *   "lin_wres"      1 (default): gr_linear_f32 with k = 128, n % 128 == 0, no residual and
@@ -78,13 +80,25 @@ const char* gr_last_error(void);
  *   "rq_pieces"     1 (default): the fused encoder's item tiles past q x grid (q whole tiles per
  *                   workgroup) run as feature-half pieces on twice as many workgroups plus a layers
  *                   2-3 kernel; 0: a one-tile pass on the first workgroups.  Identical results.
- *   "tail_h"        1 (default): a last-position SASRec forward (predict) runs its final block as
+ *   "tail_h"        2 (default): a last-position SASRec forward (predict) runs its final block as
  *                   the one-query tail on LN_a(X): q . K_j = (W_k^T q) . H_j (+ a term constant
  *                   over j that cancels in the softmax) and p . V = W_v (p . H) + b_v, so K|V of
- *                   the B n rows are never projected.  NOT bitwise: the reassociated sums round
- *                   differently (logits within the 1e-5 row-scaled tolerance, tests/
- *                   test_sasrec_gpu.py::test_tail_h_form_vs_kv_form_and_oracle); 0: K|V projected
- *                   and the reference's association order.
+ *                   the B n rows are never projected, in ONE pass over H with an online softmax
+ *                   per lane group (sas_tail_h2_kernel); 1: the same tail in two passes over H;
+ *                   0: K|V projected and the reference's association order.  1 and 2 are NOT
+ *                   bitwise to 0 or to each other: the reassociated sums round differently (logits
+ *                   within the 1e-5 row-scaled tolerance, tests/test_sasrec_gpu.py::
+ *                   test_tail_h_form_vs_kv_form_and_oracle).
+ *   "attn_wave"     1 (default): layer-wise causal attention at head width 64 / 128 runs one wave
+ *                   per (sequence, head, 32-query tile), longest tiles first, K / V straight from
+ *                   L2 into registers; 0: one 4-wave workgroup per (sequence, head) over shared LDS
+ *                   tiles; 2: the per-wave form at two waves per SIMD (hd 128); 3: 1 when
+ *                   B x heads < 512, else 0; 4: 1 with the next tile's K Q^T chain issued before
+ *                   the softmax.  Identical results.
+ *   "attn_lazy"     1 (default): lazy softmax rescaling (the running max moves only when a tile's
+ *                   max exceeds it by > 8) and masks on the diagonal / last key tile only; 0: the
+ *                   rescale on every tile (another fp32 rounding, within tolerance).
+ *   "attn_pair", "attn_occ1", "attn_alt": workgroup-kernel variants kept for A/B.
  * gr_set_option returns GR_ERR_ARG for an unknown name/value; gr_get_option returns -1 for an
  * unknown name. */
 int gr_set_option(const char* name, int64_t value);

@@ -131,7 +131,7 @@ def test_collision_groups_use_each_groups_call_order(dev, parity_log):
     assert np.array_equal(out, loop)
 
 
-@pytest.mark.parametrize("in_dim,e_dim", [(1000, 32), (1024, 32), (768, 96), (768, 128), (770, 32)])
+@pytest.mark.parametrize("in_dim,e_dim", [(1000, 32), (1024, 32), (768, 96), (768, 128), (770, 32), (392, 32)])
 def test_wider_envelope_vs_oracle(dev, in_dim, e_dim, parity_log):
     """Widths the MFMA kernels do not take or MKL's order is not pinned for (in_dim > 768,
     in_dim % 4 != 0, e_dim > 64) still encode, in rq_exact's restated order bit for bit
