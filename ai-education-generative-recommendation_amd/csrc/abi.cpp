@@ -143,7 +143,7 @@ extern "C" int gr_set_option(const char* name, int64_t value) {
   if (!strcmp(name, "emb_rows") && (value == 32 || value == 64)) { gr::g_emb_rows = value; return GR_OK; }
   if (!strcmp(name, "rt_kv2") && (value == 0 || value == 1)) { gr::g_rt_kv2 = value; return GR_OK; }
   if (!strcmp(name, "tail_h") && value >= 0 && value <= 2) { gr::g_tail_h = value; return GR_OK; }
-  if (!strcmp(name, "attn_wave") && value >= 0 && value <= 4) { gr::g_attn_wave = value; return GR_OK; }
+  if (!strcmp(name, "attn_wave") && value >= 0 && value <= 5) { gr::g_attn_wave = value; return GR_OK; }
   return gr::fail(GR_ERR_ARG, std::string("gr_set_option: unknown option or value: ") + name);
 }
 

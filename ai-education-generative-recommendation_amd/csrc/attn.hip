@@ -406,10 +406,16 @@ __global__ __launch_bounds__(256, 1) void attn_pair_kernel(const float* __restri
 // of one (sequence, head) goes to the same XCD (its K / V in that XCD's L2 / the Infinity Cache).  Per row the
 // instruction sequence is attn_mfma_kernel<HD, *, true>'s (same S chain over (it, g, s4), the same
 // lazy softmax, the same O chain over (ft, s)): bitwise the same output.
-template <int HD, bool PIPE>
-__global__ __launch_bounds__(64) void attn_wave_kernel(const float* __restrict__ qkv, float* __restrict__ out,
-                                                      int n, int H, float scale, int nbh, int qt_lo) {
+// QL (attn_wave=5): the scaled query tile parked in LDS (each lane re-reads exactly the float4s it
+// wrote: no barrier) instead of 64 registers, so two waves fit a SIMD and cover each other's loads
+// and softmax.
+template <int HD, bool PIPE, bool QL = false>
+__global__ __launch_bounds__(64, QL ? 2 : 1) void attn_wave_kernel(const float* __restrict__ qkv,
+                                                                  float* __restrict__ out, int n, int H,
+                                                                  float scale, int nbh, int qt_lo) {
   constexpr int FT = HD / 32;
+  constexpr int QP = HD + 4;   // LDS row pitch of the parked query tile
+  __shared__ __attribute__((aligned(16))) float qs[QL ? 32 * QP : 4];
   const int lane = threadIdx.x, r = lane & 31, h = lane >> 5;
   const int T = (n + 31) / 32, nt = T - qt_lo;
   // work item of this wave: XCD x = blockIdx % 8 owns the (sequence, head) pairs bh = x (mod 8);
@@ -430,13 +436,16 @@ __global__ __launch_bounds__(64) void attn_wave_kernel(const float* __restrict__
   const float* Vb = base + 2 * d;
   const int qi = qt * 32 + r;
   const int qc = qi < n ? qi : n - 1;
-  f32x4 qf[FT][4];
+  f32x4 qf[QL ? 1 : FT][4];
 #pragma unroll
   for (int it = 0; it < FT; ++it)
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
       const f32x4 v = *reinterpret_cast<const f32x4*>(Qb + (int64_t)qc * rs + 32 * it + 8 * g + 4 * h);
-      qf[it][g] = v * scale;   // q * sqrt(1/hd) (functional.py:6578)
+      if (QL)
+        *reinterpret_cast<f32x4*>(&qs[r * QP + 32 * it + 8 * g + 4 * h]) = v * scale;
+      else
+        qf[QL ? 0 : it][g] = v * scale;   // q * sqrt(1/hd) (functional.py:6578)
     }
   f32x16 O[FT];
 #pragma unroll
@@ -469,12 +478,16 @@ __global__ __launch_bounds__(64) void attn_wave_kernel(const float* __restrict__
     f32x16 S;
 #pragma unroll
     for (int v = 0; v < 16; ++v) S[v] = 0.f;
+    if (QL) asm volatile("" ::: "memory");   // re-read the parked tile (hoisted it is 64 registers)
 #pragma unroll
     for (int it = 0; it < FT; ++it)
 #pragma unroll
-      for (int g = 0; g < 4; ++g)
+      for (int g = 0; g < 4; ++g) {
+        const f32x4 q4 = QL ? *reinterpret_cast<const f32x4*>(&qs[r * QP + 32 * it + 8 * g + 4 * h])
+                            : qf[QL ? 0 : it][g];
 #pragma unroll
-        for (int s4 = 0; s4 < 4; ++s4) S = mfma32(kf[it][g][s4], qf[it][g][s4], S);
+        for (int s4 = 0; s4 < 4; ++s4) S = mfma32(kf[it][g][s4], q4[s4], S);
+      }
     return S;
   };
   // softmax of key tile kt (S -> P in place) and O += V^T P^T
@@ -703,6 +716,10 @@ int gr_attn_mfma_launch(const float* qkv, float* out, int64_t B, int n, int H, i
       const dim3 gw((unsigned)waves), bw(64);
       if (aw == 2 && hd == 128)
         hipLaunchKernelGGL(attn_wave2_kernel<128>, gw, bw, 0, st, qkv, out, n, H, scale, (int)nbh, qt_lo);
+      else if (aw == 5 && hd == 128)
+        hipLaunchKernelGGL((attn_wave_kernel<128, false, true>), gw, bw, 0, st, qkv, out, n, H, scale, (int)nbh, qt_lo);
+      else if (aw == 5)
+        hipLaunchKernelGGL((attn_wave_kernel<64, false, true>), gw, bw, 0, st, qkv, out, n, H, scale, (int)nbh, qt_lo);
       else if (aw == 4 && hd == 128)
         hipLaunchKernelGGL((attn_wave_kernel<128, true>), gw, bw, 0, st, qkv, out, n, H, scale, (int)nbh, qt_lo);
       else if (aw == 4)
