@@ -569,6 +569,157 @@ __global__ __launch_bounds__(64, QL ? 2 : 1) void attn_wave_kernel(const float* 
   }
 }
 
+// attn_wave=6: attn_wave_kernel as a PERSISTENT grid -- one wave per SIMD, each walking a static
+// list of (sequence, head, query tile) items: the items of an XCD in the longest-first order, dealt
+// to its waves in alternating (snake) rounds, so every wave gets ~ the average work (C5: 7+4+3 or
+// 6+5+2+1 = 14 tile steps each).  The next item's Q and first K / V tiles are loaded during the
+// current item's last tile step, so a wave never starts cold.  Per row the instruction sequence
+// of attn_wave_kernel: bitwise the same output.
+template <int HD>
+__global__ __launch_bounds__(64) void attn_persist_kernel(const float* __restrict__ qkv, float* __restrict__ out,
+                                                         int n, int H, float scale, int nbh, int qt_lo, int wx) {
+  constexpr int FT = HD / 32;
+  const int lane = threadIdx.x, r = lane & 31, h = lane >> 5;
+  const int T = (n + 31) / 32, nt = T - qt_lo;
+  const int x = blockIdx.x & 7, k = blockIdx.x >> 3;
+  const int mx = (nbh - x + 7) / 8, items = mx * nt;
+  const int d = H * HD;
+  const int64_t rs = 3LL * d;
+  auto item_of = [&](int rnd) {
+    const int j = rnd * wx + ((rnd & 1) ? wx - 1 - k : k);
+    return j < items ? j : -1;
+  };
+  int rnd = 0;
+  int j = item_of(0);
+  if (j < 0) return;
+  auto base_of = [&](int jj, int& qt_, int& qi_) {
+    qt_ = T - 1 - jj / mx;
+    const int bh = x + 8 * (jj % mx);
+    qi_ = qt_ * 32 + r;
+    return qkv + (int64_t)(bh / H) * n * rs + (bh % H) * HD;
+  };
+  f32x4 qf[FT][4], kf[FT][4];
+  float vf[FT][16];
+  auto load_q = [&](const float* bs, int qi_) {
+    const int qc = qi_ < n ? qi_ : n - 1;
+#pragma unroll
+    for (int it = 0; it < FT; ++it)
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        qf[it][g] = *reinterpret_cast<const f32x4*>(bs + (int64_t)qc * rs + 32 * it + 8 * g + 4 * h);
+  };
+  auto load_k = [&](const float* bs, int kt) {
+    int key = kt * 32 + r;
+    key = key < n ? key : n - 1;
+    const float* kr = bs + d + (int64_t)key * rs + 4 * h;
+#pragma unroll
+    for (int it = 0; it < FT; ++it)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) kf[it][g] = *reinterpret_cast<const f32x4*>(kr + 32 * it + 8 * g);
+  };
+  auto load_v = [&](const float* bs, int kt) {
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      int key = kt * 32 + (s & 3) + 8 * (s >> 2) + 4 * h;
+      key = key < n ? key : n - 1;
+      const float* vr = bs + 2 * d + (int64_t)key * rs + r;
+#pragma unroll
+      for (int ft = 0; ft < FT; ++ft) vf[ft][s] = vr[32 * ft];
+    }
+  };
+  int qt, qi;
+  const float* bs = base_of(j, qt, qi);
+  load_q(bs, qi);
+  load_k(bs, 0);
+  load_v(bs, 0);
+  while (true) {
+#pragma unroll
+    for (int it = 0; it < FT; ++it)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) qf[it][g] = qf[it][g] * scale;   // q * sqrt(1/hd) (functional.py:6578)
+    f32x16 O[FT];
+#pragma unroll
+    for (int ft = 0; ft < FT; ++ft)
+#pragma unroll
+      for (int v = 0; v < 16; ++v) O[ft][v] = 0.f;
+    float m = -INFINITY, l = 0.f;
+    const int nj = item_of(rnd + 1);
+    int nqt = 0, nqi = 0;
+    const float* nbs = nj >= 0 ? base_of(nj, nqt, nqi) : bs;
+    for (int kt = 0; kt <= qt; ++kt) {
+      f32x16 S;
+#pragma unroll
+      for (int v = 0; v < 16; ++v) S[v] = 0.f;
+#pragma unroll
+      for (int it = 0; it < FT; ++it)
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+#pragma unroll
+          for (int s4 = 0; s4 < 4; ++s4) S = mfma32(kf[it][g][s4], qf[it][g][s4], S);
+      if (kt < qt) {
+        load_k(bs, kt + 1);
+      } else if (nj >= 0) {   // the next item's Q and first K tile, under this step's softmax + PV
+        load_q(nbs, nqi);
+        load_k(nbs, 0);
+      }
+      float tmax = -INFINITY;
+      if (kt == qt || kt * 32 + 32 > n) {
+#pragma unroll
+        for (int v = 0; v < 16; ++v) {
+          const int key = kt * 32 + (v & 3) + 8 * (v >> 2) + 4 * h;
+          if (key > qi || key >= n) S[v] = -INFINITY;
+          tmax = fmaxf(tmax, S[v]);
+        }
+      } else {
+#pragma unroll
+        for (int v = 0; v < 16; ++v) tmax = fmaxf(tmax, S[v]);
+      }
+      tmax = fmaxf(tmax, __shfl_xor(tmax, 32));
+      const bool up = tmax > m + AT_LAZY;
+      if (__any(up)) {
+        const float mn = up ? tmax : m;
+        const float alpha = __expf(m - mn);
+        l *= alpha;
+        m = mn;
+#pragma unroll
+        for (int ft = 0; ft < FT; ++ft) O[ft] *= alpha;
+      }
+      float ts = 0.f;
+#pragma unroll
+      for (int v = 0; v < 16; ++v) {
+        const float e = __expf(S[v] - m);
+        S[v] = e;
+        ts += e;
+      }
+      ts += __shfl_xor(ts, 32);
+      l += ts;
+#pragma unroll
+      for (int ft = 0; ft < FT; ++ft)
+#pragma unroll
+        for (int s = 0; s < 16; ++s) O[ft] = mfma32(vf[ft][s], S[s], O[ft]);
+      if (kt < qt) load_v(bs, kt + 1);
+      else if (nj >= 0) load_v(nbs, 0);
+    }
+    if (qi < n) {
+      const float inv = 1.0f / l;
+      const int64_t boff = bs - qkv;   // = b n rs + hh HD
+      const int64_t bb = boff / ((int64_t)n * rs), hho = boff - bb * (int64_t)n * rs;
+      float* orow = out + (bb * n + qi) * d + hho;
+#pragma unroll
+      for (int ft = 0; ft < FT; ++ft)
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+          *reinterpret_cast<f32x4*>(orow + 32 * ft + 8 * g + 4 * h) =
+              f32x4{O[ft][4 * g], O[ft][4 * g + 1], O[ft][4 * g + 2], O[ft][4 * g + 3]} * inv;
+    }
+    if (nj < 0) break;
+    ++rnd;
+    bs = nbs;
+    qt = nqt;
+    qi = nqi;
+  }
+}
+
 // attn_wave=2: the same walk at TWO waves per SIMD (<= 256 registers): K is streamed in 32-feature
 // quarters and V in 32-feature slices, each one step ahead in a two-slot ring (K quarter it + 1,
 // or the next key tile's first quarter, is issued before quarter it's 16 MFMAs; likewise V), so
@@ -714,6 +865,21 @@ int gr_attn_mfma_launch(const float* qkv, float* out, int64_t B, int n, int H, i
     const int64_t waves = 8 * ((nbh + 7) / 8) * nt;
     if (waves <= 0x7fffffffLL) {
       const dim3 gw((unsigned)waves), bw(64);
+      if (aw == 6) {
+        static int simds = 0;
+        if (!simds) {
+          int dev = 0, cus = 0;
+          (void)hipGetDevice(&dev);
+          (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+          simds = 4 * (cus > 0 ? cus : 256);
+        }
+        const int wx = (simds + 7) / 8;
+        if (hd == 128)
+          hipLaunchKernelGGL(attn_persist_kernel<128>, dim3(8 * wx), bw, 0, st, qkv, out, n, H, scale, (int)nbh, qt_lo, wx);
+        else
+          hipLaunchKernelGGL(attn_persist_kernel<64>, dim3(8 * wx), bw, 0, st, qkv, out, n, H, scale, (int)nbh, qt_lo, wx);
+        return check_launch("sasrec attention (persistent waves)");
+      }
       if (aw == 2 && hd == 128)
         hipLaunchKernelGGL(attn_wave2_kernel<128>, gw, bw, 0, st, qkv, out, n, H, scale, (int)nbh, qt_lo);
       else if (aw == 5 && hd == 128)

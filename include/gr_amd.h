@@ -89,12 +89,14 @@ const char* gr_last_error(void);
  *                   bitwise to 0 or to each other: the reassociated sums round differently (logits
  *                   within the 1e-5 row-scaled tolerance, tests/test_sasrec_gpu.py::
  *                   test_tail_h_form_vs_kv_form_and_oracle).
- *   "attn_wave"     1 (default): layer-wise causal attention at head width 64 / 128 runs one wave
- *                   per (sequence, head, 32-query tile), longest tiles first, K / V straight from
- *                   L2 into registers; 0: one 4-wave workgroup per (sequence, head) over shared LDS
- *                   tiles; 2: the per-wave form at two waves per SIMD (hd 128); 3: 1 when
- *                   B x heads < 512, else 0; 4: 1 with the next tile's K Q^T chain issued before
- *                   the softmax.  Identical results.
+ *   "attn_wave"     6 (default): layer-wise causal attention at head width 64 / 128 on a
+ *                   persistent grid, one wave per SIMD walking a static longest-first list of
+ *                   (sequence, head, 32-query tile) items, K / V straight from L2 into registers,
+ *                   the next item's operands loaded under the current item's last step; 1: one
+ *                   wave per item (longest first); 0: one 4-wave workgroup per (sequence, head) over
+ *                   shared LDS tiles; 2: the per-wave form at two waves per SIMD (hd 128); 3: 1
+ *                   when B x heads < 512, else 0; 4: 1 with the next tile's K Q^T chain issued
+ *                   before the softmax; 5: 1 with Q parked in LDS.  Identical results.
  *   "attn_lazy"     1 (default): lazy softmax rescaling (the running max moves only when a tile's
  *                   max exceeds it by > 8) and masks on the diagonal / last key tile only; 0: the
  *                   rescale on every tile (another fp32 rounding, within tolerance).

@@ -311,13 +311,13 @@ def test_attn_wave_equals_workgroup_kernel(d, heads, n, blocks, B, dev):
     res = {}
     try:
         _lib.set_option("sas_fused", 0)
-        for opt in (0, 1, 2, 4, 5):
+        for opt in (0, 1, 2, 4, 5, 6):
             _lib.set_option("attn_wave", opt)
             res[opt] = (m.forward(seqs).cpu(), m.predict(seqs).cpu())
     finally:
-        _lib.set_option("attn_wave", 1)
+        _lib.set_option("attn_wave", 6)
         _lib.set_option("sas_fused", 1)
-    for opt in (1, 2, 4, 5):
+    for opt in (1, 2, 4, 5, 6):
         assert torch.equal(res[0][0], res[opt][0]), opt
         assert torch.equal(res[0][1], res[opt][1]), opt
 
