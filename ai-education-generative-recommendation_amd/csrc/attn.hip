@@ -24,8 +24,9 @@
 #include "gr_common.h"
 
 #ifndef GR_ADIAG
-#define GR_ADIAG 0   // diagnostic builds only (scripts/build_variant.sh), attn_wave_kernel: 1 no K/V
-                     // loads inside the key loop, 2 also no softmax (MFMA chains only) -- wrong results
+#define GR_ADIAG 0   // diagnostic builds only (scripts/build_variant.sh), attn_wave_kernel and
+                     // attn_persist_kernel: 1 no K/V loads inside an item's key loop, 2 also no
+                     // softmax (MFMA chains only) -- wrong results
 #endif
 
 namespace gr {
@@ -657,11 +658,12 @@ __global__ __launch_bounds__(64) void attn_persist_kernel(const float* __restric
 #pragma unroll
           for (int s4 = 0; s4 < 4; ++s4) S = mfma32(kf[it][g][s4], qf[it][g][s4], S);
       if (kt < qt) {
-        load_k(bs, kt + 1);
+        if (GR_ADIAG == 0) load_k(bs, kt + 1);
       } else if (nj >= 0) {   // the next item's Q and first K tile, under this step's softmax + PV
         load_q(nbs, nqi);
         load_k(nbs, 0);
       }
+      if (GR_ADIAG != 2) {
       float tmax = -INFINITY;
       if (kt == qt || kt * 32 + 32 > n) {
 #pragma unroll
@@ -693,12 +695,16 @@ __global__ __launch_bounds__(64) void attn_persist_kernel(const float* __restric
       }
       ts += __shfl_xor(ts, 32);
       l += ts;
+      }
 #pragma unroll
       for (int ft = 0; ft < FT; ++ft)
 #pragma unroll
         for (int s = 0; s < 16; ++s) O[ft] = mfma32(vf[ft][s], S[s], O[ft]);
-      if (kt < qt) load_v(bs, kt + 1);
-      else if (nj >= 0) load_v(nbs, 0);
+      if (kt < qt) {
+        if (GR_ADIAG == 0) load_v(bs, kt + 1);
+      } else if (nj >= 0) {
+        load_v(nbs, 0);
+      }
     }
     if (qi < n) {
       const float inv = 1.0f / l;
