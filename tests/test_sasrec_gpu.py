@@ -297,26 +297,33 @@ def test_tail_h_form_vs_kv_form_and_oracle(d, heads, n, blocks, B, dev):
         assert ((got - ref).abs() / ref.abs().amax(1, keepdim=True)).max().item() <= TOL, opt
 
 
-@pytest.mark.parametrize("d,heads,n,blocks,B", [(128, 1, 200, 2, 37), (128, 2, 130, 2, 9), (64, 1, 100, 2, 17),
-                                                (64, 2, 77, 1, 5), (128, 1, 33, 1, 3)])
-def test_attn_wave_equals_workgroup_kernel(d, heads, n, blocks, B, dev):
-    """Option attn_wave: the one-wave-per-query-tile attention (attn.hip attn_wave_kernel; 2: the
-    two-waves-per-SIMD form attn_wave2_kernel) against the 4-wave workgroup kernel -- the same
-    per-row instruction sequence, so hidden states and logits are bitwise equal (hd 128 / 64)."""
+@pytest.mark.parametrize("d,heads,n,blocks,B,tail_h", [(128, 1, 200, 2, 37, 2), (128, 2, 130, 2, 9, 2),
+                                                       (64, 1, 100, 2, 17, 2), (64, 2, 77, 1, 5, 2),
+                                                       (128, 1, 33, 1, 3, 2), (128, 1, 200, 2, 1500, 2),
+                                                       (128, 1, 200, 2, 300, 0), (128, 2, 97, 3, 40, 0)])
+def test_attn_wave_equals_workgroup_kernel(d, heads, n, blocks, B, tail_h, dev):
+    """Option attn_wave: the per-wave attention forms (attn.hip: 6 the persistent grid with static
+    longest-first item lists, 1 one wave per item, 2 two waves per SIMD, 4 pipelined S chain, 5 Q
+    in LDS) against the 4-wave workgroup kernel -- the same per-row instruction sequence, so hidden
+    states and logits are bitwise equal (hd 128 / 64; B 1500: ~14 items per persistent wave;
+    tail_h 0: the final block's attention as last-query-tile-only launches)."""
     from gr_amd import _lib, synth
     items = 500
     p = synth.sasrec_params(d, n, blocks, heads, 64, dev)
     m = synth.sasrec_model(items, p, dev, seed=d + n)
     seqs = synth.sequences(B, n, items, 3 + n, dev)
     res = {}
+    th = _lib.get_option("tail_h")
     try:
         _lib.set_option("sas_fused", 0)
+        _lib.set_option("tail_h", tail_h)
         for opt in (0, 1, 2, 4, 5, 6):
             _lib.set_option("attn_wave", opt)
             res[opt] = (m.forward(seqs).cpu(), m.predict(seqs).cpu())
     finally:
         _lib.set_option("attn_wave", 6)
         _lib.set_option("sas_fused", 1)
+        _lib.set_option("tail_h", th)
     for opt in (1, 2, 4, 5, 6):
         assert torch.equal(res[0][0], res[opt][0]), opt
         assert torch.equal(res[0][1], res[opt][1]), opt
