@@ -256,12 +256,17 @@ class RqBinding:
     frozen = True
 
     def packed_ptr(self):
-        """Device pointer of the up-to-date packed encoder image; None: pack per call (the default,
-        or not the fused encoder shape)."""
+        """Device pointer of the up-to-date packed encoder image; None: pack per call
+        (``frozen = False``, or not the fused encoder shape)."""
         if self.packed is None or not self.frozen:
             return None
         key = tuple(w._version for w in self.ws) + (_WEIGHT_EPOCH[0],)
         if key != self._pack_key:
+            if self._pack_key is not None:
+                # a re-pack writes a fresh image on this stream: an encode still queued on another
+                # stream keeps reading the previous one, which stays allocated until the next re-pack
+                self._prev_packed = self.packed
+                self.packed = torch.empty_like(self._prev_packed)
             with torch.cuda.device(self.device):
                 L.check(L.lib().gr_rq_encoder_pack_f32(len(self.ws), self.dims_c, self.w_arr, L.ptr(self.packed),
                                                        L.stream_of(self.device)), "gr_rq_encoder_pack_f32")
