@@ -81,6 +81,10 @@ static std::atomic<int64_t> g_rt_kv2{1};
 // and p . V reassociated through W_k / W_v, no K|V projection of the B n rows); 0: K|V projected for
 // sas_tail_kernel).  Within the logits tolerance; A/B timing.
 static std::atomic<int64_t> g_tail_h{2};
+// fused_tail_h (1 (default): the fused d <= 64 forward's final block of a last-position forward
+// in the same H form, no K / V projection of the n tokens; 0: K and V projected).  Within the
+// logits tolerance, not bitwise to 0.
+static std::atomic<int64_t> g_fused_tail_h{1};
 // attn_wave (6 (default): causal attention at hd 64 / 128 on a persistent grid of one wave per SIMD,
 // each walking a static longest-first list of (sequence, head, query tile) items with the next
 // item's Q / K / V loaded under the current item's last step (attn.hip attn_persist_kernel); 1:
@@ -114,6 +118,7 @@ int64_t option(const char* name) {
   if (!strcmp(name, "emb_rows")) return g_emb_rows.load();
   if (!strcmp(name, "rt_kv2")) return g_rt_kv2.load();
   if (!strcmp(name, "tail_h")) return g_tail_h.load();
+  if (!strcmp(name, "fused_tail_h")) return g_fused_tail_h.load();
   if (!strcmp(name, "attn_wave")) return g_attn_wave.load();
   return -1;
 }
@@ -145,6 +150,7 @@ extern "C" int gr_set_option(const char* name, int64_t value) {
   if (!strcmp(name, "emb_rows") && (value == 32 || value == 64)) { gr::g_emb_rows = value; return GR_OK; }
   if (!strcmp(name, "rt_kv2") && (value == 0 || value == 1)) { gr::g_rt_kv2 = value; return GR_OK; }
   if (!strcmp(name, "tail_h") && value >= 0 && value <= 2) { gr::g_tail_h = value; return GR_OK; }
+  if (!strcmp(name, "fused_tail_h") && (value == 0 || value == 1)) { gr::g_fused_tail_h = value; return GR_OK; }
   if (!strcmp(name, "attn_wave") && value >= 0 && value <= 6) { gr::g_attn_wave = value; return GR_OK; }
   return gr::fail(GR_ERR_ARG, std::string("gr_set_option: unknown option or value: ") + name);
 }

@@ -199,6 +199,7 @@ struct SasFusedArgs {
   int64_t item_rows;
   int nb, d, heads, mlp, n;
   float eps, scale;
+  int tail_h;   // last-position forward: the final block in the H form (option tail_h != 0)
 };
 
 // out: last_only ? [B, d] (LN_last of position n-1) : [B, n, d].
@@ -275,6 +276,106 @@ __global__ __launch_bounds__(256) void sasrec_fused_kernel(const SasFusedArgs a,
               sc[64 + f] = X[ft][tt][v];
             }
         }
+      }
+      if (tail && a.tail_h) {
+        // ---- final block in the H form (option tail_h; sasrec_tail.hip's reassociation): with one
+        // query, q . K_j = (W_k^T q) . H_j + (a term constant over j: cancels in the softmax) and
+        // sum_j p_j V_j = W_v (sum_j p_j H_j) + b_v, so K and V of the n tokens are never projected
+        // (2 x 32 DT^2 TT MFMAs per sequence).  H = LN_a(X) is parked token-major in the X area (X
+        // itself is not needed again: x[n-1] is in sc).  fp32 rounding of the reassociated sums,
+        // within the logits tolerance (not bitwise to tail_h = 0).
+        // odd row pitch (conflict-free token-major writes) when the n rows still fit the X area
+        const int PH = n * (32 * DT + 1) <= 32 * DT * 32 * TT ? 32 * DT + 1 : 32 * DT;
+        float* hs = xs;
+#pragma unroll
+        for (int ft = 0; ft < DT; ++ft)
+#pragma unroll
+          for (int tt = 0; tt < TT; ++tt)
+            if (32 * tt + r < n) {
+#pragma unroll
+              for (int v = 0; v < 16; ++v)
+                hs[(32 * tt + r) * PH + 32 * ft + (v & 3) + 8 * (v >> 2) + 4 * h] = Hn[ft][tt][v];
+            }
+        float* hl = sc;            // LN_a(x)[n-1]          [64]
+        float* xl = sc + 64;       // x[n-1]                [64]
+        float* qs = sc + 128;      // q (scaled)            [64]
+        float* os = sc + 192;      // attention output      [64]
+        float* us = sc + 256;      // u_h = sum_j p_j H_j   [64] (then LN_f(x))
+        float* qk = sc + 320;      // W_k,h^T q_h           [64] (then the FFN hidden)
+        float* ps = sc + 448;      // softmax row           [64]
+        const int f = lane;
+        const bool fon = f < d;
+        wave_lds_sync();
+        if (fon) qs[f] = gemv_row(P.w_in, P.b_in, f, d, hl) * a.scale;   // functional.py:6578
+        wave_lds_sync();
+        const float* wk = P.w_in + (int64_t)d * d;
+        const float* wv = P.w_in + 2 * (int64_t)d * d;
+#pragma unroll 1
+        for (int hh = 0; hh < (SINGLE ? 1 : a.heads); ++hh) {
+          const int f_lo = SINGLE ? 0 : hh * hd, f_hi = SINGLE ? d : f_lo + hd;
+          if (fon) {   // q'_h[c] = sum_{r in head h} W_k[r][c] q[r]
+            float acc = 0.f;
+#pragma unroll 8
+            for (int rr = f_lo; rr < f_hi; ++rr) acc = fmaf(wk[(int64_t)rr * d + f], qs[rr], acc);
+            qk[f] = acc;
+          }
+          wave_lds_sync();
+          float sv[TT];
+#pragma unroll
+          for (int tt = 0; tt < TT; ++tt) {
+            float acc = 0.f;
+#pragma unroll
+            for (int ft = 0; ft < DT; ++ft)
+#pragma unroll
+              for (int q = 0; q < 4; ++q) {
+                const f32x4 qq = *reinterpret_cast<const f32x4*>(qk + 32 * ft + 8 * q + 4 * h);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) acc = fmaf(Hn[ft][tt][4 * q + i], qq[i], acc);
+              }
+            acc += swap_halves(acc);
+            sv[tt] = (32 * tt + r < n) ? acc : -INFINITY;
+          }
+          float m = sv[0];
+#pragma unroll
+          for (int tt = 1; tt < TT; ++tt) m = fmaxf(m, sv[tt]);
+          m = half_max(m);
+          float sum = 0.f;
+#pragma unroll
+          for (int tt = 0; tt < TT; ++tt) {
+            sv[tt] = __expf(sv[tt] - m);
+            sum += sv[tt];
+          }
+          const float inv = 1.0f / half_sum(sum);
+          if (h == 0) {
+#pragma unroll
+            for (int tt = 0; tt < TT; ++tt) ps[32 * tt + r] = sv[tt] * inv;
+          }
+          wave_lds_sync();
+          if (fon) {   // u_h[c] = sum_j p_j H_j[c]
+            float acc = 0.f;
+#pragma unroll 8
+            for (int j = 0; j < n; ++j) acc = fmaf(ps[j], hs[j * PH + f], acc);
+            us[f] = acc;
+          }
+          wave_lds_sync();
+          if (f >= f_lo && f < f_hi) os[f] = gemv_row(wv, P.b_in + 2 * d, f, d, us);   // o_h = W_v,h u_h + b_v,h
+          wave_lds_sync();
+        }
+        // out_proj + residual, LN_f, FFN + residual, last LayerNorm (model.py:84-96)
+        float* ls = us;
+        float* fs = qk;            // [128]: qk, then 64 floats of ps's slot are free
+        const float x1 = fon ? xl[f] + gemv_row(P.w_o, P.b_o, f, d, os) : 0.f;
+        const float l1 = ln_lane(x1, fon, P.ln_f_w, P.ln_f_b, f, d, a.eps);
+        if (fon) ls[f] = l1;
+        wave_lds_sync();
+#pragma unroll
+        for (int m0 = 0; m0 < 128; m0 += 64)
+          if (m0 + lane < mlp) fs[m0 + lane] = fmaxf(gemv_row(P.w1, P.b1, m0 + lane, d, ls), 0.f);
+        wave_lds_sync();
+        const float x2 = fon ? x1 + gemv_row(P.w2, P.b2, f, mlp, fs) : 0.f;
+        const float y = ln_lane(x2, fon, a.ln_w, a.ln_b, f, d, a.eps);
+        if (fon) out[b * d + f] = y;
+        return;
       }
       // X is parked in this wave's LDS slice during attention (registers are the limit); the
       // empty asm keeps the compiler from forwarding the stored values instead of reloading
@@ -568,6 +669,7 @@ int gr_sasrec_fused_launch(const gr_sasrec_params* p, const int64_t* seqs, int64
   a.item_rows = p->item_rows; a.nb = p->n_blocks; a.d = d; a.heads = H; a.mlp = p->mlp; a.n = n;
   a.eps = p->eps;
   a.scale = (float)std::sqrt(1.0 / (double)(d / H));
+  a.tail_h = option("fused_tail_h") != 0 ? 1 : 0;
   const int TT = n > 32 ? 2 : 1, DT = d > 32 ? 2 : 1, MT = (p->mlp + 31) / 32;
   const dim3 g((unsigned)((B + 3) / 4)), blk(256);
   const bool exact = d == 32 * DT && p->mlp == 32 * MT;

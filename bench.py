@@ -409,8 +409,9 @@ def bench_sas_c3(a, world, rank, dev):
     targets = torch.randint(1, items + 1, (a.sas_batch,), generator=torch.Generator(device=dev).manual_seed(5), device=dev)
     rank_ms = kernel_ms(lambda: ops.score_rank(h, table, targets))
     fl = sas_flop_per_user(d, n, items)
-    fl_exe = sas_exec_flop_per_user(d, n, items, causal=False)
-    fwd_exe = sas_exec_flop_per_user(d, n, -1, causal=False)
+    th = gr_amd._lib.get_option("fused_tail_h") != 0   # the fused kernel's final block: H or K|V form
+    fl_exe = sas_exec_flop_per_user(d, n, items, causal=False, tail_h=th)
+    fwd_exe = sas_exec_flop_per_user(d, n, -1, causal=False, tail_h=th)
     res = {"metric": "seqs_scored/s", "value": a.sas_batch * world * a.steps / wall, "unit": "seqs/s",
            "ms_per_step": wall / a.steps * 1e3, "scaling": "weak",
            "config": {"workload": "sas_c3: SASRec predict, 2 blocks, d 64, n 50, H 1, mlp 64, "
@@ -425,6 +426,10 @@ def bench_sas_c3(a, world, rank, dev):
                     "forward_ms": fwd_ms, "forward_flop_per_user_executed": fwd_exe,
                     "forward_frac_executed": fwd_exe * a.sas_batch / (fwd_ms * 1e-3) / 1e12 / FP32_PEAK_TFLOPS,
                     "executed_note": "block 0 in full (the one-wave kernel computes the whole n x n "
+                                     "attention tile), the last block at position n-1 only (H form: "
+                                     "W_k^T q, the n LayerNorm rows dotted twice, W_v u; no K|V of the "
+                                     "n tokens)" if th else
+                                     "block 0 in full (the one-wave kernel computes the whole n x n "
                                      "attention tile), the last block's K|V for all n tokens and the "
                                      "rest at position n-1 only",
                     "score_ms": score_ms,

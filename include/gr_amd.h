@@ -89,6 +89,10 @@ const char* gr_last_error(void);
  *                   bitwise to 0 or to each other: the reassociated sums round differently (logits
  *                   within the 1e-5 row-scaled tolerance, tests/test_sasrec_gpu.py::
  *                   test_tail_h_form_vs_kv_form_and_oracle).
+ *   "fused_tail_h"  1 (default): the fused d <= 64 forward (sas_fused) runs a last-position
+ *                   forward's final block in the same H form (no K / V of the n tokens); 0: K and V
+ *                   projected.  NOT bitwise to 0 (reassociated sums, within the logits tolerance:
+ *                   tests/test_sasrec_gpu.py::test_fused_tail_h_vs_kv_form_and_oracle).
  *   "attn_wave"     6 (default): layer-wise causal attention at head width 64 / 128 on a
  *                   persistent grid, one wave per SIMD walking a static longest-first list of
  *                   (sequence, head, 32-query tile) items, K / V straight from L2 into registers,

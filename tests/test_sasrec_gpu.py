@@ -329,6 +329,35 @@ def test_attn_wave_equals_workgroup_kernel(d, heads, n, blocks, B, tail_h, dev):
         assert torch.equal(res[0][1], res[opt][1]), opt
 
 
+@pytest.mark.parametrize("d,heads,n,blocks,B", [(64, 1, 50, 2, 300), (64, 2, 64, 2, 33), (32, 4, 20, 1, 17),
+                                                (48, 2, 37, 3, 9), (64, 8, 63, 2, 5)])
+def test_fused_tail_h_vs_kv_form_and_oracle(d, heads, n, blocks, B, dev):
+    """Option fused_tail_h: the fused d <= 64 forward's final block for the last position in the H
+    form (no K / V of the n tokens) against the K / V form and the CPU oracle: last hidden state
+    within 5e-5, predict logits within the row-scaled tolerance (1-8 heads, padded widths)."""
+    from gr_amd import _lib, synth
+    from oracle import sasrec_oracle
+    items = 400
+    p = synth.sasrec_params(d, n, blocks, heads, 2 * d, dev)
+    m = synth.sasrec_model(items, p, dev, seed=d + heads + n)
+    seqs = synth.sequences(B, n, items, 7 + n, dev)
+    res = {}
+    try:
+        _lib.set_option("sas_fused", 1)
+        for opt in (0, 1):
+            _lib.set_option("fused_tail_h", opt)
+            res[opt] = (m.last_hidden(seqs).cpu(), m.predict(seqs).cpu())
+    finally:
+        _lib.set_option("fused_tail_h", 1)
+    sd = {k: v.detach().cpu() for k, v in m.state_dict().items()}
+    ref_f = sasrec_oracle.forward(seqs.cpu(), sd, blocks, heads, 1e-8)
+    ref = sasrec_oracle.predict(seqs.cpu(), sd, blocks, heads, 1e-8)
+    assert (res[1][0] - ref_f[:, -1, :]).abs().max().item() < 5e-5
+    assert (res[1][0] - res[0][0]).abs().max().item() < 5e-5
+    for opt in (0, 1):
+        assert ((res[opt][1] - ref).abs() / ref.abs().amax(1, keepdim=True)).max().item() <= TOL, opt
+
+
 def test_score_matches_linear_and_rank_consistency(dev):
     """Fused-rank hard part 3: every logit sees the same fp32 fma chain, so the target's score
     recomputed on any tile equals its entry in the logits (strict '>' never counts the target)."""
