@@ -330,7 +330,8 @@ def test_attn_wave_equals_workgroup_kernel(d, heads, n, blocks, B, tail_h, dev):
 
 
 @pytest.mark.parametrize("d,heads,n,blocks,B", [(64, 1, 50, 2, 300), (64, 2, 64, 2, 33), (32, 4, 20, 1, 17),
-                                                (48, 2, 37, 3, 9), (64, 8, 63, 2, 5)])
+                                                (48, 2, 37, 3, 9), (64, 8, 63, 2, 5), (32, 1, 1, 2, 11),
+                                                (16, 2, 2, 1, 4)])
 def test_fused_tail_h_vs_kv_form_and_oracle(d, heads, n, blocks, B, dev):
     """Option fused_tail_h: the fused d <= 64 forward's final block for the last position in the H
     form (no K / V of the n tokens) against the K / V form and the CPU oracle: last hidden state
