@@ -390,9 +390,13 @@ __device__ __forceinline__ void st_gemv_issue(const float* __restrict__ W, const
   }
 }
 
-// st_gemv with the first chunk from st_gemv_issue (same fma order: bitwise st_gemv's result)
+// st_gemv with the first chunk from st_gemv_issue (same fma order: bitwise st_gemv's result).
+// Epilogue: out[o] = acc + bias, then RELU: max(., 0) (NaN kept), or with `res`: res[o] + (acc +
+// bias) -- the separate passes' exact values (res may alias out: each o is one lane's).
+template <bool RELU = false>
 __device__ __forceinline__ void st_gemv_finish(const float* __restrict__ W, const float* __restrict__ bias,
-                                               const float* v, int rows, int k, float* out, const GemvRows& g) {
+                                               const float* v, int rows, int k, float* out, const GemvRows& g,
+                                               const float* res = nullptr) {
   if (GR_TDIAG == 2) return;
   const int L = k >> 2, gpw = 64 / L;
   const int lane = threadIdx.x & 63, l = lane & (L - 1);
@@ -406,7 +410,11 @@ __device__ __forceinline__ void st_gemv_finish(const float* __restrict__ W, cons
     acc = fmaf(g.a[u][2], x[2], acc);
     acc = fmaf(g.a[u][3], x[3], acc);
     acc = seg_sum(acc, L);
-    if (l == 0 && o < rows) out[o] = acc + g.bias[u];
+    if (l == 0 && o < rows) {
+      float y = acc + g.bias[u];
+      if (RELU) y = y < 0.f ? 0.f : y;
+      out[o] = res ? res[o] + y : y;
+    }
   }
   for (int o0 = grp + ST_U * ngrp; o0 < rows; o0 += ST_U * ngrp) {
     f32x4 a[ST_U];
@@ -423,7 +431,11 @@ __device__ __forceinline__ void st_gemv_finish(const float* __restrict__ W, cons
       acc = fmaf(a[u][2], x[2], acc);
       acc = fmaf(a[u][3], x[3], acc);
       acc = seg_sum(acc, L);
-      if (l == 0 && o < rows) out[o] = acc + bias[o];
+      if (l == 0 && o < rows) {
+        float y = acc + bias[o];
+        if (RELU) y = y < 0.f ? 0.f : y;
+        out[o] = res ? res[o] + y : y;
+      }
     }
   }
 }
@@ -567,19 +579,13 @@ __global__ __launch_bounds__(ST_NT, 2) void sas_tail_h2_kernel(const SasTailArgs
   st_gemv_issue(a.wo, a.bo, d, d, g0);
   st_gemv_issue(a.w1, a.b1, a.mlp, d, g1);                      // FFN1 rows, used after the LayerNorm
   __syncthreads();
-  st_gemv_finish(a.wo, a.bo, o, d, d, x1, g0);                  // out_proj
+  st_gemv_finish(a.wo, a.bo, o, d, d, x1, g0, xl);              // x + out_proj (model.py:84)
   st_gemv_issue(a.w2, a.b2, d, a.mlp, g0);
   __syncthreads();
-  for (int c = tid; c < d; c += ST_NT) x1[c] += xl[c];            // residual (model.py:84)
-  __syncthreads();
   st_layernorm(x1, lnw, lnw + d, d, a.eps, l1, stat);
-  st_gemv_finish(a.w1, a.b1, l1, a.mlp, d, fh, g1);
+  st_gemv_finish<true>(a.w1, a.b1, l1, a.mlp, d, fh, g1);       // relu(W1 . + b1)
   __syncthreads();
-  for (int c = tid; c < a.mlp; c += ST_NT) fh[c] = fh[c] < 0.f ? 0.f : fh[c];
-  __syncthreads();
-  st_gemv_finish(a.w2, a.b2, fh, d, a.mlp, o, g0);              // W2 f + b2 (o reused)
-  __syncthreads();
-  for (int c = tid; c < d; c += ST_NT) x1[c] += o[c];             // residual (model.py:94)
+  st_gemv_finish(a.w2, a.b2, fh, d, a.mlp, x1, g0, x1);         // x1 + W2 f + b2 (model.py:94)
   __syncthreads();
   st_layernorm(x1, lnw + 2 * d, lnw + 3 * d, d, a.eps, l1, stat);  // last_layernorm (model.py:96)
   for (int c = tid; c < d; c += ST_NT) out[b * d + c] = l1[c];
