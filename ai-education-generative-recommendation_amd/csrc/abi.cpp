@@ -88,10 +88,8 @@ static std::atomic<int64_t> g_fused_tail_h{1};
 // attn_wave (6 (default): causal attention at hd 64 / 128 on a persistent grid of one wave per SIMD,
 // each walking a static longest-first list of (sequence, head, query tile) items with the next
 // item's Q / K / V loaded under the current item's last step (attn.hip attn_persist_kernel); 1:
-// one wave per item, longest tiles first (attn_wave_kernel<HD, false>); 4: 1 with the next tile's
-// K Q^T chain issued before this tile's softmax; 5: 1 with Q parked in LDS (two waves per SIMD);
-// 2: the two-waves-per-SIMD form at hd 128; 0: the 4-wave workgroup kernel; 3: 1 when B * heads <
-// 512, else 0).  Bitwise the same output.
+// one wave per item, longest tiles first (attn_wave_kernel); 3: 1 when B * heads < 512, else 0;
+// 0: the 4-wave workgroup kernel).  Bitwise the same output.
 static std::atomic<int64_t> g_attn_wave{6};
 
 int64_t option(const char* name) {
@@ -151,7 +149,10 @@ extern "C" int gr_set_option(const char* name, int64_t value) {
   if (!strcmp(name, "rt_kv2") && (value == 0 || value == 1)) { gr::g_rt_kv2 = value; return GR_OK; }
   if (!strcmp(name, "tail_h") && value >= 0 && value <= 2) { gr::g_tail_h = value; return GR_OK; }
   if (!strcmp(name, "fused_tail_h") && (value == 0 || value == 1)) { gr::g_fused_tail_h = value; return GR_OK; }
-  if (!strcmp(name, "attn_wave") && value >= 0 && value <= 6) { gr::g_attn_wave = value; return GR_OK; }
+  if (!strcmp(name, "attn_wave") && (value == 0 || value == 1 || value == 3 || value == 6)) {
+    gr::g_attn_wave = value;
+    return GR_OK;
+  }
   return gr::fail(GR_ERR_ARG, std::string("gr_set_option: unknown option or value: ") + name);
 }
 

@@ -407,16 +407,10 @@ __global__ __launch_bounds__(256, 1) void attn_pair_kernel(const float* __restri
 // of one (sequence, head) goes to the same XCD (its K / V in that XCD's L2 / the Infinity Cache).  Per row the
 // instruction sequence is attn_mfma_kernel<HD, *, true>'s (same S chain over (it, g, s4), the same
 // lazy softmax, the same O chain over (ft, s)): bitwise the same output.
-// QL (attn_wave=5): the scaled query tile parked in LDS (each lane re-reads exactly the float4s it
-// wrote: no barrier) instead of 64 registers, so two waves fit a SIMD and cover each other's loads
-// and softmax.
-template <int HD, bool PIPE, bool QL = false>
-__global__ __launch_bounds__(64, QL ? 2 : 1) void attn_wave_kernel(const float* __restrict__ qkv,
-                                                                  float* __restrict__ out, int n, int H,
-                                                                  float scale, int nbh, int qt_lo) {
+template <int HD>
+__global__ __launch_bounds__(64) void attn_wave_kernel(const float* __restrict__ qkv, float* __restrict__ out,
+                                                      int n, int H, float scale, int nbh, int qt_lo) {
   constexpr int FT = HD / 32;
-  constexpr int QP = HD + 4;   // LDS row pitch of the parked query tile
-  __shared__ __attribute__((aligned(16))) float qs[QL ? 32 * QP : 4];
   const int lane = threadIdx.x, r = lane & 31, h = lane >> 5;
   const int T = (n + 31) / 32, nt = T - qt_lo;
   // work item of this wave: XCD x = blockIdx % 8 owns the (sequence, head) pairs bh = x (mod 8);
@@ -437,16 +431,13 @@ __global__ __launch_bounds__(64, QL ? 2 : 1) void attn_wave_kernel(const float* 
   const float* Vb = base + 2 * d;
   const int qi = qt * 32 + r;
   const int qc = qi < n ? qi : n - 1;
-  f32x4 qf[QL ? 1 : FT][4];
+  f32x4 qf[FT][4];
 #pragma unroll
   for (int it = 0; it < FT; ++it)
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
       const f32x4 v = *reinterpret_cast<const f32x4*>(Qb + (int64_t)qc * rs + 32 * it + 8 * g + 4 * h);
-      if (QL)
-        *reinterpret_cast<f32x4*>(&qs[r * QP + 32 * it + 8 * g + 4 * h]) = v * scale;
-      else
-        qf[QL ? 0 : it][g] = v * scale;   // q * sqrt(1/hd) (functional.py:6578)
+      qf[it][g] = v * scale;   // q * sqrt(1/hd) (functional.py:6578)
     }
   f32x16 O[FT];
 #pragma unroll
@@ -479,16 +470,12 @@ __global__ __launch_bounds__(64, QL ? 2 : 1) void attn_wave_kernel(const float* 
     f32x16 S;
 #pragma unroll
     for (int v = 0; v < 16; ++v) S[v] = 0.f;
-    if (QL) asm volatile("" ::: "memory");   // re-read the parked tile (hoisted it is 64 registers)
 #pragma unroll
     for (int it = 0; it < FT; ++it)
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const f32x4 q4 = QL ? *reinterpret_cast<const f32x4*>(&qs[r * QP + 32 * it + 8 * g + 4 * h])
-                            : qf[QL ? 0 : it][g];
+      for (int g = 0; g < 4; ++g)
 #pragma unroll
-        for (int s4 = 0; s4 < 4; ++s4) S = mfma32(kf[it][g][s4], q4[s4], S);
-      }
+        for (int s4 = 0; s4 < 4; ++s4) S = mfma32(kf[it][g][s4], qf[it][g][s4], S);
     return S;
   };
   // softmax of key tile kt (S -> P in place) and O += V^T P^T
@@ -534,29 +521,11 @@ __global__ __launch_bounds__(64, QL ? 2 : 1) void attn_wave_kernel(const float* 
   };
   load_k(0);
   load_v(0);
-  if (PIPE) {
-    // PIPE (attn_wave=4): tile kt + 1's S = K Q^T chain issued before tile kt's softmax, so the
-    // matrix pipe has work while the softmax runs (per row the same operations).  Measured 106 vs
-    // 103 us per C5 call without it (profiles/r04/ab_attn_wave.txt): not the default
-    f32x16 Sc = s_chain();
-    if (GR_ADIAG == 0 && 0 < qt) load_k(1);
-    for (int kt = 0; kt <= qt; ++kt) {
-      f32x16 Sn;
-      if (kt < qt) {
-        Sn = s_chain();
-        if (GR_ADIAG == 0 && kt + 1 < qt) load_k(kt + 2);
-      }
-      softmax_pv(Sc, kt);
-      if (GR_ADIAG == 0 && kt < qt) load_v(kt + 1);
-      Sc = Sn;
-    }
-  } else {
-    for (int kt = 0; kt <= qt; ++kt) {
-      f32x16 S = s_chain();
-      if (GR_ADIAG == 0 && kt < qt) load_k(kt + 1);   // the K operands are read at issue: their registers refill now
-      softmax_pv(S, kt);
-      if (GR_ADIAG == 0 && kt < qt) load_v(kt + 1);
-    }
+  for (int kt = 0; kt <= qt; ++kt) {
+    f32x16 S = s_chain();
+    if (GR_ADIAG == 0 && kt < qt) load_k(kt + 1);   // the K operands are read at issue: their registers refill now
+    softmax_pv(S, kt);
+    if (GR_ADIAG == 0 && kt < qt) load_v(kt + 1);
   }
   if (qi < n) {
     const float inv = 1.0f / l;
@@ -726,127 +695,6 @@ __global__ __launch_bounds__(64) void attn_persist_kernel(const float* __restric
   }
 }
 
-// attn_wave=2: the same walk at TWO waves per SIMD (<= 256 registers): K is streamed in 32-feature
-// quarters and V in 32-feature slices, each one step ahead in a two-slot ring (K quarter it + 1,
-// or the next key tile's first quarter, is issued before quarter it's 16 MFMAs; likewise V), so
-// only 64 operand registers are live instead of 128; the second wave on the SIMD covers what one
-// 16-MFMA step does not hide.  Same per-row instruction sequence: bitwise attn_wave_kernel.
-template <int HD>
-__global__ __launch_bounds__(64, 2) void attn_wave2_kernel(const float* __restrict__ qkv, float* __restrict__ out,
-                                                          int n, int H, float scale, int nbh, int qt_lo) {
-  constexpr int FT = HD / 32;
-  const int lane = threadIdx.x, r = lane & 31, h = lane >> 5;
-  const int T = (n + 31) / 32, nt = T - qt_lo;
-  const int x = blockIdx.x & 7, k = blockIdx.x >> 3;
-  const int mx = (nbh - x + 7) / 8;
-  if (k >= mx * nt) return;
-  const int bh = x + 8 * (k % mx), qt = T - 1 - k / mx;   // longest first (attn_wave_kernel)
-  const int b = bh / H, hh = bh % H;
-  const int d = H * HD;
-  const int64_t rs = 3LL * d;
-  const float* base = qkv + (int64_t)b * n * rs + hh * HD;
-  const float* Qb = base;
-  const float* Kb = base + d + 4 * h;
-  const float* Vb = base + 2 * d + r;
-  const int qi = qt * 32 + r;
-  const int qc = qi < n ? qi : n - 1;
-  f32x4 qf[FT][4];
-#pragma unroll
-  for (int it = 0; it < FT; ++it)
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const f32x4 v = *reinterpret_cast<const f32x4*>(Qb + (int64_t)qc * rs + 32 * it + 8 * g + 4 * h);
-      qf[it][g] = v * scale;
-    }
-  f32x16 O[FT];
-#pragma unroll
-  for (int ft = 0; ft < FT; ++ft)
-#pragma unroll
-    for (int v = 0; v < 16; ++v) O[ft][v] = 0.f;
-  float m = -INFINITY, l = 0.f;
-  f32x4 kq[2][4];
-  float vq[2][16];
-  auto load_k = [&](int kt, int it, int slot) {
-    int key = kt * 32 + r;
-    key = key < n ? key : n - 1;
-    const float* kr = Kb + (int64_t)key * rs + 32 * it;
-#pragma unroll
-    for (int g = 0; g < 4; ++g) kq[slot][g] = *reinterpret_cast<const f32x4*>(kr + 8 * g);
-  };
-  auto load_v = [&](int kt, int ft, int slot) {
-#pragma unroll
-    for (int s = 0; s < 16; ++s) {
-      int key = kt * 32 + (s & 3) + 8 * (s >> 2) + 4 * h;
-      key = key < n ? key : n - 1;
-      vq[slot][s] = Vb[(int64_t)key * rs + 32 * ft];
-    }
-  };
-  load_k(0, 0, 0);
-  load_v(0, 0, 0);
-  for (int kt = 0; kt <= qt; ++kt) {
-    f32x16 S;
-#pragma unroll
-    for (int v = 0; v < 16; ++v) S[v] = 0.f;
-#pragma unroll
-    for (int it = 0; it < FT; ++it) {
-      if (it + 1 < FT) load_k(kt, it + 1, (it + 1) & 1);
-      else if (kt < qt) load_k(kt + 1, 0, (it + 1) & 1);
-#pragma unroll
-      for (int g = 0; g < 4; ++g)
-#pragma unroll
-        for (int s4 = 0; s4 < 4; ++s4) S = mfma32(kq[it & 1][g][s4], qf[it][g][s4], S);
-    }
-    float tmax = -INFINITY;
-    if (kt == qt || kt * 32 + 32 > n) {
-#pragma unroll
-      for (int v = 0; v < 16; ++v) {
-        const int key = kt * 32 + (v & 3) + 8 * (v >> 2) + 4 * h;
-        if (key > qi || key >= n) S[v] = -INFINITY;
-        tmax = fmaxf(tmax, S[v]);
-      }
-    } else {
-#pragma unroll
-      for (int v = 0; v < 16; ++v) tmax = fmaxf(tmax, S[v]);
-    }
-    tmax = fmaxf(tmax, __shfl_xor(tmax, 32));
-    const bool up = tmax > m + AT_LAZY;
-    if (__any(up)) {
-      const float mn = up ? tmax : m;
-      const float alpha = __expf(m - mn);
-      l *= alpha;
-      m = mn;
-#pragma unroll
-      for (int ft = 0; ft < FT; ++ft) O[ft] *= alpha;
-    }
-    float ts = 0.f;
-#pragma unroll
-    for (int v = 0; v < 16; ++v) {
-      const float e = __expf(S[v] - m);
-      S[v] = e;
-      ts += e;
-    }
-    ts += __shfl_xor(ts, 32);
-    l += ts;
-#pragma unroll
-    for (int ft = 0; ft < FT; ++ft) {
-      if (ft + 1 < FT) load_v(kt, ft + 1, (ft + 1) & 1);
-      else if (kt < qt) load_v(kt + 1, 0, (ft + 1) & 1);
-#pragma unroll
-      for (int s = 0; s < 16; ++s) O[ft] = mfma32(vq[ft & 1][s], S[s], O[ft]);
-    }
-  }
-  if (qi < n) {
-    const float inv = 1.0f / l;
-    float* orow = out + ((int64_t)b * n + qi) * d + hh * HD;
-#pragma unroll
-    for (int ft = 0; ft < FT; ++ft)
-#pragma unroll
-      for (int g = 0; g < 4; ++g)
-        *reinterpret_cast<f32x4*>(orow + 32 * ft + 8 * g + 4 * h) =
-            f32x4{O[ft][4 * g], O[ft][4 * g + 1], O[ft][4 * g + 2], O[ft][4 * g + 3]} * inv;
-  }
-}
-
 }  // namespace gr
 
 // Returns GR_ERR_UNSUPPORTED (message untouched) for head widths the kernel is not built for.
@@ -860,12 +708,11 @@ int gr_attn_mfma_launch(const float* qkv, float* out, int64_t B, int n, int H, i
   if (B * H > 0x7fffffffLL) return GR_ERR_UNSUPPORTED;
   const int qt_lo = last_tile_only ? (n - 1) / 32 : 0;
   const dim3 g((unsigned)(B * H)), blk(256);
-  // attn_wave 3 (auto): the per-wave kernels when the workgroup kernel would not put two
-  // (sequence, head) workgroups on every CU (B H < 512: forward(seqs[:64]) 204 -> 163 us); at C5
-  // (B H = 512) the workgroup kernel measured 107 vs 111 (attn_wave_kernel) and 138 us
-  // (attn_wave2_kernel), profiles/r04/ab_attn_wave.txt
+  // attn_wave: 6 (default) the persistent grid, 1 one wave per item, 3 the per-wave kernel only when
+  // B H < 512 (the rule before the longest-first order), 0 the workgroup kernel
+  // (profiles/r04/ab_attn_*.txt)
   const int64_t aw = option("attn_wave");
-  const bool wave = aw == 3 ? B * H < 512 : aw != 0;   // 3: the pre-longest-first rule, kept for A/B
+  const bool wave = aw == 3 ? B * H < 512 : aw != 0;
   if ((hd == 64 || hd == 128) && wave && option("attn_lazy") != 0) {
     const int64_t nbh = B * H, nt = (n + 31) / 32 - qt_lo;
     const int64_t waves = 8 * ((nbh + 7) / 8) * nt;
@@ -886,20 +733,10 @@ int gr_attn_mfma_launch(const float* qkv, float* out, int64_t B, int n, int H, i
           hipLaunchKernelGGL(attn_persist_kernel<64>, dim3(8 * wx), bw, 0, st, qkv, out, n, H, scale, (int)nbh, qt_lo, wx);
         return check_launch("sasrec attention (persistent waves)");
       }
-      if (aw == 2 && hd == 128)
-        hipLaunchKernelGGL(attn_wave2_kernel<128>, gw, bw, 0, st, qkv, out, n, H, scale, (int)nbh, qt_lo);
-      else if (aw == 5 && hd == 128)
-        hipLaunchKernelGGL((attn_wave_kernel<128, false, true>), gw, bw, 0, st, qkv, out, n, H, scale, (int)nbh, qt_lo);
-      else if (aw == 5)
-        hipLaunchKernelGGL((attn_wave_kernel<64, false, true>), gw, bw, 0, st, qkv, out, n, H, scale, (int)nbh, qt_lo);
-      else if (aw == 4 && hd == 128)
-        hipLaunchKernelGGL((attn_wave_kernel<128, true>), gw, bw, 0, st, qkv, out, n, H, scale, (int)nbh, qt_lo);
-      else if (aw == 4)
-        hipLaunchKernelGGL((attn_wave_kernel<64, true>), gw, bw, 0, st, qkv, out, n, H, scale, (int)nbh, qt_lo);
-      else if (hd == 128)
-        hipLaunchKernelGGL((attn_wave_kernel<128, false>), gw, bw, 0, st, qkv, out, n, H, scale, (int)nbh, qt_lo);
+      if (hd == 128)
+        hipLaunchKernelGGL(attn_wave_kernel<128>, gw, bw, 0, st, qkv, out, n, H, scale, (int)nbh, qt_lo);
       else
-        hipLaunchKernelGGL((attn_wave_kernel<64, false>), gw, bw, 0, st, qkv, out, n, H, scale, (int)nbh, qt_lo);
+        hipLaunchKernelGGL(attn_wave_kernel<64>, gw, bw, 0, st, qkv, out, n, H, scale, (int)nbh, qt_lo);
       return check_launch("sasrec attention (one wave per query tile)");
     }
   }

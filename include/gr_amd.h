@@ -98,9 +98,7 @@ const char* gr_last_error(void);
  *                   (sequence, head, 32-query tile) items, K / V straight from L2 into registers,
  *                   the next item's operands loaded under the current item's last step; 1: one
  *                   wave per item (longest first); 0: one 4-wave workgroup per (sequence, head) over
- *                   shared LDS tiles; 2: the per-wave form at two waves per SIMD (hd 128); 3: 1
- *                   when B x heads < 512, else 0; 4: 1 with the next tile's K Q^T chain issued
- *                   before the softmax; 5: 1 with Q parked in LDS.  Identical results.
+ *                   shared LDS tiles; 3: 1 when B x heads < 512, else 0.  Identical results.
  *   "attn_lazy"     1 (default): lazy softmax rescaling (the running max moves only when a tile's
  *                   max exceeds it by > 8) and masks on the diagonal / last key tile only; 0: the
  *                   rescale on every tile (another fp32 rounding, within tolerance).
