@@ -1029,6 +1029,17 @@ def main():
                         "device_name": torch.cuda.get_device_name(dev)}
     else:
         line["dist"] = {"backend": None, "world_size": 1, "note": "no process group (N = 1)"}
+    # every leg's headline number once more at the END of the line, where a truncated log tail shows it
+    summ = {}
+    for key, name in (("value", "c2_items_per_s"),):
+        if line.get(key) is not None:
+            summ[name] = line[key]
+    for leg, name in (("sasrec", "c3_seqs_per_s"), ("rq_c4", "c4_items_per_s"), ("sasrec_c5", "c5_seqs_per_s"),
+                      ("c5_shard", "c5_shard_seqs_per_s"), ("sasrec_train_step", "sasrec_train_step_seqs_per_s"),
+                      ("rq_train_step", "rq_train_step_items_per_s"), ("sasrec_train", "sasrec_train_seqs_per_s")):
+        if isinstance(line.get(leg), dict) and line[leg].get("value") is not None:
+            summ[name] = line[leg]["value"]
+    line["summary"] = summ
     if rank == 0:
         print(json.dumps(line), flush=True)
     if dist.is_initialized():
