@@ -54,6 +54,11 @@ static std::atomic<int64_t> g_attn_lazy{1};
 // topk_impl (1 (default): gr_score_topk_f32 = tile-max counting pass + select/re-score kernel;
 // 0: sample pass + exact list pass + merges)
 static std::atomic<int64_t> g_topk_impl{1};
+// topk_half (tile design: 1 = the tile pass records the max of every 16-row half tile and the select
+// kernel re-scores half tiles; 0 = 32-row tiles; 2 (default) = half tiles where the re-scored bytes
+// saved exceed the extra maxima traffic: catalogs below ~3,700 chunks per 128 features).  Bitwise
+// the same results.
+static std::atomic<int64_t> g_topk_half{2};
 // rt_w8 (1 (default): the post-attention row tile runs 8 waves per 64-row tile; 0: 4 waves)
 static std::atomic<int64_t> g_rt_w8{1};
 // lin_w8 (1 (default): gr_linear_f32's 128x128 / 128x64 tiles run 8 waves per workgroup; 0: 4)
@@ -108,6 +113,7 @@ int64_t option(const char* name) {
   if (!strcmp(name, "attn_alt")) return g_attn_alt.load();
   if (!strcmp(name, "attn_lazy")) return g_attn_lazy.load();
   if (!strcmp(name, "topk_impl")) return g_topk_impl.load();
+  if (!strcmp(name, "topk_half")) return g_topk_half.load();
   if (!strcmp(name, "rt_w8")) return g_rt_w8.load();
   if (!strcmp(name, "lin_w8")) return g_lin_w8.load();
   if (!strcmp(name, "lin_wres")) return g_lin_wres.load();
@@ -140,6 +146,7 @@ extern "C" int gr_set_option(const char* name, int64_t value) {
   if (!strcmp(name, "attn_alt") && (value == 0 || value == 1)) { gr::g_attn_alt = value; return GR_OK; }
   if (!strcmp(name, "attn_lazy") && (value == 0 || value == 1)) { gr::g_attn_lazy = value; return GR_OK; }
   if (!strcmp(name, "topk_impl") && (value == 0 || value == 1)) { gr::g_topk_impl = value; return GR_OK; }
+  if (!strcmp(name, "topk_half") && value >= 0 && value <= 2) { gr::g_topk_half = value; return GR_OK; }
   if (!strcmp(name, "rt_w8") && (value == 0 || value == 1)) { gr::g_rt_w8 = value; return GR_OK; }
   if (!strcmp(name, "lin_w8") && (value == 0 || value == 1)) { gr::g_lin_w8 = value; return GR_OK; }
   if (!strcmp(name, "lin_wres") && (value == 0 || value == 1)) { gr::g_lin_wres = value; return GR_OK; }

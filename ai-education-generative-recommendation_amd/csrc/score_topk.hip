@@ -233,21 +233,27 @@ __global__ __launch_bounds__(256, 2) void score_topk_kernel(
     // writing 32- or 64-byte runs per user measured slower (1097-1101 vs 1078-1080 us at C5,
     // 175.6-176.4 vs 172 us on a shard, same results; profiles/r03_ab_topk_staged.txt): the call is
     // MFMA-bound and the extra LDS traffic / barriers cost more than the write traffic saved
-    if (mode == 2) {
+    if (mode >= 2) {   // MODE 3 (topk_half): the maxima of 16-row half tiles (v < 8: rows 0-15)
 #pragma unroll
       for (int ut = 0; ut < UT; ++ut) {
         const int64_t u = u0 + ut * 32 + r;
 #pragma unroll
         for (int it = 0; it < 2; ++it) {
-          float m = -INFINITY;   // fmaxf skips the NaN of rows past the catalog
+          float m = -INFINITY, m1 = -INFINITY;   // fmaxf skips the NaN of rows past the catalog
 #pragma unroll
           for (int v = 0; v < 16; ++v) {
             const float x = acc[ut][it][v];
             cgt[ut] += x > th[ut] ? 1 : 0;
-            m = fmaxf(m, x);
+            if (mode == 3 && v >= 8) m1 = fmaxf(m1, x);
+            else m = fmaxf(m, x);
           }
           m = fmaxf(m, __shfl_xor(m, 32));
-          if (hh == 0 && u < B) cv[u * seg_stride + 2 * vc + it] = m;
+          if (mode == 3) {
+            m1 = fmaxf(m1, __shfl_xor(m1, 32));
+            if (hh == 0 && u < B) *reinterpret_cast<f32x2*>(cv + u * seg_stride + 4 * vc + 2 * it) = f32x2{m, m1};
+          } else if (hh == 0 && u < B) {
+            cv[u * seg_stride + 2 * vc + it] = m;
+          }
         }
       }
       if (vc + 1 < v_end) swrite(buf ^ 1);
@@ -302,7 +308,7 @@ __global__ __launch_bounds__(256, 2) void score_topk_kernel(
   for (int ut = 0; ut < UT; ++ut) {
     const int x = cgt[ut] + __shfl_xor(cgt[ut], 32);
     const int64_t u = u0 + ut * 32 + r;
-    if (mode == 2) {   // per-(user, slice) partial counts, summed by the select kernel
+    if (mode >= 2) {   // per-(user, slice) partial counts, summed by the select kernel
       if (hh == 0 && u < B) reinterpret_cast<unsigned*>(ci)[u * slices + sl] = (unsigned)x;
     } else if (mode == 1) {
       if (cnt_out && sl == 0 && hh == 0 && u < B) cnt_out[u] = 0ull;
@@ -310,7 +316,7 @@ __global__ __launch_bounds__(256, 2) void score_topk_kernel(
       atomicAdd(&cnt_out[u], (unsigned long long)x);
     }
   }
-  if (mode == 2) return;
+  if (mode >= 2) return;
   // candidate segments of each user: the exact pass writes one per slice (the merged list of its
   // two lane halves), the sample pass one per (slice, half) — merging unsorted bucket maxima costs
   // more than the merge kernel saves on a pass that scores one chunk per workgroup
@@ -344,7 +350,7 @@ __global__ __launch_bounds__(256, 2) void topk_select_kernel(const float* __rest
                                                           const unsigned* __restrict__ cpart, int slices,
                                                           unsigned long long* __restrict__ cnt_out,
                                                           float* __restrict__ vals, int64_t* __restrict__ ids,
-                                                          int) {
+                                                          int half) {
   constexpr int KG = D / 32;
   __shared__ int list[256];
   __shared__ int nlist;
@@ -431,8 +437,9 @@ __global__ __launch_bounds__(256, 2) void topk_select_kernel(const float* __rest
     }
     __syncthreads();
     const int n = nlist;
-    for (int e = 2 * w + (lane >> 5); e < n; e += 8) {
-      const int64_t row = (int64_t)list[e] * 32 + r;
+    // tiles of 32 rows: two per wave pass; half tiles of 16 rows (topk_half): four
+    for (int e = half ? 4 * w + (lane >> 4) : 2 * w + (lane >> 5); e < n; e += half ? 16 : 8) {
+      const int64_t row = half ? (int64_t)list[e] * 16 + (lane & 15) : (int64_t)list[e] * 32 + r;
       const int64_t rc = row < rows ? row : rows - 1;
       const float* tr = table + rc * D;
       float x = 0.f;
@@ -545,7 +552,13 @@ static TileWs tile_ws(int64_t B, int64_t rows, int d) {
   w.ublocks = (B + uw - 1) / uw;
   w.chunks = (rows + TK_CHUNK - 1) / TK_CHUNK;
   w.slices = slices_for(w.ublocks, w.chunks, d);
-  w.T = 2 * w.chunks;
+  // tile maxima per user: 32-row tiles, or 16-row half tiles (topk_half) -- half the rows the select
+  // kernel re-scores (~11 tiles x 16 rows x 4d bytes per user) for twice the maxima, written once
+  // and read twice (2 x 4 x 3 bytes more per chunk and user): auto (2) takes half tiles where that
+  // nets (a C5 shard: 165 -> 161 us; 1M rows: 1035 -> 1055 us, profiles/r04/ab_topk_half.txt)
+  const int64_t half = option("topk_half");
+  const bool ht = half == 1 || (half == 2 && 24 * w.chunks < 704LL * d);
+  w.T = (ht ? 4 : 2) * w.chunks;
   w.tmax = align_up((size_t)B * w.T * sizeof(float), 256);
   w.cpart = align_up((size_t)B * w.slices * sizeof(unsigned), 256);
   w.total = w.tmax + w.cpart + 256;
@@ -587,6 +600,14 @@ static void launch_pass(int d, dim3 grid, hipStream_t st, const float* h, int64_
       case 32: GR_TK_PASS(32, 2); break;
       case 64: GR_TK_PASS(64, 2); break;
       default: GR_TK_PASS(128, 2); break;
+    }
+    return;
+  }
+  if (mode == 3) {
+    switch (d) {
+      case 32: GR_TK_PASS(32, 3); break;
+      case 64: GR_TK_PASS(64, 3); break;
+      default: GR_TK_PASS(128, 3); break;
     }
     return;
   }
@@ -659,13 +680,14 @@ extern "C" int gr_score_topk_f32(const float* h, int64_t B, int32_t d, const flo
     auto runt = [&](auto kc_tag) -> int {
       constexpr int KC = decltype(kc_tag)::value;
       launch_pass<KC>(d, dim3((unsigned)(tw.ublocks * tw.slices)), st, h, B, table, rows, thresholds, mask_col0,
-                      nullptr, nullptr, 0, tw.chunks, 2, 1, tmax, reinterpret_cast<int64_t*>(cpart), tw.T, 0,
+                      nullptr, nullptr, 0, tw.chunks, tw.T == 4 * tw.chunks ? 3 : 2, 1, tmax,
+                      reinterpret_cast<int64_t*>(cpart), tw.T, 0,
                       (int)tw.ublocks, (int)tw.slices);
       int rc = check_launch("gr_score_topk_f32 (tile pass)");
       if (rc) return rc;
 #define GR_TK_SEL(DD) hipLaunchKernelGGL((topk_select_kernel<DD, KC>), dim3((unsigned)B), dim3(256), 0, st, h, B, \
                                          table, rows, mask_col0, k, id_offset, tmax, tw.T, cpart, (int)tw.slices, \
-                                         cnt, vals_out, ids_out, 0)
+                                         cnt, vals_out, ids_out, tw.T == 4 * tw.chunks ? 1 : 0)
       switch (d) {
         case 32: GR_TK_SEL(32); break;
         case 64: GR_TK_SEL(64); break;

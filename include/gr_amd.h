@@ -67,6 +67,10 @@ const char* gr_last_error(void);
  *                   3: direct, plain stores; 4: the rotated kernel.  Identical results.
  *   "topk_sample"   1 (default): gr_score_topk_f32 prunes with a threshold from a strided sample
  *                   pass when the catalog is long enough; 0: one pass.  Identical results.
+ *   "topk_half"     2 (default): gr_score_topk_f32's tile pass records the max of every 16-row
+ *                   half tile when the catalog is below ~3,700 64-row chunks per 128 features (the
+ *                   select kernel then re-scores half as many rows), else of every 32-row tile;
+ *                   1: always half tiles; 0: never.  Identical results.
  *   "lin_wres"      1 (default): gr_linear_f32 with k = 128, n % 128 == 0, no residual and
  *                   m >= 96 x 256 runs a persistent kernel that keeps each wave's 32 columns of w in
  *                   registers (the C5 block-0 in-projection); 0: the tiled kernel.  Identical results.

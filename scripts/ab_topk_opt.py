@@ -1,7 +1,7 @@
 """One gr_set_option switch on gr_score_topk_f32 at the C5 shard and full C5 shapes (and C3's d 64):
 steady-state HIP-event time and bitwise equality of (values, ids, counts) across the settings.
 
-    python scripts/ab_topk_opt.py [--opt tile_w8=0,1]
+    python scripts/ab_topk_opt.py [--opt topk_half=0,1,2]
 """
 import argparse
 import os

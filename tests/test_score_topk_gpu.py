@@ -29,24 +29,28 @@ def _reference(h, t, k, id_offset, thr, mask_col0):
 
 def _check(h, t, k, id_offset=0, mask_col0=True, seed=0):
     """Every plan against the materialised reference: the tile design (tile maxima + re-scored
-    tiles, the default), and the list design with its sample-thresholded two passes and one pass."""
+    tiles, the default) with 32-row and 16-row tiles (topk_half), and the list design with its
+    sample-thresholded two passes and one pass."""
     from gr_amd import _lib, ops
     g = torch.Generator(device=h.device).manual_seed(seed)
     thr = torch.randn(h.shape[0], generator=g, device=h.device)
     rv, ri, rc = _reference(h, t, k, id_offset, thr, mask_col0)
+    half0 = _lib.get_option("topk_half")
     try:
-        for impl, sample in ((1, 1), (0, 1), (0, 0)):
+        for impl, sample, half in ((1, 1, 0), (1, 1, 1), (0, 1, 0), (0, 0, 0)):
             _lib.set_option("topk_impl", impl)
             _lib.set_option("topk_sample", sample)
+            _lib.set_option("topk_half", half)
             v, i, c = ops.score_topk(h, t, k, id_offset, thresholds=thr, mask_col0=mask_col0)
-            assert torch.equal(i, ri), (impl, sample)
-            assert torch.equal(v, rv), (impl, sample)
-            assert torch.equal(c, rc), (impl, sample)
+            assert torch.equal(i, ri), (impl, sample, half)
+            assert torch.equal(v, rv), (impl, sample, half)
+            assert torch.equal(c, rc), (impl, sample, half)
             v2, i2 = ops.score_topk(h, t, k, id_offset, mask_col0=mask_col0)   # without counts
-            assert torch.equal(v2, rv) and torch.equal(i2, ri), (impl, sample)
+            assert torch.equal(v2, rv) and torch.equal(i2, ri), (impl, sample, half)
     finally:
         _lib.set_option("topk_impl", 1)
         _lib.set_option("topk_sample", 1)
+        _lib.set_option("topk_half", half0)
 
 
 @pytest.mark.parametrize("B,d,rows,k", [(1, 64, 70, 10), (300, 64, 100001, 10), (64, 128, 5000, 16),
