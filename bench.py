@@ -240,9 +240,11 @@ def kernel_ms(fn, reps=50, warmup=2):
     return e0.elapsed_time(e1) / reps
 
 
-# one gr_score_topk_f32 call (tile design, topk_impl 1): the tile pass (MODE 2) + the select kernel
+# one gr_score_topk_f32 call (tile design, topk_impl 1): the tile pass (MODE 2: 32-row tile maxima,
+# at 1M rows; MODE 3: 16-row half tiles, topk_half's choice on a shard) + the select kernel
 TOPK_PASS = "score_topk_kernel<128,10,2>"
-TOPK_CALL_KERNELS = [TOPK_PASS, "topk_select_kernel<128,10>"]
+TOPK_PASS_HALF = "score_topk_kernel<128,10,3>"
+TOPK_CALL_KERNELS = [TOPK_PASS, TOPK_PASS_HALF, "topk_select_kernel<128,10>"]
 
 
 def call_traffic(leg, kernels, anchor):
@@ -855,9 +857,10 @@ def bench_c5_shard(a, table, h, targets, dev, shards=8):
             "config": {"workload": f"c5_shard: {B} users x one {hi - lo}-row catalog shard (1/{shards} of "
                                    f"{table.shape[0]}), d {d}, target logit + rank + top-{k}",
                        "rows": hi - lo, "users": B},
-            "roofline": roofline(TOPK_PASS, flop, topk_ms, "shard",
+            "roofline": roofline(TOPK_PASS_HALF, flop, topk_ms, "shard",
                                  call_kernels=TOPK_CALL_KERNELS,
-                                 note="one gr_score_topk_f32 call on the shard (all its launches); flop "
+                                 note="one gr_score_topk_f32 call on the shard (all its launches: the tile "
+                                      "pass with 16-row half-tile maxima, topk_half auto, + the select); flop "
                                       "counts the scoring GEMM once; traffic is the whole call's"),
             "call": {"device_ms": dev_ms, "score_topk_ms": topk_ms, "score_count_ms": cnt_ms,
                      "frac_of_fp32_peak_step": flop / (dev_ms * 1e-3) / 1e12 / FP32_PEAK_TFLOPS}}

@@ -54,13 +54,8 @@ for s in $STEPS; do
             -d "$OUT/pmc_$c" -o run -- python3 "$ROOT/bench.py" --steps 5 --warmup 2 --no-cpu-baseline
         cd "$ROOT"
       done ;;
-    pmc3)  # HBM bytes per kernel of the bench command itself (FETCH_SIZE / WRITE_SIZE, separate passes)
-      export TMPDIR=/tmp
-      cd /tmp
-      step pmcb_FETCH 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmcb_FETCH" -o run -- python3 "$ROOT/bench.py" --steps 3 --warmup 1 --no-cpu-baseline --skip c4 && \
-      step pmcb_WRITE 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmcb_WRITE" -o run -- python3 "$ROOT/bench.py" --steps 3 --warmup 1 --no-cpu-baseline --skip c4 && \
-      python3 "$ROOT/scripts/pmc_traffic.py" "$OUT/pmcb_FETCH" "$OUT/pmcb_WRITE" "$TAG" > "$OUT/traffic.json"
-      cd "$ROOT" ;;
+    pmc3)  # HBM bytes per kernel and bench leg (FETCH_SIZE / WRITE_SIZE, separate passes): scripts/pmc_legs.sh
+      step pmc_legs 1100 bash "$ROOT/scripts/pmc_legs.sh" "$TAG" ;;
     pmc2)  # HBM bytes per kernel (FETCH_SIZE / WRITE_SIZE in separate passes) + SQ counters, RQ and SASRec
       export TMPDIR=/tmp
       cd /tmp
