@@ -359,15 +359,36 @@ __global__ __launch_bounds__(256, 2) void topk_select_kernel(const float* __rest
   const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, w = tid >> 6;
   const int64_t u = blockIdx.x;
   const float* tm = tmax + u * T;
+  __shared__ __attribute__((aligned(16))) float hs[D];   // the user's vector (LDS broadcast reads)
+  // Every independent global read is issued up front (the user's vector, the partial counts, and --
+  // when T <= KR * MB * 256, a C5 shard's 7,812 half-tile maxima -- all the thread's tile maxima,
+  // kept in registers for the qualifying-tile pass instead of a second read): one round trip
+  // instead of four on this latency-bound kernel.
+  constexpr int MB = 16, KR = 2;
+  const bool kept = T <= (int64_t)256 * MB * KR;
+  float kv[KR][MB];
+  if (kept) {
+#pragma unroll
+    for (int rr = 0; rr < KR; ++rr)
+#pragma unroll
+      for (int b = 0; b < MB; ++b) {
+        const int64_t q = tid + 256 * (rr * MB + b);
+        kv[rr][b] = q < T ? tm[q] : -INFINITY;
+      }
+  }
+  f32x4 h4 = {0.f, 0.f, 0.f, 0.f};
+  if (tid < D / 4) h4 = *reinterpret_cast<const f32x4*>(h + u * D + 4 * tid);
+  unsigned long long c = 0;
+  if (cnt_out)
+    for (int i = tid; i < slices; i += 256) c += cpart[u * slices + i];
   if (tid == 0) {
     nlist = 0;
     csum = 0ull;
     mk_s = -INFINITY;
   }
+  if (tid < D / 4) *reinterpret_cast<f32x4*>(hs + 4 * tid) = h4;
   __syncthreads();
   if (cnt_out) {
-    unsigned long long c = 0;
-    for (int i = tid; i < slices; i += 256) c += cpart[u * slices + i];
     for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
     if (lane == 0 && c) atomicAdd(&csum, c);
   }
@@ -376,17 +397,23 @@ __global__ __launch_bounds__(256, 2) void topk_select_kernel(const float* __rest
   // every top-k item lies in a tile whose max is >= tau (about k + 1 tiles: the k largest tiles
   // rarely share a thread).  One fmax per tile, no per-thread sorted lists (their insertions took
   // most of this kernel's 89 us at C5, profiles/r03_ab_topk_select_tau.txt).
-  constexpr int MB = 16;
   float mx = -INFINITY;
-  for (int64_t q0 = tid; q0 < T; q0 += 256 * MB) {
-    float v[MB];
+  if (kept) {
 #pragma unroll
-    for (int b = 0; b < MB; ++b) {
-      const int64_t q = q0 + 256 * b;
-      v[b] = q < T ? tm[q] : -INFINITY;
+    for (int rr = 0; rr < KR; ++rr)
+#pragma unroll
+      for (int b = 0; b < MB; ++b) mx = fmaxf(mx, kv[rr][b]);
+  } else {
+    for (int64_t q0 = tid; q0 < T; q0 += 256 * MB) {
+      float v[MB];
+#pragma unroll
+      for (int b = 0; b < MB; ++b) {
+        const int64_t q = q0 + 256 * b;
+        v[b] = q < T ? tm[q] : -INFINITY;
+      }
+#pragma unroll
+      for (int b = 0; b < MB; ++b) mx = fmaxf(mx, v[b]);
     }
-#pragma unroll
-    for (int b = 0; b < MB; ++b) mx = fmaxf(mx, v[b]);
   }
   {
     TopList<1> tl;
@@ -399,28 +426,40 @@ __global__ __launch_bounds__(256, 2) void topk_select_kernel(const float* __rest
   __syncthreads();
   const float mk = mk_s;
   if (cnt_out && tid == 0) cnt_out[u] = csum;
-  // The qualifying tiles (max >= tau), from a second read of the thread's tiles (cache-resident);
-  // more than the LDS list holds (ties) -> every tile is re-checked, 256 at a time.
+  // The qualifying tiles (max >= tau), from the kept registers or a second read of the thread's
+  // tiles (cache-resident); more than the LDS list holds (ties) -> every tile is re-checked, 256 at
+  // a time.
   if (mx >= mk) {
-    for (int64_t q0 = tid; q0 < T; q0 += 256 * MB) {
-      float v[MB];
+    if (kept) {
 #pragma unroll
-      for (int b = 0; b < MB; ++b) {
-        const int64_t q = q0 + 256 * b;
-        v[b] = q < T ? tm[q] : -INFINITY;
-      }
+      for (int rr = 0; rr < KR; ++rr)
 #pragma unroll
-      for (int b = 0; b < MB; ++b)
-        if (q0 + 256 * b < T && v[b] >= mk) {
-          const int at = atomicAdd(&nlist, 1);
-          if (at < 256) list[at] = (int)(q0 + 256 * b);
+        for (int b = 0; b < MB; ++b) {
+          const int64_t q = tid + 256 * (rr * MB + b);
+          if (q < T && kv[rr][b] >= mk) {
+            const int at = atomicAdd(&nlist, 1);
+            if (at < 256) list[at] = (int)q;
+          }
         }
+    } else {
+      for (int64_t q0 = tid; q0 < T; q0 += 256 * MB) {
+        float v[MB];
+#pragma unroll
+        for (int b = 0; b < MB; ++b) {
+          const int64_t q = q0 + 256 * b;
+          v[b] = q < T ? tm[q] : -INFINITY;
+        }
+#pragma unroll
+        for (int b = 0; b < MB; ++b)
+          if (q0 + 256 * b < T && v[b] >= mk) {
+            const int at = atomicAdd(&nlist, 1);
+            if (at < 256) list[at] = (int)(q0 + 256 * b);
+          }
+      }
     }
   }
   __syncthreads();
   const bool slow = nlist > 256;
-  __shared__ __attribute__((aligned(16))) float hs[D];   // the user's vector (LDS broadcast reads)
-  if (tid < D / 4) *reinterpret_cast<f32x4*>(hs + 4 * tid) = *reinterpret_cast<const f32x4*>(h + u * D + 4 * tid);
   TopList<KC> best;
   best.init();
   // Re-scoring on the VALU: one lane per row (two tiles per wave pass), each logit as the fmaf chain
