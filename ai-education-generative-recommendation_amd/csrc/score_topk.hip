@@ -335,7 +335,8 @@ __global__ __launch_bounds__(256, 2) void score_topk_kernel(
 }
 
 // Tile design (topk_impl 1, the default).  The tile pass (MODE 2) scores every chunk once, counts,
-// and records per user the max logit of every 32-row tile.  Let M_k be the k-th largest tile max:
+// and records per user the max logit of every 32-row tile (MODE 3, topk_half: of every 16-row half
+// tile; the argument below holds for tiles of any size).  Let M_k be the k-th largest tile max:
 // those k tiles hold k distinct items >= M_k, so the user's k-th best logit is >= M_k and every
 // top-k item lies in a tile whose max is >= M_k (about k tiles; more only on exact ties).  This
 // kernel (one workgroup per user) finds a threshold tau <= M_k (below), re-scores just the tiles
