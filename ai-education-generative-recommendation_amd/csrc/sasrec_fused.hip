@@ -313,10 +313,13 @@ __global__ __launch_bounds__(256) void sasrec_fused_kernel(const SasFusedArgs a,
 #pragma unroll 1
         for (int hh = 0; hh < (SINGLE ? 1 : a.heads); ++hh) {
           const int f_lo = SINGLE ? 0 : hh * hd, f_hi = SINGLE ? d : f_lo + hd;
-          if (fon) {   // q'_h[c] = sum_{r in head h} W_k[r][c] q[r]
+          {   // q'_h[c] = sum_{r in head h} W_k[r][c] q[r]; the padded features c in [d, 32 DT) get
+              // an explicit 0 (the score loop below reads all 32 DT, against Hn's zero padding)
             float acc = 0.f;
+            if (fon) {
 #pragma unroll 8
-            for (int rr = f_lo; rr < f_hi; ++rr) acc = fmaf(wk[(int64_t)rr * d + f], qs[rr], acc);
+              for (int rr = f_lo; rr < f_hi; ++rr) acc = fmaf(wk[(int64_t)rr * d + f], qs[rr], acc);
+            }
             qk[f] = acc;
           }
           wave_lds_sync();

@@ -17,7 +17,11 @@ shard across ranks with no collective ("scaling": "weak").  The same JSON line c
   * "rq_c4"     — C4: 4x1024 codebooks, a fixed 10M-item catalog split over the ranks (strong);
   * "sasrec_c5" — C5: d 128, n 200, 1M-item catalog sharded over the ranks: users' hidden states
                   all-gathered, every rank scores its catalog shard, strict-'>' counts all-reduced
-                  and per-shard top-10 all-gathered over RCCL (strong scaling).
+                  and per-shard top-10 all-gathered over RCCL; 512 users per rank (B = 512 N, weak
+                  scaling: each rank forwards 512 sequences and scores B users x 1/N of the catalog);
+  * "c5_rank"   — one rank's step of the N = 8 C5 point on one GPU (forward of its 512 users,
+                  target logits + fused rank/top-10 of all 4096 users on a 125k-row shard, merge of
+                  the 8 x 10 candidates), with the per-kernel split.
 Each "roofline" is for the DOMINANT kernel of its path, timed alone with HIP events on the launch
 stream; "traffic" (HBM bytes per launch) comes from the committed rocprofv3 PMC summary
 (profiles/traffic.json, FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM).  Rank 0 at N=1 also
@@ -153,7 +157,11 @@ def parse():
     ap.add_argument("--rq-items", type=int, default=100_000)
     ap.add_argument("--sas-batch", type=int, default=2048)
     ap.add_argument("--c4-items", type=int, default=10_000_000)
-    ap.add_argument("--c5-batch", type=int, default=512)
+    ap.add_argument("--c5-batch", type=int, default=512,
+                    help="C5 users PER RANK per step: B = c5_batch x N users, so every rank forwards "
+                         "c5_batch sequences and scores B users against its 1/N of the catalog")
+    ap.add_argument("--c5-rank-world", type=int, default=8,
+                    help="c5_rank leg: the world size whose per-rank step it times on one GPU")
     ap.add_argument("--c5-items", type=int, default=1_000_000)
     ap.add_argument("--c5-pipeline", type=int, default=1,
                     help="C5 at N>1: user sub-batches per step whose exchange overlaps the next one's scoring")
@@ -294,47 +302,100 @@ def cpu_model():
     return "unknown"
 
 
-def cpu_median(fn, units, unit, sample, warm=3, reps=10):
+def cpu_median(fn, units, unit, sample, warm=3, reps=10, agree=None):
     """the CPU restatement timed with 3 warmups then the median of 10 calls, on
-    ``cpu_threads()`` host threads; returns the cpu_baseline object (``units`` per call)."""
+    ``cpu_threads()`` host threads; returns the cpu_baseline object (``units`` per call).
+    ``agree(out)`` compares the last call's output with the GPU's on the same inputs; its dict is
+    reported as ``agreement`` (§8(d): the restatement's agreement on the bench host, reported
+    separately from the fixture-host parity)."""
     torch.set_num_threads(cpu_threads())
     for _ in range(warm):
         fn()
     ts = []
+    out = None
     for _ in range(reps):
         t0 = time.perf_counter()
-        fn()
+        out = fn()
         ts.append(time.perf_counter() - t0)
     med = float(np.median(ts))
-    return {"value": units / med, "unit": unit, "cores": torch.get_num_threads(), "kind": "port",
-            "cpu": cpu_model(), "timing": f"{warm} warmups + median of {reps} calls "
-            f"(median {med * 1e3:.1f} ms, min {min(ts) * 1e3:.1f}, max {max(ts) * 1e3:.1f})", "sample": sample}
+    res = {"value": units / med, "unit": unit, "cores": torch.get_num_threads(), "kind": "port",
+           "cpu": cpu_model(), "timing": f"{warm} warmups + median of {reps} calls "
+           f"(median {med * 1e3:.1f} ms, min {min(ts) * 1e3:.1f}, max {max(ts) * 1e3:.1f})", "sample": sample}
+    if agree is not None:
+        res["agreement"] = agree(out)
+    return res
+
+
+def rq_agreement(cpu_idx, gpu_idx):
+    """Rows whose semantic IDs differ between the host restatement and the GPU."""
+    cpu_idx, gpu_idx = cpu_idx.cpu(), gpu_idx.cpu()
+    diff = (cpu_idx != gpu_idx).any(1)
+    return {"rows": int(cpu_idx.shape[0]), "rows_ids_differ": int(diff.sum()),
+            "note": "oracle/rq_oracle (torch CPU ops, this host's MKL) vs the GPU get_indices on the same "
+                    "items; the bit-exact claim is pinned on the fixture host's reference outputs "
+                    "(tests/golden), this count is this host's CPU path"}
+
+
+def sas_agreement(cpu_logits, gpu_logits, seed=0):
+    """Max row-scaled logit error and strict ranks (SASRec/evaluate.py:27-32, column 0 masked) on
+    the same users, with half the targets from the host path's top-20 and half uniform."""
+    c = cpu_logits.float()
+    g_ = gpu_logits.float().cpu()
+    scale = c.abs().amax(1)
+    err = float(((g_ - c).abs().amax(1) / scale).max())
+    B, rows = c.shape
+    rng = np.random.default_rng(seed)
+    cm, gm = c.clone(), g_.clone()
+    cm[:, 0] = -1e9
+    gm[:, 0] = -1e9
+    top20 = torch.topk(cm, 20, dim=1).indices.numpy()
+    tg = torch.from_numpy(np.where(rng.random(B) < 0.5, top20[np.arange(B), rng.integers(0, 20, B)],
+                                   rng.integers(1, rows, B)).astype(np.int64))[:, None]
+    rc = (cm > cm.gather(1, tg)).sum(1) + 1
+    rg = (gm > gm.gather(1, tg)).sum(1) + 1
+    return {"users": B, "max_row_scaled_logit_err": err, "tolerance": 1e-5,
+            "ranks_differ": int((rc != rg).sum()), "hr10_cpu": float((rc <= 10).double().mean()),
+            "hr10_gpu": float((rg <= 10).double().mean()),
+            "note": "oracle/sasrec_oracle.predict on this host's CPU vs the GPU's logits of the same users; "
+                    "targets half from the host path's top-20, half uniform"}
 
 
 def cpu_rq_baseline(model, n_items, tag):
     """Oracle restatement of get_indices (oracle/rq_oracle.py) on host cores, one call of
-    ``n_items`` synthetic items of the same workload."""
+    ``n_items`` synthetic items of the same workload; ``agreement``: its IDs against the GPU's."""
     from oracle import rq_oracle
     lin = model.encoder.linears()
     ws = [l.weight.detach().cpu() for l in lin]
     bs = [l.bias.detach().cpu() for l in lin]
     cbs = [c.cpu() for c in model.rq.codebooks()]
-    x = synth.items(n_items, 12345, "cuda").cpu()
+    xg = synth.items(n_items, 12345, "cuda")
+    gpu_idx = model.get_indices(xg).cpu()
+    x = xg.cpu()
     return cpu_median(lambda: rq_oracle.get_indices(x, ws, bs, cbs), n_items, "items/s",
-                      f"oracle/rq_oracle.get_indices, {tag}: batch of {n_items} synthetic items (fp32 torch CPU)")
+                      f"oracle/rq_oracle.get_indices, {tag}: batch of {n_items} synthetic items (fp32 torch CPU)",
+                      agree=lambda out: rq_agreement(out, gpu_idx))
 
 
-def cpu_sas_baseline(model, B, n, items, tag, table=None):
+def cpu_sas_baseline(model, B, n, items, tag, table=None, params=None):
     """Oracle restatement of predict (oracle/sasrec_oracle.py) on host cores, one call of B users
-    (``table``: the full [items+1, d] item table when the model holds a compact one)."""
+    (``table``: the full [items+1, d] item table when the model holds a compact one; the GPU side
+    then rebuilds the compact model for these users from ``params``); ``agreement``: its logits and
+    ranks against the GPU's on the same users."""
     from oracle import sasrec_oracle
     sd = {k: v.detach().cpu() for k, v in model.state_dict().items()}
+    seqs_g = synth.sequences(B, n, items, 777, "cuda")
     if table is not None:
         sd["item_emb.weight"] = table.detach().cpu()
-    seqs = synth.sequences(B, n, items, 777, "cuda").cpu()
+        mr, sr = synth.sasrec_rank_model(items, params, seqs_g, seqs_g.device, seed=5)
+        gpu_logits = ops.score(mr.last_hidden(sr), table).cpu()
+        del mr
+    else:
+        gpu_logits = model.predict(seqs_g).cpu()
+    seqs = seqs_g.cpu()
     return cpu_median(lambda: sasrec_oracle.predict(seqs, sd, model.num_blocks, model.num_heads, 1e-8),
                       B, "seqs/s", f"oracle/sasrec_oracle.predict, {tag}: batch of {B} users "
-                      f"(d {model.d}, n {n}, {items}-item catalog, logits [B, {items + 1}])")
+                      f"(d {model.d}, n {n}, {items}-item catalog, logits [B, {items + 1}])",
+                      agree=lambda out: sas_agreement(out, gpu_logits))
 
 
 def bench_rq_c2(a, world, rank, dev):
@@ -448,7 +509,7 @@ def bench_sas_c5(a, world, rank, dev, time_it=True):
     users, hidden states are all-gathered, each rank scores ALL users against its catalog shard,
     then counts are all-reduced and top-10 lists all-gathered (gr_amd.dist)."""
     from gr_amd import dist as D
-    d, n, items, B = 128, 200, a.c5_items, a.c5_batch
+    d, n, items, B = 128, 200, a.c5_items, a.c5_batch * world   # c5_batch users per rank (weak)
     p = synth.sasrec_params(d, n, 2, 1, 64, dev)
     seqs = synth.sequences(B, n, items, 5000, dev)            # same users on every rank
     targets = torch.randint(1, items + 1, (B,), generator=torch.Generator(device=dev).manual_seed(6), device=dev)
@@ -492,10 +553,11 @@ def bench_sas_c5(a, world, rank, dev, time_it=True):
     th = gr_amd._lib.get_option("tail_h") != 0   # the C5 forward's final block: H form or K|V form
     fl_exe = sas_exec_flop_per_user(d, n, items, causal=True, tail_h=th)
     fwd_exe = sas_exec_flop_per_user(d, n, -1, causal=True, tail_h=th)
-    res = {"metric": "seqs_scored/s", "value": B * steps / wall, "unit": "seqs/s", "scaling": "strong",
+    res = {"metric": "seqs_scored/s", "value": B * steps / wall, "unit": "seqs/s", "scaling": "weak",
             "ms_per_step": wall / steps * 1e3, "steps": steps,
             "config": {"workload": "sas_c5: SASRec d 128, n 200, 2 blocks, 1M-item catalog, rank + top-10",
-                       "users_per_step": B, "catalog_rows": items + 1, "rows_per_rank": hi - lo,
+                       "users_per_step": B, "users_per_rank": a.c5_batch, "catalog_rows": items + 1,
+                       "rows_per_rank": hi - lo,
                        "users_forwarded_per_rank": uhi - ulo, "table_rows_built_per_rank": (hi - lo) + model.item_num,
                        "setup_s": setup_s,
                        "parallelism": f"catalog-sharded x{world}: RCCL all-gather h + top-k, all-reduce counts"
@@ -866,6 +928,92 @@ def bench_c5_shard(a, table, h, targets, dev, shards=8):
                      "frac_of_fp32_peak_step": flop / (dev_ms * 1e-3) / 1e12 / FP32_PEAK_TFLOPS}}
 
 
+def bench_c5_rank(a, dev):
+    """the per-rank unit of the N-GPU C5 point (N = ``--c5-rank-world``, 8),
+    timed on one GPU.  Rank 0's step of ``bench_sas_c5`` at world N: the transformer forward of its
+    own c5_batch users, then -- on the all-gathered hidden states of all B = c5_batch x N users --
+    the owner's target logits (gr_score_pairs_f32), the fused strict count + local top-10 over its
+    catalog shard (rows [0, (items+1)/N), which also masks row 0; gr_score_topk_f32) and the merge of
+    the N x 10 gathered candidates (dist.merge_topk).  The collectives themselves (all-gather of
+    B x d floats, two all-reduces of B scalars, all-gather of B x 10 candidates: about 2.4 MB per
+    rank at N = 8) are not on one GPU; ``collective_bytes_per_rank`` states them.  ``value`` = the B
+    users of one N-GPU step / this rank's device time per step: the N-GPU throughput when the
+    collectives overlap the scoring."""
+    from gr_amd import dist as D
+    W = a.c5_rank_world
+    d, n, items, k = 128, 200, a.c5_items, 10
+    B = a.c5_batch * W
+    p = synth.sasrec_params(d, n, 2, 1, 64, dev)
+    seqs = synth.sequences(B, n, items, 5000, dev)
+    targets = torch.randint(1, items + 1, (B,), generator=torch.Generator(device=dev).manual_seed(6), device=dev)
+    lo, hi = D.shard_range(items + 1, 0, W)
+    shard = synth.table_rows(torch.arange(lo, hi, device=dev), d, 7, dev)
+    hs = []
+    for r in range(W):   # every rank's hidden states (what the all-gather delivers), built once
+        ulo, uhi = D.shard_range(B, r, W)
+        mr, sr = synth.sasrec_rank_model(items, p, seqs[ulo:uhi], dev, seed=5)
+        hs.append(mr.last_hidden(sr))
+        if r == 0:
+            model, lseqs = mr, sr
+    h = torch.cat(hs)
+    del hs
+    t = targets
+    own = (t >= lo) & (t < hi)
+    loc = torch.where(own, t - lo, torch.zeros_like(t))
+    m0 = lo == 0
+    # the other ranks' candidates: this shard's lists with ids moved into their shards (the merge's
+    # cost depends on the [B, N k] shape, not on the values)
+    _, v0, i0 = D.sharded_rank_topk(h, shard, lo, targets, k=k)
+    cand_v = torch.cat([v0] * W, 1)
+    cand_i = torch.cat([i0 + D.shard_range(items + 1, r, W)[0] for r in range(W)], 1)
+
+    def forward():
+        return model.last_hidden(lseqs)
+
+    def pairs():
+        return torch.where(own, ops.score_pairs(h, shard, loc, mask_col0=m0), torch.zeros_like(h[:, 0]))
+
+    ts = pairs()
+
+    def topk():
+        return ops.score_topk(h, shard, k, lo, thresholds=ts, mask_col0=m0)
+
+    def merge():
+        return D.merge_topk(cand_v, cand_i, k)
+
+    def step():
+        forward()
+        tl = pairs()
+        _, _, c = ops.score_topk(h, shard, k, lo, thresholds=tl, mask_col0=m0)
+        merge()
+        return c + 1
+
+    wall, dev_ms = timed(step, max(2, min(a.steps, 10)), 2, 1)
+    split = {"forward_ms": kernel_ms(forward), "score_pairs_ms": kernel_ms(pairs),
+             "score_topk_ms": kernel_ms(topk), "merge_topk_ms": kernel_ms(merge)}
+    fl_topk = 2 * d * (hi - lo) * B
+    coll = B * d * 4 + B * 4 + B * 8 + B * k * 16
+    return {"metric": "seqs_scored/s", "value": B / (dev_ms * 1e-3), "unit": "seqs/s",
+            "scaling": f"one rank of the N = {W} C5 point, projected to the whole job",
+            "ms_per_step": dev_ms, "wall_ms_per_step": wall / max(2, min(a.steps, 10)) * 1e3,
+            "config": {"workload": f"c5_rank: rank 0 of N = {W}: forward of {B // W} users (d {d}, n {n}), "
+                                   f"target logits + rank + top-{k} of all {B} users on rows [{lo}, {hi}) "
+                                   f"of the {items + 1}-row catalog, merge of {W} x {k} candidates",
+                       "users_per_step": B, "users_forwarded": B // W, "rows": hi - lo},
+            "projected_value_note": f"value = the {B} users of one N = {W} step / this rank's device time per "
+                                    f"step: the N-GPU throughput when the ~{coll / 1e6:.1f} MB of collectives "
+                                    f"per rank overlap (dist.sharded_rank_topk_batches) or cost nothing",
+            "collective_bytes_per_rank": coll,
+            "split": split,
+            "roofline": roofline("score_topk_kernel<128,10,", fl_topk, split["score_topk_ms"], "c5_rank",
+                                 call_kernels=TOPK_CALL_KERNELS,
+                                 note=f"one gr_score_topk_f32 call of {B} users on the {hi - lo}-row shard"),
+            "call": {"device_ms": dev_ms,
+                     "flop_per_step": sas_exec_flop_per_user(d, n, -1, causal=True, tail_h=True) * (B // W) + fl_topk,
+                     "frac_of_fp32_peak_executed": (sas_exec_flop_per_user(d, n, -1, causal=True, tail_h=True) * (B // W)
+                                                    + fl_topk) / (dev_ms * 1e-3) / 1e12 / FP32_PEAK_TFLOPS}}
+
+
 def _call_pattern(fn, units, reps=200):
     """Per-call cost of a small drop-in call at the reference's own batch size: host time to issue
     one call (no sync), device time of one call (HIP events), and the pipelined wall time per call
@@ -919,7 +1067,7 @@ def bench_calls(rq_model, sas_model, sas_n, sas_items, dev, cpu=True):
     return out
 
 
-LEGS = ["c2", "calls", "sasrec", "c4", "c5", "shard", "train", "train_step", "rq_train_step"]
+LEGS = ["c2", "calls", "sasrec", "c4", "c5", "shard", "c5_rank", "train", "train_step", "rq_train_step"]
 OPT_LEGS = []   # run only when named in --legs
 
 
@@ -1012,11 +1160,15 @@ def main():
         if "c5" in legs:
             line["sasrec_c5"] = c5
             if cpu:   # at N = 1 the rank's shard is the whole table
-                line["sasrec_c5"]["cpu_baseline"] = cpu_sas_baseline(c5_model, 128, 200, a.c5_items, "C5",
-                                                                     table=table5)
+                line["sasrec_c5"]["cpu_baseline"] = cpu_sas_baseline(
+                    c5_model, 128, 200, a.c5_items, "C5", table=table5,
+                    params=synth.sasrec_params(128, 200, 2, 1, 64, dev))
         if "shard" in legs and world == 1:
             line["c5_shard"] = bench_c5_shard(a, table5, h5, t5, dev)
         del c5_model, h5, table5
+        torch.cuda.empty_cache()
+    if "c5_rank" in legs and world == 1:
+        line["c5_rank"] = bench_c5_rank(a, dev)
         torch.cuda.empty_cache()
     if "train_step" in legs:
         line["sasrec_train_step"] = bench_sas_train_step(a, world, rank, dev)
@@ -1038,7 +1190,7 @@ def main():
         if line.get(key) is not None:
             summ[name] = line[key]
     for leg, name in (("sasrec", "c3_seqs_per_s"), ("rq_c4", "c4_items_per_s"), ("sasrec_c5", "c5_seqs_per_s"),
-                      ("c5_shard", "c5_shard_seqs_per_s"), ("sasrec_train_step", "sasrec_train_step_seqs_per_s"),
+                      ("c5_shard", "c5_shard_seqs_per_s"), ("c5_rank", "c5_rank_projected_seqs_per_s"), ("sasrec_train_step", "sasrec_train_step_seqs_per_s"),
                       ("rq_train_step", "rq_train_step_items_per_s"), ("sasrec_train", "sasrec_train_seqs_per_s")):
         if isinstance(line.get(leg), dict) and line[leg].get("value") is not None:
             summ[name] = line[leg]["value"]

@@ -1,17 +1,21 @@
-"""SASRec at BASELINE's full catalog sizes against the CPU oracle (the full-size C3 /
-C5 parity had been HIP-vs-HIP).
+"""SASRec at BASELINE's full catalog sizes against the CPU oracle, over the WHOLE bench batch
+(every one of the bench's 2,048 C3 users and 512 C5 users, not a sample).
 
 A real ``SASRec`` with the bench's weights (``synth.sasrec_model``) scores the bench's sequences on
-the GPU at the bench batch; a sample of users is then recomputed by ``oracle/sasrec_oracle.predict``
-(SASRec/model.py:98-108) on the host and compared:
+the GPU at the bench batch; ``oracle/sasrec_oracle.forward`` (SASRec/model.py:49-96) runs the same
+users on the host and the oracle logits (model.py:98-108) are formed in user chunks, so host memory
+stays bounded at the 1M-row catalog.  Per user:
 
-* logits: ``|gpu - oracle| <= 1e-5 * max|row|`` (north_star's tolerance, row-scaled);
+* logits: ``|gpu - oracle| <= 1e-5 * max|row|`` (north_star's tolerance, row-scaled), every user;
 * ranks (SASRec/evaluate.py:27-32): exact for every user whose oracle target logit has no
   competitor within 2 delta (delta = 1e-5 row scale, the logits bar); every user's GPU rank lies
   in the band the logits bar allows, ``#{l > t + 2 delta} + 1 <= rank <= #{l > t - 2 delta} + 1``;
+* HR@10 and NDCG@10 of the whole batch (evaluate.py:35-47, float64 ``np.mean``) equal the oracle's;
 * top-10 (C5, ``dist.sharded_rank_topk`` and an 8-shard merge on one GPU): values within delta of
   the oracle's value for the same id, ids equal to the oracle's top-10 wherever consecutive oracle
   values are more than 2 delta apart, and always inside ``{j : l_j >= v_10 - 2 delta}``.
+
+Half of the users' targets come from the oracle's top-20 (non-trivial HR@10), half are uniform.
 """
 import numpy as np
 import pytest
@@ -21,122 +25,149 @@ from oracle import sasrec_oracle
 
 pytestmark = pytest.mark.gpu
 TOL = 1e-5
+CHUNK = 64          # users per host-side oracle logits chunk ([64, 1M] fp32 = 256 MB at C5)
 
 
-def _oracle(model, seqs_cpu):
+def _sd(model, table=None):
     sd = {k: v.detach().cpu() for k, v in model.state_dict().items()}
-    return sasrec_oracle.predict(seqs_cpu, sd, model.num_blocks, model.num_heads, model.layernorm_eps)
+    if table is not None:
+        sd["item_emb.weight"] = table.detach().cpu()
+    return sd
 
 
-def _targets(ref, seed):
-    """Half the users' targets from the oracle's top-20 (non-trivial HR), half uniform."""
-    g = np.random.default_rng(seed)
-    lg = ref.clone()
-    lg[:, 0] = -1e9
-    top20 = torch.topk(lg, 20, dim=1).indices.numpy()
-    B, rows = ref.shape
-    return torch.from_numpy(np.where(g.random(B) < 0.5, top20[np.arange(B), g.integers(0, 20, B)],
-                                     g.integers(1, rows, B)).astype(np.int64))
+def _oracle_hidden(model, seqs_cpu, sd):
+    """LN_last(x)[:, -1, :] of the oracle forward (model.py:96, 104)."""
+    return sasrec_oracle.forward(seqs_cpu, sd, model.num_blocks, model.num_heads,
+                                 model.layernorm_eps)[:, -1, :].contiguous()
 
 
-def _rank_bands(ref, targets, delta):
-    lg = ref.double().clone()
-    lg[:, 0] = -1e9
-    t = lg.gather(1, targets[:, None])
-    exact = ((lg > t).sum(1) + 1).numpy()
-    lo = ((lg > t + 2 * delta[:, None]).sum(1) + 1).numpy()
-    hi = ((lg > t - 2 * delta[:, None]).sum(1) + 1).numpy()     # counts the target itself: +1 slack
-    isolated = lo == hi - 1                                      # only the target in the band
-    return exact, lo, hi, isolated
+def _hr_ndcg(ranks, k=10):
+    from gr_amd import evaluate
+    return evaluate.hr_ndcg(ranks, k)
 
 
-def _check_logits(got, ref):
-    scale = ref.abs().amax(1)
-    err = ((got - ref).abs().amax(1) / scale)
-    return float(err.max()), scale * TOL
+class _Batch:
+    """Accumulates per-user comparisons of one whole batch, chunk by chunk."""
 
+    def __init__(self, seed):
+        self.g = np.random.default_rng(seed)
+        self.err = 0.0
+        self.targets, self.exact, self.lo, self.hi, self.iso = [], [], [], [], []
+        self.topk_exact = 0
+        self.topk_checked = 0
 
-def _check_ranks(ranks, ref, targets, delta):
-    exact, lo, hi, iso = _rank_bands(ref, targets, delta)
-    assert ((ranks >= lo) & (ranks <= hi)).all(), (ranks, lo, hi)
-    assert np.array_equal(ranks[iso], exact[iso])
-    return exact, iso
+    def add(self, got, ref):
+        """``got``, ``ref``: [c, rows] fp32 logits of the same users (GPU, oracle).  Returns the
+        chunk's targets and per-user delta."""
+        scale = ref.abs().amax(1)
+        self.err = max(self.err, float(((got - ref).abs().amax(1) / scale).max()))
+        delta = (scale * TOL).double()
+        lg = ref.double()
+        lg[:, 0] = -1e9
+        c, rows = lg.shape
+        top20 = torch.topk(lg, 20, dim=1).indices.numpy()
+        tg = torch.from_numpy(np.where(self.g.random(c) < 0.5, top20[np.arange(c), self.g.integers(0, 20, c)],
+                                       self.g.integers(1, rows, c)).astype(np.int64))
+        t = lg.gather(1, tg[:, None])
+        self.exact.append(((lg > t).sum(1) + 1).numpy())
+        lo = ((lg > t + 2 * delta[:, None]).sum(1) + 1).numpy()
+        hi = ((lg > t - 2 * delta[:, None]).sum(1) + 1).numpy()   # counts the target itself: +1 slack
+        self.lo.append(lo)
+        self.hi.append(hi)
+        self.iso.append(lo == hi - 1)                                 # only the target in the band
+        self.targets.append(tg)
+        return tg, delta, lg
 
+    def topk(self, v, i, lg, delta, k=10):
+        """GPU top-k (values ``v``, ids ``i``, [c, k]) against the chunk's masked oracle logits."""
+        ov, oi = torch.topk(lg, k + 1, dim=1)             # descending; ties only matter where excluded
+        v, i = v.double().cpu(), i.cpu()
+        vb = lg.gather(1, i)                               # oracle value at the GPU's ids
+        assert ((vb - v).abs() <= delta[:, None]).all()
+        assert (vb >= ov[:, k - 1:k] - 2 * delta[:, None]).all()     # inside the top-k band
+        assert (i.sort(1).values[:, 1:] != i.sort(1).values[:, :-1]).all()   # distinct ids
+        gaps = ov[:, :k] - ov[:, 1:k + 1]
+        sep = (gaps > 2 * delta[:, None]).all(1)
+        assert torch.equal(i[sep], oi[sep, :k])
+        self.topk_exact += int(sep.sum())
+        self.topk_checked += len(sep)
 
-def _check_topk(v, i, ref, delta, k=10):
-    lg = ref.double().clone()
-    lg[:, 0] = -1e9
-    ov, oi = torch.sort(lg, dim=1, descending=True, stable=True)
-    ov, oi = ov[:, :k + 1], oi[:, :k + 1]
-    v, i = v.double().cpu(), i.cpu()
-    n_exact = 0
-    for b in range(lg.shape[0]):
-        vb = lg[b, i[b]]                                        # oracle value at the GPU's ids
-        assert (vb - v[b]).abs().max() <= delta[b], b
-        assert (vb >= ov[b, k - 1] - 2 * delta[b]).all(), b      # inside the top-k band
-        gaps = ov[b, :k] - ov[b, 1:k + 1]
-        if (gaps > 2 * delta[b]).all():
-            assert torch.equal(i[b], oi[b, :k]), b
-            n_exact += 1
-    return n_exact
+    def finish(self, ranks, parity_log, **info):
+        exact, lo, hi, iso = (np.concatenate(x) for x in (self.exact, self.lo, self.hi, self.iso))
+        assert ((ranks >= lo) & (ranks <= hi)).all(), np.nonzero((ranks < lo) | (ranks > hi))
+        assert np.array_equal(ranks[iso], exact[iso])
+        hr_o, nd_o = _hr_ndcg(exact)
+        hr_g, nd_g = _hr_ndcg(ranks)
+        rec = dict(users=len(ranks), max_row_scaled_logit_err=self.err,
+                   ranks_exact=int((ranks == exact).sum()), ranks_isolated=int(iso.sum()),
+                   ranks_in_band=int(((ranks >= lo) & (ranks <= hi)).sum()),
+                   hr10_oracle=hr_o, hr10_gpu=hr_g, ndcg10_oracle=nd_o, ndcg10_gpu=nd_g, **info)
+        if self.topk_checked:
+            rec.update(top10_users_checked=self.topk_checked, top10_exact_users=self.topk_exact)
+        parity_log(**rec)
+        assert self.err <= TOL
+        assert hr_g == hr_o and nd_g == nd_o, (hr_g, hr_o, nd_g, nd_o)
 
 
 def test_c3_full_catalog_vs_oracle(dev, parity_log):
-    """C3: 2 blocks, d 64, n 50, 100,001-row table; the bench's 2048-user batch on the GPU, 16 users
-    (first 8, last 8) through the oracle."""
+    """C3: 2 blocks, d 64, n 50, 100,001-row table; the bench's 2048-user batch, EVERY user through
+    the oracle: contiguous predict logits, the rank over materialised logits and the fused rank."""
     from gr_amd import evaluate, ops, synth
     items, n, B = 100_000, 50, 2048
     model = synth.sasrec_model(items, synth.sasrec_params(64, n, 2, 1, 64, dev), dev)
     seqs = synth.sequences(B, n, items, 2000, dev)
-    pick = torch.cat([torch.arange(0, 8), torch.arange(B - 8, B)])
     logits = model.predict(seqs)
-    got = logits[pick.to(dev)].cpu()
-    ref = _oracle(model, seqs[pick.to(dev)].cpu())
-    err, delta = _check_logits(got, ref)
-    targets = _targets(ref, 3)
-    tg_all = torch.randint(1, items + 1, (B,), device=dev)
-    tg_all[pick.to(dev)] = targets.to(dev)
-    r_mat = ops.rank(logits, tg_all)[pick.to(dev)].cpu().numpy()
-    r_fused = evaluate.rank_batch(model, seqs, tg_all)[pick.to(dev)].cpu().numpy()
-    exact, iso = _check_ranks(r_mat, ref, targets, delta)
+    sd = _sd(model)
+    h_ref = _oracle_hidden(model, seqs.cpu(), sd)
+    table = sd["item_emb.weight"]
+    acc = _Batch(3)
+    for c0 in range(0, B, CHUNK):
+        ref = h_ref[c0:c0 + CHUNK].matmul(table.t())             # model.py:107
+        acc.add(logits[c0:c0 + CHUNK].cpu(), ref)
+    tg = torch.cat(acc.targets).to(dev)
+    r_mat = ops.rank(logits, tg).cpu().numpy()
+    r_fused = evaluate.rank_batch(model, seqs, tg).cpu().numpy()
     assert np.array_equal(r_fused, r_mat)
-    parity_log(kind="sasrec_full_size", config="C3 (100,001 rows, d 64, n 50)", users=len(pick),
-               max_row_scaled_logit_err=err, ranks_exact=int((r_mat == exact).sum()),
-               ranks_isolated=int(iso.sum()), hr10_oracle=float((exact <= 10).mean()),
-               hr10_gpu=float((r_mat <= 10).mean()))
-    assert err <= TOL
+    acc.finish(r_mat, parity_log, kind="sasrec_full_size", config="C3 (100,001 rows, d 64, n 50), whole batch")
 
 
 def test_c5_full_catalog_vs_oracle(dev, parity_log):
-    """C5: d 128, n 200, 1,000,001-row table; the bench's 512 users through the GPU transformer,
-    8 users (first 4, last 4) through the oracle; predict logits, the single-shard and the 8-shard
-    catalog-sharded rank + top-10."""
+    """C5: d 128, n 200, 1,000,001-row table; the bench's 512 users, EVERY user through the oracle;
+    predict logits, the single-shard and the 8-shard catalog-sharded rank + top-10."""
     from gr_amd import dist as D, ops, synth
     items, n, B, k = 1_000_000, 200, 512, 10
     model = synth.sasrec_model(items, synth.sasrec_params(128, n, 2, 1, 64, dev), dev, seed=5)
     seqs = synth.sequences(B, n, items, 5000, dev)
-    pick = torch.cat([torch.arange(0, 4), torch.arange(B - 4, B)]).to(dev)
-    h_all = model.last_hidden(seqs)
-    h = h_all[pick]
-    got = model.predict(seqs[pick]).cpu()
-    ref = _oracle(model, seqs[pick].cpu())
-    err, delta = _check_logits(got, ref)
-    assert torch.equal(ops.score(h, model.item_emb.weight.detach()), model.predict(seqs[pick]))
-    targets = _targets(ref, 7)
+    h = model.last_hidden(seqs)
+    sd = _sd(model)
+    h_ref = _oracle_hidden(model, seqs.cpu(), sd)
     table = model.item_emb.weight.detach()
-    rank1, v1, i1 = D.sharded_rank_topk(h, table, 0, targets.to(dev), k=k)
-    exact, iso = _check_ranks(rank1.cpu().numpy(), ref, targets, delta)
-    n_exact1 = _check_topk(v1, i1, ref, delta, k)
+    table_cpu = sd["item_emb.weight"]
+    acc = _Batch(7)
+    chunks = []
+    for c0 in range(0, B, CHUNK):
+        got = model.predict(seqs[c0:c0 + CHUNK])
+        if c0 == 0:   # predict = the scoring kernel on the forward's hidden states, bit for bit
+            assert torch.equal(ops.score(h[:CHUNK], table), got)
+        ref = h_ref[c0:c0 + CHUNK].matmul(table_cpu.t())           # model.py:107
+        tg, delta, lg = acc.add(got.cpu(), ref)
+        del got, ref
+        _, v1, i1 = D.sharded_rank_topk(h[c0:c0 + CHUNK], table, 0, tg.to(dev), k=k)
+        acc.topk(v1, i1, lg, delta, k)
+        chunks.append((v1, i1))
+        del lg
+    targets = torch.cat(acc.targets).to(dev)
+    rank1, v1, i1 = D.sharded_rank_topk(h, table, 0, targets, k=k)
+    assert torch.equal(v1, torch.cat([c[0] for c in chunks])) and torch.equal(i1, torch.cat([c[1] for c in chunks]))
     # 8 catalog shards on one GPU: the per-rank kernels of the 8-GPU run, merged as dist._exchange
     rows = items + 1
-    tg = targets.to(dev)
-    ts = torch.zeros(len(pick), device=dev)
+    ts = torch.zeros(B, device=dev)
     shards = [D.shard_range(rows, r, 8) for r in range(8)]
     for lo, hi in shards:
-        own = (tg >= lo) & (tg < hi)
-        loc = torch.where(own, tg - lo, torch.zeros_like(tg))
+        own = (targets >= lo) & (targets < hi)
+        loc = torch.where(own, targets - lo, torch.zeros_like(targets))
         ts += torch.where(own, ops.score_pairs(h, table[lo:hi], loc, mask_col0=(lo == 0)), torch.zeros_like(ts))
-    cnt = torch.zeros(len(pick), dtype=torch.int64, device=dev)
+    cnt = torch.zeros(B, dtype=torch.int64, device=dev)
     vs, is_ = [], []
     for lo, hi in shards:
         v, i, c = ops.score_topk(h, table[lo:hi], k, lo, thresholds=ts, mask_col0=(lo == 0))
@@ -145,11 +176,8 @@ def test_c5_full_catalog_vs_oracle(dev, parity_log):
         is_.append(i)
     v8, i8 = D.merge_topk(torch.cat(vs, 1), torch.cat(is_, 1), k)
     assert torch.equal(cnt + 1, rank1) and torch.equal(v8, v1) and torch.equal(i8, i1)
-    parity_log(kind="sasrec_full_size", config="C5 (1,000,001 rows, d 128, n 200)", users=len(pick),
-               max_row_scaled_logit_err=err, ranks_exact=int((rank1.cpu().numpy() == exact).sum()),
-               ranks_isolated=int(iso.sum()), top10_exact_users=n_exact1,
-               hr10_oracle=float((exact <= 10).mean()))
-    assert err <= TOL
+    acc.finish(rank1.cpu().numpy(), parity_log, kind="sasrec_full_size",
+               config="C5 (1,000,001 rows, d 128, n 200), whole batch")
 
 
 def test_c5_per_rank_construction_matches_full_table(dev):
