@@ -24,9 +24,9 @@
 #include "gr_common.h"
 
 #ifndef GR_ADIAG
-#define GR_ADIAG 0   // diagnostic builds only (scripts/build_variant.sh), attn_wave_kernel and
-                     // attn_persist_kernel: 1 no K/V loads inside an item's key loop, 2 also no
-                     // softmax (MFMA chains only) -- wrong results
+#define GR_ADIAG 0   // diagnostic builds only (scripts/build_variant.sh), attn_persist_kernel: 1 no
+                     // K/V loads inside an item's key loop, 2 also no softmax (MFMA chains only) --
+                     // wrong results
 #endif
 
 namespace gr {
@@ -40,15 +40,18 @@ struct AttnTile {                  // one 32-query tile owned by a wave
   float m, l;                      // running max / sum of this lane's query
 };
 
-// Two workgroups per CU: at hd = 128 that caps the kernel at 256 VGPRs (a few spill), and still
-// measured 85 vs 114 us per C5 call (steady state) — the second workgroup's MFMAs fill the gaps
-// of the first's barriers and softmax.
 constexpr float AT_LAZY = 8.f;   // lazy-rescale threshold (natural-log units)
 
-template <int HD, int OCC, bool LAZY>
-__global__ __launch_bounds__(256, OCC) void attn_mfma_kernel(const float* __restrict__ qkv,
-                                                             float* __restrict__ out, int n, int H,
-                                                             float scale, int qt_lo, int alt) {
+// Two workgroups per CU: at hd = 128 that caps the kernel at 256 VGPRs (a few spill), and still
+// measured 85 vs 114 us per C5 call against one (steady state) — the second workgroup's MFMAs
+// fill the gaps of the first's barriers and softmax.  Used for hd = 32 (and for the persistent
+// kernel's head widths only if its grid would not fit).
+template <int HD>
+__global__ __launch_bounds__(256, 2) void attn_mfma_kernel(const float* __restrict__ qkv,
+                                                           float* __restrict__ out, int n, int H,
+                                                           float scale, int qt_lo) {
+  constexpr bool LAZY = true;
+  constexpr int alt = 1;
   constexpr int FT = HD / 32;
   constexpr int KP = HD + 4;   // K row pitch: conflict-free ds_read_b128 of 16 rows
   constexpr int VP = HD + 8;   // V row pitch: the two lane halves (4 rows apart) on disjoint banks
@@ -235,316 +238,19 @@ __global__ __launch_bounds__(256, OCC) void attn_mfma_kernel(const float* __rest
   }
 }
 
-// Full-sequence variant (every query tile; the first blocks of a forward): one workgroup per
-// (sequence, head) with ONE wave per SIMD (512-register budget, no spills), each wave owning a
-// PAIR of query tiles (T-1-p, p) so that every wave walks the same number of (query tile, key
-// tile) steps: at n = 200 (T = 7) the waves do 8, 8, 8 and 4 steps against 7, 6, 5, 4 then 3, 2,
-// 1 in two rounds of single tiles.  A key tile's K fragments (ds_read_b128) and V values
-// (ds_read_b32) each feed both tiles' MFMAs.  Per row the instruction sequence is the same as in
-// attn_mfma_kernel (same chains, same online-softmax order).
-template <int HD>
-__global__ __launch_bounds__(256, 1) void attn_pair_kernel(const float* __restrict__ qkv,
-                                                           float* __restrict__ out, int n, int H,
-                                                           float scale) {
-  constexpr int FT = HD / 32;
-  constexpr int KP = HD + 4;
-  constexpr int VP = HD + 8;
-  constexpr int LV = AT_KT * HD / 4 / 256;
-  __shared__ __attribute__((aligned(16))) float ks[2][AT_KT * KP];
-  __shared__ __attribute__((aligned(16))) float vs[2][AT_KT * VP];
-  const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, h = lane >> 5;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int bh = blockIdx.x, b = bh / H, hh = bh % H;
-  const int d = H * HD;
-  const int64_t rs = 3LL * d;
-  const float* base = qkv + (int64_t)b * n * rs + hh * HD;
-  const float* Qb = base;
-  const float* Kb = base + d;
-  const float* Vb = base + 2 * d;
-  const int T = (n + 31) / 32;
-  const int NP = (T + 1) / 2;   // pairs (T-1-p, p); the middle tile of an odd T pairs with none
-
-  for (int p0 = 0; p0 < NP; p0 += 4) {
-    const int pr = p0 + w;
-    // tiles of this wave: qa >= qb (qb = -1: none); waves past the last pair idle this round
-    const int qa = pr < NP ? T - 1 - pr : -1;
-    const int qb = (pr < NP && pr < T - 1 - pr) ? pr : -1;
-    const int myq[2] = {qa, qb};
-    AttnTile<HD> at[2];
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int qt = myq[u] < 0 ? 0 : myq[u];
-      const int qi = qt * 32 + r;
-      const int qc = qi < n ? qi : n - 1;
-#pragma unroll
-      for (int it = 0; it < FT; ++it)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const f32x4 v = *reinterpret_cast<const f32x4*>(Qb + (int64_t)qc * rs + 32 * it + 8 * g + 4 * h);
-          at[u].qf[it][g] = v * scale;   // q * sqrt(1/hd) (functional.py:6578)
-        }
-#pragma unroll
-      for (int ft = 0; ft < FT; ++ft)
-#pragma unroll
-        for (int v = 0; v < 16; ++v) at[u].O[ft][v] = 0.f;
-      at[u].m = -INFINITY;
-      at[u].l = 0.f;
-    }
-    const int kmax = T - 1 - p0;   // the largest query tile of the round = the last key tile
-    f32x4 pk[LV], pv[LV];
-    auto gload = [&](int kt) {
-#pragma unroll
-      for (int i = 0; i < LV; ++i) {
-        const int f = tid + 256 * i, row = f / (HD / 4), col = (f % (HD / 4)) * 4;
-        int key = kt * AT_KT + row;
-        key = key < n ? key : n - 1;
-        pk[i] = *reinterpret_cast<const f32x4*>(Kb + (int64_t)key * rs + col);
-        pv[i] = *reinterpret_cast<const f32x4*>(Vb + (int64_t)key * rs + col);
-      }
-    };
-    auto swrite = [&](int bf) {
-#pragma unroll
-      for (int i = 0; i < LV; ++i) {
-        const int f = tid + 256 * i, row = f / (HD / 4), col = (f % (HD / 4)) * 4;
-        *reinterpret_cast<f32x4*>(&ks[bf][row * KP + col]) = pk[i];
-        *reinterpret_cast<f32x4*>(&vs[bf][row * VP + col]) = pv[i];
-      }
-    };
-    auto tile_step = [&](auto nu_tag, int kt, int bf) {
-      constexpr int NU = decltype(nu_tag)::value;
-      f32x16 S[NU];
-#pragma unroll
-      for (int u = 0; u < NU; ++u)
-#pragma unroll
-        for (int v = 0; v < 16; ++v) S[u][v] = 0.f;
-      const float* kr = &ks[bf][r * KP + 4 * h];
-#pragma unroll
-      for (int it = 0; it < FT; ++it)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const f32x4 kv = *reinterpret_cast<const f32x4*>(kr + 32 * it + 8 * g);
-#pragma unroll
-          for (int s4 = 0; s4 < 4; ++s4)
-#pragma unroll
-            for (int u = 0; u < NU; ++u) S[u] = mfma32(kv[s4], at[u].qf[it][g][s4], S[u]);
-        }
-#pragma unroll
-      for (int u = 0; u < NU; ++u) {
-        AttnTile<HD>& A = at[u];
-        const int qi = myq[u] * 32 + r;
-        float tmax = -INFINITY;
-#pragma unroll
-        for (int v = 0; v < 16; ++v) {
-          const int key = kt * 32 + (v & 3) + 8 * (v >> 2) + 4 * h;
-          if (key > qi || key >= n) S[u][v] = -INFINITY;
-          tmax = fmaxf(tmax, S[u][v]);
-        }
-        tmax = fmaxf(tmax, __shfl_xor(tmax, 32));
-        const float mn = fmaxf(A.m, tmax);
-        const float alpha = __expf(A.m - mn);
-        float ts = 0.f;
-#pragma unroll
-        for (int v = 0; v < 16; ++v) {
-          const float e = __expf(S[u][v] - mn);
-          S[u][v] = e;
-          ts += e;
-        }
-        ts += __shfl_xor(ts, 32);
-        A.l = A.l * alpha + ts;
-        A.m = mn;
-#pragma unroll
-        for (int ft = 0; ft < FT; ++ft) A.O[ft] *= alpha;
-      }
-#pragma unroll
-      for (int ft = 0; ft < FT; ++ft)
-#pragma unroll
-        for (int s = 0; s < 16; ++s) {
-          const int key = (s & 3) + 8 * (s >> 2) + 4 * h;
-          const float vv = kt * 32 + key < n ? vs[bf][key * VP + 32 * ft + r] : 0.f;
-#pragma unroll
-          for (int u = 0; u < NU; ++u) at[u].O[ft] = mfma32(vv, S[u][s], at[u].O[ft]);
-        }
-    };
-    gload(0);
-    swrite(0);
-    __syncthreads();
-    for (int kt = 0; kt <= kmax; ++kt) {
-      const int bf = kt & 1;
-      if (kt + 1 <= kmax) gload(kt + 1);
-      if (qb >= kt) tile_step(std::integral_constant<int, 2>{}, kt, bf);        // wave-uniform
-      else if (qa >= kt) tile_step(std::integral_constant<int, 1>{}, kt, bf);
-      if (kt + 1 <= kmax) swrite(bf ^ 1);
-      __syncthreads();
-    }
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      if (myq[u] < 0) continue;
-      const int qi = myq[u] * 32 + r;
-      if (qi >= n) continue;
-      const float inv = 1.0f / at[u].l;
-      float* orow = out + ((int64_t)b * n + qi) * d + hh * HD;
-#pragma unroll
-      for (int ft = 0; ft < FT; ++ft)
-#pragma unroll
-        for (int g = 0; g < 4; ++g)
-          *reinterpret_cast<f32x4*>(orow + 32 * ft + 8 * g + 4 * h) =
-              f32x4{at[u].O[ft][4 * g], at[u].O[ft][4 * g + 1], at[u].O[ft][4 * g + 2], at[u].O[ft][4 * g + 3]} * inv;
-    }
-    __syncthreads();   // the next round restages K / V
-  }
-}
-
-// One wave per (sequence, head, query tile), no lockstep (option attn_wave, the default): the
-// workgroup kernel above walks its 4 waves' key tiles together over shared K/V tiles, so at n = 200
-// (T = 7 query tiles) a workgroup runs 7 + 3 key-tile iterations for 28 (query, key) tile steps
-// and a SIMD idles ~30 % of them.  Here each wave walks exactly its own
-// qt + 1 key tiles, reading K and V straight from global (L2) into registers as the MFMA operands
-// -- K fragments kf[it][g] = K[key 32 kt + r][32 it + 8 g + 4 h .. +3] (the A operand), V values
-// vf[ft][s] = V[key 32 kt + (s&3) + 8 (s>>2) + 4 h][32 ft + r] -- with the next tile's K issued
-// right after this tile's S = K Q^T MFMAs and its V after the O += V P^T MFMAs (each hidden
-// behind the other half of the step).  One wave per SIMD (~300 VGPRs of operands and
-// accumulators); the hardware deals the waves out longest query tiles first, and every query tile
-// of one (sequence, head) goes to the same XCD (its K / V in that XCD's L2 / the Infinity Cache).  Per row the
-// instruction sequence is attn_mfma_kernel<HD, *, true>'s (same S chain over (it, g, s4), the same
-// lazy softmax, the same O chain over (ft, s)): bitwise the same output.
-template <int HD>
-__global__ __launch_bounds__(64) void attn_wave_kernel(const float* __restrict__ qkv, float* __restrict__ out,
-                                                      int n, int H, float scale, int nbh, int qt_lo) {
-  constexpr int FT = HD / 32;
-  const int lane = threadIdx.x, r = lane & 31, h = lane >> 5;
-  const int T = (n + 31) / 32, nt = T - qt_lo;
-  // work item of this wave: XCD x = blockIdx % 8 owns the (sequence, head) pairs bh = x (mod 8);
-  // within it, pair-major with the query tiles in descending order
-  const int x = blockIdx.x & 7, k = blockIdx.x >> 3;
-  const int mx = (nbh - x + 7) / 8;   // pairs on this XCD
-  if (k >= mx * nt) return;
-  // longest first: every pair's last query tile, then every pair's second-to-last, ...  (a greedy
-  // dispatcher then finishes in ~ the average per-SIMD work; pair-major order measured 18 tile steps
-  // per SIMD against the average 14 at C5)
-  const int bh = x + 8 * (k % mx), qt = T - 1 - k / mx;
-  const int b = bh / H, hh = bh % H;
-  const int d = H * HD;
-  const int64_t rs = 3LL * d;
-  const float* base = qkv + (int64_t)b * n * rs + hh * HD;
-  const float* Qb = base;
-  const float* Kb = base + d;
-  const float* Vb = base + 2 * d;
-  const int qi = qt * 32 + r;
-  const int qc = qi < n ? qi : n - 1;
-  f32x4 qf[FT][4];
-#pragma unroll
-  for (int it = 0; it < FT; ++it)
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const f32x4 v = *reinterpret_cast<const f32x4*>(Qb + (int64_t)qc * rs + 32 * it + 8 * g + 4 * h);
-      qf[it][g] = v * scale;   // q * sqrt(1/hd) (functional.py:6578)
-    }
-  f32x16 O[FT];
-#pragma unroll
-  for (int ft = 0; ft < FT; ++ft)
-#pragma unroll
-    for (int v = 0; v < 16; ++v) O[ft][v] = 0.f;
-  float m = -INFINITY, l = 0.f;
-  f32x4 kf[FT][4];
-  float vf[FT][16];
-  auto load_k = [&](int kt) {
-    int key = kt * 32 + r;
-    key = key < n ? key : n - 1;
-    const float* kr = Kb + (int64_t)key * rs + 4 * h;
-#pragma unroll
-    for (int it = 0; it < FT; ++it)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) kf[it][g] = *reinterpret_cast<const f32x4*>(kr + 32 * it + 8 * g);
-  };
-  auto load_v = [&](int kt) {
-#pragma unroll
-    for (int s = 0; s < 16; ++s) {
-      int key = kt * 32 + (s & 3) + 8 * (s >> 2) + 4 * h;
-      key = key < n ? key : n - 1;   // keys past n: P = 0 against a clamped (finite) row
-      const float* vr = Vb + (int64_t)key * rs + r;
-#pragma unroll
-      for (int ft = 0; ft < FT; ++ft) vf[ft][s] = vr[32 * ft];
-    }
-  };
-  auto s_chain = [&]() {
-    f32x16 S;
-#pragma unroll
-    for (int v = 0; v < 16; ++v) S[v] = 0.f;
-#pragma unroll
-    for (int it = 0; it < FT; ++it)
-#pragma unroll
-      for (int g = 0; g < 4; ++g)
-#pragma unroll
-        for (int s4 = 0; s4 < 4; ++s4) S = mfma32(kf[it][g][s4], qf[it][g][s4], S);
-    return S;
-  };
-  // softmax of key tile kt (S -> P in place) and O += V^T P^T
-  auto softmax_pv = [&](f32x16& S, int kt) {
-    if (GR_ADIAG != 2) {
-      // causal / padding mask on the diagonal tile and the last key tile (attn_mfma_kernel, LAZY)
-      float tmax = -INFINITY;
-      if (kt == qt || kt * 32 + 32 > n) {
-#pragma unroll
-        for (int v = 0; v < 16; ++v) {
-          const int key = kt * 32 + (v & 3) + 8 * (v >> 2) + 4 * h;
-          if (key > qi || key >= n) S[v] = -INFINITY;
-          tmax = fmaxf(tmax, S[v]);
-        }
-      } else {
-#pragma unroll
-        for (int v = 0; v < 16; ++v) tmax = fmaxf(tmax, S[v]);
-      }
-      tmax = fmaxf(tmax, __shfl_xor(tmax, 32));
-      const bool up = tmax > m + AT_LAZY;   // lazy rescaling (attn_mfma_kernel)
-      if (__any(up)) {
-        const float mn = up ? tmax : m;
-        const float alpha = __expf(m - mn);
-        l *= alpha;
-        m = mn;
-#pragma unroll
-        for (int ft = 0; ft < FT; ++ft) O[ft] *= alpha;
-      }
-      float ts = 0.f;
-#pragma unroll
-      for (int v = 0; v < 16; ++v) {
-        const float e = __expf(S[v] - m);
-        S[v] = e;
-        ts += e;
-      }
-      ts += __shfl_xor(ts, 32);
-      l += ts;
-    }
-#pragma unroll
-    for (int ft = 0; ft < FT; ++ft)
-#pragma unroll
-      for (int s = 0; s < 16; ++s) O[ft] = mfma32(vf[ft][s], S[s], O[ft]);
-  };
-  load_k(0);
-  load_v(0);
-  for (int kt = 0; kt <= qt; ++kt) {
-    f32x16 S = s_chain();
-    if (GR_ADIAG == 0 && kt < qt) load_k(kt + 1);   // the K operands are read at issue: their registers refill now
-    softmax_pv(S, kt);
-    if (GR_ADIAG == 0 && kt < qt) load_v(kt + 1);
-  }
-  if (qi < n) {
-    const float inv = 1.0f / l;
-    float* orow = out + ((int64_t)b * n + qi) * d + hh * HD;
-#pragma unroll
-    for (int ft = 0; ft < FT; ++ft)
-#pragma unroll
-      for (int g = 0; g < 4; ++g)
-        *reinterpret_cast<f32x4*>(orow + 32 * ft + 8 * g + 4 * h) =
-            f32x4{O[ft][4 * g], O[ft][4 * g + 1], O[ft][4 * g + 2], O[ft][4 * g + 3]} * inv;
-  }
-}
-
-// attn_wave=6: attn_wave_kernel as a PERSISTENT grid -- one wave per SIMD, each walking a static
-// list of (sequence, head, query tile) items: the items of an XCD in the longest-first order, dealt
-// to its waves in alternating (snake) rounds, so every wave gets ~ the average work (C5: 7+4+3 or
-// 6+5+2+1 = 14 tile steps each).  The next item's Q and first K / V tiles are loaded during the
-// current item's last tile step, so a wave never starts cold.  Per row the instruction sequence
-// of attn_wave_kernel: bitwise the same output.
+// hd 64 / 128 (C5): a PERSISTENT grid -- one wave per SIMD, each walking a static list of
+// (sequence, head, 32-query tile) items, with no LDS and no barriers: a wave walks exactly its own
+// item's qt + 1 key tiles, K fragments and V values straight from L2 into registers one tile ahead.
+// The items of an XCD (bh = x mod 8: every query tile of one (sequence, head) on the same XCD,
+// its K / V in that XCD's L2 / the Infinity Cache) in the longest-first order -- every pair's last
+// query tile, then every pair's second-to-last, ... -- dealt to its waves in alternating (snake)
+// rounds, so every wave gets ~ the average work (C5: 7+4+3 or 6+5+2+1 = 14 tile steps each).  The
+// next item's Q and first K / V tiles are loaded during the current item's last tile step, so a
+// wave never starts cold.  Per row the instruction sequence of attn_mfma_kernel (same S chain over
+// (it, g, s4), the same lazy softmax, the same O chain over (ft, s)): bitwise the same output.
+// (Measured and removed in round 5: the 4-wave workgroup kernel for hd 64 / 128, 107 vs 97 us at C5;
+// one wave per item without the persistent lists, 111 us; one workgroup per (sequence, head) with
+// each wave owning a pair of query tiles, 902 vs 693 us per forward: it spilled.)
 template <int HD>
 __global__ __launch_bounds__(64) void attn_persist_kernel(const float* __restrict__ qkv, float* __restrict__ out,
                                                          int n, int H, float scale, int nbh, int qt_lo, int wx) {
@@ -707,65 +413,27 @@ int gr_attn_mfma_launch(const float* qkv, float* out, int64_t B, int n, int H, i
   if (!aligned16(qkv) || !aligned16(out)) return GR_ERR_UNSUPPORTED;
   if (B * H > 0x7fffffffLL) return GR_ERR_UNSUPPORTED;
   const int qt_lo = last_tile_only ? (n - 1) / 32 : 0;
-  const dim3 g((unsigned)(B * H)), blk(256);
-  // attn_wave: 6 (default) the persistent grid, 1 one wave per item, 3 the per-wave kernel only when
-  // B H < 512 (the rule before the longest-first order), 0 the workgroup kernel
-  // (profiles/r04/ab_attn_*.txt)
-  const int64_t aw = option("attn_wave");
-  const bool wave = aw == 3 ? B * H < 512 : aw != 0;
-  if ((hd == 64 || hd == 128) && wave && option("attn_lazy") != 0) {
-    const int64_t nbh = B * H, nt = (n + 31) / 32 - qt_lo;
-    const int64_t waves = 8 * ((nbh + 7) / 8) * nt;
-    if (waves <= 0x7fffffffLL) {
-      const dim3 gw((unsigned)waves), bw(64);
-      if (aw == 6) {
-        static int simds = 0;
-        if (!simds) {
-          int dev = 0, cus = 0;
-          (void)hipGetDevice(&dev);
-          (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-          simds = 4 * (cus > 0 ? cus : 256);
-        }
-        const int wx = (simds + 7) / 8;
-        if (hd == 128)
-          hipLaunchKernelGGL(attn_persist_kernel<128>, dim3(8 * wx), bw, 0, st, qkv, out, n, H, scale, (int)nbh, qt_lo, wx);
-        else
-          hipLaunchKernelGGL(attn_persist_kernel<64>, dim3(8 * wx), bw, 0, st, qkv, out, n, H, scale, (int)nbh, qt_lo, wx);
-        return check_launch("sasrec attention (persistent waves)");
-      }
-      if (hd == 128)
-        hipLaunchKernelGGL(attn_wave_kernel<128>, gw, bw, 0, st, qkv, out, n, H, scale, (int)nbh, qt_lo);
-      else
-        hipLaunchKernelGGL(attn_wave_kernel<64>, gw, bw, 0, st, qkv, out, n, H, scale, (int)nbh, qt_lo);
-      return check_launch("sasrec attention (one wave per query tile)");
+  const int64_t nbh = B * H;
+  if (hd != 32 && nbh * ((n + 31) / 32) <= 0x7fffffffLL) {   // the persistent grid
+    static int simds = 0;
+    if (!simds) {
+      int dev = 0, cus = 0;
+      (void)hipGetDevice(&dev);
+      (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+      simds = 4 * (cus > 0 ? cus : 256);
     }
+    const int wx = (simds + 7) / 8;
+    if (hd == 128)
+      hipLaunchKernelGGL(attn_persist_kernel<128>, dim3(8 * wx), dim3(64), 0, st, qkv, out, n, H, scale, (int)nbh, qt_lo, wx);
+    else
+      hipLaunchKernelGGL(attn_persist_kernel<64>, dim3(8 * wx), dim3(64), 0, st, qkv, out, n, H, scale, (int)nbh, qt_lo, wx);
+    return check_launch("sasrec attention (persistent waves)");
   }
-  if (!last_tile_only && option("attn_pair") != 0) {
-    switch (hd) {
-      case 32: hipLaunchKernelGGL(attn_pair_kernel<32>, g, blk, 0, st, qkv, out, n, H, scale); break;
-      case 64: hipLaunchKernelGGL(attn_pair_kernel<64>, g, blk, 0, st, qkv, out, n, H, scale); break;
-      default: hipLaunchKernelGGL(attn_pair_kernel<128>, g, blk, 0, st, qkv, out, n, H, scale); break;
-    }
-    return check_launch("sasrec attention (mfma, paired tiles)");
-  }
-  // attn_occ1 (hd 128): one workgroup per CU at 512 registers (no spills) instead of two at 256
-  const bool occ1 = option("attn_occ1") != 0;
-  const int alt = option("attn_alt") != 0 ? 1 : 0;
-  const bool lazy = option("attn_lazy") != 0;   // lazy softmax rescaling, diagonal-only masks
+  const dim3 g((unsigned)nbh), blk(256);
   switch (hd) {
-    case 32:
-      if (lazy) hipLaunchKernelGGL((attn_mfma_kernel<32, 2, true>), g, blk, 0, st, qkv, out, n, H, scale, qt_lo, alt);
-      else hipLaunchKernelGGL((attn_mfma_kernel<32, 2, false>), g, blk, 0, st, qkv, out, n, H, scale, qt_lo, alt);
-      break;
-    case 64:
-      if (lazy) hipLaunchKernelGGL((attn_mfma_kernel<64, 2, true>), g, blk, 0, st, qkv, out, n, H, scale, qt_lo, alt);
-      else hipLaunchKernelGGL((attn_mfma_kernel<64, 2, false>), g, blk, 0, st, qkv, out, n, H, scale, qt_lo, alt);
-      break;
-    default:
-      if (occ1) hipLaunchKernelGGL((attn_mfma_kernel<128, 1, false>), g, blk, 0, st, qkv, out, n, H, scale, qt_lo, alt);
-      else if (lazy) hipLaunchKernelGGL((attn_mfma_kernel<128, 2, true>), g, blk, 0, st, qkv, out, n, H, scale, qt_lo, alt);
-      else hipLaunchKernelGGL((attn_mfma_kernel<128, 2, false>), g, blk, 0, st, qkv, out, n, H, scale, qt_lo, alt);
-      break;
+    case 32: hipLaunchKernelGGL(attn_mfma_kernel<32>, g, blk, 0, st, qkv, out, n, H, scale, qt_lo); break;
+    case 64: hipLaunchKernelGGL(attn_mfma_kernel<64>, g, blk, 0, st, qkv, out, n, H, scale, qt_lo); break;
+    default: hipLaunchKernelGGL(attn_mfma_kernel<128>, g, blk, 0, st, qkv, out, n, H, scale, qt_lo); break;
   }
   return check_launch("sasrec attention (mfma)");
 }

@@ -219,6 +219,13 @@ __device__ __forceinline__ float mkl_dot(MklPlan p, XA xa, WA wa, int K, float b
 // k-block width of a long call (>= 256 rows) for inner size K: mkl_plan's MKL_CHAIN width.
 __host__ __device__ inline int mkl_kblock(int K) { return mkl_plan(1 << 20, K, 256).kb; }
 
+// The scoring chain's feature order (score.hip, rank_fused.hip, score_topk.hip): a d-vector is read
+// as d / 8 float4 groups per lane, lane half hh of group gq holding features 8 gq + 4 hh .. +3, and
+// step (gq, s) of the v_mfma_f32_32x32x2_f32 chain adds feature 8 gq + s (lane half 0) then
+// 8 gq + 4 + s (lane half 1).  For d >= 32 this is the "32 g + 8 q + 4 hh" order of rounds 1-4
+// (gq = 4 g + q); d = 16 is the same chain over two groups.
+__device__ __forceinline__ int sc_feat(int gq, int hh) { return 8 * gq + 4 * hh; }
+
 // f32-input MFMA 16x16x4: an fma chain over its four k slots in ascending order (lane group
 // l >> 4 = k; profiles/r03_mfma_order.txt).  Lane l supplies A[i = l&15][k = l>>4] and
 // B[k = l>>4][j = l&15]; D register v of lane l holds row 4 (l>>4) + v, column l&15.
@@ -241,8 +248,6 @@ int gr_attn_mfma_launch(const float* qkv, float* out, int64_t B, int n, int H, i
                         int last_tile_only, hipStream_t st);
 int gr_score_launch(const float* h, int64_t B, int32_t d, const float* table, int64_t rows,
                     float* logits, int64_t ld, hipStream_t st);
-int gr_sasrec_tail_launch(const gr_sasrec_params* p, int blk, const float* X, const float* KV,
-                          int64_t B, int32_t n, float* out, hipStream_t st);
 int gr_post_attn_launch(const gr_sasrec_params* p, int blk, const float* ln_next_w, const float* ln_next_b,
                         const float* wn, const float* bn, int nout, const float* O, float* X, float* H,
                         int64_t M, hipStream_t st);

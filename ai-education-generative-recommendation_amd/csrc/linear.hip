@@ -370,15 +370,10 @@ int gr_linear_launch(const float* x, int64_t m, int32_t k, const float* w, int32
     hipLaunchKernelGGL(kern, dim3((unsigned)(groups * per)), dim3(WR_NT), 0, stream, x, w, bias, y, m, n, ldy, groups);
     return check_launch("gr_linear_f32 (resident w)");
   }
-  // 8 waves per 128-row tile (4 per SIMD at two workgroups per CU; option lin_w8, the default):
-  // C5 block-0 in-projection 137 -> 124 us, bitwise the same chain
-  const bool w8 = option("lin_w8") != 0;
-  if (n >= 128)
-    return w8 ? launch_tile<128, 128, 2, 4, 512>(x, m, k, w, n, bias, residual, ldr, act, y, ldy, stream)
-              : launch_tile<128, 128, 2, 2>(x, m, k, w, n, bias, residual, ldr, act, y, ldy, stream);
-  if (n > 32)
-    return w8 ? launch_tile<128, 64, 4, 2, 512>(x, m, k, w, n, bias, residual, ldr, act, y, ldy, stream)
-              : launch_tile<128, 64, 2, 2>(x, m, k, w, n, bias, residual, ldr, act, y, ldy, stream);
+  // 8 waves per 128-row tile (4 per SIMD at two workgroups per CU): C5 block-0 in-projection
+  // 137 -> 124 us against 4 waves, bitwise the same chain (profiles/r02_ab_lin_w8.txt)
+  if (n >= 128) return launch_tile<128, 128, 2, 4, 512>(x, m, k, w, n, bias, residual, ldr, act, y, ldy, stream);
+  if (n > 32) return launch_tile<128, 64, 4, 2, 512>(x, m, k, w, n, bias, residual, ldr, act, y, ldy, stream);
   return launch_tile<128, 32, 4, 1>(x, m, k, w, n, bias, residual, ldr, act, y, ldy, stream);
 }
 

@@ -6,9 +6,9 @@
 //   rank[u]  = count_gt(thr = pairs) + 1
 //
 // Both kernels evaluate every logit with EXACTLY the instruction sequence of the scoring kernel
-// (score.hip): the same v_mfma_f32_32x32x2_f32 operand layout and k order (step s of 32-deep group g
-// takes features 32g + 8(s>>2) + (s&3) + 4h), so t[u] is bitwise the logit the full scoring would
-// have produced and the target never counts itself (SURVEY §7 hard part 3).
+// (score.hip): the same v_mfma_f32_32x32x2_f32 operand layout and k order (gr_common.h sc_feat), so
+// t[u] is bitwise the logit the full scoring would have produced and the target never counts
+// itself (SURVEY §7 hard part 3).  d = 16, 32, 64 or 128.
 //
 // count_gt is the scoring kernel with the logits stream replaced by a compare-and-count epilogue:
 // MFMA-bound (12.8 Mflop per user at C3) and reads only the table.  Workgroup = 4 waves x 32 users,
@@ -28,7 +28,7 @@ __global__ __launch_bounds__(64) void score_pairs_kernel(const float* __restrict
                                                          int64_t rows, const int64_t* __restrict__ ids,
                                                          int mask_col0, float* __restrict__ out,
                                                          int32_t* err) {
-  constexpr int KG = D / 32;
+  constexpr int NQ = D / 8;
   const int lane = threadIdx.x, r = lane & 31, hh = lane >> 5;
   const int64_t u0 = (int64_t)blockIdx.x * 32;
   const int64_t u = u0 + r;
@@ -43,14 +43,12 @@ __global__ __launch_bounds__(64) void score_pairs_kernel(const float* __restrict
   for (int v = 0; v < 16; ++v) acc[v] = 0.f;
   // A: user r of the tile; B: the target row of user r (column r of the tile)
 #pragma unroll
-  for (int g = 0; g < KG; ++g)
+  for (int gq = 0; gq < NQ; ++gq) {
+    const f32x4 a = *reinterpret_cast<const f32x4*>(h + uc * D + sc_feat(gq, hh));
+    const f32x4 b = *reinterpret_cast<const f32x4*>(table + t * D + sc_feat(gq, hh));
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const f32x4 a = *reinterpret_cast<const f32x4*>(h + uc * D + 32 * g + 8 * q + 4 * hh);
-      const f32x4 b = *reinterpret_cast<const f32x4*>(table + t * D + 32 * g + 8 * q + 4 * hh);
-#pragma unroll
-      for (int s = 0; s < 4; ++s) acc = mfma32(a[s], b[s], acc);
-    }
+    for (int s = 0; s < 4; ++s) acc = mfma32(a[s], b[s], acc);
+  }
   // diagonal: row (v&3) + 8(v>>2) + 4hh == column r
   float d = 0.f;
 #pragma unroll
@@ -71,9 +69,10 @@ __global__ __launch_bounds__(256, 2) void score_count_kernel(const float* __rest
                                                             int mask_col0,
                                                             unsigned long long* __restrict__ cnt_out,
                                                             int ublocks, int slices) {
-  constexpr int KG = D / 32;
+  constexpr int NQ = D / 8;
   constexpr int P = D + 4;
   constexpr int LV = RK_CHUNK * D / 4 / 256;
+  static_assert(LV >= 1 && RK_CHUNK * D / 4 % 256 == 0, "chunk staging assumes d % 16 == 0");
   __shared__ __attribute__((aligned(16))) float tab[2][RK_CHUNK * P];
   const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, hh = lane >> 5;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -85,19 +84,17 @@ __global__ __launch_bounds__(256, 2) void score_count_kernel(const float* __rest
   constexpr int UT = RK_UT;
   const int64_t u0 = ((int64_t)ub * 4 + w) * (32 * UT);
 
-  f32x4 hf[UT][KG][4];
+  f32x4 hf[UT][NQ];
   float th[UT][16];
 #pragma unroll
   for (int ut = 0; ut < UT; ++ut) {
     const int64_t u = u0 + ut * 32 + r;
     const int64_t uc = u < B ? u : B - 1;
 #pragma unroll
-    for (int g = 0; g < KG; ++g)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const f32x4 v = *reinterpret_cast<const f32x4*>(h + uc * D + 32 * g + 8 * q + 4 * hh);
-        hf[ut][g][q] = u < B ? v : f32x4{0.f, 0.f, 0.f, 0.f};
-      }
+    for (int gq = 0; gq < NQ; ++gq) {
+      const f32x4 v = *reinterpret_cast<const f32x4*>(h + uc * D + sc_feat(gq, hh));
+      hf[ut][gq] = u < B ? v : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
 #pragma unroll
     for (int v = 0; v < 16; ++v) {
       const int64_t uu = u0 + ut * 32 + (v & 3) + 8 * (v >> 2) + 4 * hh;
@@ -142,19 +139,17 @@ __global__ __launch_bounds__(256, 2) void score_count_kernel(const float* __rest
         for (int v = 0; v < 16; ++v) acc[ut][it][v] = 0.f;
     const float* tb = &tab[buf][r * P + 4 * hh];
 #pragma unroll
-    for (int g = 0; g < KG; ++g)
+    for (int gq = 0; gq < NQ; ++gq) {
+      f32x4 bt[2];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        f32x4 bt[2];
+      for (int it = 0; it < 2; ++it) bt[it] = *reinterpret_cast<const f32x4*>(tb + it * 32 * P + 8 * gq);
 #pragma unroll
-        for (int it = 0; it < 2; ++it) bt[it] = *reinterpret_cast<const f32x4*>(tb + it * 32 * P + 32 * g + 8 * q);
+      for (int s = 0; s < 4; ++s)
 #pragma unroll
-        for (int s = 0; s < 4; ++s)
+        for (int it = 0; it < 2; ++it)
 #pragma unroll
-          for (int it = 0; it < 2; ++it)
-#pragma unroll
-            for (int ut = 0; ut < UT; ++ut) acc[ut][it] = mfma32(hf[ut][g][q][s], bt[it][s], acc[ut][it]);
-      }
+          for (int ut = 0; ut < UT; ++ut) acc[ut][it] = mfma32(hf[ut][gq][s], bt[it][s], acc[ut][it]);
+    }
     const int64_t c0 = c * RK_CHUNK;
     if (c0 + RK_CHUNK <= rows && !(mask_col0 && c0 == 0)) {   // steady state: no column masks
 #pragma unroll
@@ -216,12 +211,13 @@ extern "C" int gr_score_pairs_f32(const float* h, int64_t B, int32_t d, const fl
   if (B < 0 || rows < 1) return fail(GR_ERR_ARG, "gr_score_pairs_f32: bad shape");
   if (B == 0) return GR_OK;
   if (!h || !table || !ids || !out) return fail(GR_ERR_ARG, "gr_score_pairs_f32: null pointer");
-  if (d != 32 && d != 64 && d != 128)
-    return fail(GR_ERR_UNSUPPORTED, "gr_score_pairs_f32: d must be 32, 64 or 128");
+  if (d != 16 && d != 32 && d != 64 && d != 128)
+    return fail(GR_ERR_UNSUPPORTED, "gr_score_pairs_f32: d must be 16, 32, 64 or 128");
   if (!aligned16(h) || !aligned16(table)) return fail(GR_ERR_ARG, "gr_score_pairs_f32: h / table not 16-byte aligned");
   const unsigned grid = (unsigned)((B + 31) / 32);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   switch (d) {
+    case 16: hipLaunchKernelGGL(score_pairs_kernel<16>, dim3(grid), dim3(64), 0, st, h, B, table, rows, ids, mask_col0, out, err_flag); break;
     case 32: hipLaunchKernelGGL(score_pairs_kernel<32>, dim3(grid), dim3(64), 0, st, h, B, table, rows, ids, mask_col0, out, err_flag); break;
     case 64: hipLaunchKernelGGL(score_pairs_kernel<64>, dim3(grid), dim3(64), 0, st, h, B, table, rows, ids, mask_col0, out, err_flag); break;
     default: hipLaunchKernelGGL(score_pairs_kernel<128>, dim3(grid), dim3(64), 0, st, h, B, table, rows, ids, mask_col0, out, err_flag); break;
@@ -237,8 +233,8 @@ extern "C" int gr_score_count_gt_f32(const float* h, int64_t B, int32_t d, const
   if (B < 0 || rows < 0) return fail(GR_ERR_ARG, "gr_score_count_gt_f32: bad shape");
   if (B == 0) return GR_OK;
   if (!h || !table || !thresholds || !counts_out) return fail(GR_ERR_ARG, "gr_score_count_gt_f32: null pointer");
-  if (d != 32 && d != 64 && d != 128)
-    return fail(GR_ERR_UNSUPPORTED, "gr_score_count_gt_f32: d must be 32, 64 or 128");
+  if (d != 16 && d != 32 && d != 64 && d != 128)
+    return fail(GR_ERR_UNSUPPORTED, "gr_score_count_gt_f32: d must be 16, 32, 64 or 128");
   if (!aligned16(h) || !aligned16(table)) return fail(GR_ERR_ARG, "gr_score_count_gt_f32: h / table not 16-byte aligned");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (gr_fill32_launch(counts_out, 0u, B * 2, st) != GR_OK)
@@ -254,6 +250,7 @@ extern "C" int gr_score_count_gt_f32(const float* h, int64_t B, int32_t d, const
   const dim3 g((unsigned)(ublocks * slices)), b(256);
   auto* cnt = reinterpret_cast<unsigned long long*>(counts_out);
   switch (d) {
+    case 16: hipLaunchKernelGGL(score_count_kernel<16>, g, b, 0, st, h, B, table, rows, thresholds, mask_col0, cnt, (int)ublocks, (int)slices); break;
     case 32: hipLaunchKernelGGL(score_count_kernel<32>, g, b, 0, st, h, B, table, rows, thresholds, mask_col0, cnt, (int)ublocks, (int)slices); break;
     case 64: hipLaunchKernelGGL(score_count_kernel<64>, g, b, 0, st, h, B, table, rows, thresholds, mask_col0, cnt, (int)ublocks, (int)slices); break;
     default: hipLaunchKernelGGL(score_count_kernel<128>, g, b, 0, st, h, B, table, rows, thresholds, mask_col0, cnt, (int)ublocks, (int)slices); break;

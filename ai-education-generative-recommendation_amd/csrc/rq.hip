@@ -339,7 +339,7 @@ static int launch_quantize_e(const float* z, int64_t n, int e, int L, const RQLe
                           (int)lds) != hipSuccess)
     return fail(GR_ERR_HIP, "rq quantize: cannot raise the LDS limit");
   hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(RQ_W * 64), lds, st, z, n, e, L, lv, kch, idx,
-                     best, gap, (int)tiles, (int)(option("rq_split") != 0));
+                     best, gap, (int)tiles, 1);
   return check_launch("gr_rq_quantize_f32");
 }
 

@@ -684,7 +684,7 @@ int gr_rq_encoder_fused_launch(const float* x, int64_t n, int32_t n_linear, cons
   if (!lds_ok) return fail(GR_ERR_HIP, "rq fused encoder: cannot raise the LDS limit");
   // leftover-tile pieces when the MKL split halves the chunks (in = 768) and tiles % grid != 0
   const int64_t left = tiles % grid;
-  float* h1g = (scratch && left && 2 * csplit * FXC == dims[0] && option("rq_pieces") != 0) ? scratch : nullptr;
+  float* h1g = (scratch && left && 2 * csplit * FXC == dims[0]) ? scratch : nullptr;
   hipLaunchKernelGGL((rq_encoder_kernel<256, 128>), dim3((unsigned)grid), dim3(64 * FWV), Cfg::LDS * sizeof(float), st, x, n,
                      dims[0], csplit, wp[0], biases[0], wp[1], biases[1], wp[2], biases[2], z_out, (int)tiles, h1g);
   int rc = check_launch("rq fused encoder");

@@ -302,22 +302,19 @@ static int run_forward_rowtile(const gr_sasrec_params* p, const int64_t* seqs, i
   const int64_t rows = B * n;
   const int nb = p->n_blocks;
   const bool tail = last_only && tail_out && gr_sasrec_tail_ok(p, n);
-  // tail_h: the final block's one-query tail works on LN_a(X) itself (sas_tail_h_kernel), so no
-  // K|V projection of its B n rows is computed; otherwise K|V are projected for sas_tail_kernel
-  const bool tail_h = tail && option("tail_h") != 0;
-  // block i's in-projection, fused into the kernel that produces its LayerNorm input: Q|K|V, K|V
-  // only for the final block of a last-position forward (its one query is the tail's), or none
-  // (wn = null: that kernel writes the LayerNorm output, [rows x d]) for the H-form tail
+  // block i's in-projection, fused into the kernel that produces its LayerNorm input: Q|K|V, or
+  // none for the final block of a last-position forward (wn = null: that kernel writes the
+  // LayerNorm output, [rows x d]): its one-query tail works on LN_a(X) itself (sas_tail_h2_kernel),
+  // so no K|V projection of its B n rows is computed
   auto proj = [&](int i, const float** wn, const float** bn, int* nout) {
-    const bool kv = tail && i == nb - 1;
-    if (kv && tail_h) {
+    if (tail && i == nb - 1) {
       *wn = *bn = nullptr;
       *nout = 0;
       return;
     }
-    *wn = p->in_proj_w[i] + (kv ? (int64_t)d * d : 0);
-    *bn = p->in_proj_b[i] + (kv ? d : 0);
-    *nout = kv ? 2 * d : 3 * d;
+    *wn = p->in_proj_w[i];
+    *bn = p->in_proj_b[i];
+    *nout = 3 * d;
   };
   const float *wn, *bn;
   int nout;
@@ -340,9 +337,8 @@ static int run_forward_rowtile(const gr_sasrec_params* p, const int64_t* seqs, i
   const float scale = (float)std::sqrt(1.0 / (double)hd);
   for (int i = 0; i < nb; ++i) {
     const bool last = i == nb - 1;
-    if (last && tail) {   // w.qkv holds LN_a(X) [rows x d] (H form) or K|V [rows x 2d]
-      rc = tail_h ? gr_sasrec_tail_h_launch(p, i, w.x, w.qkv, B, n, tail_out, st)
-                  : gr_sasrec_tail_launch(p, i, w.x, w.qkv, B, n, tail_out, st);
+    if (last && tail) {   // w.qkv holds LN_a(X) [rows x d]
+      rc = gr_sasrec_tail_h_launch(p, i, w.x, w.qkv, B, n, tail_out, st);
       if (rc) return rc;
       fin->done = true;
       return GR_OK;
@@ -410,17 +406,9 @@ static int run_forward(const gr_sasrec_params* p, const int64_t* seqs, int64_t B
     int rc = run_layernorm(w.x, rows, d, 1, 0, p->attn_ln_w[i], p->attn_ln_b[i], p->eps, w.h, st);
     if (rc) return rc;
     if (last_only && tail_out && i == p->n_blocks - 1) {
-      // final block for position n-1 only: the one-query tail (sasrec_tail.hip) writes the final
-      // hidden states, last LayerNorm included -- on LN_a(X) itself (tail_h), or on K | V of every
-      // token (rows d .. 3d of W_in)
-      if (option("tail_h") != 0 && gr_sasrec_tail_ok(p, n)) {
-        rc = gr_sasrec_tail_h_launch(p, i, w.x, w.h, B, n, tail_out, st);
-      } else {
-        rc = gr_linear_launch(w.h, rows, d, p->in_proj_w[i] + (int64_t)d * d, 2 * d, p->in_proj_b[i] + d,
-                              nullptr, 0, GR_ACT_NONE, w.qkv, 2 * d, st);
-        if (rc) return rc;
-        rc = gr_sasrec_tail_launch(p, i, w.x, w.qkv, B, n, tail_out, st);
-      }
+      // final block for position n-1 only: the one-query tail (sasrec_tail.hip) on LN_a(X) writes
+      // the final hidden states, last LayerNorm included
+      rc = gr_sasrec_tail_h_launch(p, i, w.x, w.h, B, n, tail_out, st);
       if (rc == GR_OK) {
         fin->done = true;
         return GR_OK;

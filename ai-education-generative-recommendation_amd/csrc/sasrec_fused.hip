@@ -199,7 +199,6 @@ struct SasFusedArgs {
   int64_t item_rows;
   int nb, d, heads, mlp, n;
   float eps, scale;
-  int tail_h;   // last-position forward: the final block in the H form (option tail_h != 0)
 };
 
 // out: last_only ? [B, d] (LN_last of position n-1) : [B, n, d].
@@ -277,13 +276,15 @@ __global__ __launch_bounds__(256) void sasrec_fused_kernel(const SasFusedArgs a,
             }
         }
       }
-      if (tail && a.tail_h) {
-        // ---- final block in the H form (option tail_h; sasrec_tail.hip's reassociation): with one
-        // query, q . K_j = (W_k^T q) . H_j + (a term constant over j: cancels in the softmax) and
-        // sum_j p_j V_j = W_v (sum_j p_j H_j) + b_v, so K and V of the n tokens are never projected
-        // (2 x 32 DT^2 TT MFMAs per sequence).  H = LN_a(X) is parked token-major in the X area (X
-        // itself is not needed again: x[n-1] is in sc).  fp32 rounding of the reassociated sums,
-        // within the logits tolerance (not bitwise to tail_h = 0).
+      if (tail) {
+        // ---- final block when only position n-1 is needed (model.py:104), in the H form
+        // (sasrec_tail.hip's reassociation): with one query, q . K_j = (W_k^T q) . H_j + (a term
+        // constant over j: cancels in the softmax) and sum_j p_j V_j = W_v (sum_j p_j H_j) + b_v, so
+        // K and V of the n tokens are never projected (2 x 32 DT^2 TT MFMAs per sequence), and the
+        // rest of the block is lane-parallel GEMVs (one feature per lane, d <= 64).  H = LN_a(X) is
+        // parked token-major in the X area (X itself is not needed again: x[n-1] is in sc).  fp32
+        // rounding of the reassociated sums, within the logits tolerance (round 4's K|V form,
+        // 124 vs 112 us per C3 forward, was removed in round 5).
         // odd row pitch (conflict-free token-major writes) when the n rows still fit the X area
         const int PH = n * (32 * DT + 1) <= 32 * DT * 32 * TT ? 32 * DT + 1 : 32 * DT;
         float* hs = xs;
@@ -417,93 +418,6 @@ __global__ __launch_bounds__(256) void sasrec_fused_kernel(const SasFusedArgs a,
         }
       }
       __builtin_amdgcn_sched_barrier(0);
-      if (tail) {
-        // ---- final block when only position n-1 is needed (model.py:104): the rest of the
-        // block is one query row, so it runs as lane-parallel GEMVs instead of 32-token MFMA
-        // tiles (K and V above still cover every key).  One feature per lane (d <= 64).
-        float* hl = sc;            // LN_a(x)[n-1]          [64]
-        float* xl = sc + 64;       // x[n-1]                [64]
-        float* qs = sc + 128;      // q (scaled)            [64]
-        float* os = sc + 192;      // attention output      [64]
-        float* ls = sc + 256;      // LN_f(x)               [64]
-        float* fs = sc + 320;      // relu(W1 . + b1)       [128]
-        float* ps = sc + 448;      // softmax rows per head [8][64]
-        const int f = lane;
-        const bool fon = f < d;
-        wave_lds_sync();
-        // q = (Wq h + bq) * sqrt(1/hd)   (functional.py:6578)
-        if (fon) qs[f] = gemv_row(P.w_in, P.b_in, f, d, hl) * a.scale;
-        wave_lds_sync();
-        // scores of every key against the one query, softmax per head over keys 0..n-1
-#pragma unroll 1
-        for (int hh = 0; hh < (SINGLE ? 1 : a.heads); ++hh) {
-          const int f_lo = SINGLE ? 0 : hh * hd, f_hi = SINGLE ? d : f_lo + hd;
-          float sv[TT];
-#pragma unroll
-          for (int tt = 0; tt < TT; ++tt) {
-            float acc = 0.f;
-#pragma unroll
-            for (int ft = 0; ft < DT; ++ft)
-#pragma unroll
-              for (int q = 0; q < 4; ++q) {
-                const int c = 32 * ft + 8 * q + 4 * h;
-                const f32x4 qq = *reinterpret_cast<const f32x4*>(qs + c);
-#pragma unroll
-                for (int i = 0; i < 4; ++i)
-                  acc = (c + i >= f_lo && c + i < f_hi) ? fmaf(K[ft][tt][4 * q + i], qq[i], acc) : acc;
-              }
-            acc += swap_halves(acc);
-            sv[tt] = (32 * tt + r < n) ? acc : -INFINITY;
-          }
-          float m = sv[0];
-#pragma unroll
-          for (int tt = 1; tt < TT; ++tt) m = fmaxf(m, sv[tt]);
-          m = half_max(m);
-          float sum = 0.f;
-#pragma unroll
-          for (int tt = 0; tt < TT; ++tt) {
-            sv[tt] = __expf(sv[tt] - m);
-            sum += sv[tt];
-          }
-          const float inv = 1.0f / half_sum(sum);
-          if (h == 0) {
-#pragma unroll
-            for (int tt = 0; tt < TT; ++tt) ps[hh * 64 + 32 * tt + r] = sv[tt] * inv;
-          }
-        }
-        wave_lds_sync();
-        // o[f] = sum_j p_head(f)[j] V[j][f]
-#pragma unroll
-        for (int ft = 0; ft < DT; ++ft) {
-          const int fo = 32 * ft + r;
-          const float* pr = ps + (SINGLE ? 0 : (fo < d ? fo / hd : 0)) * 64;
-          float acc = 0.f;
-#pragma unroll
-          for (int tt = 0; tt < TT; ++tt)
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-              const f32x4 pp = *reinterpret_cast<const f32x4*>(pr + 32 * tt + 8 * q + 4 * h);
-#pragma unroll
-              for (int i = 0; i < 4; ++i) acc = fmaf(V[tt][ft][4 * q + i], pp[i], acc);
-            }
-          acc += swap_halves(acc);
-          if (h == 0 && fo < d) os[fo] = acc;
-        }
-        wave_lds_sync();
-        // out_proj + residual, LN_f, FFN + residual, last LayerNorm (model.py:84-96)
-        const float x1 = fon ? xl[f] + gemv_row(P.w_o, P.b_o, f, d, os) : 0.f;
-        const float l1 = ln_lane(x1, fon, P.ln_f_w, P.ln_f_b, f, d, a.eps);
-        if (fon) ls[f] = l1;
-        wave_lds_sync();
-#pragma unroll
-        for (int m0 = 0; m0 < 128; m0 += 64)
-          if (m0 + lane < mlp) fs[m0 + lane] = fmaxf(gemv_row(P.w1, P.b1, m0 + lane, d, ls), 0.f);
-        wave_lds_sync();
-        const float x2 = fon ? x1 + gemv_row(P.w2, P.b2, f, mlp, fs) : 0.f;
-        const float y = ln_lane(x2, fon, a.ln_w, a.ln_b, f, d, a.eps);
-        if (fon) out[b * d + f] = y;
-        return;
-      }
       const bool narrow = !SINGLE && hd < 32;   // heads narrower than a feature tile: step masks
       // one query tile at a time: Q^T tile, per-head S^T -> P^T -> O^T, out_proj, residual
 #pragma unroll
@@ -672,7 +586,6 @@ int gr_sasrec_fused_launch(const gr_sasrec_params* p, const int64_t* seqs, int64
   a.item_rows = p->item_rows; a.nb = p->n_blocks; a.d = d; a.heads = H; a.mlp = p->mlp; a.n = n;
   a.eps = p->eps;
   a.scale = (float)std::sqrt(1.0 / (double)(d / H));
-  a.tail_h = option("fused_tail_h") != 0 ? 1 : 0;
   const int TT = n > 32 ? 2 : 1, DT = d > 32 ? 2 : 1, MT = (p->mlp + 31) / 32;
   const dim3 g((unsigned)((B + 3) / 4)), blk(256);
   const bool exact = d == 32 * DT && p->mlp == 32 * MT;

@@ -28,8 +28,8 @@ constexpr int RT_P = RT_D + 4;       // LDS row pitch of a [64 x 128] image (con
 struct RowTileArgs {
   const float *wo, *bo, *ln_f_w, *ln_f_b, *w1, *b1, *w2, *b2, *ln_n_w, *ln_n_b;
   const float *wn, *bn;   // the next block's in-projection (rows of W_in / b_in), or null
-  int mlp, nout;          // nout: 3d (Q|K|V) or 2d (K|V only, the final block of a tail forward)
-  int kv2;                // post_attn8: nout / 32 % 8 == 0 and option rt_kv2 (one column tile per wave)
+  int mlp, nout;          // nout: 3d (the next block's Q|K|V)
+  int kv2;                // post_attn8: nout / 32 % 8 == 0 (one column tile per wave over both row tiles)
   float eps;
 };
 
@@ -191,122 +191,6 @@ __device__ __forceinline__ void rt_project(const float* img, const float* __rest
   }
 }
 
-template <int MT>
-__global__ __launch_bounds__(256, 2) void post_attn_kernel(const RowTileArgs a, const float* __restrict__ O,
-                                                           float* X, float* __restrict__ Hn, int64_t M) {
-  constexpr int MLP = 32 * MT;
-  constexpr int FP = MLP + 4;
-  __shared__ __attribute__((aligned(16))) float bufA[RT_BM * RT_P];   // O, then F
-  __shared__ __attribute__((aligned(16))) float bufB[RT_BM * RT_P];   // X, X1 -> H1, X2
-  const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, h = lane >> 5;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int64_t m0 = (int64_t)xcd_remap(blockIdx.x, gridDim.x) * RT_BM;
-  const int64_t left = M - m0;
-  // ---- O and X tiles -> LDS: all 16 loads in flight at once (clamped rows, no branch around a
-  // load); rows past M are zeroed when written and never stored
-  {
-    f32x4 o[8], x[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int f = tid + 256 * i, row = f >> 5, c = (f & 31) * 4;
-      const int64_t g = m0 + (row < left ? row : left - 1);
-      o[i] = *reinterpret_cast<const f32x4*>(O + g * RT_D + c);
-      x[i] = *reinterpret_cast<const f32x4*>(X + g * RT_D + c);
-    }
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int f = tid + 256 * i, row = f >> 5, c = (f & 31) * 4;
-      const bool ok = row < left;
-      *reinterpret_cast<f32x4*>(bufA + row * RT_P + c) = ok ? o[i] : f32x4{0.f, 0.f, 0.f, 0.f};
-      *reinterpret_cast<f32x4*>(bufB + row * RT_P + c) = ok ? x[i] : f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-  }
-  __syncthreads();
-  const int col = 32 * w + r;
-  // ---- X1 = X + O . Wo^T + bo  (register v of lane (r, h): row 32rt + (v&3) + 8(v>>2) + 4h)
-  f32x16 x1[2];
-  {
-    f32x16 acc[2];
-    const float bo = a.bo[col];
-#pragma unroll
-    for (int rt = 0; rt < 2; ++rt)
-#pragma unroll
-      for (int v = 0; v < 16; ++v) acc[rt][v] = 0.f;
-    rt_gemm<RT_D>(acc, bufA, RT_P, a.wo, col, r, h);
-#pragma unroll
-    for (int rt = 0; rt < 2; ++rt)
-#pragma unroll
-      for (int v = 0; v < 16; ++v) {
-        const int row = 32 * rt + (v & 3) + 8 * (v >> 2) + 4 * h;
-        x1[rt][v] = bufB[row * RT_P + col] + (acc[rt][v] + bo);
-      }
-  }
-  __syncthreads();   // every wave has read its X and O values
-#pragma unroll
-  for (int rt = 0; rt < 2; ++rt)
-#pragma unroll
-    for (int v = 0; v < 16; ++v) bufB[(32 * rt + (v & 3) + 8 * (v >> 2) + 4 * h) * RT_P + col] = x1[rt][v];
-  __syncthreads();
-  rt_layernorm(bufB, a.ln_f_w, a.ln_f_b, a.eps, nullptr, 0);          // H1 = LN_f(X1), in place
-  __syncthreads();
-  // ---- F = relu(H1 . W1^T + b1) -> bufA  (tiles: 2 row tiles x MT column tiles over the 4 waves)
-  for (int t = w; t < 2 * MT; t += 4) {
-    const int rt = t / MT, ct = t % MT;
-    f32x16 acc = {};
-    const float* wr = a.w1 + (int64_t)(32 * ct + r) * RT_D + 4 * h;
-    const float* ar = bufB + (32 * rt + r) * RT_P + 4 * h;
-#pragma unroll
-    for (int kc = 0; kc < RT_D / 8; ++kc) {
-      const f32x4 b = *reinterpret_cast<const f32x4*>(wr + 8 * kc);
-      const f32x4 x = *reinterpret_cast<const f32x4*>(ar + 8 * kc);
-#pragma unroll
-      for (int s = 0; s < 4; ++s) acc = mfma32(x[s], b[s], acc);
-    }
-    const float b1 = a.b1[32 * ct + r];
-#pragma unroll
-    for (int v = 0; v < 16; ++v) {
-      const float y = acc[v] + b1;
-      bufA[(32 * rt + (v & 3) + 8 * (v >> 2) + 4 * h) * FP + 32 * ct + r] = y < 0.f ? 0.f : y;
-    }
-  }
-  __syncthreads();
-  // ---- X2 = X1 + F . W2^T + b2
-  {
-    f32x16 acc[2];
-    const float b2 = a.b2[col];
-#pragma unroll
-    for (int rt = 0; rt < 2; ++rt)
-#pragma unroll
-      for (int v = 0; v < 16; ++v) acc[rt][v] = 0.f;
-    rt_gemm<MLP>(acc, bufA, FP, a.w2, col, r, h);
-#pragma unroll
-    for (int rt = 0; rt < 2; ++rt)
-#pragma unroll
-      for (int v = 0; v < 16; ++v)
-        bufB[(32 * rt + (v & 3) + 8 * (v >> 2) + 4 * h) * RT_P + col] = x1[rt][v] + (acc[rt][v] + b2);
-  }
-  __syncthreads();
-  // ---- X2 -> X (in place: the tile was read above); then either H2 = LN_next(X2) -> Hn, or the
-  // next block's in-projection of LN_next(X2) -> Hn as [rows x nout] (the LN stays in LDS)
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int f = tid + 256 * i, row = f >> 5, c = (f & 31) * 4;
-    if (row < left) *reinterpret_cast<f32x4*>(X + (m0 + row) * RT_D + c) = *reinterpret_cast<const f32x4*>(bufB + row * RT_P + c);
-  }
-  if (a.wn) {
-    __syncthreads();   // the X2 stores have read the image the LayerNorm rewrites
-    rt_layernorm(bufB, a.ln_n_w, a.ln_n_b, a.eps, nullptr, 0);
-    __syncthreads();
-    rt_project(bufB, a.wn, a.bn, a.nout, Hn + m0 * a.nout, left);
-  } else {
-    rt_layernorm(bufB, a.ln_n_w, a.ln_n_b, a.eps, Hn + m0 * RT_D, left);
-  }
-}
-
-// ---- 8-wave form of the row tile (option rt_w8): 512 threads per 64-row tile, one 32 x 32 output
-// tile per wave per 128-wide product (4 waves per SIMD with two workgroups per CU instead of 2),
-// LayerNorm statistics from 8 threads per row.  Same products and order of operations per element
-// except the LayerNorm sums (8 partial sums per row instead of 4).
 template <int K>
 __device__ __forceinline__ void rt_gemm1(f32x16& acc, const float* A, int ap, const float* __restrict__ W,
                                          int wrow, int r, int h) {
@@ -721,7 +605,7 @@ __global__ __launch_bounds__(64 * NW, 1) void embed_proj_kernel(const int64_t* _
 
 // Shapes: d == 128, mlp in {32, 64, 128}; anything else returns GR_ERR_UNSUPPORTED (the caller
 // keeps the kernel-per-op sequence).  ln_next_* = the next block's attention LayerNorm, or the
-// last LayerNorm after the final block.  wn / bn (nout = 3d or 2d columns): the next block's
+// last LayerNorm after the final block.  wn / bn (nout = 3d columns): the next block's
 // in-projection, computed from the LayerNorm image and written to H as [M x nout]; null: H gets
 // the LayerNorm output itself [M x d].
 int gr_post_attn_launch(const gr_sasrec_params* p, int blk, const float* ln_next_w, const float* ln_next_b,
@@ -737,7 +621,7 @@ int gr_post_attn_launch(const gr_sasrec_params* p, int blk, const float* ln_next
   a.w2 = p->ffn2_w[blk]; a.b2 = p->ffn2_b[blk];
   a.ln_n_w = ln_next_w; a.ln_n_b = ln_next_b;
   a.wn = wn; a.bn = bn; a.nout = nout;
-  a.kv2 = wn && (nout / 32) % 8 == 0 && option("rt_kv2") != 0;
+  a.kv2 = wn && (nout / 32) % 8 == 0;
   a.mlp = mlp; a.eps = p->eps;
   const float* ptrs[] = {a.wo, a.w1, a.w2, a.ln_f_w, a.ln_f_b, a.ln_n_w, a.ln_n_b, O, X, H};
   for (const float* q : ptrs)
@@ -745,20 +629,13 @@ int gr_post_attn_launch(const gr_sasrec_params* p, int blk, const float* ln_next
   if (wn && (!aligned16(wn) || !bn || nout % 32 || nout < 32)) return GR_ERR_UNSUPPORTED;
   const int64_t tiles = (M + RT_BM - 1) / RT_BM;
   if (tiles > 0x7fffffffLL) return GR_ERR_UNSUPPORTED;
-  if (option("rt_w8") != 0) {
-    switch (mlp) {
-      case 32: hipLaunchKernelGGL(post_attn8_kernel<1>, dim3((unsigned)tiles), dim3(512), 0, st, a, O, X, H, M); break;
-      case 64: hipLaunchKernelGGL(post_attn8_kernel<2>, dim3((unsigned)tiles), dim3(512), 0, st, a, O, X, H, M); break;
-      default: hipLaunchKernelGGL(post_attn8_kernel<4>, dim3((unsigned)tiles), dim3(512), 0, st, a, O, X, H, M); break;
-    }
-    return check_launch("sasrec post-attention row tile (8 waves)");
-  }
+  // 8 waves per 64-row tile (4 per SIMD); the 4-wave form measured 200 vs 182 us per C5 forward
   switch (mlp) {
-    case 32: hipLaunchKernelGGL(post_attn_kernel<1>, dim3((unsigned)tiles), dim3(256), 0, st, a, O, X, H, M); break;
-    case 64: hipLaunchKernelGGL(post_attn_kernel<2>, dim3((unsigned)tiles), dim3(256), 0, st, a, O, X, H, M); break;
-    default: hipLaunchKernelGGL(post_attn_kernel<4>, dim3((unsigned)tiles), dim3(256), 0, st, a, O, X, H, M); break;
+    case 32: hipLaunchKernelGGL(post_attn8_kernel<1>, dim3((unsigned)tiles), dim3(512), 0, st, a, O, X, H, M); break;
+    case 64: hipLaunchKernelGGL(post_attn8_kernel<2>, dim3((unsigned)tiles), dim3(512), 0, st, a, O, X, H, M); break;
+    default: hipLaunchKernelGGL(post_attn8_kernel<4>, dim3((unsigned)tiles), dim3(512), 0, st, a, O, X, H, M); break;
   }
-  return check_launch("sasrec post-attention row tile");
+  return check_launch("sasrec post-attention row tile (8 waves)");
 }
 
 int gr_embed_ln_launch(const gr_sasrec_params* p, const int64_t* seqs, int64_t M, int32_t n, const float* wn,
@@ -774,14 +651,15 @@ int gr_embed_ln_launch(const gr_sasrec_params* p, const int64_t* seqs, int64_t M
   return check_launch("sasrec embed + layernorm");
 }
 
-// Block 0 fused: X, then QKV = LN_a0(X) . W^T + b ([M x nout], nout = 3d or 2d) by embed_proj_kernel
+// Block 0 fused: X, then QKV = LN_a0(X) . W^T + b ([M x 3d]) by embed_proj_kernel
 // (d == 128 only; GR_ERR_UNSUPPORTED otherwise -- the caller keeps embed_ln + gr_linear).  One
-// workgroup per CU over contiguous ranges of 32 RC-row tiles (option emb_rows: 32 rows, or 64; C5
-// forward 403 vs 414 us: 3200 tiles over 256 CUs balance better than 1600).
+// workgroup per CU over contiguous ranges of 32-row tiles (64-row tiles measured C5 forward 414 vs
+// 403 us: 3200 tiles over 256 CUs balance better than 1600).  RC (row tiles of 32 per step) stays a
+// template parameter of the kernel; the launcher uses 1.
 int gr_embed_proj_launch(const gr_sasrec_params* p, const int64_t* seqs, int64_t M, int32_t n, const float* wn,
                          const float* bn, int nout, float* X, float* QKV, int32_t* err, hipStream_t st) {
   using namespace gr;
-  if (p->d != RT_D || p->n_blocks < 1 || (nout != 3 * RT_D && nout != 2 * RT_D)) return GR_ERR_UNSUPPORTED;
+  if (p->d != RT_D || p->n_blocks < 1 || nout != 3 * RT_D) return GR_ERR_UNSUPPORTED;
   if (!aligned16(p->attn_ln_w[0]) || !aligned16(p->attn_ln_b[0]) || !aligned16(wn) || !bn)
     return GR_ERR_UNSUPPORTED;
   if (M * nout >= (1LL << 40)) return GR_ERR_UNSUPPORTED;
@@ -791,17 +669,12 @@ int gr_embed_proj_launch(const gr_sasrec_params* p, const int64_t* seqs, int64_t
     if (hipGetDevice(&dev) != hipSuccess) dev = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1) cus = 256;
   }
-  const bool r64 = option("emb_rows") == 64;
-  const int64_t tiles = (M + (r64 ? 63 : 31)) / (r64 ? 64 : 32);
+  const int64_t tiles = (M + 31) / 32;
   const unsigned g = (unsigned)(tiles < cus ? tiles : cus);
 #define GR_EMB_PROJ(NW, RC)                                                                              \
   hipLaunchKernelGGL((embed_proj_kernel<NW, RC>), dim3(g), dim3(64 * NW), 0, st, seqs, M, n, p->item_emb, \
                      p->item_rows, p->pos_emb, p->attn_ln_w[0], p->attn_ln_b[0], p->eps, wn, bn, X, QKV, err)
-  if (nout == 3 * RT_D) {
-    if (r64) GR_EMB_PROJ(12, 2); else GR_EMB_PROJ(12, 1);
-  } else {
-    if (r64) GR_EMB_PROJ(8, 2); else GR_EMB_PROJ(8, 1);
-  }
+  GR_EMB_PROJ(12, 1);
 #undef GR_EMB_PROJ
   return check_launch("sasrec embed + layernorm + in-projection");
 }

@@ -1,9 +1,9 @@
 // Final SASRec block for position n-1 only (the `log_feats[:, -1, :]` of SASRec/model.py:104 in
 // predict, and the `[:, -1, :]` of SASRec/evaluate.py:26 / train.py:45 through it).
 //
-// In the final block only one query row per sequence reaches the output, so after the K / V
-// projection of every token (a plain GEMM over the B*n rows, N = 2d) the rest of the block is a
-// handful of GEMVs per sequence: one workgroup per sequence computes
+// In the final block only one query row per sequence reaches the output, so the block is a
+// handful of GEMVs per sequence and one pass over its LayerNorm rows H = LN_a(X): one workgroup per
+// sequence computes
 //   h  = LN_a(x[n-1]);  q = (Wq h + bq) * sqrt(1/hd)                   (functional.py:6578)
 //   p  = softmax over keys 0..n-1 of q . K^T, per head                   (causal: the last query
 //                                                                         sees every key)
@@ -18,8 +18,8 @@
 #include "gr_common.h"
 
 #ifndef GR_TDIAG
-#define GR_TDIAG 0   // diagnostic builds only (scripts/build_variant.sh): 1 no H passes (scores / u),
-                     // 2 no GEMVs, 3 no W_k^T q phase -- wrong results, phase costs of sas_tail_h_kernel
+#define GR_TDIAG 0   // diagnostic builds only (scripts/build_variant.sh): 1 no H pass, 2 no GEMVs,
+                     // 3 no W_k^T q phase -- wrong results, phase costs of sas_tail_h2_kernel
 #endif
 
 namespace gr {
@@ -98,278 +98,18 @@ __device__ __forceinline__ void st_layernorm(const float* in, const float* __res
   __syncthreads();
 }
 
-__global__ __launch_bounds__(ST_NT) void sas_tail_kernel(const SasTailArgs a, const float* __restrict__ X,
-                                                       const float* __restrict__ KV, float* __restrict__ out) {
-  __shared__ __attribute__((aligned(16))) float xl[ST_MAX_D], hl[ST_MAX_D], q[ST_MAX_D], o[ST_MAX_D],
-      x1[ST_MAX_D], l1[ST_MAX_D], fh[ST_MAX_MLP], P[ST_MAX_H * ST_MAX_N], part[ST_NT * 4],
-      red[2 * ST_MAX_H * ST_NW], stat[2];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int64_t b = blockIdx.x;
-  const int d = a.d, n = a.n, H = a.heads, hd = d / H;
-  const int L = d >> 2, gpw = 64 / L, l = lane & (L - 1);
-  const int grp = wave * gpw + lane / L, ngrp = ST_NW * gpw;
-  const int hl4 = hd >> 2;                  // lanes per head within a group
-  const float* xr = X + (b * n + n - 1) * d;
-  const float* kv = KV + b * n * 2 * d;     // row j: K[j] = kv[j*2d .. +d), V[j] = kv[j*2d + d .. +d)
-  for (int c = tid; c < d; c += ST_NT) xl[c] = xr[c];
-  __syncthreads();
-  st_layernorm(xl, a.ln_a_w, a.ln_a_b, d, a.eps, hl, stat);
-  st_gemv(a.wq, a.bq, hl, d, d, q);
-  __syncthreads();
-  // scores: one lane group per key, lane l holds q[4l .. 4l+3] (scaled after the bias, :6578)
-  const f32x4 q4 = *reinterpret_cast<const f32x4*>(q + 4 * l) * a.scale;
-  const int myh = (4 * l) / hd;
-  float mx = -INFINITY;
-  for (int j0 = grp; j0 < n; j0 += ST_U * ngrp) {
-    f32x4 k4[ST_U];
-#pragma unroll
-    for (int u = 0; u < ST_U; ++u) {
-      const int j = j0 + u * ngrp;
-      k4[u] = j < n ? *reinterpret_cast<const f32x4*>(kv + (int64_t)j * 2 * d + 4 * l) : f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-#pragma unroll
-    for (int u = 0; u < ST_U; ++u) {
-      const int j = j0 + u * ngrp;
-      float s = k4[u][0] * q4[0];
-      s = fmaf(k4[u][1], q4[1], s);
-      s = fmaf(k4[u][2], q4[2], s);
-      s = fmaf(k4[u][3], q4[3], s);
-      s = seg_sum(s, hl4);                 // per head: the head's hd/4 lanes
-      if (j < n && (l & (hl4 - 1)) == 0) {
-        P[myh * n + j] = s;
-        mx = fmaxf(mx, s);
-      }
-    }
-  }
-  __syncthreads();
-  // softmax over keys per head (functional.py:6590): max, exp, sum
-  for (int hh = 0; hh < H; ++hh) {
-    float m = -INFINITY;
-    for (int j = tid; j < n; j += ST_NT) m = fmaxf(m, P[hh * n + j]);
-    for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off));
-    if (lane == 0) red[hh * ST_NW + wave] = m;
-  }
-  __syncthreads();
-  for (int hh = 0; hh < H; ++hh) {
-    float m = red[hh * ST_NW];
-    for (int u = 1; u < ST_NW; ++u) m = fmaxf(m, red[hh * ST_NW + u]);
-    float sm = 0.f;
-    for (int j = tid; j < n; j += ST_NT) {
-      const float e = __expf(P[hh * n + j] - m);
-      P[hh * n + j] = e;
-      sm += e;
-    }
-    for (int off = 32; off > 0; off >>= 1) sm += __shfl_xor(sm, off);
-    if (lane == 0) red[ST_MAX_H * ST_NW + hh * ST_NW + wave] = sm;
-  }
-  __syncthreads();
-  // o = p . V: lane group g sums keys g, g + ngrp, ...; lane l covers features 4l .. 4l+3
-  {
-    const float* sb = red + ST_MAX_H * ST_NW + myh * ST_NW;
-    float tot = sb[0];
-    for (int u = 1; u < ST_NW; ++u) tot += sb[u];
-    const float inv = 1.0f / tot;
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-    for (int j0 = grp; j0 < n; j0 += ST_U * ngrp) {
-      f32x4 v4[ST_U];
-#pragma unroll
-      for (int u = 0; u < ST_U; ++u) {
-        const int j = j0 + u * ngrp;
-        v4[u] = j < n ? *reinterpret_cast<const f32x4*>(kv + (int64_t)j * 2 * d + d + 4 * l) : f32x4{0.f, 0.f, 0.f, 0.f};
-      }
-#pragma unroll
-      for (int u = 0; u < ST_U; ++u) {
-        const int j = j0 + u * ngrp;
-        const float pj = j < n ? P[myh * n + j] * inv : 0.f;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) acc[e] = fmaf(pj, v4[u][e], acc[e]);
-      }
-    }
-    *reinterpret_cast<f32x4*>(part + grp * d + 4 * l) = acc;
-    __syncthreads();
-    for (int c = tid; c < d; c += ST_NT) {
-      float t = 0.f;
-      for (int g = 0; g < ngrp; ++g) t += part[g * d + c];
-      o[c] = t;
-    }
-    __syncthreads();
-  }
-  st_gemv(a.wo, a.bo, o, d, d, x1);                          // out_proj
-  __syncthreads();
-  for (int c = tid; c < d; c += ST_NT) x1[c] += xl[c];         // residual (model.py:84)
-  __syncthreads();
-  st_layernorm(x1, a.ln_f_w, a.ln_f_b, d, a.eps, l1, stat);
-  st_gemv(a.w1, a.b1, l1, a.mlp, d, fh);
-  __syncthreads();
-  for (int c = tid; c < a.mlp; c += ST_NT) fh[c] = fh[c] < 0.f ? 0.f : fh[c];
-  __syncthreads();
-  st_gemv(a.w2, a.b2, fh, d, a.mlp, o);                      // W2 f + b2 (o reused)
-  __syncthreads();
-  for (int c = tid; c < d; c += ST_NT) x1[c] += o[c];          // residual (model.py:94)
-  __syncthreads();
-  st_layernorm(x1, a.ln_w, a.ln_b, d, a.eps, l1, stat);      // last_layernorm (model.py:96)
-  for (int c = tid; c < d; c += ST_NT) out[b * d + c] = l1[c];
-}
-
 // The same final block without K or V: with one query per sequence, attention needs only the
 // LayerNorm output H of every position (functional.py:6578-6600 reassociated):
 //   q . K_j = q . (Wk H_j + bk) = (Wk_h^T q_h) . H_j + q_h . bk_h   -- the last term is the same for
 //                                                                    every key: softmax drops it
 //   sum_j p_j V_j = Wv_h (sum_j p_j H_j) + bv_h                      -- the p_j of a head sum to 1
 // so per sequence: q = Wq h + bq (scaled), q'_h = Wk_h^T q_h (a d-vector per head), scores q'_h . H_j,
-// softmax, u_h = sum_j p_j H_j, o_h = Wv_h u_h + bv_h, then out-proj, FFN and the last LayerNorm as
-// in sas_tail_kernel.  The final block's K|V projection over all B n rows (2 d^2 flop per token)
+// softmax, u_h = sum_j p_j H_j, o_h = Wv_h u_h + bv_h, then out-proj, FFN and the last LayerNorm.  The final block's K|V projection over all B n rows (2 d^2 flop per token)
 // is never computed, and the kernel reads the n d-rows of H instead of the n 2d-rows of K|V.  fp32;
 // the reassociation rounds differently from the reference formulation, within the logits
 // tolerance (tests/test_sasrec_gpu.py).
-__global__ __launch_bounds__(ST_NT) void sas_tail_h_kernel(const SasTailArgs a, const float* __restrict__ X,
-                                                         const float* __restrict__ Hs, const float* __restrict__ wk,
-                                                         const float* __restrict__ wv, const float* __restrict__ bv,
-                                                         float* __restrict__ out) {
-  __shared__ __attribute__((aligned(16))) float xl[ST_MAX_D], hl[ST_MAX_D], q[ST_MAX_D], o[ST_MAX_D],
-      x1[ST_MAX_D], l1[ST_MAX_D], fh[ST_MAX_MLP], qk[ST_MAX_H * ST_MAX_D], u[ST_MAX_H * ST_MAX_D],
-      P[ST_MAX_H * ST_MAX_N], part[ST_NT * 4], red[2 * ST_MAX_H * ST_NW], stat[2];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int64_t b = blockIdx.x;
-  const int d = a.d, n = a.n, H = a.heads, hd = d / H;
-  const int L = d >> 2, gpw = 64 / L, l = lane & (L - 1);
-  const int grp = wave * gpw + lane / L, ngrp = ST_NW * gpw;
-  const float* xr = X + (b * n + n - 1) * d;
-  const float* hb = Hs + b * n * d;         // row j: LN_a of position j (keys and values)
-  for (int c = tid; c < d; c += ST_NT) {
-    xl[c] = xr[c];
-    hl[c] = hb[(int64_t)(n - 1) * d + c];
-  }
-  __syncthreads();
-  st_gemv(a.wq, a.bq, hl, d, d, q);
-  __syncthreads();
-  {   // q'_h[c] = sum_r Wk[h hd + r][c] q[h hd + r]: each thread a float4 of columns over one of RG
-      // r ranges (rows of Wk read coalesced, all of a thread's rows in flight together), the RG
-      // partials summed in order
-    const int hdn = H * d, hdn4 = hdn >> 2, cq = d >> 2;
-    const int RG = hdn4 >= ST_NT ? 1 : ST_NT / hdn4, rl = (hd + RG - 1) / RG;
-    for (int i = tid; i < (GR_TDIAG == 3 ? 0 : hdn4 * RG); i += ST_NT) {
-      const int idx4 = i % hdn4, rg = i / hdn4, hh = idx4 / cq, c4 = idx4 - hh * cq;
-      const int r0 = rg * rl, r1 = r0 + rl < hd ? r0 + rl : hd;
-      const float* wc = wk + (int64_t)hh * hd * d + 4 * c4;
-      const float* qh = q + hh * hd;
-      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll 8
-      for (int r = r0; r < r1; ++r) {
-        const f32x4 w4 = *reinterpret_cast<const f32x4*>(wc + (int64_t)r * d);
-        const float qr = qh[r] * a.scale;   // q * sqrt(1/hd) (functional.py:6578)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) acc[e] = fmaf(w4[e], qr, acc[e]);
-      }
-      *reinterpret_cast<f32x4*>(part + rg * hdn + 4 * idx4) = acc;
-    }
-    __syncthreads();
-    for (int idx = tid; idx < hdn; idx += ST_NT) {
-      float t = part[idx];
-      for (int rg = 1; rg < RG; ++rg) t += part[rg * hdn + idx];
-      qk[idx] = t;
-    }
-  }
-  __syncthreads();
-  // scores: one lane group per key, lane l holds H_j[4l .. 4l+3]; every head dots the whole row
-  for (int j0 = grp; j0 < (GR_TDIAG == 1 ? 0 : n); j0 += ST_U * ngrp) {
-    f32x4 h4[ST_U];
-#pragma unroll
-    for (int uu = 0; uu < ST_U; ++uu) {
-      const int j = j0 + uu * ngrp;
-      h4[uu] = j < n ? *reinterpret_cast<const f32x4*>(hb + (int64_t)j * d + 4 * l) : f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-#pragma unroll
-    for (int uu = 0; uu < ST_U; ++uu) {
-      const int j = j0 + uu * ngrp;
-#pragma unroll
-      for (int hh = 0; hh < ST_MAX_H; ++hh) {
-        if (hh >= H) break;
-        const f32x4 q4 = *reinterpret_cast<const f32x4*>(qk + hh * d + 4 * l);
-        float sc = h4[uu][0] * q4[0];
-        sc = fmaf(h4[uu][1], q4[1], sc);
-        sc = fmaf(h4[uu][2], q4[2], sc);
-        sc = fmaf(h4[uu][3], q4[3], sc);
-        sc = seg_sum(sc, L);
-        if (j < n && l == 0) P[hh * n + j] = sc;
-      }
-    }
-  }
-  __syncthreads();
-  // softmax over keys per head (functional.py:6590): max, exp, sum
-  for (int hh = 0; hh < H; ++hh) {
-    float m = -INFINITY;
-    for (int j = tid; j < n; j += ST_NT) m = fmaxf(m, P[hh * n + j]);
-    for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off));
-    if (lane == 0) red[hh * ST_NW + wave] = m;
-  }
-  __syncthreads();
-  for (int hh = 0; hh < H; ++hh) {
-    float m = red[hh * ST_NW];
-    for (int w2 = 1; w2 < ST_NW; ++w2) m = fmaxf(m, red[hh * ST_NW + w2]);
-    float sm = 0.f;
-    for (int j = tid; j < n; j += ST_NT) {
-      const float e = __expf(P[hh * n + j] - m);
-      P[hh * n + j] = e;
-      sm += e;
-    }
-    for (int off = 32; off > 0; off >>= 1) sm += __shfl_xor(sm, off);
-    if (lane == 0) red[ST_MAX_H * ST_NW + hh * ST_NW + wave] = sm;
-  }
-  __syncthreads();
-  // u_h = sum_j p_j H_j, one head at a time through the group partials
-  for (int hh = 0; hh < H; ++hh) {
-    const float* sb = red + ST_MAX_H * ST_NW + hh * ST_NW;
-    float tot = sb[0];
-    for (int w2 = 1; w2 < ST_NW; ++w2) tot += sb[w2];
-    const float inv = 1.0f / tot;
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-    for (int j0 = grp; j0 < (GR_TDIAG == 1 ? 0 : n); j0 += ST_U * ngrp) {
-      f32x4 h4[ST_U];
-#pragma unroll
-      for (int uu = 0; uu < ST_U; ++uu) {
-        const int j = j0 + uu * ngrp;
-        h4[uu] = j < n ? *reinterpret_cast<const f32x4*>(hb + (int64_t)j * d + 4 * l) : f32x4{0.f, 0.f, 0.f, 0.f};
-      }
-#pragma unroll
-      for (int uu = 0; uu < ST_U; ++uu) {
-        const int j = j0 + uu * ngrp;
-        const float pj = j < n ? P[hh * n + j] * inv : 0.f;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) acc[e] = fmaf(pj, h4[uu][e], acc[e]);
-      }
-    }
-    *reinterpret_cast<f32x4*>(part + grp * d + 4 * l) = acc;
-    __syncthreads();
-    for (int c = tid; c < d; c += ST_NT) {
-      float t = 0.f;
-      for (int g = 0; g < ngrp; ++g) t += part[g * d + c];
-      u[hh * d + c] = t;
-    }
-    __syncthreads();
-  }
-  for (int hh = 0; hh < H; ++hh)                                // o_h = Wv_h u_h + bv_h
-    st_gemv(wv + (int64_t)hh * hd * d, bv + hh * hd, u + hh * d, hd, d, o + hh * hd);
-  __syncthreads();
-  st_gemv(a.wo, a.bo, o, d, d, x1);                             // out_proj
-  __syncthreads();
-  for (int c = tid; c < d; c += ST_NT) x1[c] += xl[c];            // residual (model.py:84)
-  __syncthreads();
-  st_layernorm(x1, a.ln_f_w, a.ln_f_b, d, a.eps, l1, stat);
-  st_gemv(a.w1, a.b1, l1, a.mlp, d, fh);
-  __syncthreads();
-  for (int c = tid; c < a.mlp; c += ST_NT) fh[c] = fh[c] < 0.f ? 0.f : fh[c];
-  __syncthreads();
-  st_gemv(a.w2, a.b2, fh, d, a.mlp, o);                         // W2 f + b2 (o reused)
-  __syncthreads();
-  for (int c = tid; c < d; c += ST_NT) x1[c] += o[c];             // residual (model.py:94)
-  __syncthreads();
-  st_layernorm(x1, a.ln_w, a.ln_b, d, a.eps, l1, stat);         // last_layernorm (model.py:96)
-  for (int c = tid; c < d; c += ST_NT) out[b * d + c] = l1[c];
-}
-
 // A GEMV's first row chunk (rows grp + u ngrp, u < ST_U: every row when rows <= ST_U ngrp) and its
-// biases, loaded ahead of the vector it multiplies (tail_h=2): the kernel is a chain of dependent
+// biases, loaded ahead of the vector it multiplies: the kernel is a chain of dependent
 // phases, and each L2 round trip of the weights now overlaps the phase before.  The biases travel
 // with the rows, so no later load waits behind a prefetch in the in-order load counter.
 struct GemvRows {
@@ -440,12 +180,15 @@ __device__ __forceinline__ void st_gemv_finish(const float* __restrict__ W, cons
   }
 }
 
-// tail_h=2 (default): sas_tail_h_kernel's block with (1) ONE pass over the H rows -- each lane
-// group keeps an online softmax (running max m, sum l, and u = sum_j e^(s_j - m) H_j) over its keys,
-// and the groups' states are merged in group order (the old form read H twice: scores, then u);
+// The kernel (one workgroup per sequence): (1) ONE pass over the H rows -- each lane group keeps an
+// online softmax (running max m, sum l, and u = sum_j e^(s_j - m) H_j) over its keys, and the
+// groups' states are merged in group order (round 3's two-pass form read H twice, 106 vs 56 MB per
+// C5 launch: 48 -> 39 us; it and the K|V form, which projected K|V of all B n rows first, were
+// removed in round 5);
 // (2) every GEMV's weights and biases loaded one or two phases ahead (GemvRows), and the LayerNorm
-// weights staged in LDS at the start; <= 128 VGPRs, so two workgroups (sequences) share a CU.  Same math; the softmax's fp32 rounding differs from the
-// two-pass form (within the logits tolerance, tests/test_sasrec_gpu.py::test_tail_h_form_*).
+// weights staged in LDS at the start; <= 128 VGPRs, so two workgroups (sequences) share a CU.  The
+// reassociated sums round differently from the reference formulation, within the logits
+// tolerance (tests/test_sasrec_gpu.py::test_tail_h_form_vs_full_block_and_oracle).
 // HM = the number of heads (a power of two <= 8).
 template <int HM>
 __global__ __launch_bounds__(ST_NT, 2) void sas_tail_h2_kernel(const SasTailArgs a, const float* __restrict__ X,
@@ -487,7 +230,7 @@ __global__ __launch_bounds__(ST_NT, 2) void sas_tail_h2_kernel(const SasTailArgs
   st_gemv_finish(a.wq, a.bq, hl, d, d, q, g0);
   st_gemv_issue(wv, bv, hd, d, g0);                 // head 0's W_v rows, used after the H pass
   __syncthreads();
-  if (GR_TDIAG != 3) {   // q'_h = W_k,h^T q_h (sas_tail_h_kernel's order)
+  if (GR_TDIAG != 3) {   // q'_h = W_k,h^T q_h
     const float* qh = q + kh * hd;
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -594,10 +337,8 @@ __global__ __launch_bounds__(ST_NT, 2) void sas_tail_h2_kernel(const SasTailArgs
 }  // namespace gr
 
 // Returns GR_ERR_UNSUPPORTED for shapes outside the kernel's limits (the caller keeps the
-// layer-wise final block).  X: [B, n, d] residual stream entering the final block; KV: [B, n, 2d]
-// = LN_a(X) . W_in[d:3d]^T + b_in[d:3d]; out: [B, d] = the final hidden state of position n-1.
-// The shapes sas_tail_kernel covers: lane groups of k/4 lanes (k = d for the scores / V / Wq / Wo /
-// W1 reads, k = mlp for W2), at most 8 heads and 1024 keys.
+// layer-wise final block): lane groups of k/4 lanes (k = d for the scores / Wq / Wo / W1 reads,
+// k = mlp for W2), at most 8 heads and 1024 keys.
 bool gr_sasrec_tail_ok(const gr_sasrec_params* p, int32_t n) {
   using namespace gr;
   const int d = p->d, H = p->n_heads;
@@ -606,30 +347,9 @@ bool gr_sasrec_tail_ok(const gr_sasrec_params* p, int32_t n) {
            n > ST_MAX_N || p->mlp > ST_MAX_MLP || p->mlp % 4 || !pow2(p->mlp / 4) || p->mlp / 4 > 64);
 }
 
-int gr_sasrec_tail_launch(const gr_sasrec_params* p, int blk, const float* X, const float* KV,
-                          int64_t B, int32_t n, float* out, hipStream_t st) {
-  using namespace gr;
-  const int d = p->d, H = p->n_heads;
-  if (!gr_sasrec_tail_ok(p, n) || B > 0x7fffffffLL) return GR_ERR_UNSUPPORTED;
-  SasTailArgs a;
-  a.ln_a_w = p->attn_ln_w[blk]; a.ln_a_b = p->attn_ln_b[blk];
-  a.wq = p->in_proj_w[blk];     a.bq = p->in_proj_b[blk];
-  a.wo = p->out_proj_w[blk];    a.bo = p->out_proj_b[blk];
-  a.ln_f_w = p->ffn_ln_w[blk];  a.ln_f_b = p->ffn_ln_b[blk];
-  a.w1 = p->ffn1_w[blk];        a.b1 = p->ffn1_b[blk];
-  a.w2 = p->ffn2_w[blk];        a.b2 = p->ffn2_b[blk];
-  a.ln_w = p->last_ln_w;        a.ln_b = p->last_ln_b;
-  const float* ptrs[] = {a.wq, a.wo, a.w1, a.w2, X, KV};
-  for (const float* q : ptrs)
-    if (!aligned16(q)) return GR_ERR_UNSUPPORTED;
-  a.d = d; a.n = n; a.heads = H; a.mlp = p->mlp; a.eps = p->eps;
-  a.scale = (float)std::sqrt(1.0 / (double)(d / H));
-  hipLaunchKernelGGL(sas_tail_kernel, dim3((unsigned)B), dim3(ST_NT), 0, st, a, X, KV, out);
-  return check_launch("sasrec tail");
-}
-
-// The K/V-free form (sas_tail_h_kernel): Hs [B, n, d] = LN_a(X) of the final block (the LayerNorm
-// output the K|V projection would have read).  Same shape limits as gr_sasrec_tail_launch.
+// X: [B, n, d] residual stream entering the final block; Hs [B, n, d] = LN_a(X) of the final block
+// (the LayerNorm output the K|V projection would have read); out: [B, d] = the final hidden state
+// of position n-1.
 int gr_sasrec_tail_h_launch(const gr_sasrec_params* p, int blk, const float* X, const float* Hs,
                             int64_t B, int32_t n, float* out, hipStream_t st) {
   using namespace gr;
@@ -651,15 +371,11 @@ int gr_sasrec_tail_h_launch(const gr_sasrec_params* p, int blk, const float* X, 
     if (!aligned16(q)) return GR_ERR_UNSUPPORTED;
   a.d = d; a.n = n; a.heads = H; a.mlp = p->mlp; a.eps = p->eps;
   a.scale = (float)std::sqrt(1.0 / (double)(d / H));
-  if (option("tail_h") == 2) {
-    switch (H) {
-      case 1: hipLaunchKernelGGL(sas_tail_h2_kernel<1>, dim3((unsigned)B), dim3(ST_NT), 0, st, a, X, Hs, wk, wv, bv, out); break;
-      case 2: hipLaunchKernelGGL(sas_tail_h2_kernel<2>, dim3((unsigned)B), dim3(ST_NT), 0, st, a, X, Hs, wk, wv, bv, out); break;
-      case 4: hipLaunchKernelGGL(sas_tail_h2_kernel<4>, dim3((unsigned)B), dim3(ST_NT), 0, st, a, X, Hs, wk, wv, bv, out); break;
-      default: hipLaunchKernelGGL(sas_tail_h2_kernel<8>, dim3((unsigned)B), dim3(ST_NT), 0, st, a, X, Hs, wk, wv, bv, out); break;
-    }
-    return check_launch("sasrec tail (H form, one pass)");
+  switch (H) {
+    case 1: hipLaunchKernelGGL(sas_tail_h2_kernel<1>, dim3((unsigned)B), dim3(ST_NT), 0, st, a, X, Hs, wk, wv, bv, out); break;
+    case 2: hipLaunchKernelGGL(sas_tail_h2_kernel<2>, dim3((unsigned)B), dim3(ST_NT), 0, st, a, X, Hs, wk, wv, bv, out); break;
+    case 4: hipLaunchKernelGGL(sas_tail_h2_kernel<4>, dim3((unsigned)B), dim3(ST_NT), 0, st, a, X, Hs, wk, wv, bv, out); break;
+    default: hipLaunchKernelGGL(sas_tail_h2_kernel<8>, dim3((unsigned)B), dim3(ST_NT), 0, st, a, X, Hs, wk, wv, bv, out); break;
   }
-  hipLaunchKernelGGL(sas_tail_h_kernel, dim3((unsigned)B), dim3(ST_NT), 0, st, a, X, Hs, wk, wv, bv, out);
-  return check_launch("sasrec tail (H form)");
+  return check_launch("sasrec tail (H form, one pass)");
 }

@@ -1,40 +1,34 @@
 // Full-catalog scoring logits[B, rows] = h[B, d] . table[rows, d]^T for small d (SASRec/model.py:107)
 //
-// The reduction is short (d = 32..128) and the output is huge (B x rows fp32: 819 MB at C3), so the
-// kernel is built around the output stream.  Measured on MI355X (scripts/ab_score.py): the MFMA
-// work alone and the store stream alone each take roughly the whole budget, and a wave that issues
-// both serialises them (a store that cannot issue holds up the wave's next MFMA).  So the roles are
-// split between the two waves of every SIMD:
-//   * workgroup = 2 CW = 8 waves, one workgroup per CU; 64 CW = 256 users, one contiguous slice of
-//     the catalog walked in CHUNKS of 32 items;
-//   * waves 0..CW-1 (compute): each keeps 64 users' hidden states in registers (2 MFMA row tiles, the A
-//     operand) and per chunk runs 2 x (d/2) v_mfma_f32_32x32x2_f32 against the chunk's table rows
-//     (LDS, rows padded to d+4 floats: conflict-free ds_read_b128), then writes its 64x32 logits
-//     tile into an LDS output ring (3 chunks deep);
-//   * waves CW..2CW-1 (store): per chunk, stream the table rows of the NEXT chunk HBM -> LDS, and write
-//     the PREVIOUS chunk's logits to HBM.  The reference's row stride N+1 is odd, so a logits row
-//     starts at an arbitrary dword of a 128-byte line; the store waves therefore write, for every
-//     row, the 32 items that fill one WHOLE line (they straddle two chunks of the ring), so each
-//     store instruction writes two complete, aligned lines of two rows and no line is ever written
-//     in pieces except at the two ends of a slice;
-//   * one barrier per chunk hands the ring and the table buffers over between the roles.
-// Every logit is the same k-ordered fp32 fma chain whatever its position (step s of 32-deep group g
-// takes features 32g + 8(s>>2) + (s&3) + 4h, h = lane half), so a target's logit recomputed in any
-// shard or batch position is bit-identical — the strict '>' rank never counts the target itself
+// The reduction is short (d = 16..128) and the output is huge (B x rows fp32: 819 MB at C3), so the
+// kernels are built around the output stream.  Three forms, chosen by the logits layout (launcher
+// at the end):
+//   * score_direct_kernel: every logits row on a 128-byte line (row stride a multiple of 32) or the
+//     logits small enough for the Infinity Cache to merge partial lines: accumulators stored as
+//     they stand, between the next chunk's MFMAs;
+//   * score_rot_kernel (d <= 64): the reference's contiguous [B, N+1] layout (odd row stride) above
+//     the Infinity Cache size: lanes rotated by each row's line offset, whole lines stored;
+//   * score_kernel (d = 128, the same layout; the rotated form spills at d = 128): compute / store
+//     wave specialisation through an LDS ring:
+//       - workgroup = 8 waves, one workgroup per CU; 4 compute waves = 256 users, one contiguous
+//         slice of the catalog walked in CHUNKS of 32 items;
+//       - compute waves keep 64 users' hidden states in registers (2 MFMA row tiles, the A operand)
+//         and per chunk run 2 x (d/2) v_mfma_f32_32x32x2_f32 against the chunk's table rows (LDS,
+//         rows padded to d+4 floats: conflict-free ds_read_b128), then write their 64x32 logits
+//         tile into an LDS output ring (3 chunks deep);
+//       - store waves stream the table rows of the NEXT chunk HBM -> LDS and write the PREVIOUS
+//         chunk's logits to HBM as whole, aligned 128-byte lines of each row (the 32 items that
+//         fill a line straddle two chunks of the ring); one barrier per chunk hands over.
+// Every logit is the same k-ordered fp32 fma chain whatever its position (gr_common.h sc_feat: step
+// s of float4 group gq takes feature 8 gq + s, then 8 gq + 4 + s), so a target's logit recomputed in
+// any shard or batch position is bit-identical — the strict '>' rank never counts the target itself
 // (SURVEY §7 hard part 3).
 #include "gr_common.h"
 
 namespace gr {
 
 constexpr int SC_CHUNK = 32;   // items per chunk (one 32-item MFMA tile)
-// compute waves per workgroup (64 users each) and as many store waves.  4: one compute and one
-// store wave on every SIMD.  (2, with two workgroups per CU, measured 1.3x slower at C3: the
-// dispatcher may stack both workgroups' compute waves on the same two SIMDs.)
-// Compute waves per workgroup (256 users: 64 per wave as two 32-user MFMA tiles).  8 waves of 32
-// users (two per SIMD, so one wave's ring epilogue overlaps the other's MFMAs) measured no faster
-// at d = 64 (375 vs 372 us at C3); the kernel keeps the generality (UT tiles per wave).
-template <int D, bool FLAGS = false> struct ScCW { static constexpr int value = 4; };
-constexpr int SC_RING = 3;     // chunks of logits staged in LDS
+constexpr int SC_RING = 3;     // chunks of logits staged in LDS (ring kernel)
 
 // Line alignment of a logits row: the first item of a 128-byte line in row ul (mod 32), given the
 // dword index mod 32 of the workgroup's first row (pbase) and the row stride ld.
@@ -42,79 +36,40 @@ __device__ __forceinline__ int line_shift(uint32_t pbase, int ul, int64_t ld) {
   return (int)((32u - ((pbase + (uint32_t)((int64_t)ul * ld)) & 31u)) & 31u);
 }
 
-// Intra-workgroup hand-off through LDS words (FLAGS variant): a wave publishes after its own LDS
-// traffic has retired (lgkmcnt(0)), one lane writes the word; a waiting wave polls with relaxed
-// loads and s_sleep.  Global stores stay in flight across a publish (no vmcnt wait).
-__device__ __forceinline__ void lds_publish_add(int* w, int v, int lane) {
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  if (lane == 0) __hip_atomic_fetch_add(w, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-__device__ __forceinline__ void lds_publish_set(int* w, int v, int lane) {
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  if (lane == 0) __hip_atomic_store(w, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-__device__ __forceinline__ void lds_wait_ge(int* w, int target) {
-  while (__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < target)
-    __builtin_amdgcn_s_sleep(1);
-  asm volatile("" ::: "memory");
-}
-// every one of the N words w[0..N) >= target (per-wave progress counters: a sum could be met by
-// one wave running ahead while another has not finished its part)
-template <int N>
-__device__ __forceinline__ void lds_wait_all_ge(int* w, int target) {
-  while (true) {
-    int m = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-#pragma unroll
-    for (int i = 1; i < N; ++i) m = min(m, __hip_atomic_load(w + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
-    if (m >= target) break;
-    __builtin_amdgcn_s_sleep(1);
-  }
-  asm volatile("" ::: "memory");
-}
+// Table-chunk staging by 256 threads: float4 slot f of a chunk is row f / (D/4), column 4 (f % (D/4));
+// d = 16 leaves half the threads idle.
+template <int D> struct ScStage {
+  static constexpr int NF = SC_CHUNK * D / 4;
+  static constexpr int LV = (NF + 255) / 256;
+};
 
-// Store waves per workgroup (64 logits rows each).  8 waves of 32 rows were measured 1.6x slower
-// at d = 64: the compute waves spill at 3 waves per SIMD.
-template <int D, bool FLAGS> struct ScSW { static constexpr int value = 4; };
-
-template <int D, bool FLAGS>
-__global__ __launch_bounds__(64 * (ScCW<D, FLAGS>::value + ScSW<D, FLAGS>::value), 1) void score_kernel(const float* __restrict__ h, int64_t B,
+// The ring kernel (see the header): 4 compute + 4 store waves, one workgroup per CU; the XCD's
+// workgroups share one user block and sweep the catalog.
+template <int D>
+__global__ __launch_bounds__(512, 1) void score_kernel(const float* __restrict__ h, int64_t B,
                                                    const float* __restrict__ table, int64_t rows,
                                                    float* __restrict__ out, int64_t ld,
-                                                   int ublocks, int slices, int ubmajor) {
-  constexpr int KG = D / 32;                       // 32-deep k groups
+                                                   int ublocks, int slices) {
+  constexpr int NQ = D / 8;                        // float4 feature groups (sc_feat)
   constexpr int P = D + 4;                         // LDS table row pitch (floats)
-  constexpr int CW = ScCW<D, FLAGS>::value, SC_USERS = 256;   // compute waves; users per workgroup
-  constexpr int UT = SC_USERS / (32 * CW);                     // 32-user MFMA tiles per compute wave
-  constexpr int UPW = 32 * UT;                                 // users per compute wave
-  constexpr int SWN = ScSW<D, FLAGS>::value;       // store waves
+  constexpr int CW = 4, SC_USERS = 256;            // compute waves; users per workgroup
+  constexpr int UT = SC_USERS / (32 * CW);         // 32-user MFMA tiles per compute wave
+  constexpr int UPW = 32 * UT;                     // users per compute wave
+  constexpr int SWN = 4;                           // store waves
   constexpr int RPW = SC_USERS / SWN;              // logits rows per store wave
   constexpr int SI = RPW / 8;                      // store instructions (8 rows each) per line
-  constexpr int LV = SC_CHUNK * D / 4 / 256;        // float4 per staging thread per chunk (256 threads)
-  constexpr int LVC = SC_CHUNK * D / 4 / (64 * CW);  // ... per compute-wave thread (FLAGS staging)
-  static_assert(LVC >= 1, "table chunk too small for the compute waves to stage");
+  constexpr int LV = ScStage<D>::LV;               // float4 per staging thread per chunk (256 threads)
   constexpr int RW = SC_RING * SC_CHUNK;           // ring width per user row (items)
   __shared__ __attribute__((aligned(16))) float tab[2][SC_CHUNK * P];
   __shared__ __attribute__((aligned(16))) float ring[SC_USERS * RW];
-  // FLAGS variant: the compute waves stage the table themselves (so the store waves issue no
-  // vector-memory loads, and no vmcnt wait for a load ever drains their stores), and the roles
-  // hand over through LDS words instead of one barrier per chunk: [w] table chunks compute wave w
-  // has staged (its quarter), [CW + w] table chunks it has consumed, [2CW + w] chunks of logits it
-  // has put in the ring, [3CW + sw] lines store wave sw has taken out of the ring.
-  __shared__ __attribute__((aligned(16))) int sy[3 * ScCW<D, FLAGS>::value + ScSW<D, FLAGS>::value];
   const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, hh = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wgid = xcd_remap(blockIdx.x, gridDim.x);
-  // slice-major within an XCD: the 32 workgroups an XCD runs share one user block and sweep the
-  // catalog (logits rows of one block, whole row range), not one column band of every row
-  const int ub = ubmajor ? wgid / slices : wgid % ublocks;
-  const int sl = ubmajor ? wgid % slices : wgid / ublocks;
+  const int ub = wgid / slices, sl = wgid % slices;
+  (void)ublocks;
   const int64_t chunks = (rows + SC_CHUNK - 1) / SC_CHUNK;
   const int64_t c_begin = chunks * sl / slices, c_end = chunks * (sl + 1) / slices;
   if (c_begin >= c_end) return;   // whole workgroup: uniform
-  if (FLAGS) {
-    if (tid < 3 * CW + SWN) sy[tid] = 0;
-    __syncthreads();
-  }
   const int64_t s_lo = c_begin * SC_CHUNK;
   const int64_t s_hi = c_end * SC_CHUNK < rows ? c_end * SC_CHUNK : rows;
   const int64_t ubase = (int64_t)ub * SC_USERS;   // first user of the workgroup
@@ -128,18 +83,16 @@ __global__ __launch_bounds__(64 * (ScCW<D, FLAGS>::value + ScSW<D, FLAGS>::value
   if (wave < CW) {
     // ------------------------------------------------------------------ compute waves
     const int64_t u0 = ubase + wave * UPW;
-    f32x4 hf[UT][KG][4];   // lane (r, hh) of user tile ut: h[u][32g + 8q + 4hh .. +3]
+    f32x4 hf[UT][NQ];   // lane (r, hh) of user tile ut: h[u][sc_feat(gq, hh) .. +3]
 #pragma unroll
     for (int ut = 0; ut < UT; ++ut) {
       const int64_t u = u0 + ut * 32 + r;
       const int64_t uc = u < B ? u : B - 1;   // clamped load, zeroed below
 #pragma unroll
-      for (int g = 0; g < KG; ++g)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const f32x4 v = *reinterpret_cast<const f32x4*>(h + uc * D + 32 * g + 8 * q + 4 * hh);
-          hf[ut][g][q] = u < B ? v : f32x4{0.f, 0.f, 0.f, 0.f};
-        }
+      for (int gq = 0; gq < NQ; ++gq) {
+        const f32x4 v = *reinterpret_cast<const f32x4*>(h + uc * D + sc_feat(gq, hh));
+        hf[ut][gq] = u < B ? v : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
     }
     // ring position of item r of chunk 0 for each of the lane's 32 rows (register v of user
     // tile ut holds row 64 wave + 32 ut + rho(v) + 4 hh): (r - a) mod RW
@@ -152,87 +105,43 @@ __global__ __launch_bounds__(64 * (ScCW<D, FLAGS>::value + ScSW<D, FLAGS>::value
         const int p = r - line_shift(pbase, ul, ld);
         rpos[ut][v] = ul * RW + (p < 0 ? p + RW : p);
       }
-    f32x4 cst[LVC];   // FLAGS: this wave's share of the next table chunk, loaded a chunk ahead
-    auto cgload = [&](int64_t c) {
-#pragma unroll
-      for (int i = 0; i < LVC; ++i) {
-        const int f = tid + 64 * CW * i, row = f / (D / 4), col = (f % (D / 4)) * 4;
-        int64_t item = c * SC_CHUNK + row;
-        item = item < rows ? item : rows - 1;   // past-the-end items are never stored
-        cst[i] = *reinterpret_cast<const f32x4*>(table + item * D + col);
-      }
-    };
-    auto cswrite = [&](int b) {
-#pragma unroll
-      for (int i = 0; i < LVC; ++i) {
-        const int f = tid + 64 * CW * i, row = f / (D / 4), col = (f % (D / 4)) * 4;
-        *reinterpret_cast<f32x4*>(&tab[b][row * P + col]) = cst[i];
-      }
-    };
-    if (FLAGS) {
-      cgload(c_begin);
-      cswrite(0);
-      lds_publish_set(&sy[wave], 1, lane);   // table chunk 0: this wave's quarter staged
-      if (c_begin + 1 < c_end) cgload(c_begin + 1);
-    } else {
-      __syncthreads();   // table chunk c_begin staged by the store waves
-    }
-    {
-      int cm = (int)((c_begin * SC_CHUNK) % RW);   // 32k mod RW
+    __syncthreads();   // table chunk c_begin staged by the store waves
+    int cm = (int)((c_begin * SC_CHUNK) % RW);   // 32k mod RW
 #pragma unroll 1
-      for (int64_t k = c_begin; k < c_end; ++k) {
-        const int kb = (int)((k - c_begin) & 1);
-        const int j = (int)(k - c_begin);
-        if (FLAGS) lds_wait_all_ge<CW>(&sy[0], j + 1);   // table chunk j staged by every compute wave
-        f32x16 acc[UT];
+    for (int64_t k = c_begin; k < c_end; ++k) {
+      const int kb = (int)((k - c_begin) & 1);
+      f32x16 acc[UT];
 #pragma unroll
-        for (int ut = 0; ut < UT; ++ut)
+      for (int ut = 0; ut < UT; ++ut)
 #pragma unroll
-          for (int v = 0; v < 16; ++v) acc[ut][v] = 0.f;
-        const float* tb = &tab[kb][r * P + 4 * hh];
+        for (int v = 0; v < 16; ++v) acc[ut][v] = 0.f;
+      const float* tb = &tab[kb][r * P + 4 * hh];
 #pragma unroll
-        for (int g = 0; g < KG; ++g)
+      for (int gq = 0; gq < NQ; ++gq) {
+        const f32x4 bt = *reinterpret_cast<const f32x4*>(tb + 8 * gq);
 #pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const f32x4 bt = *reinterpret_cast<const f32x4*>(tb + 32 * g + 8 * q);
+        for (int s = 0; s < 4; ++s)
 #pragma unroll
-            for (int s = 0; s < 4; ++s)
-#pragma unroll
-              for (int ut = 0; ut < UT; ++ut) acc[ut] = mfma32(hf[ut][g][q][s], bt[s], acc[ut]);
-          }
-        if (FLAGS) {
-          lds_publish_set(&sy[CW + wave], j + 1, lane);   // done reading table chunk j
-          if (k + 1 < c_end) {   // stage chunk j+1 into the buffer chunk j-1 used
-            lds_wait_all_ge<CW>(&sy[CW], j);              // ... once every wave is done with j-1
-            cswrite((j + 1) & 1);
-            lds_publish_set(&sy[wave], j + 2, lane);
-            if (k + 2 < c_end) cgload(k + 2);             // a whole chunk period ahead
-          }
-          // its ring slots drained by the store wave of its rows
-          lds_wait_ge(&sy[3 * CW + wave * UPW / RPW], j + 2 - SC_RING);
-        }
-        // logits tile -> ring (row-shifted); a position past the row's RW wraps back by RW
-#pragma unroll
-        for (int ut = 0; ut < UT; ++ut)
-#pragma unroll
-          for (int v = 0; v < 16; ++v) {
-            const int ul_end = (wave * UPW + ut * 32 + (v & 3) + 8 * (v >> 2) + 4 * hh + 1) * RW;
-            const int p = rpos[ut][v] + cm;
-            ring[p >= ul_end ? p - RW : p] = acc[ut][v];
-          }
-        if (FLAGS) lds_publish_set(&sy[2 * CW + wave], j + 1, lane);
-        else __syncthreads();
-        cm = cm + SC_CHUNK == RW ? 0 : cm + SC_CHUNK;
+          for (int ut = 0; ut < UT; ++ut) acc[ut] = mfma32(hf[ut][gq][s], bt[s], acc[ut]);
       }
-      if (!FLAGS) __syncthreads();   // the store waves' final iteration
+      // logits tile -> ring (row-shifted); a position past the row's RW wraps back by RW
+#pragma unroll
+      for (int ut = 0; ut < UT; ++ut)
+#pragma unroll
+        for (int v = 0; v < 16; ++v) {
+          const int ul_end = (wave * UPW + ut * 32 + (v & 3) + 8 * (v >> 2) + 4 * hh + 1) * RW;
+          const int p = rpos[ut][v] + cm;
+          ring[p >= ul_end ? p - RW : p] = acc[ut][v];
+        }
+      __syncthreads();
+      cm = cm + SC_CHUNK == RW ? 0 : cm + SC_CHUNK;
     }
+    __syncthreads();   // the store waves' final iteration
     // (Spreading the ring writes of chunk j-1 between the MFMAs of chunk j was measured slower:
     // 341 vs 296 us at C3.)
   } else {
     // ------------------------------------------------------------------ store waves
     const int sw = wave - CW, stid = tid - 64 * CW;
-    constexpr int CPS = RPW / UPW;               // compute waves whose rows one store wave writes
-    const int cw_of = sw * CPS;                  // the first of them
     // table chunks are loaded two chunks ahead (register double buffer): the HBM / L2 latency
     // spans a whole chunk period instead of being exposed before every barrier
     f32x4 st[2][LV];
@@ -242,21 +151,19 @@ __global__ __launch_bounds__(64 * (ScCW<D, FLAGS>::value + ScSW<D, FLAGS>::value
         const int f = stid + 256 * i, row = f / (D / 4), col = (f % (D / 4)) * 4;
         int64_t item = c * SC_CHUNK + row;
         item = item < rows ? item : rows - 1;   // past-the-end items are never stored
-        st[sb][i] = *reinterpret_cast<const f32x4*>(table + item * D + col);
+        if (f < ScStage<D>::NF) st[sb][i] = *reinterpret_cast<const f32x4*>(table + item * D + col);
       }
     };
     auto swrite = [&](int b, int sb) {
 #pragma unroll
       for (int i = 0; i < LV; ++i) {
         const int f = stid + 256 * i, row = f / (D / 4), col = (f % (D / 4)) * 4;
-        *reinterpret_cast<f32x4*>(&tab[b][row * P + col]) = st[sb][i];
+        if (f < ScStage<D>::NF) *reinterpret_cast<f32x4*>(&tab[b][row * P + col]) = st[sb][i];
       }
     };
-    if (!FLAGS) {
-      gload(c_begin, 0);
-      if (c_begin + 1 < c_end) gload(c_begin + 1, 1);
-      swrite(0, 0);
-    }
+    gload(c_begin, 0);
+    if (c_begin + 1 < c_end) gload(c_begin + 1, 1);
+    swrite(0, 0);
     // Store instruction i covers local rows RPW sw + 8i + (lane >> 3); lane part e = lane & 7
     // holds items 4e..4e+3 of the row's line [32c - 32 + a, 32c + a) for chunk c: 8 rows x one
     // whole, aligned 128-byte line per instruction (dwordx4 per lane).  Descriptor 32 items before
@@ -289,17 +196,12 @@ __global__ __launch_bounds__(64 * (ScCW<D, FLAGS>::value + ScSW<D, FLAGS>::value
         }
       }
     };
-    if (!FLAGS) __syncthreads();
+    __syncthreads();
     // ring position of the line read at iteration k (the line ending in chunk k-1): 32(k-2) mod RW
     int lm = (int)((((c_begin - 2) * SC_CHUNK) % RW + RW) % RW);
     auto iter = [&](int64_t k, auto par_sel) {   // par = (k - c_begin) & 1: register buffer of chunk k+1
       constexpr int par = decltype(par_sel)::value;
-      if (!FLAGS && k + 2 < c_end) gload(k + 2, par);   // chunk k+2 into the buffer chunk k freed
-      const int j = (int)(k - c_begin);
-      if (FLAGS && k > c_begin) {   // chunk k-1 in the ring, from every compute wave of these rows
-#pragma unroll
-        for (int q = 0; q < CPS; ++q) lds_wait_ge(&sy[2 * CW + cw_of + q], j);
-      }
+      if (k + 2 < c_end) gload(k + 2, par);   // chunk k+2 into the buffer chunk k freed
       if (k > c_begin) {   // the line ending inside chunk c = k-1 (k-2 still held)
         const int64_t c = k - 1, c0 = c * SC_CHUNK;
         const int soff = (int)(c0 * 4);
@@ -320,11 +222,8 @@ __global__ __launch_bounds__(64 * (ScCW<D, FLAGS>::value + ScSW<D, FLAGS>::value
           for (int i = 0; i < SI; ++i) store_items(i, c + 1, s_lo, s_hi, lt);
         }
       }
-      if (FLAGS && k > c_begin) lds_publish_set(&sy[3 * CW + sw], j, lane);   // line k-1 taken
-      if (!FLAGS) {
-        if (k + 1 < c_end) swrite(par ^ 1, par ^ 1);
-        __syncthreads();
-      }
+      if (k + 1 < c_end) swrite(par ^ 1, par ^ 1);
+      __syncthreads();
       lm = lm + SC_CHUNK == RW ? 0 : lm + SC_CHUNK;
     };
     int64_t k = c_begin;
@@ -337,7 +236,7 @@ __global__ __launch_bounds__(64 * (ScCW<D, FLAGS>::value + ScSW<D, FLAGS>::value
   }
 }
 
-// Direct-store variant (option score_impl = 1): no store waves and no ring.  Each of the 4 waves
+// Direct-store variant: no store waves and no ring.  Each of the 4 waves
 // scores 64 users against the chunk and writes its accumulators as they stand: register v of lane
 // (r, h) is row (v&3) + 8(v>>2) + 4h, column r, so one dword store per register covers two rows x
 // 32 consecutive logits (two 128-B segments, unaligned when the row stride is odd: the next
@@ -348,9 +247,9 @@ __global__ __launch_bounds__(256, 2) void score_direct_kernel(const float* __res
                                                             const float* __restrict__ table, int64_t rows,
                                                             float* __restrict__ out, int64_t ld,
                                                             int ublocks, int slices, int slice_major) {
-  constexpr int KG = D / 32;
+  constexpr int NQ = D / 8;
   constexpr int P = D + 4;
-  constexpr int LV = SC_CHUNK * D / 4 / 256;
+  constexpr int LV = ScStage<D>::LV;
   __shared__ __attribute__((aligned(16))) float tab[2][SC_CHUNK * P];
   const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, hh = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -363,18 +262,16 @@ __global__ __launch_bounds__(256, 2) void score_direct_kernel(const float* __res
   const int64_t c_begin = chunks * sl / slices, c_end = chunks * (sl + 1) / slices;
   if (c_begin >= c_end) return;
   const int64_t u0 = (int64_t)ub * 256 + wave * 64;
-  f32x4 hf[2][KG][4];
+  f32x4 hf[2][NQ];
 #pragma unroll
   for (int ut = 0; ut < 2; ++ut) {
     const int64_t u = u0 + ut * 32 + r;
     const int64_t uc = u < B ? u : B - 1;
 #pragma unroll
-    for (int g = 0; g < KG; ++g)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const f32x4 v = *reinterpret_cast<const f32x4*>(h + uc * D + 32 * g + 8 * q + 4 * hh);
-        hf[ut][g][q] = u < B ? v : f32x4{0.f, 0.f, 0.f, 0.f};
-      }
+    for (int gq = 0; gq < NQ; ++gq) {
+      const f32x4 v = *reinterpret_cast<const f32x4*>(h + uc * D + sc_feat(gq, hh));
+      hf[ut][gq] = u < B ? v : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
   }
   // row pointers of the lane's 32 rows (register v of user tile ut), column r
   const bool full_rows = u0 + 64 <= B;
@@ -385,14 +282,14 @@ __global__ __launch_bounds__(256, 2) void score_direct_kernel(const float* __res
       const int f = tid + 256 * i, row = f / (D / 4), col = (f % (D / 4)) * 4;
       int64_t item = c * SC_CHUNK + row;
       item = item < rows ? item : rows - 1;
-      st[i] = *reinterpret_cast<const f32x4*>(table + item * D + col);
+      if (f < ScStage<D>::NF) st[i] = *reinterpret_cast<const f32x4*>(table + item * D + col);
     }
   };
   auto swrite = [&](int b) {
 #pragma unroll
     for (int i = 0; i < LV; ++i) {
       const int f = tid + 256 * i, row = f / (D / 4), col = (f % (D / 4)) * 4;
-      *reinterpret_cast<f32x4*>(&tab[b][row * P + col]) = st[i];
+      if (f < ScStage<D>::NF) *reinterpret_cast<f32x4*>(&tab[b][row * P + col]) = st[i];
     }
   };
   gload(c_begin);
@@ -415,7 +312,7 @@ __global__ __launch_bounds__(256, 2) void score_direct_kernel(const float* __res
     }
     else if (u0 + rl < B && col < rows) *op = prev[ut][v];
   };
-  constexpr int STEPS = KG * 16;             // (g, q, s) steps of a chunk, 2 MFMAs each
+  constexpr int STEPS = NQ * 4;              // (gq, s) steps of a chunk, 2 MFMAs each
   constexpr int PER = 32 / STEPS > 0 ? 32 / STEPS : 1;   // stores per step
   constexpr int EVERY = STEPS / 32 > 0 ? STEPS / 32 : 1;  // steps per store
 #pragma unroll 1
@@ -429,15 +326,13 @@ __global__ __launch_bounds__(256, 2) void score_direct_kernel(const float* __res
       for (int v = 0; v < 16; ++v) acc[ut][v] = 0.f;
     const float* tb = &tab[kb][r * P + 4 * hh];
 #pragma unroll
-    for (int g = 0; g < KG; ++g)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const f32x4 bt = *reinterpret_cast<const f32x4*>(tb + 32 * g + 8 * q);
+    for (int gq = 0; gq < NQ; ++gq) {
+        const f32x4 bt = *reinterpret_cast<const f32x4*>(tb + 8 * gq);
 #pragma unroll
         for (int s4 = 0; s4 < 4; ++s4) {
-          const int step = (g * 4 + q) * 4 + s4;
+          const int step = gq * 4 + s4;
 #pragma unroll
-          for (int ut = 0; ut < 2; ++ut) acc[ut] = mfma32(hf[ut][g][q][s4], bt[s4], acc[ut]);
+          for (int ut = 0; ut < 2; ++ut) acc[ut] = mfma32(hf[ut][gq][s4], bt[s4], acc[ut]);
           if (have_prev && step % EVERY == 0) {
 #pragma unroll
             for (int e = 0; e < PER; ++e) store_one((step / EVERY) * PER + e);
@@ -475,9 +370,9 @@ __global__ __launch_bounds__(256, 2) void score_rot_kernel(const float* __restri
                                                          const float* __restrict__ table, int64_t rows,
                                                          float* __restrict__ out, int64_t ld,
                                                          int ublocks, int slices, int slice_major) {
-  constexpr int KG = D / 32;
+  constexpr int NQ = D / 8;
   constexpr int P = D + 4;
-  constexpr int LV = SC_CHUNK * D / 4 / 256;
+  constexpr int LV = ScStage<D>::LV;
   __shared__ __attribute__((aligned(16))) float tab[2][SC_CHUNK * P];
   const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, hh = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -488,18 +383,16 @@ __global__ __launch_bounds__(256, 2) void score_rot_kernel(const float* __restri
   const int64_t c_begin = chunks * sl / slices, c_end = chunks * (sl + 1) / slices;
   if (c_begin >= c_end) return;
   const int64_t u0 = (int64_t)ub * 256 + wave * 64;
-  f32x4 hf[2][KG][4];
+  f32x4 hf[2][NQ];
 #pragma unroll
   for (int ut = 0; ut < 2; ++ut) {
     const int64_t u = u0 + ut * 32 + r;
     const int64_t uc = u < B ? u : B - 1;
 #pragma unroll
-    for (int g = 0; g < KG; ++g)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const f32x4 v = *reinterpret_cast<const f32x4*>(h + uc * D + 32 * g + 8 * q + 4 * hh);
-        hf[ut][g][q] = u < B ? v : f32x4{0.f, 0.f, 0.f, 0.f};
-      }
+    for (int gq = 0; gq < NQ; ++gq) {
+      const f32x4 v = *reinterpret_cast<const f32x4*>(h + uc * D + sc_feat(gq, hh));
+      hf[ut][gq] = u < B ? v : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
   }
   const bool full_rows = u0 + 64 <= B;
   // per register v: row rl(v) of user tile 0 (tile 1's row rl + 32 has the same line offset o,
@@ -527,14 +420,14 @@ __global__ __launch_bounds__(256, 2) void score_rot_kernel(const float* __restri
       const int f = tid + 256 * i, row = f / (D / 4), col = (f % (D / 4)) * 4;
       int64_t item = c * SC_CHUNK + row;
       item = item < rows ? item : rows - 1;
-      st[i] = *reinterpret_cast<const f32x4*>(table + item * D + col);
+      if (f < ScStage<D>::NF) st[i] = *reinterpret_cast<const f32x4*>(table + item * D + col);
     }
   };
   auto swrite = [&](int b) {
 #pragma unroll
     for (int i = 0; i < LV; ++i) {
       const int f = tid + 256 * i, row = f / (D / 4), col = (f % (D / 4)) * 4;
-      *reinterpret_cast<f32x4*>(&tab[b][row * P + col]) = st[i];
+      if (f < ScStage<D>::NF) *reinterpret_cast<f32x4*>(&tab[b][row * P + col]) = st[i];
     }
   };
   gload(c_begin);
@@ -564,7 +457,7 @@ __global__ __launch_bounds__(256, 2) void score_rot_kernel(const float* __restri
     }
   };
   auto line_interior = [&](int64_t L) { return full_rows && L > c_begin && (L + 1) * SC_CHUNK <= rows; };
-  constexpr int STEPS = KG * 16;                          // (g, q, s) steps of a chunk, 2 MFMAs each
+  constexpr int STEPS = NQ * 4;                           // (gq, s) steps of a chunk, 2 MFMAs each
   constexpr int PER = 32 / STEPS > 0 ? 32 / STEPS : 1;    // stores per step
   constexpr int EVERY = STEPS / 32 > 0 ? STEPS / 32 : 1;  // steps per store
 #pragma unroll 1
@@ -579,15 +472,13 @@ __global__ __launch_bounds__(256, 2) void score_rot_kernel(const float* __restri
       for (int v = 0; v < 16; ++v) acc[ut][v] = 0.f;
     const float* tb = &tab[kb][r * P + 4 * hh];
 #pragma unroll
-    for (int g = 0; g < KG; ++g)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const f32x4 bt = *reinterpret_cast<const f32x4*>(tb + 32 * g + 8 * q);
+    for (int gq = 0; gq < NQ; ++gq) {
+        const f32x4 bt = *reinterpret_cast<const f32x4*>(tb + 8 * gq);
 #pragma unroll
         for (int s4 = 0; s4 < 4; ++s4) {
-          const int step = (g * 4 + q) * 4 + s4;
+          const int step = gq * 4 + s4;
 #pragma unroll
-          for (int ut = 0; ut < 2; ++ut) acc[ut] = mfma32(hf[ut][g][q][s4], bt[s4], acc[ut]);
+          for (int ut = 0; ut < 2; ++ut) acc[ut] = mfma32(hf[ut][gq][s4], bt[s4], acc[ut]);
           if (inter && step % EVERY == 0) {
 #pragma unroll
             for (int e = 0; e < PER; ++e) store_reg(k - 1, (step / EVERY) * PER + e, true);
@@ -626,7 +517,7 @@ __global__ __launch_bounds__(256, 2) void score_rot_kernel(const float* __restri
 int gr_score_launch(const float* h, int64_t B, int32_t d, const float* table, int64_t rows,
                     float* logits, int64_t ld, hipStream_t st) {
   using namespace gr;
-  if (d != 32 && d != 64 && d != 128) return GR_ERR_UNSUPPORTED;
+  if (d != 16 && d != 32 && d != 64 && d != 128) return GR_ERR_UNSUPPORTED;
   if (!aligned16(h) || !aligned16(table) || (reinterpret_cast<uintptr_t>(logits) & 3))
     return GR_ERR_UNSUPPORTED;
   if (B == 0 || rows == 0) return GR_OK;
@@ -639,76 +530,58 @@ int gr_score_launch(const float* h, int64_t B, int32_t d, const float* table, in
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
       cus = 256;
   }
-  const int cw = 4, users = 64 * cw, per_cu = 4 / cw;
-  const int64_t ublocks = (B + users - 1) / users;
+  const int64_t ublocks = (B + 255) / 256;
   const int64_t chunks = (rows + SC_CHUNK - 1) / SC_CHUNK;
-  int64_t slices = (per_cu * cus + ublocks - 1) / ublocks;   // all workgroups resident at once
-  if (slices > chunks) slices = chunks;
-  if (slices < 1) slices = 1;
-  if (ublocks * slices > 0x7fffffffLL) return fail(GR_ERR_UNSUPPORTED, "gr_score_f32: grid too large");
-  const dim3 g((unsigned)(ublocks * slices));
-  const bool flags = option("score_flags") != 0 && d <= 64;   // d = 128 spills at 2 waves / SIMD
-  const int ubmajor = (int)option("score_ubmajor");
-  // Direct accumulator stores when every logits row starts on a 128-byte line (row stride a
-  // multiple of 32 floats, 128-B aligned base): 265 us vs the ring's 296 at C3 shapes.  The
-  // reference's own layout (stride N+1, odd) straddles lines and keeps the ring (456 vs 296 us).
-  int64_t impl = option("score_impl");
+  // direct / rotated kernels: two workgroups per CU; the ring kernel: one
+  auto slices_for = [&](int per_cu) {
+    int64_t sl = (per_cu * cus + ublocks - 1) / ublocks;   // all workgroups resident at once
+    if (sl > chunks) sl = chunks;
+    return sl < 1 ? (int64_t)1 : sl;
+  };
+  const int64_t sl2 = slices_for(2);
+  if (ublocks * sl2 > 0x7fffffffLL) return fail(GR_ERR_UNSUPPORTED, "gr_score_f32: grid too large");
+  const dim3 g2((unsigned)(ublocks * sl2)), blk(256);
+  // An XCD's workgroups share catalog slices across the user blocks (each table chunk read from
+  // HBM once per XCD; 255 vs 261 us at C3 against user-block-major, profiles/r02_ab_score_slice_major.txt).
+  const int smaj = 1;
+  // Every logits row on a 128-byte line (row stride a multiple of 32 floats, 128-B aligned base):
+  // direct accumulator stores with the streaming hint (265 vs the ring's 296 us at C3 shapes).
   const bool lines_aligned = ld % 32 == 0 && (reinterpret_cast<uintptr_t>(logits) & 127) == 0;
-  // Rows off the 128-byte grid (the reference's contiguous [B, N+1] logits, d <= 64): up to ~160 MB of
-  // logits the halves of every straddled line meet in the 256 MB Infinity Cache, so the direct
-  // kernel's plain stores cost nothing (C3 B 512: 136 vs 135 us padded); beyond it they reach HBM as
-  // partial lines (B 2048: 593 vs 393 us) and the rotated whole-line kernel runs (412 us;
-  // profiles/r04/ab_predict_contiguous.txt).
+  // Rows off the 128-byte grid (the reference's contiguous [B, N+1] logits): up to ~160 MB of logits
+  // the halves of every straddled line meet in the 256 MB Infinity Cache, so the direct kernel's
+  // plain stores cost nothing (C3 B 512: 136 vs 135 us padded); beyond it they reach HBM as partial
+  // lines (B 2048: 593 vs 393 us) and the rotated whole-line kernel runs (412 us;
+  // profiles/r04/ab_predict_contiguous.txt), or at d = 128 (where the rotated form spills) the ring.
   const bool fits_mall = (double)B * (double)ld * 4.0 <= 160e6;
-  if (!lines_aligned && d <= 64 && impl == 2 && fits_mall) impl = 3;
-  if (!lines_aligned && d <= 64 && (impl == 2 || impl == 4)) {   // rotated whole-line stores
-    int64_t sl2 = (2 * cus + ublocks - 1) / ublocks;
-    if (sl2 > chunks) sl2 = chunks;
-    if (sl2 < 1) sl2 = 1;
-    const dim3 g2((unsigned)(ublocks * sl2));
-    const int smaj = option("score_slice_major") != 0 ? 1 : 0;
-    const bool pre = impl == 2;   // store offsets precomputed per register (4: on the fly; A/B)
-    auto k = d == 32 ? (pre ? score_rot_kernel<32, true> : score_rot_kernel<32, false>)
-                     : (pre ? score_rot_kernel<64, true> : score_rot_kernel<64, false>);
-    hipLaunchKernelGGL(k, g2, dim3(256), 0, st, h, B, table, rows, logits, ld, (int)ublocks, (int)sl2, smaj);
-    return check_launch("gr_score_f32 (rotated lines)");
+#define GR_SC_DIRECT(DD, NTS) hipLaunchKernelGGL((score_direct_kernel<DD, NTS>), g2, blk, 0, st, h, B, table, rows, \
+                                                 logits, ld, (int)ublocks, (int)sl2, smaj)
+#define GR_SC_SWITCH(M, ...)            \
+  switch (d) {                          \
+    case 16: M(16, __VA_ARGS__); break; \
+    case 32: M(32, __VA_ARGS__); break; \
+    case 64: M(64, __VA_ARGS__); break; \
+    default: M(128, __VA_ARGS__); break; \
   }
-  if (impl == 3) {   // direct stores through L2 (no streaming hint), any row alignment
-    int64_t sl2 = (2 * cus + ublocks - 1) / ublocks;
-    if (sl2 > chunks) sl2 = chunks;
-    if (sl2 < 1) sl2 = 1;
-    const dim3 g2((unsigned)(ublocks * sl2));
-    const int smaj = option("score_slice_major") != 0 ? 1 : 0;
-    switch (d) {
-      case 32: hipLaunchKernelGGL((score_direct_kernel<32, false>), g2, dim3(256), 0, st, h, B, table, rows, logits, ld, (int)ublocks, (int)sl2, smaj); break;
-      case 64: hipLaunchKernelGGL((score_direct_kernel<64, false>), g2, dim3(256), 0, st, h, B, table, rows, logits, ld, (int)ublocks, (int)sl2, smaj); break;
-      default: hipLaunchKernelGGL((score_direct_kernel<128, false>), g2, dim3(256), 0, st, h, B, table, rows, logits, ld, (int)ublocks, (int)sl2, smaj); break;
-    }
-    return check_launch("gr_score_f32 (direct, cached stores)");
-  }
-  if (impl == 1 || (impl == 2 && lines_aligned)) {
-    int64_t sl2 = (2 * cus + ublocks - 1) / ublocks;
-    if (sl2 > chunks) sl2 = chunks;
-    if (sl2 < 1) sl2 = 1;
-    const dim3 g2((unsigned)(ublocks * sl2));
-    const int smaj = option("score_slice_major") != 0 ? 1 : 0;
-    switch (d) {
-      case 32: hipLaunchKernelGGL(score_direct_kernel<32>, g2, dim3(256), 0, st, h, B, table, rows, logits, ld, (int)ublocks, (int)sl2, smaj); break;
-      case 64: hipLaunchKernelGGL(score_direct_kernel<64>, g2, dim3(256), 0, st, h, B, table, rows, logits, ld, (int)ublocks, (int)sl2, smaj); break;
-      default: hipLaunchKernelGGL(score_direct_kernel<128>, g2, dim3(256), 0, st, h, B, table, rows, logits, ld, (int)ublocks, (int)sl2, smaj); break;
-    }
+  if (lines_aligned) {
+    GR_SC_SWITCH(GR_SC_DIRECT, true)
     return check_launch("gr_score_f32 (direct)");
   }
-#define GR_SC_LAUNCH(DD)                                                                           \
-  if (flags) hipLaunchKernelGGL((score_kernel<DD, true>), g, dim3(64 * (ScCW<DD, true>::value + ScSW<DD, true>::value)), \
-                                0, st, h, B, table, rows, logits, ld, (int)ublocks, (int)slices, ubmajor); \
-  else hipLaunchKernelGGL((score_kernel<DD, false>), g, dim3(64 * (ScCW<DD, false>::value + ScSW<DD, false>::value)), 0, \
-                          st, h, B, table, rows, logits, ld, (int)ublocks, (int)slices, ubmajor);
-  switch (d) {
-    case 32: GR_SC_LAUNCH(32) break;
-    case 64: GR_SC_LAUNCH(64) break;
-    default: GR_SC_LAUNCH(128) break;
+  if (fits_mall) {   // cached stores: L2 / the Infinity Cache merge the two halves of each line
+    GR_SC_SWITCH(GR_SC_DIRECT, false)
+    return check_launch("gr_score_f32 (direct, cached stores)");
   }
-#undef GR_SC_LAUNCH
-  return check_launch("gr_score_f32");
+#undef GR_SC_DIRECT
+#undef GR_SC_SWITCH
+  switch (d) {   // rotated whole-line stores
+    case 16: hipLaunchKernelGGL((score_rot_kernel<16, true>), g2, blk, 0, st, h, B, table, rows, logits, ld, (int)ublocks, (int)sl2, smaj); break;
+    case 32: hipLaunchKernelGGL((score_rot_kernel<32, true>), g2, blk, 0, st, h, B, table, rows, logits, ld, (int)ublocks, (int)sl2, smaj); break;
+    case 64: hipLaunchKernelGGL((score_rot_kernel<64, true>), g2, blk, 0, st, h, B, table, rows, logits, ld, (int)ublocks, (int)sl2, smaj); break;
+    default: {
+      const int64_t sl1 = slices_for(1);
+      hipLaunchKernelGGL(score_kernel<128>, dim3((unsigned)(ublocks * sl1)), dim3(512), 0, st, h, B, table, rows,
+                         logits, ld, (int)ublocks, (int)sl1);
+      return check_launch("gr_score_f32 (ring)");
+    }
+  }
+  return check_launch("gr_score_f32 (rotated lines)");
 }

@@ -77,7 +77,7 @@ def sharded_rank_topk(h, table_shard, row_offset, targets, k=10, group=None, mas
     world = _world(group)
     rows = table_shard.shape[0]
     if (scorer is None and counter is None and topk_fn is None and h.is_cuda and rows > 0
-            and 1 <= k <= 16 and h.shape[1] in (32, 64, 128)):
+            and 1 <= k <= 16 and h.shape[1] in (16, 32, 64, 128)):
         return _sharded_rank_topk_fused(h, table_shard, row_offset, targets, k, group, mask_row0, world)
     s_fn, c_fn, t_fn = _default_ops()
     scorer, counter, topk_fn = scorer or s_fn, counter or c_fn, topk_fn or t_fn
@@ -163,7 +163,7 @@ def sharded_rank_topk_batches(hs, table_shard, row_offset, targets, k=10, group=
                 for h, t in zip(hs, targets)]
     rows = table_shard.shape[0]
     fused = (scorer is None and counter is None and topk_fn is None and hs[0].is_cuda and rows > 0
-             and 1 <= k <= 16 and hs[0].shape[1] in (32, 64, 128))
+             and 1 <= k <= 16 and hs[0].shape[1] in (16, 32, 64, 128))
     if not fused:
         s_fn, c_fn, t_fn = _default_ops()
         scorer, counter, topk_fn = scorer or s_fn, counter or c_fn, topk_fn or t_fn

@@ -27,7 +27,7 @@ def rank_batch(model, input_ids, targets, materialize=False):
         logits[:, 0] = -1e9
         t = logits.gather(1, targets.unsqueeze(1))
         return (logits > t).sum(dim=1) + 1
-    if model.d not in (32, 64, 128):   # the fused kernels' widths; others: predict + rank kernel
+    if model.d not in (16, 32, 64, 128):   # the fused kernels' widths; others: predict + rank kernel
         return ops.rank(model.predict(input_ids), targets, mask_col0=True)
     h = model.last_hidden(input_ids)
     return ops.score_rank(h, model.item_emb.weight.detach(), targets, mask_col0=True)

@@ -100,7 +100,7 @@ def sas_exec_flop_per_user(d, n, items, mlp=64, blocks=2, causal=True, tail_h=Fa
     attention over the causal n(n+1)/2 query-key pairs (``causal``; the one-wave C3 kernel computes
     the whole n x n tile, ``causal=False``); the last block at position n-1 only (q, one query's
     attention, out-proj, FFN) plus, in the K|V form, the K|V projection of all n tokens -- the
-    H-form tail (``tail_h``, sas_tail_h_kernel) instead computes W_k^T q and W_v u (2 d^2 each)
+    H-form tail (``tail_h``, sas_tail_h2_kernel) instead computes W_k^T q and W_v u (2 d^2 each)
     and dots every head's d-vector with the n LayerNorm rows (4 n d per head); scoring
     2*d*(items+1) (``items`` = -1: forward only)."""
     pairs = n * (n + 1) // 2 if causal else n * n
@@ -248,7 +248,7 @@ def kernel_ms(fn, reps=50, warmup=2):
     return e0.elapsed_time(e1) / reps
 
 
-# one gr_score_topk_f32 call (tile design, topk_impl 1): the tile pass (MODE 2: 32-row tile maxima,
+# one gr_score_topk_f32 call: the tile pass (MODE 2: 32-row tile maxima,
 # at 1M rows; MODE 3: 16-row half tiles, topk_half's choice on a shard) + the select kernel
 TOPK_PASS = "score_topk_kernel<128,10,2>"
 TOPK_PASS_HALF = "score_topk_kernel<128,10,3>"
@@ -472,7 +472,7 @@ def bench_sas_c3(a, world, rank, dev):
     targets = torch.randint(1, items + 1, (a.sas_batch,), generator=torch.Generator(device=dev).manual_seed(5), device=dev)
     rank_ms = kernel_ms(lambda: ops.score_rank(h, table, targets))
     fl = sas_flop_per_user(d, n, items)
-    th = gr_amd._lib.get_option("fused_tail_h") != 0   # the fused kernel's final block: H or K|V form
+    th = True   # the fused kernel's final block runs in the H form
     fl_exe = sas_exec_flop_per_user(d, n, items, causal=False, tail_h=th)
     fwd_exe = sas_exec_flop_per_user(d, n, -1, causal=False, tail_h=th)
     res = {"metric": "seqs_scored/s", "value": a.sas_batch * world * a.steps / wall, "unit": "seqs/s",
@@ -550,7 +550,7 @@ def bench_sas_c5(a, world, rank, dev, time_it=True):
     topk_ms = kernel_ms(lambda: ops.score_topk(h, shard, 10, lo, thresholds=ts, mask_col0=(lo == 0)))
     fwd_ms = kernel_ms(lambda: model.last_hidden(lseqs))
     fl_ref = sas_flop_per_user(d, n, items)
-    th = gr_amd._lib.get_option("tail_h") != 0   # the C5 forward's final block: H form or K|V form
+    th = True   # the C5 forward's final block runs in the H form (sas_tail_h2_kernel)
     fl_exe = sas_exec_flop_per_user(d, n, items, causal=True, tail_h=th)
     fwd_exe = sas_exec_flop_per_user(d, n, -1, causal=True, tail_h=th)
     res = {"metric": "seqs_scored/s", "value": B * steps / wall, "unit": "seqs/s", "scaling": "weak",

@@ -46,67 +46,35 @@ extern "C" {
 const char* gr_version(void);
 /* Message of the last failed call on this thread ("" if none). */
 const char* gr_last_error(void);
-/* Process-wide path / tuning options (no reference counterpart; used for A/B measurement):
+/* Process-wide path switches (no reference counterpart).  Each selects between two kernel paths
+ * that give BITWISE identical results, so the tests can run both; no option changes numerics, and
+ * the defaults are what every caller wants.  (Round 5 removed the A/B knobs of slower variants and
+ * the two numerics-changing ones: the final SASRec block of a last-position forward always runs
+ * the H form below.)
  *   "rq_fused"      1 (default): gr_rq_encode_f32 runs the fused persistent kernel when the encoder
  *                   shape is in -> 256 -> 128 -> 32; 0: the layer-wise path (exact gr_linear +
- *                   quantize).  Bitwise identical results.
- *   "rq_split"      1 (default): a quantize workgroup's leftover item tiles are split into code
- *                   quarters, one per SIMD; 0: round-robin.  Bitwise identical results.
+ *                   quantize).
  *   "sas_fused"     1 (default): gr_sasrec_forward_f32 / gr_sasrec_predict_f32 run the fused
  *                   register-resident forward kernel when n <= 64, d <= 64 (d and the head width
  *                   multiples of 8), mlp <= 128, num_blocks <= 8; 0: the layer-wise pipeline
- *                   (the workspace query follows the option in force when it is called)
- *   "score_flags"   1 (default): the scoring kernel (d <= 64) hands chunks between its compute and
- *                   store waves through LDS words; 0: one barrier per chunk.  Identical results.
- *   "score_ubmajor" 1 (default): one XCD's workgroups share a user block; 0: a catalog slice.
- *   "score_impl"    2 (default): the compute waves store their accumulators directly when every
- *                   logits row starts on a 128-byte line (row stride % 32 == 0, aligned base);
- *                   otherwise (d <= 64) plain direct stores when the logits fit the 160 MB
- *                   Infinity Cache, else the lane-rotated whole-line kernel (score_rot_kernel);
- *                   0: compute / store wave specialisation with an LDS ring; 1: always direct;
- *                   3: direct, plain stores; 4: the rotated kernel.  Identical results.
- *   "topk_sample"   1 (default): gr_score_topk_f32 prunes with a threshold from a strided sample
- *                   pass when the catalog is long enough; 0: one pass.  Identical results.
+ *                   (the workspace query follows the option in force when it is called).
+ *   "sas_rowtile"   1 (default): d = 128 forwards on the row-tile kernels; 0: one kernel per op.
+ *   "lin_wres"      1 (default): gr_linear_f32 with k = 128, n % 128 == 0, no residual and
+ *                   m >= 96 x 256 runs a persistent kernel that keeps each wave's 32 columns of w in
+ *                   registers (the C5 block-0 in-projection); 0: the tiled kernel.
+ *   "emb_proj"      1 (default): the d = 128 forward's block 0 (embedding gather + LN_a0 +
+ *                   in-projection) runs as one persistent kernel with W_in in registers; 0: the
+ *                   embed_ln kernel then gr_linear_f32.
  *   "topk_half"     2 (default): gr_score_topk_f32's tile pass records the max of every 16-row
  *                   half tile when the catalog is below ~3,700 64-row chunks per 128 features (the
  *                   select kernel then re-scores half as many rows), else of every 32-row tile;
- *                   1: always half tiles; 0: never.  Identical results.
- *   "lin_wres"      1 (default): gr_linear_f32 with k = 128, n % 128 == 0, no residual and
- *                   m >= 96 x 256 runs a persistent kernel that keeps each wave's 32 columns of w in
- *                   registers (the C5 block-0 in-projection); 0: the tiled kernel.  Identical results.
- *   "emb_proj"      1 (default): the d = 128 forward's block 0 (embedding gather + LN_a0 +
- *                   in-projection) runs as one persistent kernel with W_in in registers; 0: the
- *                   embed_ln kernel then gr_linear_f32.  Identical results.
- *   "emb_rows"      32 (default) or 64: rows per tile of that kernel.  Identical results.
- *   "rt_kv2"        1 (default): the post-attention row tile's next-block projection, when its
- *                   width is a multiple of 256, runs one column tile per wave over both row tiles;
- *                   0: one 32 x 32 tile per task.  Identical results.
- *   "rq_pieces"     1 (default): the fused encoder's item tiles past q x grid (q whole tiles per
- *                   workgroup) run as feature-half pieces on twice as many workgroups plus a layers
- *                   2-3 kernel; 0: a one-tile pass on the first workgroups.  Identical results.
- *   "tail_h"        2 (default): a last-position SASRec forward (predict) runs its final block as
- *                   the one-query tail on LN_a(X): q . K_j = (W_k^T q) . H_j (+ a term constant
- *                   over j that cancels in the softmax) and p . V = W_v (p . H) + b_v, so K|V of
- *                   the B n rows are never projected, in ONE pass over H with an online softmax
- *                   per lane group (sas_tail_h2_kernel); 1: the same tail in two passes over H;
- *                   0: K|V projected and the reference's association order.  1 and 2 are NOT
- *                   bitwise to 0 or to each other: the reassociated sums round differently (logits
- *                   within the 1e-5 row-scaled tolerance, tests/test_sasrec_gpu.py::
- *                   test_tail_h_form_vs_kv_form_and_oracle).
- *   "fused_tail_h"  1 (default): the fused d <= 64 forward (sas_fused) runs a last-position
- *                   forward's final block in the same H form (no K / V of the n tokens); 0: K and V
- *                   projected.  NOT bitwise to 0 (reassociated sums, within the logits tolerance:
- *                   tests/test_sasrec_gpu.py::test_fused_tail_h_vs_kv_form_and_oracle).
- *   "attn_wave"     6 (default): layer-wise causal attention at head width 64 / 128 on a
- *                   persistent grid, one wave per SIMD walking a static longest-first list of
- *                   (sequence, head, 32-query tile) items, K / V straight from L2 into registers,
- *                   the next item's operands loaded under the current item's last step; 1: one
- *                   wave per item (longest first); 0: one 4-wave workgroup per (sequence, head) over
- *                   shared LDS tiles; 3: 1 when B x heads < 512, else 0.  Identical results.
- *   "attn_lazy"     1 (default): lazy softmax rescaling (the running max moves only when a tile's
- *                   max exceeds it by > 8) and masks on the diagonal / last key tile only; 0: the
- *                   rescale on every tile (another fp32 rounding, within tolerance).
- *   "attn_pair", "attn_occ1", "attn_alt": workgroup-kernel variants kept for A/B.
+ *                   1: always half tiles; 0: never.
+ * A last-position forward (predict, last_hidden) runs its final block as the one-query tail on
+ * LN_a(X): q . K_j = (W_k^T q) . H_j (+ a term constant over j that cancels in the softmax) and
+ * p . V = W_v (p . H) + b_v, so K|V of the B n rows are never projected (sas_tail_h2_kernel; the
+ * fused d <= 64 kernel likewise).  The reassociated sums round differently from the reference
+ * formulation: logits within the 1e-5 row-scaled tolerance (tests/test_sasrec_gpu.py::
+ * test_tail_h_form_vs_full_block_and_oracle).
  * gr_set_option returns GR_ERR_ARG for an unknown name/value; gr_get_option returns -1 for an
  * unknown name. */
 int gr_set_option(const char* name, int64_t value);
@@ -405,7 +373,7 @@ int gr_topk_f32(const float* logits, int64_t B, int64_t cols, int64_t ld, int32_
 
 /* ------------------------------------------------------------------------------------------ */
 /* Fused rank without materialising logits (SASRec/evaluate.py:26-32).  Every
- * logit is evaluated with exactly the instruction sequence of gr_score_f32 (d in {32, 64, 128}), so
+ * logit is evaluated with exactly the instruction sequence of gr_score_f32 (d in {16, 32, 64, 128}), so
  * the values below are bitwise the entries gr_score_f32 / gr_sasrec_predict_f32 would write.
  *
  * Target logits: out[b] = h[b] . table[ids[b]] (-1e9 when mask_col0 and ids[b] == 0, the
@@ -428,7 +396,7 @@ int gr_score_count_gt_f32(const float* h, int64_t B, int32_t d, const float* tab
  * taken as -1e9 when mask_col0.  vals_out[B, k] / ids_out[B, k]: the k largest, value descending,
  * ties to the lower column, ids = column + id_offset (-1 / -inf pad rows with fewer than k
  * columns).  thresholds / counts_out (both or neither): counts_out[b] = #{j : l[b, j] > thr[b]}.
- * d in {32, 64, 128}, 1 <= k <= 16, rows < 2^31, B <= 65535.  Replaces gr_score_f32 + gr_topk_f32
+ * d in {16, 32, 64, 128}, 1 <= k <= 16, rows < 2^31, B <= 65535.  Replaces gr_score_f32 + gr_topk_f32
  * (which read the logits back) when only the top-k / ranks are needed. */
 size_t gr_score_topk_workspace_bytes(int64_t B, int32_t d, int64_t rows, int32_t k);
 int gr_score_topk_f32(const float* h, int64_t B, int32_t d, const float* table, int64_t rows,

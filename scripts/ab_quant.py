@@ -2,7 +2,7 @@
 default): 20 calls captured in one graph and replayed, so the host's per-call cost (~40-80 us of
 Python + ctypes, which bounded scripts/ab_opt.py's quantize numbers) is off the clock.
 
-    python scripts/ab_quant.py --opt rq_split=0,1 [--L 3 --K 256] [--n 3200,25600,100000]
+    python scripts/ab_quant.py --opt rq_fused=0,1 [--L 3 --K 256] [--n 3200,25600,100000]
 """
 import argparse
 import os
@@ -37,7 +37,7 @@ def graph_us(fn, calls=20, reps=10):
 
 
 ap = argparse.ArgumentParser()
-ap.add_argument("--opt", default="rq_split=0,1")
+ap.add_argument("--opt", default="rq_fused=0,1")
 ap.add_argument("--L", type=int, default=3)
 ap.add_argument("--K", type=int, default=256)
 ap.add_argument("--n", default="3200,25600,51200,100000,409600")

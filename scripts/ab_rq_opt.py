@@ -1,7 +1,7 @@
 """Device-time A/B of RQVAE.get_indices under gr_set_option settings (graph-captured, 20 calls per
 replay), same inputs; IDs compared bitwise with the first setting.
 
-    python scripts/ab_rq_opt.py --opt rq_pieces=0,1 [--n 100000,65536] [--L 3 --K 256]
+    python scripts/ab_rq_opt.py --opt rq_fused=0,1 [--n 100000,65536] [--L 3 --K 256]
 """
 import argparse
 import os
@@ -13,7 +13,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from gr_amd import _lib as L, synth  # noqa: E402
 
 ap = argparse.ArgumentParser()
-ap.add_argument("--opt", default="rq_pieces=0,1")
+ap.add_argument("--opt", default="rq_fused=0,1")
 ap.add_argument("--n", default="100000")
 ap.add_argument("--L", type=int, default=3)
 ap.add_argument("--K", type=int, default=256)

@@ -1,7 +1,7 @@
 """A/B timing of the SASRec forward paths (steady state, HIP events): per option setting, the
 mean device time of ``model.last_hidden`` (predict's forward) and ``model.forward`` (all positions).
 
-    python scripts/ab_sas.py [--d 128 --n 200 --B 512 --items 1000000] [--opt attn_pair=0,1]
+    python scripts/ab_sas.py [--d 128 --n 200 --B 512 --items 1000000] [--opt emb_proj=0,1]
 """
 import argparse
 import os
@@ -37,7 +37,7 @@ ap.add_argument("--n", type=int, default=200)
 ap.add_argument("--B", type=int, default=512)
 ap.add_argument("--items", type=int, default=1_000_000)
 ap.add_argument("--fused", type=int, default=1)
-ap.add_argument("--opt", default="attn_pair=0,1")
+ap.add_argument("--opt", default="emb_proj=0,1")
 a = ap.parse_args()
 dev = torch.device("cuda:0")
 p = synth.sasrec_params(a.d, a.n, 2, 1, 64, dev)

@@ -1,7 +1,7 @@
 #!/bin/bash
 # SQ counters of the C5 forward's kernels (scripts/prof_kernels.py --what c5fwd) under a given
 # option setting; two --pmc passes, each under its own limit.
-#   scripts/pmc_attn.sh TAG attn_wave=1
+#   scripts/pmc_attn.sh TAG emb_proj=0
 set -u
 ROOT=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 OUT=$ROOT/gpurun_out/$1

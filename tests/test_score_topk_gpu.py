@@ -28,28 +28,23 @@ def _reference(h, t, k, id_offset, thr, mask_col0):
 
 
 def _check(h, t, k, id_offset=0, mask_col0=True, seed=0):
-    """Every plan against the materialised reference: the tile design (tile maxima + re-scored
-    tiles, the default) with 32-row and 16-row tiles (topk_half), and the list design with its
-    sample-thresholded two passes and one pass."""
+    """Both tile sizes of the fused call (32-row tile maxima and 16-row half tiles, option
+    topk_half) against the materialised reference, with and without counts."""
     from gr_amd import _lib, ops
     g = torch.Generator(device=h.device).manual_seed(seed)
     thr = torch.randn(h.shape[0], generator=g, device=h.device)
     rv, ri, rc = _reference(h, t, k, id_offset, thr, mask_col0)
     half0 = _lib.get_option("topk_half")
     try:
-        for impl, sample, half in ((1, 1, 0), (1, 1, 1), (0, 1, 0), (0, 0, 0)):
-            _lib.set_option("topk_impl", impl)
-            _lib.set_option("topk_sample", sample)
+        for half in (0, 1):
             _lib.set_option("topk_half", half)
             v, i, c = ops.score_topk(h, t, k, id_offset, thresholds=thr, mask_col0=mask_col0)
-            assert torch.equal(i, ri), (impl, sample, half)
-            assert torch.equal(v, rv), (impl, sample, half)
-            assert torch.equal(c, rc), (impl, sample, half)
+            assert torch.equal(i, ri), half
+            assert torch.equal(v, rv), half
+            assert torch.equal(c, rc), half
             v2, i2 = ops.score_topk(h, t, k, id_offset, mask_col0=mask_col0)   # without counts
-            assert torch.equal(v2, rv) and torch.equal(i2, ri), (impl, sample, half)
+            assert torch.equal(v2, rv) and torch.equal(i2, ri), half
     finally:
-        _lib.set_option("topk_impl", 1)
-        _lib.set_option("topk_sample", 1)
         _lib.set_option("topk_half", half0)
 
 
@@ -57,6 +52,7 @@ def _check(h, t, k, id_offset=0, mask_col0=True, seed=0):
                                         (257, 32, 1000, 1), (70, 64, 64, 10), (5, 128, 7, 10),
                                         (513, 128, 20011, 10), (33, 32, 1, 3), (512, 128, 300007, 10),
                                         (100, 32, 150001, 4), (40, 64, 262145, 16),
+                                        (200, 16, 707, 10), (65, 16, 100001, 16),   # d 16: SASRec/main.py:12
                                         (512, 128, 1000001, 10)])   # C5 full size: 512 users x 1M-item catalog
 def test_score_topk_random(B, d, rows, k, dev):
     g = torch.Generator().manual_seed(B * 7 + d + rows)
@@ -132,33 +128,26 @@ def test_score_topk_rejects_bad_args(dev):
         ops.score_topk(torch.randn(4, 48, device=dev), torch.randn(100, 48, device=dev), 5)
 
 
-@pytest.mark.parametrize("B,d,rows,ld", [(300, 64, 100001, 100001), (2048, 64, 20001, 20032), (77, 32, 5003, 5003),
-                                         (129, 128, 9000, 9001)])
-def test_score_kernel_variants_identical(B, d, rows, ld, dev):
-    """Every scoring-kernel variant (LDS-word or barrier hand-off, XCD mapping, direct stores)
-    writes the same bits, ragged users / rows and odd row strides included."""
-    from gr_amd import _lib, ops
+@pytest.mark.parametrize("B,d,rows", [(300, 64, 100001), (2048, 64, 20001), (77, 32, 5003), (1100, 128, 40001),
+                                      (129, 128, 9000), (2600, 16, 16001), (50, 16, 707)])
+def test_score_layouts_identical(B, d, rows, dev):
+    """gr_score_f32 picks its kernel by the logits layout: rows on 128-byte lines (direct stores),
+    the reference's contiguous [B, N+1] rows below the Infinity Cache size (direct, cached stores)
+    and above it (rotated whole lines; the LDS ring at d 128).  Every layout holds the same bits,
+    ragged users / rows included, and nothing is written past a row's columns."""
+    from gr_amd import ops
     g = torch.Generator().manual_seed(B + rows)
     h = torch.randn(B, d, generator=g).to(dev)
     t = torch.randn(rows, d, generator=g).to(dev)
-    outs = []
-    try:
-        for opts in [dict(score_impl=0), dict(score_impl=0, score_flags=0), dict(score_impl=0, score_ubmajor=0),
-                     dict(score_impl=1), dict(score_impl=2)]:
-            for k, v in opts.items():
-                _lib.set_option(k, v)
-            buf = torch.full((B, ld), 7.0, device=dev)
-            ops.score(h, t, out=buf[:, :rows])
-            outs.append(buf)
-            for k in opts:
-                _lib.set_option(k, {"score_flags": 1, "score_ubmajor": 1, "score_impl": 2}[k])
-    finally:
-        _lib.set_option("score_flags", 1)
-        _lib.set_option("score_ubmajor", 1)
-        _lib.set_option("score_impl", 2)
-    for o in outs[1:]:
-        assert torch.equal(o, outs[0])
-    assert (outs[0][:, rows:] == 7.0).all()   # nothing written past the row's columns
+    ld = (rows + 31) // 32 * 32
+    pad = torch.full((B, ld + 32), 7.0, device=dev)
+    ops.score(h, t, out=pad[:, :rows])          # row stride ld + 32: every row on a 128-B line
+    assert (pad[:, rows:] == 7.0).all()
+    cont = torch.full((B * rows + 64,), 7.0, device=dev)
+    view = cont[32:32 + B * rows].view(B, rows)   # contiguous rows, base off the 128-B grid
+    ops.score(h, t, out=view)
+    assert torch.equal(view, pad[:, :rows])
+    assert (cont[:32] == 7.0).all() and (cont[32 + B * rows:] == 7.0).all()
 
 
 def _gloo_gpu_worker(rank, world, port, data, out, backend="gloo"):
