@@ -45,7 +45,11 @@ def all_gather_rows(t, group=None, sizes=None):
 
 def merge_topk(vals, ids, k):
     """Top-k of candidate lists [B, C] (values, global ids): value descending, ties to the lower id;
-    ids < 0 are padding."""
+    ids < 0 are padding.  On the GPU one wave per row (ops.merge_topk, gr_merge_topk_f32); the
+    torch form below (two stable sorts) serves CPU tensors (the gloo tests) with the same result."""
+    if vals.is_cuda and vals.shape[1] <= 256:
+        from . import ops
+        return ops.merge_topk(vals, ids, k)
     v = torch.where(ids < 0, torch.full_like(vals, float("-inf")), vals)
     big = torch.iinfo(torch.int64).max
     i = torch.where(ids < 0, torch.full_like(ids, big), ids)
@@ -109,18 +113,41 @@ def sharded_rank_topk(h, table_shard, row_offset, targets, k=10, group=None, mas
     return _exchange(cnt, v, i, k, group, world)
 
 
+def _pack(v, i):
+    """[ids | value bits] per user as int64 words: the one tensor the candidates travel in."""
+    return torch.cat([i, v.contiguous().view(torch.int32).to(torch.int64)], 1)
+
+
+def _gather_packed(packed, world, group, async_op=False):
+    """All-gather of the packed candidates: into one [world, B, 2 kk] tensor over RCCL (the merge
+    kernel reads it as is), a list of per-rank tensors otherwise (gloo)."""
+    if packed.is_cuda and dist.get_backend(group) == "nccl":
+        out = torch.empty((world,) + tuple(packed.shape), dtype=packed.dtype, device=packed.device)
+        work = dist.all_gather_into_tensor(out.view(-1, packed.shape[1]), packed, group=group, async_op=async_op)
+        return out, work
+    parts = [torch.empty_like(packed) for _ in range(world)]
+    return parts, dist.all_gather(parts, packed, group=group, async_op=async_op)
+
+
+def _merge_gathered(gathered, world, kk, k):
+    if not torch.is_tensor(gathered) and gathered[0].is_cuda:   # gloo on device tensors (rehearsal)
+        gathered = torch.stack(gathered)
+    if torch.is_tensor(gathered):   # [world, B, 2 kk] on the GPU: one kernel unpacks and merges
+        from . import ops
+        return ops.merge_topk_packed(gathered, world, kk, k)
+    ids = torch.cat([p_[:, :kk] for p_ in gathered], 1)
+    vals = torch.cat([p_[:, kk:].to(torch.int32).view(torch.float32) for p_ in gathered], 1)
+    return merge_topk(vals, ids, k)
+
+
 def _exchange(cnt, v, i, k, group, world):
     """Steps 2-3 of the module docstring: global counts and the merged top-k.  The (value, id)
     candidates travel as ONE int64 all-gather: [ids | value bits] per user."""
     if world:
         dist.all_reduce(cnt, op=dist.ReduceOp.SUM, group=group)
         kk = v.shape[1]
-        packed = torch.cat([i, v.contiguous().view(torch.int32).to(torch.int64)], 1)
-        parts = [torch.empty_like(packed) for _ in range(world)]
-        dist.all_gather(parts, packed, group=group)
-        ids = torch.cat([p_[:, :kk] for p_ in parts], 1)
-        vals = torch.cat([p_[:, kk:].to(torch.int32).view(torch.float32) for p_ in parts], 1)
-        v, i = merge_topk(vals, ids, k)
+        gathered, _ = _gather_packed(_pack(v, i), world, group)
+        v, i = _merge_gathered(gathered, world, kk, k)
     return cnt + 1, v, i
 
 
@@ -203,18 +230,15 @@ def sharded_rank_topk_batches(hs, table_shard, row_offset, targets, k=10, group=
         if kk < k:
             v = torch.cat([v, torch.full((v.shape[0], k - kk), float("-inf"), dtype=v.dtype, device=v.device)], 1)
             i = torch.cat([i, torch.full((i.shape[0], k - kk), -1, dtype=i.dtype, device=i.device)], 1)
-        packed = torch.cat([i, v.contiguous().view(torch.int32).to(torch.int64)], 1)
-        parts = [torch.empty_like(packed) for _ in range(world)]
-        return (cnt, parts, dist.all_reduce(cnt, op=dist.ReduceOp.SUM, group=group, async_op=True),
-                dist.all_gather(parts, packed, group=group, async_op=True))
+        w1 = dist.all_reduce(cnt, op=dist.ReduceOp.SUM, group=group, async_op=True)
+        gathered, w2 = _gather_packed(_pack(v, i), world, group, async_op=True)
+        return cnt, gathered, w1, w2
 
     def finish(sc):
-        cnt, parts, w1, w2 = sc
+        cnt, gathered, w1, w2 = sc
         w1.wait()
         w2.wait()
-        ids = torch.cat([p_[:, :k] for p_ in parts], 1)
-        vals = torch.cat([p_[:, k:].to(torch.int32).view(torch.float32) for p_ in parts], 1)
-        v, i = merge_topk(vals, ids, k)
+        v, i = _merge_gathered(gathered, world, k, k)
         return cnt + 1, v, i
 
     out, prev = [], None

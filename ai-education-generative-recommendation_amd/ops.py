@@ -192,6 +192,36 @@ def score_topk(h, table, k, id_offset=0, thresholds=None, mask_col0=True):
     return (vals, ids) if th is None else (vals, ids, cnt)
 
 
+def merge_topk(vals, ids, k):
+    """Top-k of candidate lists [B, C] (values, global ids) by (value desc, id asc), ids < 0 padding
+    (emitted as (-inf, -1)): the merge of the catalog shards' lists (gr_merge_topk_f32)."""
+    L.require_gpu(vals, ids)
+    B, C = vals.shape
+    v = L.as_f32(vals)
+    i = ids.to(torch.int64).contiguous()
+    out_v = torch.empty((B, k), dtype=torch.float32, device=vals.device)
+    out_i = torch.empty((B, k), dtype=torch.int64, device=vals.device)
+    with torch.cuda.device(vals.device):
+        L.check(L.lib().gr_merge_topk_f32(L.ptr(v), v.stride(0), L.ptr(i), i.stride(0), B, C, k,
+                                          L.ptr(out_v), L.ptr(out_i), L.stream_of(vals.device)),
+                "gr_merge_topk_f32")
+    return out_v, out_i
+
+
+def merge_topk_packed(packed, world, kk, k):
+    """The merge straight from the exchange's all-gathered int64 buffer [world, B, 2 kk] (per rank
+    and row kk ids, then kk value bit patterns; dist._exchange)."""
+    L.require_gpu(packed)
+    packed = packed.contiguous()
+    B = packed.numel() // (world * 2 * kk)
+    out_v = torch.empty((B, k), dtype=torch.float32, device=packed.device)
+    out_i = torch.empty((B, k), dtype=torch.int64, device=packed.device)
+    with torch.cuda.device(packed.device):
+        L.check(L.lib().gr_merge_topk_packed(L.ptr(packed), world, B, kk, k, L.ptr(out_v), L.ptr(out_i),
+                                             L.stream_of(packed.device)), "gr_merge_topk_packed")
+    return out_v, out_i
+
+
 def rq_quantize(z, codebooks, with_gap=False):
     """Residual quantization of latents (RQ-VAE/models/rq.py:39-56, use_sk=False).
 

@@ -934,7 +934,7 @@ def bench_c5_rank(a, dev):
     own c5_batch users, then -- on the all-gathered hidden states of all B = c5_batch x N users --
     the owner's target logits (gr_score_pairs_f32), the fused strict count + local top-10 over its
     catalog shard (rows [0, (items+1)/N), which also masks row 0; gr_score_topk_f32) and the merge of
-    the N x 10 gathered candidates (dist.merge_topk).  The collectives themselves (all-gather of
+    the N x 10 gathered candidates (gr_merge_topk_packed).  The collectives themselves (all-gather of
     B x d floats, two all-reduces of B scalars, all-gather of B x 10 candidates: about 2.4 MB per
     rank at N = 8) are not on one GPU; ``collective_bytes_per_rank`` states them.  ``value`` = the B
     users of one N-GPU step / this rank's device time per step: the N-GPU throughput when the
@@ -964,8 +964,7 @@ def bench_c5_rank(a, dev):
     # the other ranks' candidates: this shard's lists with ids moved into their shards (the merge's
     # cost depends on the [B, N k] shape, not on the values)
     _, v0, i0 = D.sharded_rank_topk(h, shard, lo, targets, k=k)
-    cand_v = torch.cat([v0] * W, 1)
-    cand_i = torch.cat([i0 + D.shard_range(items + 1, r, W)[0] for r in range(W)], 1)
+    gathered = torch.stack([D._pack(v0, i0 + D.shard_range(items + 1, r, W)[0]) for r in range(W)])
 
     def forward():
         return model.last_hidden(lseqs)
@@ -978,8 +977,8 @@ def bench_c5_rank(a, dev):
     def topk():
         return ops.score_topk(h, shard, k, lo, thresholds=ts, mask_col0=m0)
 
-    def merge():
-        return D.merge_topk(cand_v, cand_i, k)
+    def merge():   # what dist._exchange runs on the all-gathered [W, B, 2k] buffer
+        return ops.merge_topk_packed(gathered, W, k, k)
 
     def step():
         forward()

@@ -405,6 +405,17 @@ int gr_score_topk_f32(const float* h, int64_t B, int32_t d, const float* table, 
                       size_t workspace_bytes, void* stream);
 
 /* ------------------------------------------------------------------------------------------ */
+/* Merge of catalog shards' top-k lists (the catalog-sharded counterpart of
+ * SASRec/evaluate.py's per-user ranking): per row b, the k best of C candidates (cand_vals[b, c],
+ * cand_ids[b, c]) by (value desc, id asc); ids < 0 are padding, emitted as (-inf, -1) when fewer
+ * than k real candidates remain.  C <= 256.  ldv / ldi: row strides (elements). */
+int gr_merge_topk_f32(const float* cand_vals, int64_t ldv, const int64_t* cand_ids, int64_t ldi,
+                      int64_t B, int32_t C, int32_t k, float* vals_out, int64_t* ids_out, void* stream);
+/* The same merge straight from the all-gathered exchange buffer: packed [world][B][2 kk] int64, per
+ * (rank, row) kk ids then kk values (float bits in the low 32 bits of each word).  world kk <= 256. */
+int gr_merge_topk_packed(const int64_t* packed, int32_t world, int64_t B, int32_t kk, int32_t k,
+                         float* vals_out, int64_t* ids_out, void* stream);
+
 /* Training-side scoring (SASRec/train.py:131-160) without the [B, n, rows]
  * score matrix.  feats[B, n, d] = model.forward(input_seqs), table[rows, d] = item_emb.weight,
  * targets[B, n] = o_t (0 = padding, masked), negs[B, num_neg] (shared by the user's n positions,
