@@ -20,6 +20,7 @@
 // instruction sequence whichever tiles are launched, so a last-tile-only launch (the final block of
 // a last-position forward) reproduces the full launch's rows bit for bit.
 #include <cmath>
+#include <type_traits>
 
 #include "gr_common.h"
 
@@ -275,7 +276,11 @@ __global__ __launch_bounds__(64) void attn_persist_kernel(const float* __restric
     return qkv + (int64_t)(bh / H) * n * rs + (bh % H) * HD;
   };
   f32x4 qf[FT][4], kf[FT][4];
-  float vf[FT][16];
+  // V: lane (r, h) holds the FT consecutive features FT r .. FT r + FT - 1 of key (s&3) + 8(s>>2) + 4h
+  // as one vector per s, so O[ft]'s accumulator row i is feature FT i + ft (16 vector loads per
+  // lane and tile instead of 16 FT scalar loads; the same values in the same chains: bitwise equal)
+  using VT = typename std::conditional<FT == 4, f32x4, f32x2>::type;
+  VT vf[16];
   auto load_q = [&](const float* bs, int qi_) {
     const int qc = qi_ < n ? qi_ : n - 1;
 #pragma unroll
@@ -298,9 +303,7 @@ __global__ __launch_bounds__(64) void attn_persist_kernel(const float* __restric
     for (int s = 0; s < 16; ++s) {
       int key = kt * 32 + (s & 3) + 8 * (s >> 2) + 4 * h;
       key = key < n ? key : n - 1;
-      const float* vr = bs + 2 * d + (int64_t)key * rs + r;
-#pragma unroll
-      for (int ft = 0; ft < FT; ++ft) vf[ft][s] = vr[32 * ft];
+      vf[s] = *reinterpret_cast<const VT*>(bs + 2 * d + (int64_t)key * rs + FT * r);
     }
   };
   int qt, qi;
@@ -374,7 +377,7 @@ __global__ __launch_bounds__(64) void attn_persist_kernel(const float* __restric
 #pragma unroll
       for (int ft = 0; ft < FT; ++ft)
 #pragma unroll
-        for (int s = 0; s < 16; ++s) O[ft] = mfma32(vf[ft][s], S[s], O[ft]);
+        for (int s = 0; s < 16; ++s) O[ft] = mfma32(vf[s][ft], S[s], O[ft]);
       if (kt < qt) {
         if (GR_ADIAG == 0) load_v(bs, kt + 1);
       } else if (nj >= 0) {
@@ -387,11 +390,12 @@ __global__ __launch_bounds__(64) void attn_persist_kernel(const float* __restric
       const int64_t bb = boff / ((int64_t)n * rs), hho = boff - bb * (int64_t)n * rs;
       float* orow = out + (bb * n + qi) * d + hho;
 #pragma unroll
-      for (int ft = 0; ft < FT; ++ft)
+      for (int v = 0; v < 16; ++v) {   // accumulator row i = feature block FT i .. FT i + FT - 1
+        VT o;
 #pragma unroll
-        for (int g = 0; g < 4; ++g)
-          *reinterpret_cast<f32x4*>(orow + 32 * ft + 8 * g + 4 * h) =
-              f32x4{O[ft][4 * g], O[ft][4 * g + 1], O[ft][4 * g + 2], O[ft][4 * g + 3]} * inv;
+        for (int ft = 0; ft < FT; ++ft) o[ft] = O[ft][v] * inv;
+        *reinterpret_cast<VT*>(orow + FT * ((v & 3) + 8 * (v >> 2) + 4 * h)) = o;
+      }
     }
     if (nj < 0) break;
     ++rnd;

