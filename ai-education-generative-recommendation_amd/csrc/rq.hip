@@ -51,10 +51,10 @@ constexpr size_t RQ_PART_BYTES = 2 * RQ_SPLIT_MAX * 4 * 32 * 3 * sizeof(float);
 template <int EP>
 struct RQMaxT { static constexpr int value = EP >= 64 ? 2 : 4; };
 
-// Stage codes [c0, c0 + cnt) of a level into the LDS image (de-interleaved rows) and their norms.
+// Codes [c0, c0 + cnt) of a level into the LDS image (de-interleaved rows); no barrier.
 template <int EP, int NT, bool FULL>
-__device__ __forceinline__ void stage_codes(const float* __restrict__ cb, int e, int c0, int cnt,
-                                            float* cbs, float* cns, int tid) {
+__device__ __forceinline__ void stage_rows(const float* __restrict__ cb, int e, int c0, int cnt, float* cbs,
+                                           int tid) {
   constexpr int HQ = EP / 8;
   if (FULL) {   // 16-byte rows: a float4 of features 4u..4u+3 -> two 8-byte halves
     for (int f = tid; f < cnt * (EP / 4); f += NT) {
@@ -69,7 +69,13 @@ __device__ __forceinline__ void stage_codes(const float* __restrict__ cb, int e,
       cbs[feat_off<EP>(c, k)] = k < e ? cb[(int64_t)(c0 + c) * e + k] : 0.f;
     }
   }
-  __syncthreads();
+}
+
+// ATen-order norms of the cnt staged rows (and +inf for the padding rows up to a multiple of 32);
+// the rows must be visible (a barrier after stage_rows); no barrier.
+template <int EP, int NT, bool FULL>
+__device__ __forceinline__ void stage_norms(int e, int cnt, const float* cbs, float* cns, int tid) {
+  constexpr int HQ = EP / 8;
   for (int c = tid; c < ((cnt + 31) & ~31); c += NT) {
     float s = __builtin_inff();   // codes past K can never win
     if (c < cnt) {
@@ -88,6 +94,15 @@ __device__ __forceinline__ void stage_codes(const float* __restrict__ cb, int e,
     }
     cns[c] = s;
   }
+}
+
+// Stage codes [c0, c0 + cnt) of a level into the LDS image (de-interleaved rows) and their norms.
+template <int EP, int NT, bool FULL>
+__device__ __forceinline__ void stage_codes(const float* __restrict__ cb, int e, int c0, int cnt,
+                                            float* cbs, float* cns, int tid) {
+  stage_rows<EP, NT, FULL>(cb, e, c0, cnt, cbs, tid);
+  __syncthreads();
+  stage_norms<EP, NT, FULL>(e, cnt, cbs, cns, tid);
   __syncthreads();
 }
 
@@ -95,7 +110,7 @@ __device__ __forceinline__ void stage_codes(const float* __restrict__ cb, int e,
 template <int EP, bool SECOND, bool FULL>
 __global__ __launch_bounds__(RQ_W * 64) void rq_quantize_kernel(
     const float* __restrict__ z, int64_t n, int e_in, int L, RQLevels lv, int kch, int64_t* __restrict__ idx_out,
-    float* __restrict__ best_out, float* __restrict__ gap_out, int tiles, int split_ok) {
+    float* __restrict__ best_out, float* __restrict__ gap_out, int tiles, int split_ok, int resident) {
 #pragma clang fp contract(off)
   const int e = FULL ? EP : e_in;
   static_assert(EP % 8 == 0 && EP <= 64, "e");
@@ -106,6 +121,9 @@ __global__ __launch_bounds__(RQ_W * 64) void rq_quantize_kernel(
   float* cbs = sm;                     // [kch][EP] de-interleaved, swizzled
   float* cns = sm + kch * EP;          // [kch]
   float* part = cns + kch;             // [2][RQ_SPLIT_MAX][4][32][3] split-tile partials
+  // resident: every level's codebook resident at once (kch = the levels' codes, each level padded to a
+  // multiple of 32), staged and normed before the first level -- one round of load latency instead
+  // of one per level, for short calls whose workgroups quantize a tile or two
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r = lane & 31, h = lane >> 5;
   const int t_begin = (int)((int64_t)blockIdx.x * tiles / gridDim.x);
   const int t_end = (int)((int64_t)(blockIdx.x + 1) * tiles / gridDim.x);
@@ -153,9 +171,28 @@ __global__ __launch_bounds__(RQ_W * 64) void rq_quantize_kernel(
     }
   }
 
+  if (resident) {
+    int off = 0;
+    for (int l = 0; l < L; ++l) {
+      stage_rows<EP, NT, FULL>(lv.cb[l], e, 0, lv.K[l], cbs + off * EP, tid);
+      off += (lv.K[l] + 31) & ~31;
+    }
+    __syncthreads();
+    off = 0;
+    for (int l = 0; l < L; ++l) {
+      stage_norms<EP, NT, FULL>(e, lv.K[l], cbs + off * EP, cns + off, tid);
+      off += (lv.K[l] + 31) & ~31;
+    }
+    __syncthreads();
+  }
+  int loff = 0;   // res: this level's first row in the resident image
   for (int l = 0; l < L; ++l) {
     const int K = lv.K[l];
     const float* cb = lv.cb[l];
+    float* cbi = resident ? cbs + loff * EP : cbs;   // the level's (or chunk's) LDS image and norms
+    float* cni = resident ? cns + loff : cns;
+    const int kst = resident ? K : kch;              // codes per chunk
+    loff += (K + 31) & ~31;
     float rn[RQ_MAXT], best[RQ_MAXT], second[RQ_MAXT];
     int bi[RQ_MAXT];
 #pragma unroll
@@ -165,11 +202,13 @@ __global__ __launch_bounds__(RQ_W * 64) void rq_quantize_kernel(
       second[i] = __builtin_inff();
       bi[i] = 0x7fffffff;
     }
-    const int c_last = ((K - 1) / kch) * kch;   // first code of the chunk left in LDS
-    for (int c0 = 0; c0 < K; c0 += kch) {
-      const int cnt = min(kch, K - c0);
-      __syncthreads();   // previous chunk / level fully consumed
-      stage_codes<EP, NT, FULL>(cb, e, c0, cnt, cbs, cns, tid);
+    const int c_last = ((K - 1) / kst) * kst;   // first code of the chunk left in LDS
+    for (int c0 = 0; c0 < K; c0 += kst) {
+      const int cnt = min(kst, K - c0);
+      if (!resident) {
+        __syncthreads();   // previous chunk / level fully consumed
+        stage_codes<EP, NT, FULL>(cb, e, c0, cnt, cbs, cns, tid);
+      }
       const int ct_n = (cnt + 31) >> 5;
       const int q_lo = simd * ct_n / 4, q_hi = (simd + 1) * ct_n / 4;   // this SIMD's code quarter
 #pragma unroll 1
@@ -179,11 +218,11 @@ __global__ __launch_bounds__(RQ_W * 64) void rq_quantize_kernel(
         f32x4 a[HQ];
 #pragma unroll
         for (int j = 0; j < HQ; ++j)
-          a[j] = *reinterpret_cast<const f32x4*>(cbs + cb_off<EP>(code, HQ * h + j));
+          a[j] = *reinterpret_cast<const f32x4*>(cbi + cb_off<EP>(code, HQ * h + j));
         float cnv[16];
 #pragma unroll
         for (int g4 = 0; g4 < 4; ++g4) {
-          const f32x4 q = *reinterpret_cast<const f32x4*>(cns + ct * 32 + 8 * g4 + 4 * h);
+          const f32x4 q = *reinterpret_cast<const f32x4*>(cni + ct * 32 + 8 * g4 + 4 * h);
 #pragma unroll
           for (int i = 0; i < 4; ++i) cnv[4 * g4 + i] = q[i];
         }
@@ -268,7 +307,7 @@ __global__ __launch_bounds__(RQ_W * 64) void rq_quantize_kernel(
         if (b >= c_last) {   // the winner's row is still in the LDS image
 #pragma unroll
           for (int j = 0; j < HQ; ++j)
-            cw[j] = *reinterpret_cast<const f32x4*>(cbs + cb_off<EP>(b - c_last, HQ * h + j));
+            cw[j] = *reinterpret_cast<const f32x4*>(cbi + cb_off<EP>(b - c_last, HQ * h + j));
         } else {
 #pragma unroll
           for (int j = 0; j < HQ; ++j)
@@ -320,12 +359,19 @@ static int launch_quantize_e(const float* z, int64_t n, int e, int L, const RQLe
   int kmax = 0;
   for (int l = 0; l < L; ++l) kmax = lv.K[l] > kmax ? lv.K[l] : kmax;
   const int kch_max = 1024 * 32 / EP;                        // 128 KiB of codebook per chunk
-  const int kch = ((kmax < kch_max ? kmax : kch_max) + 31) & ~31;
+  int kch = ((kmax < kch_max ? kmax : kch_max) + 31) & ~31;
+  const int64_t tiles = (n + 31) / 32;
+  // short calls (one tile per workgroup at most): every level resident from the start when the
+  // levels fit 160 KiB of LDS (3 x 256 codes at e = 32: 99 KiB)
+  int ktot = 0;
+  for (int l = 0; l < L; ++l) ktot += (lv.K[l] + 31) & ~31;
+  const bool res = tiles <= (int64_t)cu_count() &&
+                   (size_t)ktot * EP * 4 + (size_t)ktot * 4 + RQ_PART_BYTES <= 160 * 1024;
+  if (res) kch = ktot;
   const size_t lds = (size_t)kch * EP * 4 + (size_t)kch * 4 + RQ_PART_BYTES;
   // persistent: one 8-wave workgroup per CU (2 waves per SIMD at this register budget), each with
   // a contiguous balanced range of tiles; more workgroups only when a range would exceed the
   // register-resident residuals (W x MT tiles)
-  const int64_t tiles = (n + 31) / 32;
   int64_t grid = (int64_t)cu_count();
   const int64_t min_grid = (tiles + RQ_W * RQMaxT<EP>::value - 1) / (RQ_W * RQMaxT<EP>::value);
   if (grid < min_grid) grid = min_grid;
@@ -339,7 +385,7 @@ static int launch_quantize_e(const float* z, int64_t n, int e, int L, const RQLe
                           (int)lds) != hipSuccess)
     return fail(GR_ERR_HIP, "rq quantize: cannot raise the LDS limit");
   hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(RQ_W * 64), lds, st, z, n, e, L, lv, kch, idx,
-                     best, gap, (int)tiles, 1);
+                     best, gap, (int)tiles, 1, res ? 1 : 0);
   return check_launch("gr_rq_quantize_f32");
 }
 

@@ -415,19 +415,23 @@ __device__ __forceinline__ void rq_fused_pass(FusedCtx<H1, H2>& cx, int tb, int 
 // rows [FT, 2 FT): block 1's); the block-1 waves hand their sums to the block-0 waves through LDS,
 // which form y = (b1 + block 0) + block 1 exactly as every other pass.  The x image's chunk 0 is
 // already staged (k-split layout) by the pass before; chunk NC/2 - 1 prefetches nothing.
-template <int H1, int H2>
+// PF = 64 (quarter pieces, the short-call plan): waves 0-3 only (feature group w & 1, block w >> 1,
+// one chain per SIMD); waves 4-7 stage x and keep the barriers.
+template <int H1, int H2, int PF = 128>
 __device__ __forceinline__ void rq_piece_pass(FusedCtx<H1, H2>& cx, int tb, int fh, float* __restrict__ h1g,
                                               const float* __restrict__ W1) {
 #pragma clang fp contract(off)
   using C = FusedCfg<H1, H2>;
   constexpr int PI = C::PI;
-  const int w = cx.w, r = cx.r, h = cx.h, fg = w & 3, blk = w >> 2;
+  constexpr int NG = PF / 32;          // feature groups of the piece
+  const int w = cx.w, r = cx.r, h = cx.h, fg = w % NG, blk = (w / NG) & 1;
+  const bool act = w < 2 * NG;         // wave-uniform
   const int NC = cx.NC / 2, kbo = cx.csplit * FXC;
-  const int f0 = 128 * fh + 32 * fg;   // this wave's first feature
+  const int f0 = PF * fh + 32 * fg;    // this wave's first feature
   const float* w1row = W1 + (int64_t)(f0 + r) * cx.D0 + 16 * h + blk * kbo;
   f32x4 awc[4];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) awc[j] = *reinterpret_cast<const f32x4*>(w1row + 4 * j);
+  for (int j = 0; j < 4; ++j) awc[j] = act ? *reinterpret_cast<const f32x4*>(w1row + 4 * j) : f32x4{0.f, 0.f, 0.f, 0.f};
   const float* xsrc[C::XV];
   bool xok[C::XV];
 #pragma unroll
@@ -449,7 +453,8 @@ __device__ __forceinline__ void rq_piece_pass(FusedCtx<H1, H2>& cx, int tb, int 
       const int gn = gi + 1 < 2 * NC ? gi + 1 : gi;
       f32x4 awn[4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) awn[j] = *reinterpret_cast<const f32x4*>(w1row + gn * 32 + 4 * j);
+      for (int j = 0; j < 4; ++j)
+        awn[j] = act ? *reinterpret_cast<const f32x4*>(w1row + gn * 32 + 4 * j) : f32x4{0.f, 0.f, 0.f, 0.f};
       const float* xb = cx.xs + cx.buf * PI * FXP + (blk * FT + r) * FXP + 16 * h + g * 32;
       f32x4 bx[4];
 #pragma unroll
@@ -458,10 +463,12 @@ __device__ __forceinline__ void rq_piece_pass(FusedCtx<H1, H2>& cx, int tb, int 
 #pragma unroll
         for (int i = 0; i < C::XV; ++i) cx.xr[i] = *reinterpret_cast<const f32x4*>(xsrc[i] + (c + 1) * FXC);
       }
+      if (act) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
+        for (int j = 0; j < 4; ++j)
 #pragma unroll
-        for (int s = 0; s < 4; ++s) acc = mfma32(awc[j][s], bx[j][s], acc);
+          for (int s = 0; s < 4; ++s) acc = mfma32(awc[j][s], bx[j][s], acc);
+      }
       if (g == 1 && more) {
 #pragma unroll
         for (int i = 0; i < C::XV; ++i) {
@@ -478,13 +485,13 @@ __device__ __forceinline__ void rq_piece_pass(FusedCtx<H1, H2>& cx, int tb, int 
   }
   // block 1's sums -> LDS (the h1 image is free here), then y = (b1 + block 0) + block 1, ReLU
   float* hand = cx.h1s + (fg * 64 + (cx.tid & 63)) * 16;
-  if (blk == 1) {
+  if (act && blk == 1) {
 #pragma unroll
     for (int v4 = 0; v4 < 4; ++v4)
       *reinterpret_cast<f32x4*>(hand + 4 * v4) = f32x4{acc[4 * v4], acc[4 * v4 + 1], acc[4 * v4 + 2], acc[4 * v4 + 3]};
   }
   __syncthreads();
-  if (blk == 0) {
+  if (act && blk == 0) {
     const int64_t item = (int64_t)tb * FT + r;
 #pragma unroll
     for (int g4 = 0; g4 < 4; ++g4) {
@@ -510,14 +517,19 @@ __global__ __launch_bounds__(64 * FWV, 1) void rq_encoder_kernel(
     const float* __restrict__ x, int64_t n, int D0, int csplit, const float* __restrict__ W1,
     const float* __restrict__ b1, const float* __restrict__ W2, const float* __restrict__ b2,
     const float* __restrict__ W3, const float* __restrict__ b3, float* __restrict__ z_out,
-    int tiles, float* __restrict__ h1g) {
+    int tiles, float* __restrict__ h1g, int pq) {
   using C = FusedCfg<H1, H2>;
   extern __shared__ __attribute__((aligned(16))) float sm[];
+  // pq: pieces per leftover tile (2: feature halves; 4: quarters, the short-call plan)
   const int G = gridDim.x, q = tiles / G, b = blockIdx.x;
-  const int npieces = h1g ? 2 * (tiles - q * G) : 0;
+  const int npieces = h1g ? pq * (tiles - q * G) : 0;
   const int t_begin = h1g ? b * q : (int)((int64_t)b * tiles / G);
   const int t_end = h1g ? t_begin + q : (int)((int64_t)(b + 1) * tiles / G);
-  if (t_begin >= t_end) return;
+  const int piece0 = b < npieces ? b : -1;          // this workgroup's first piece
+  // q = 0 (a short call, every tile as pieces: gr_rq_encoder_fused_launch's small-n plan): no whole
+  // tiles, only pieces
+  const bool pieces_only = t_begin >= t_end;
+  if (pieces_only && piece0 < 0) return;
   FusedCtx<H1, H2> cx;
   cx.x = x; cx.n = n; cx.D0 = D0; cx.NC = D0 / FXC; cx.csplit = csplit; cx.t_end = t_end;
   cx.W2 = W2; cx.b1 = b1; cx.b2 = b2; cx.W3 = W3; cx.b3 = b3; cx.z_out = z_out;
@@ -538,9 +550,9 @@ __global__ __launch_bounds__(64 * FWV, 1) void rq_encoder_kernel(
   // an odd last tile runs as a k-split pass when MKL's block edge halves the chunks (in = 768)
   const bool kso = 2 * csplit == cx.NC;
   const bool ks = kso && ((t_end - t_begin) & 1);
-  const int piece0 = b < npieces ? b : -1;          // this workgroup's first piece
-  const int ptile = piece0 >= 0 ? q * G + (piece0 >> 1) : -1;
-  cx.gload_x(t_begin, 0, ks && t_end - t_begin == 1);
+  const int ptile = piece0 >= 0 ? q * G + piece0 / pq : -1;
+  // the first chunk of the first tile (k-split layout for a single k-split tile or a piece)
+  cx.gload_x(pieces_only ? ptile : t_begin, 0, pieces_only || (ks && t_end - t_begin == 1));
   cx.swrite_x(0);
   __syncthreads();
   int tb = t_begin;
@@ -553,13 +565,15 @@ __global__ __launch_bounds__(64 * FWV, 1) void rq_encoder_kernel(
     else rq_fused_pass<1, H1, H2>(cx, tb, ptile, ptile >= 0);
   }
   for (int pc = piece0; pc >= 0 && pc < npieces; pc += G) {
-    const int t = q * G + (pc >> 1);
+    const int t = q * G + pc / pq;
     if (pc != piece0) {   // a second piece: stage its first chunk (k-split layout)
       cx.gload_x(t, 0, true);
       cx.swrite_x(cx.buf);
       __syncthreads();
     }
-    rq_piece_pass<H1, H2>(cx, t, pc & 1, h1g + (int64_t)(pc >> 1) * FT * H1, W1);
+    float* dst = h1g + (int64_t)(pc / pq) * FT * H1;
+    if (pq == 4) rq_piece_pass<H1, H2, 64>(cx, t, pc & 3, dst, W1);
+    else rq_piece_pass<H1, H2, 128>(cx, t, pc & 1, dst, W1);
   }
 }
 
@@ -675,18 +689,26 @@ int gr_rq_encoder_fused_launch(const float* x, int64_t n, int32_t n_linear, cons
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
       cus = 256;
   }
-  const int64_t grid = tiles < cus ? tiles : cus;
   const int csplit = kb < dims[0] ? kb / FXC : dims[0] / FXC;
+  const bool can_split = scratch && 2 * csplit * FXC == dims[0];
+  // A short call (at most a quarter tile per CU, e.g. the reference's batch of 64 items): every tile
+  // as four feature-quarter pieces, each on its own workgroup with one MKL-block chain per SIMD
+  // (layer 1 in a quarter of the time of a whole-tile pass on one CU), and rq_leftover_kernel for
+  // layers 2-3; otherwise one workgroup per CU over whole tiles with the tiles past q x grid as
+  // feature-half pieces
+  const bool small = can_split && 4 * tiles <= cus;
+  const int64_t grid = small ? 4 * tiles : tiles < cus ? tiles : cus;
   using Cfg = FusedCfg<256, 128>;
   static bool lds_ok = hipFuncSetAttribute(reinterpret_cast<const void*>(rq_encoder_kernel<256, 128>),
                                            hipFuncAttributeMaxDynamicSharedMemorySize,
                                            (int)(Cfg::LDS * sizeof(float))) == hipSuccess;
   if (!lds_ok) return fail(GR_ERR_HIP, "rq fused encoder: cannot raise the LDS limit");
   // leftover-tile pieces when the MKL split halves the chunks (in = 768) and tiles % grid != 0
-  const int64_t left = tiles % grid;
-  float* h1g = (scratch && left && 2 * csplit * FXC == dims[0]) ? scratch : nullptr;
+  const int64_t left = small ? tiles : tiles % grid;
+  float* h1g = (can_split && left) ? scratch : nullptr;
   hipLaunchKernelGGL((rq_encoder_kernel<256, 128>), dim3((unsigned)grid), dim3(64 * FWV), Cfg::LDS * sizeof(float), st, x, n,
-                     dims[0], csplit, wp[0], biases[0], wp[1], biases[1], wp[2], biases[2], z_out, (int)tiles, h1g);
+                     dims[0], csplit, wp[0], biases[0], wp[1], biases[1], wp[2], biases[2], z_out, (int)tiles, h1g,
+                     small ? 4 : 2);
   int rc = check_launch("rq fused encoder");
   if (rc || !h1g) return rc;
   hipLaunchKernelGGL((rq_leftover_kernel<256, 128>), dim3((unsigned)left), dim3(256), 0, st, h1g, n,

@@ -16,7 +16,7 @@ from gr_amd import synth  # noqa: E402
 ap = argparse.ArgumentParser()
 ap.add_argument("--what", default="c5fwd,c2")
 ap.add_argument("--calls", type=int, default=5)
-ap.add_argument("--opt", default="", help="gr_set_option settings, e.g. lin_wres=0,attn_lazy=1")
+ap.add_argument("--opt", default="", help="gr_set_option settings, e.g. lin_wres=0,emb_proj=0")
 a = ap.parse_args()
 if os.environ.get("GR_DIAG_LIB"):   # diagnostic build (build.py --abl MACRO): results may be wrong
     from gr_amd import _lib
@@ -47,5 +47,17 @@ if "c2" in what:
     x = synth.items(100_000, 1000, dev)
     for _ in range(a.calls):
         rq.get_indices(x)
+    torch.cuda.synchronize()
+if "rq64" in what:   # the reference's call pattern: get_indices(x[64]) (RQ-VAE/infer.py:84-95)
+    rq = synth.rqvae_model(3, 256, dev)
+    x = synth.items(64, 77, dev)
+    for _ in range(a.calls):
+        rq.get_indices(x)
+    torch.cuda.synchronize()
+if "pred128" in what:   # predict(seqs[128]) at C3 weights (SASRec/evaluate.py:13, 26)
+    sm = synth.sasrec_model(100_000, synth.sasrec_params(64, 50, 2, 1, 64, dev), dev)
+    seqs = synth.sequences(128, 50, 100_000, 78, dev)
+    for _ in range(a.calls):
+        sm.predict(seqs)
     torch.cuda.synchronize()
 print("done", what, flush=True)
