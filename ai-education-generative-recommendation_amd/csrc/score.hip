@@ -236,13 +236,14 @@ __global__ __launch_bounds__(512, 1) void score_kernel(const float* __restrict__
   }
 }
 
-// Direct-store variant: no store waves and no ring.  Each of the 4 waves
-// scores 64 users against the chunk and writes its accumulators as they stand: register v of lane
+// Direct-store variant: no store waves and no ring.  Each of the 4 waves scores 32 UT users
+// (UT = 2; 1 for calls of <= 128 users, which would otherwise leave half the waves empty) against
+// the chunk and writes its accumulators as they stand: register v of lane
 // (r, h) is row (v&3) + 8(v>>2) + 4h, column r, so one dword store per register covers two rows x
 // 32 consecutive logits (two 128-B segments, unaligned when the row stride is odd: the next
 // chunk's stores complete the lines in L2).  Two workgroups per CU, so one wave's MFMAs run while
 // another's stores drain.
-template <int D, bool NTS = true>
+template <int D, bool NTS = true, int UT = 2>
 __global__ __launch_bounds__(256, 2) void score_direct_kernel(const float* __restrict__ h, int64_t B,
                                                             const float* __restrict__ table, int64_t rows,
                                                             float* __restrict__ out, int64_t ld,
@@ -261,10 +262,10 @@ __global__ __launch_bounds__(256, 2) void score_direct_kernel(const float* __res
   const int64_t chunks = (rows + SC_CHUNK - 1) / SC_CHUNK;
   const int64_t c_begin = chunks * sl / slices, c_end = chunks * (sl + 1) / slices;
   if (c_begin >= c_end) return;
-  const int64_t u0 = (int64_t)ub * 256 + wave * 64;
-  f32x4 hf[2][NQ];
+  const int64_t u0 = (int64_t)ub * (128 * UT) + wave * (32 * UT);
+  f32x4 hf[UT][NQ];
 #pragma unroll
-  for (int ut = 0; ut < 2; ++ut) {
+  for (int ut = 0; ut < UT; ++ut) {
     const int64_t u = u0 + ut * 32 + r;
     const int64_t uc = u < B ? u : B - 1;
 #pragma unroll
@@ -274,7 +275,7 @@ __global__ __launch_bounds__(256, 2) void score_direct_kernel(const float* __res
     }
   }
   // row pointers of the lane's 32 rows (register v of user tile ut), column r
-  const bool full_rows = u0 + 64 <= B;
+  const bool full_rows = u0 + 32 * UT <= B;
   f32x4 st[LV];
   auto gload = [&](int64_t c) {
 #pragma unroll
@@ -299,7 +300,7 @@ __global__ __launch_bounds__(256, 2) void score_direct_kernel(const float* __res
   float* obase = out + u0 * ld + r;
   // software pipeline: the logits of chunk k-1 (prev) are stored one register at a time between
   // the MFMAs of chunk k, so the wave's stores trickle out at a steady rate instead of a burst
-  f32x16 prev[2];
+  f32x16 prev[UT];
   int64_t pk = -1;   // chunk held in prev (-1: none)
   auto store_one = [&](int t) {   // register t of prev: user tile t >> 4, register t & 15
     const int ut = t >> 4, v = t & 15;
@@ -312,16 +313,17 @@ __global__ __launch_bounds__(256, 2) void score_direct_kernel(const float* __res
     }
     else if (u0 + rl < B && col < rows) *op = prev[ut][v];
   };
-  constexpr int STEPS = NQ * 4;              // (gq, s) steps of a chunk, 2 MFMAs each
-  constexpr int PER = 32 / STEPS > 0 ? 32 / STEPS : 1;   // stores per step
-  constexpr int EVERY = STEPS / 32 > 0 ? STEPS / 32 : 1;  // steps per store
+  constexpr int NST = 16 * UT;               // stores per chunk (one per accumulator register)
+  constexpr int STEPS = NQ * 4;              // (gq, s) steps of a chunk, UT MFMAs each
+  constexpr int PER = NST / STEPS > 0 ? NST / STEPS : 1;   // stores per step
+  constexpr int EVERY = STEPS / NST > 0 ? STEPS / NST : 1;  // steps per store
 #pragma unroll 1
   for (int64_t k = c_begin; k < c_end; ++k) {
     const int kb = (int)((k - c_begin) & 1);
     const bool have_prev = pk >= 0;
-    f32x16 acc[2];
+    f32x16 acc[UT];
 #pragma unroll
-    for (int ut = 0; ut < 2; ++ut)
+    for (int ut = 0; ut < UT; ++ut)
 #pragma unroll
       for (int v = 0; v < 16; ++v) acc[ut][v] = 0.f;
     const float* tb = &tab[kb][r * P + 4 * hh];
@@ -332,7 +334,7 @@ __global__ __launch_bounds__(256, 2) void score_direct_kernel(const float* __res
         for (int s4 = 0; s4 < 4; ++s4) {
           const int step = gq * 4 + s4;
 #pragma unroll
-          for (int ut = 0; ut < 2; ++ut) acc[ut] = mfma32(hf[ut][gq][s4], bt[s4], acc[ut]);
+          for (int ut = 0; ut < UT; ++ut) acc[ut] = mfma32(hf[ut][gq][s4], bt[s4], acc[ut]);
           if (have_prev && step % EVERY == 0) {
 #pragma unroll
             for (int e = 0; e < PER; ++e) store_one((step / EVERY) * PER + e);
@@ -343,13 +345,13 @@ __global__ __launch_bounds__(256, 2) void score_direct_kernel(const float* __res
       swrite(kb ^ 1);
       if (k + 2 < c_end) gload(k + 2);
     }
-    prev[0] = acc[0];
-    prev[1] = acc[1];
+#pragma unroll
+    for (int ut = 0; ut < UT; ++ut) prev[ut] = acc[ut];
     pk = k;
     __syncthreads();
   }
 #pragma unroll
-  for (int t = 0; t < 32; ++t) store_one(t);
+  for (int t = 0; t < NST; ++t) store_one(t);
 }
 
 // Direct stores into rows that do not start on a 128-byte line (the reference's own contiguous
@@ -530,7 +532,10 @@ int gr_score_launch(const float* h, int64_t B, int32_t d, const float* table, in
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
       cus = 256;
   }
-  const int64_t ublocks = (B + 255) / 256;
+  // calls of <= 128 users (the reference's eval batch, evaluate.py:13): the direct kernel with one
+  // 32-user tile per wave (128 users per workgroup), every wave busy
+  const bool ut1 = B <= 128;
+  const int64_t ublocks = ut1 ? 1 : (B + 255) / 256;
   const int64_t chunks = (rows + SC_CHUNK - 1) / SC_CHUNK;
   // direct / rotated kernels: two workgroups per CU; the ring kernel: one
   auto slices_for = [&](int per_cu) {
@@ -553,8 +558,13 @@ int gr_score_launch(const float* h, int64_t B, int32_t d, const float* table, in
   // lines (B 2048: 593 vs 393 us) and the rotated whole-line kernel runs (412 us;
   // profiles/r04/ab_predict_contiguous.txt), or at d = 128 (where the rotated form spills) the ring.
   const bool fits_mall = (double)B * (double)ld * 4.0 <= 160e6;
-#define GR_SC_DIRECT(DD, NTS) hipLaunchKernelGGL((score_direct_kernel<DD, NTS>), g2, blk, 0, st, h, B, table, rows, \
-                                                 logits, ld, (int)ublocks, (int)sl2, smaj)
+#define GR_SC_DIRECT(DD, NTS)                                                                             \
+  if (ut1)                                                                                                \
+    hipLaunchKernelGGL((score_direct_kernel<DD, NTS, 1>), g2, blk, 0, st, h, B, table, rows, logits, ld, \
+                       (int)ublocks, (int)sl2, smaj);                                                     \
+  else                                                                                                    \
+    hipLaunchKernelGGL((score_direct_kernel<DD, NTS, 2>), g2, blk, 0, st, h, B, table, rows, logits, ld, \
+                       (int)ublocks, (int)sl2, smaj)
 #define GR_SC_SWITCH(M, ...)            \
   switch (d) {                          \
     case 16: M(16, __VA_ARGS__); break; \
