@@ -34,7 +34,11 @@
 
 #ifndef GR_QDIAG
 #define GR_QDIAG 0   // diagnostic builds only (scripts/build_variant.sh): 1 no argmin, 2 no MFMA,
-#endif               // 3 no codebook norms, 4 no residual norms (wrong IDs in all of them)
+#endif               // 3 no codebook norms, 4 no residual norms, 5 no level loop (wrong IDs in all)
+
+#ifndef GR_QRES
+#define GR_QRES 1    // 0: never keep every level's codebook resident (A/B builds)
+#endif
 
 namespace gr {
 
@@ -185,8 +189,8 @@ __global__ __launch_bounds__(RQ_W * 64) void rq_quantize_kernel(
     }
     __syncthreads();
   }
-  int loff = 0;   // res: this level's first row in the resident image
-  for (int l = 0; l < L; ++l) {
+  int loff = 0;   // resident: this level's first row in the resident image
+  for (int l = 0; l < (GR_QDIAG == 5 ? 0 : L); ++l) {
     const int K = lv.K[l];
     const float* cb = lv.cb[l];
     float* cbi = resident ? cbs + loff * EP : cbs;   // the level's (or chunk's) LDS image and norms
@@ -365,7 +369,7 @@ static int launch_quantize_e(const float* z, int64_t n, int e, int L, const RQLe
   // levels fit 160 KiB of LDS (3 x 256 codes at e = 32: 99 KiB)
   int ktot = 0;
   for (int l = 0; l < L; ++l) ktot += (lv.K[l] + 31) & ~31;
-  const bool res = tiles <= (int64_t)cu_count() &&
+  const bool res = GR_QRES && tiles <= (int64_t)cu_count() &&
                    (size_t)ktot * EP * 4 + (size_t)ktot * 4 + RQ_PART_BYTES <= 160 * 1024;
   if (res) kch = ktot;
   const size_t lds = (size_t)kch * EP * 4 + (size_t)kch * 4 + RQ_PART_BYTES;
