@@ -41,6 +41,7 @@ __device__ __forceinline__ int line_shift(uint32_t pbase, int ul, int64_t ld) {
 template <int D> struct ScStage {
   static constexpr int NF = SC_CHUNK * D / 4;
   static constexpr int LV = (NF + 255) / 256;
+  static constexpr bool FULL = NF % 256 == 0;   // every thread stages LV whole float4s: no guard
 };
 
 // The ring kernel (see the header): 4 compute + 4 store waves, one workgroup per CU; the XCD's
@@ -151,14 +152,14 @@ __global__ __launch_bounds__(512, 1) void score_kernel(const float* __restrict__
         const int f = stid + 256 * i, row = f / (D / 4), col = (f % (D / 4)) * 4;
         int64_t item = c * SC_CHUNK + row;
         item = item < rows ? item : rows - 1;   // past-the-end items are never stored
-        if (f < ScStage<D>::NF) st[sb][i] = *reinterpret_cast<const f32x4*>(table + item * D + col);
+        if (ScStage<D>::FULL || f < ScStage<D>::NF) st[sb][i] = *reinterpret_cast<const f32x4*>(table + item * D + col);
       }
     };
     auto swrite = [&](int b, int sb) {
 #pragma unroll
       for (int i = 0; i < LV; ++i) {
         const int f = stid + 256 * i, row = f / (D / 4), col = (f % (D / 4)) * 4;
-        if (f < ScStage<D>::NF) *reinterpret_cast<f32x4*>(&tab[b][row * P + col]) = st[sb][i];
+        if (ScStage<D>::FULL || f < ScStage<D>::NF) *reinterpret_cast<f32x4*>(&tab[b][row * P + col]) = st[sb][i];
       }
     };
     gload(c_begin, 0);
@@ -283,14 +284,14 @@ __global__ __launch_bounds__(256, 2) void score_direct_kernel(const float* __res
       const int f = tid + 256 * i, row = f / (D / 4), col = (f % (D / 4)) * 4;
       int64_t item = c * SC_CHUNK + row;
       item = item < rows ? item : rows - 1;
-      if (f < ScStage<D>::NF) st[i] = *reinterpret_cast<const f32x4*>(table + item * D + col);
+      if (ScStage<D>::FULL || f < ScStage<D>::NF) st[i] = *reinterpret_cast<const f32x4*>(table + item * D + col);
     }
   };
   auto swrite = [&](int b) {
 #pragma unroll
     for (int i = 0; i < LV; ++i) {
       const int f = tid + 256 * i, row = f / (D / 4), col = (f % (D / 4)) * 4;
-      if (f < ScStage<D>::NF) *reinterpret_cast<f32x4*>(&tab[b][row * P + col]) = st[i];
+      if (ScStage<D>::FULL || f < ScStage<D>::NF) *reinterpret_cast<f32x4*>(&tab[b][row * P + col]) = st[i];
     }
   };
   gload(c_begin);
@@ -422,14 +423,14 @@ __global__ __launch_bounds__(256, 2) void score_rot_kernel(const float* __restri
       const int f = tid + 256 * i, row = f / (D / 4), col = (f % (D / 4)) * 4;
       int64_t item = c * SC_CHUNK + row;
       item = item < rows ? item : rows - 1;
-      if (f < ScStage<D>::NF) st[i] = *reinterpret_cast<const f32x4*>(table + item * D + col);
+      if (ScStage<D>::FULL || f < ScStage<D>::NF) st[i] = *reinterpret_cast<const f32x4*>(table + item * D + col);
     }
   };
   auto swrite = [&](int b) {
 #pragma unroll
     for (int i = 0; i < LV; ++i) {
       const int f = tid + 256 * i, row = f / (D / 4), col = (f % (D / 4)) * 4;
-      if (f < ScStage<D>::NF) *reinterpret_cast<f32x4*>(&tab[b][row * P + col]) = st[i];
+      if (ScStage<D>::FULL || f < ScStage<D>::NF) *reinterpret_cast<f32x4*>(&tab[b][row * P + col]) = st[i];
     }
   };
   gload(c_begin);

@@ -42,6 +42,14 @@ if "shard" in what:   # one C5 catalog shard (125,000 rows) against 512 users: g
     for _ in range(a.calls):
         ops.score_topk(h, shard, 10, 0, thresholds=ts, mask_col0=True)
     torch.cuda.synchronize()
+if "rankshard" in what:   # the c5_rank leg's scoring: 4096 users x one 125,000-row shard
+    from gr_amd import ops
+    h = torch.randn(4096, 128, device=dev) * 0.3
+    shard = synth.table_rows(torch.arange(125_000, device=dev), 128, 7, dev)
+    ts = torch.zeros(4096, device=dev)
+    for _ in range(a.calls):
+        ops.score_topk(h, shard, 10, 0, thresholds=ts, mask_col0=True)
+    torch.cuda.synchronize()
 if "c2" in what:
     rq = synth.rqvae_model(3, 256, dev)
     x = synth.items(100_000, 1000, dev)
