@@ -249,7 +249,9 @@ __global__ __launch_bounds__(256, 2) void score_direct_kernel(const float* __res
                                                             const float* __restrict__ table, int64_t rows,
                                                             float* __restrict__ out, int64_t ld,
                                                             int ublocks, int slices, int slice_major) {
-  constexpr int NQ = D / 8;
+  // feature groups as (g, q): g over 32-deep groups, q over float4 slots (sc_feat(4 g + q, hh));
+  // the nested form keeps rounds 1-4's register layout and schedule at d >= 32
+  constexpr int KG = D >= 32 ? D / 32 : 1, QN = D >= 32 ? 4 : D / 8;
   constexpr int P = D + 4;
   constexpr int LV = ScStage<D>::LV;
   __shared__ __attribute__((aligned(16))) float tab[2][SC_CHUNK * P];
@@ -264,16 +266,18 @@ __global__ __launch_bounds__(256, 2) void score_direct_kernel(const float* __res
   const int64_t c_begin = chunks * sl / slices, c_end = chunks * (sl + 1) / slices;
   if (c_begin >= c_end) return;
   const int64_t u0 = (int64_t)ub * (128 * UT) + wave * (32 * UT);
-  f32x4 hf[UT][NQ];
+  f32x4 hf[UT][KG][QN];
 #pragma unroll
   for (int ut = 0; ut < UT; ++ut) {
     const int64_t u = u0 + ut * 32 + r;
     const int64_t uc = u < B ? u : B - 1;
 #pragma unroll
-    for (int gq = 0; gq < NQ; ++gq) {
-      const f32x4 v = *reinterpret_cast<const f32x4*>(h + uc * D + sc_feat(gq, hh));
-      hf[ut][gq] = u < B ? v : f32x4{0.f, 0.f, 0.f, 0.f};
-    }
+    for (int g = 0; g < KG; ++g)
+#pragma unroll
+      for (int q = 0; q < QN; ++q) {
+        const f32x4 v = *reinterpret_cast<const f32x4*>(h + uc * D + 32 * g + 8 * q + 4 * hh);
+        hf[ut][g][q] = u < B ? v : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
   }
   // row pointers of the lane's 32 rows (register v of user tile ut), column r
   const bool full_rows = u0 + 32 * UT <= B;
@@ -315,7 +319,7 @@ __global__ __launch_bounds__(256, 2) void score_direct_kernel(const float* __res
     else if (u0 + rl < B && col < rows) *op = prev[ut][v];
   };
   constexpr int NST = 16 * UT;               // stores per chunk (one per accumulator register)
-  constexpr int STEPS = NQ * 4;              // (gq, s) steps of a chunk, UT MFMAs each
+  constexpr int STEPS = KG * QN * 4;         // (g, q, s) steps of a chunk, UT MFMAs each
   constexpr int PER = NST / STEPS > 0 ? NST / STEPS : 1;   // stores per step
   constexpr int EVERY = STEPS / NST > 0 ? STEPS / NST : 1;  // steps per store
 #pragma unroll 1
@@ -329,13 +333,15 @@ __global__ __launch_bounds__(256, 2) void score_direct_kernel(const float* __res
       for (int v = 0; v < 16; ++v) acc[ut][v] = 0.f;
     const float* tb = &tab[kb][r * P + 4 * hh];
 #pragma unroll
-    for (int gq = 0; gq < NQ; ++gq) {
-        const f32x4 bt = *reinterpret_cast<const f32x4*>(tb + 8 * gq);
+    for (int g = 0; g < KG; ++g)
+#pragma unroll
+      for (int q = 0; q < QN; ++q) {
+        const f32x4 bt = *reinterpret_cast<const f32x4*>(tb + 32 * g + 8 * q);
 #pragma unroll
         for (int s4 = 0; s4 < 4; ++s4) {
-          const int step = gq * 4 + s4;
+          const int step = (g * QN + q) * 4 + s4;
 #pragma unroll
-          for (int ut = 0; ut < UT; ++ut) acc[ut] = mfma32(hf[ut][gq][s4], bt[s4], acc[ut]);
+          for (int ut = 0; ut < UT; ++ut) acc[ut] = mfma32(hf[ut][g][q][s4], bt[s4], acc[ut]);
           if (have_prev && step % EVERY == 0) {
 #pragma unroll
             for (int e = 0; e < PER; ++e) store_one((step / EVERY) * PER + e);
@@ -373,7 +379,9 @@ __global__ __launch_bounds__(256, 2) void score_rot_kernel(const float* __restri
                                                          const float* __restrict__ table, int64_t rows,
                                                          float* __restrict__ out, int64_t ld,
                                                          int ublocks, int slices, int slice_major) {
-  constexpr int NQ = D / 8;
+  // feature groups as (g, q): g over 32-deep groups, q over float4 slots (sc_feat(4 g + q, hh));
+  // the nested form keeps rounds 1-4's register layout and schedule at d >= 32
+  constexpr int KG = D >= 32 ? D / 32 : 1, QN = D >= 32 ? 4 : D / 8;
   constexpr int P = D + 4;
   constexpr int LV = ScStage<D>::LV;
   __shared__ __attribute__((aligned(16))) float tab[2][SC_CHUNK * P];
@@ -386,16 +394,18 @@ __global__ __launch_bounds__(256, 2) void score_rot_kernel(const float* __restri
   const int64_t c_begin = chunks * sl / slices, c_end = chunks * (sl + 1) / slices;
   if (c_begin >= c_end) return;
   const int64_t u0 = (int64_t)ub * 256 + wave * 64;
-  f32x4 hf[2][NQ];
+  f32x4 hf[2][KG][QN];
 #pragma unroll
   for (int ut = 0; ut < 2; ++ut) {
     const int64_t u = u0 + ut * 32 + r;
     const int64_t uc = u < B ? u : B - 1;
 #pragma unroll
-    for (int gq = 0; gq < NQ; ++gq) {
-      const f32x4 v = *reinterpret_cast<const f32x4*>(h + uc * D + sc_feat(gq, hh));
-      hf[ut][gq] = u < B ? v : f32x4{0.f, 0.f, 0.f, 0.f};
-    }
+    for (int g = 0; g < KG; ++g)
+#pragma unroll
+      for (int q = 0; q < QN; ++q) {
+        const f32x4 v = *reinterpret_cast<const f32x4*>(h + uc * D + 32 * g + 8 * q + 4 * hh);
+        hf[ut][g][q] = u < B ? v : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
   }
   const bool full_rows = u0 + 64 <= B;
   // per register v: row rl(v) of user tile 0 (tile 1's row rl + 32 has the same line offset o,
@@ -460,7 +470,7 @@ __global__ __launch_bounds__(256, 2) void score_rot_kernel(const float* __restri
     }
   };
   auto line_interior = [&](int64_t L) { return full_rows && L > c_begin && (L + 1) * SC_CHUNK <= rows; };
-  constexpr int STEPS = NQ * 4;                           // (gq, s) steps of a chunk, 2 MFMAs each
+  constexpr int STEPS = KG * QN * 4;                      // (g, q, s) steps of a chunk, 2 MFMAs each
   constexpr int PER = 32 / STEPS > 0 ? 32 / STEPS : 1;    // stores per step
   constexpr int EVERY = STEPS / 32 > 0 ? STEPS / 32 : 1;  // steps per store
 #pragma unroll 1
@@ -475,13 +485,15 @@ __global__ __launch_bounds__(256, 2) void score_rot_kernel(const float* __restri
       for (int v = 0; v < 16; ++v) acc[ut][v] = 0.f;
     const float* tb = &tab[kb][r * P + 4 * hh];
 #pragma unroll
-    for (int gq = 0; gq < NQ; ++gq) {
-        const f32x4 bt = *reinterpret_cast<const f32x4*>(tb + 8 * gq);
+    for (int g = 0; g < KG; ++g)
+#pragma unroll
+      for (int q = 0; q < QN; ++q) {
+        const f32x4 bt = *reinterpret_cast<const f32x4*>(tb + 32 * g + 8 * q);
 #pragma unroll
         for (int s4 = 0; s4 < 4; ++s4) {
-          const int step = gq * 4 + s4;
+          const int step = (g * QN + q) * 4 + s4;
 #pragma unroll
-          for (int ut = 0; ut < 2; ++ut) acc[ut] = mfma32(hf[ut][gq][s4], bt[s4], acc[ut]);
+          for (int ut = 0; ut < 2; ++ut) acc[ut] = mfma32(hf[ut][g][q][s4], bt[s4], acc[ut]);
           if (inter && step % EVERY == 0) {
 #pragma unroll
             for (int e = 0; e < PER; ++e) store_reg(k - 1, (step / EVERY) * PER + e, true);
