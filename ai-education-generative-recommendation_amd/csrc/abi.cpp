@@ -21,8 +21,10 @@ struct Opt {
 };
 // rq_fused (1: the fused persistent encoder kernel when the shape allows, 0: layer-wise kernels)
 static std::atomic<int64_t> g_rq_fused{1};
-// sas_fused (1: the one-wave fused SASRec forward when n <= 64 and d <= 64, 0: layer-wise kernels)
-static std::atomic<int64_t> g_sas_fused{1};
+// sas_fused (the fused SASRec forward when n <= 64 and d <= 64: 2 = one or two waves per sequence
+// by batch size (two only when n > 32), 3 = two waves whenever n > 32, 1 = one wave per sequence;
+// 0: layer-wise kernels)
+static std::atomic<int64_t> g_sas_fused{2};
 // sas_rowtile (1: d = 128 forwards on the row-tile kernels of sasrec_rowtile.hip, 0: one kernel per op)
 static std::atomic<int64_t> g_sas_rowtile{1};
 // lin_wres (1: gr_linear_f32 with k = 128, n % 128 == 0, no residual, m >= 96 x 256 keeps 32-column
@@ -36,7 +38,7 @@ static std::atomic<int64_t> g_emb_proj{1};
 static std::atomic<int64_t> g_topk_half{2};
 
 static const Opt kOpts[] = {
-    {"rq_fused", &g_rq_fused, 0, 1},   {"sas_fused", &g_sas_fused, 0, 1}, {"sas_rowtile", &g_sas_rowtile, 0, 1},
+    {"rq_fused", &g_rq_fused, 0, 1},   {"sas_fused", &g_sas_fused, 0, 3}, {"sas_rowtile", &g_sas_rowtile, 0, 1},
     {"lin_wres", &g_lin_wres, 0, 1},   {"emb_proj", &g_emb_proj, 0, 1},   {"topk_half", &g_topk_half, 0, 2},
 };
 

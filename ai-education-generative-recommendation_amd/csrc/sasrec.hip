@@ -219,7 +219,7 @@ struct SasWs {
 // The fused kernel (sasrec_fused.hip) covers n <= 64, d <= 64; it needs only the [B, d] last
 // hidden states.  Must agree with the shape test of gr_sasrec_fused_launch.
 static bool fused_ok(const gr_sasrec_params* p, int32_t n) {
-  return option("sas_fused") == 1 && n <= 64 && p->d <= 64 && p->d % 8 == 0 &&
+  return option("sas_fused") >= 1 && n <= 64 && p->d <= 64 && p->d % 8 == 0 &&
          (p->d / p->n_heads) % 8 == 0 && p->mlp <= 128 && p->n_blocks <= 8;
 }
 

@@ -54,10 +54,13 @@ const char* gr_last_error(void);
  *   "rq_fused"      1 (default): gr_rq_encode_f32 runs the fused persistent kernel when the encoder
  *                   shape is in -> 256 -> 128 -> 32; 0: the layer-wise path (exact gr_linear +
  *                   quantize).
- *   "sas_fused"     1 (default): gr_sasrec_forward_f32 / gr_sasrec_predict_f32 run the fused
+ *   "sas_fused"     2 (default): gr_sasrec_forward_f32 / gr_sasrec_predict_f32 run the fused
  *                   register-resident forward kernel when n <= 64, d <= 64 (d and the head width
- *                   multiples of 8), mlp <= 128, num_blocks <= 8; 0: the layer-wise pipeline
- *                   (the workspace query follows the option in force when it is called).
+ *                   multiples of 8), mlp <= 128, num_blocks <= 8: one wave per sequence, or two
+ *                   (one per 32-token tile) when n > 32 and the batch size favours it; 3: two
+ *                   waves whenever n > 32; 1: always one; 0: the layer-wise pipeline (the
+ *                   workspace query follows the option in force when it is called).  The fused
+ *                   forms give bitwise the same results.
  *   "sas_rowtile"   1 (default): d = 128 forwards on the row-tile kernels; 0: one kernel per op.
  *   "lin_wres"      1 (default): gr_linear_f32 with k = 128, n % 128 == 0, no residual and
  *                   m >= 96 x 256 runs a persistent kernel that keeps each wave's 32 columns of w in

@@ -17,15 +17,15 @@ TOL = 1e-5
 SAS = ["sas_csv_c1", "sas_syn_c3", "sas_syn_c5", "sas_syn_h2", "sas_syn_d32_h4"]
 
 
-@pytest.fixture(params=[1, 0], ids=["fused", "layerwise"])
+@pytest.fixture(params=[3, 1, 0], ids=["fused2", "fused", "layerwise"])
 def sas_path(request):
-    """Run a test through the register-resident fused forward (n <= 64, d <= 64) and through the
-    layer-wise pipeline: both must meet the same bar (shapes outside the fused kernel's range run
-    layer-wise either way)."""
+    """Run a test through the register-resident fused forward (n <= 64, d <= 64: two waves per
+    sequence when n > 32, or one), and through the layer-wise pipeline: all must meet the same bar
+    (shapes outside the fused kernel's range run layer-wise either way)."""
     from gr_amd import _lib
     _lib.set_option("sas_fused", request.param)
     yield request.param
-    _lib.set_option("sas_fused", 1)
+    _lib.set_option("sas_fused", 2)
 
 
 def build(name, dev):
@@ -304,7 +304,7 @@ def test_attn_persist_vs_oracle(d, heads, n, blocks, B, dev):
         f = m.forward(seqs)
         sub = m.forward(seqs[:3])
     finally:
-        _lib.set_option("sas_fused", 1)
+        _lib.set_option("sas_fused", 2)
     assert torch.equal(sub, f[:3])
     pick = torch.arange(0, B, max(1, B // 64), device=dev)
     sd = {k: v.detach().cpu() for k, v in m.state_dict().items()}
@@ -326,10 +326,13 @@ def test_fused_tail_h_vs_full_block_and_oracle(d, heads, n, blocks, B, dev):
     p = synth.sasrec_params(d, n, blocks, heads, 2 * d, dev)
     m = synth.sasrec_model(items, p, dev, seed=d + heads + n)
     seqs = synth.sequences(B, n, items, 7 + n, dev)
-    _lib.set_option("sas_fused", 1)
-    h_h = m.last_hidden(seqs).cpu()
-    full = m.forward(seqs)[:, -1, :].cpu()
-    got = m.predict(seqs).cpu()
+    _lib.set_option("sas_fused", 3)
+    try:
+        h_h = m.last_hidden(seqs).cpu()
+        full = m.forward(seqs)[:, -1, :].cpu()
+        got = m.predict(seqs).cpu()
+    finally:
+        _lib.set_option("sas_fused", 2)
     sd = {k: v.detach().cpu() for k, v in m.state_dict().items()}
     ref_f = sasrec_oracle.forward(seqs.cpu(), sd, blocks, heads, 1e-8)
     ref = sasrec_oracle.predict(seqs.cpu(), sd, blocks, heads, 1e-8)
@@ -434,20 +437,51 @@ def test_fused_forward_vs_oracle(d, heads, mlp, n, blocks, B, dev):
     widths, narrow heads, n = 1, tile boundaries) against the CPU oracle, forward and predict."""
     from gr_amd import _lib, synth
     from oracle import sasrec_oracle
-    _lib.set_option("sas_fused", 1)
     items = 500
     p = synth.sasrec_params(d, n, blocks, heads, mlp, dev)
     m = synth.sasrec_model(items, p, dev, seed=d + n + blocks)
     seqs = synth.sequences(B, n, items, 3 + n, dev)
     sd = {k: v.detach().cpu() for k, v in m.state_dict().items()}
     ref_f = sasrec_oracle.forward(seqs.cpu(), sd, blocks, heads, 1e-8)
-    got_f = m.forward(seqs).cpu()
-    assert (got_f - ref_f).abs().max().item() < 5e-5
     ref = sasrec_oracle.predict(seqs.cpu(), sd, blocks, heads, 1e-8)
-    got = m.predict(seqs).cpu()
-    err = ((got - ref).abs() / ref.abs().amax(1, keepdim=True)).max().item()
-    assert err <= TOL, err
-    assert (m.last_hidden(seqs).cpu() - ref_f[:, -1, :]).abs().max().item() < 5e-5
+    try:
+        for opt in (1, 3):   # one wave per sequence; two when n > 32
+            _lib.set_option("sas_fused", opt)
+            got_f = m.forward(seqs).cpu()
+            assert (got_f - ref_f).abs().max().item() < 5e-5
+            got = m.predict(seqs).cpu()
+            err = ((got - ref).abs() / ref.abs().amax(1, keepdim=True)).max().item()
+            assert err <= TOL, err
+            assert (m.last_hidden(seqs).cpu() - ref_f[:, -1, :]).abs().max().item() < 5e-5
+    finally:
+        _lib.set_option("sas_fused", 2)
+
+
+@pytest.mark.parametrize("d,heads,mlp,n,blocks,B", [
+    (64, 1, 64, 50, 2, 37), (64, 1, 64, 64, 2, 5), (32, 1, 32, 33, 3, 7), (48, 2, 96, 40, 2, 11),
+    (40, 5, 20, 64, 1, 13), (64, 2, 64, 50, 8, 2), (64, 8, 128, 63, 2, 5), (16, 2, 32, 47, 2, 6),
+    (64, 1, 64, 50, 2, 300),
+])
+def test_fused_two_waves_equal_one_wave(d, heads, mlp, n, blocks, B, dev):
+    """sas_fused = 3 (two waves per sequence, wave w owning token tile w, tile 0's K / V handed
+    to wave 1 through LDS) runs the one-wave kernel's instruction sequence per token tile: forward,
+    last_hidden and predict bitwise equal to sas_fused = 1 (32 < n <= 64, exact and padded widths,
+    1-8 heads, 1-8 blocks).  The default (2) picks one of the two by batch size."""
+    from gr_amd import _lib, synth
+    items = 500
+    p = synth.sasrec_params(d, n, blocks, heads, mlp, dev)
+    m = synth.sasrec_model(items, p, dev, seed=d + n + blocks + 1)
+    seqs = synth.sequences(B, n, items, 5 + n, dev)
+    res = {}
+    try:
+        for opt in (1, 3):
+            _lib.set_option("sas_fused", opt)
+            res[opt] = (m.forward(seqs), m.last_hidden(seqs), m.predict(seqs))
+    finally:
+        _lib.set_option("sas_fused", 2)
+    for a_, b_ in zip(res[1], res[3]):
+        assert torch.isfinite(a_).all()
+        assert torch.equal(a_, b_)
 
 
 @pytest.mark.parametrize("B,cols,ld", [(7, 100001, 100001), (33, 250000, 250003), (300, 5, 5), (2, 1, 1)])
