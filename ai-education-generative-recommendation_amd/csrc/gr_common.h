@@ -242,6 +242,10 @@ int gr_rq_encoder_fused_launch(const float* x, int64_t n, int32_t n_linear, cons
 int gr_rq_encoder_pack_launch(int32_t n_linear, const int32_t* dims, const float* const* weights, float* pack,
                               hipStream_t st);
 size_t gr_rq_fused_pack_floats(int32_t n_linear, const int32_t* dims);
+bool gr_rq_small_ok(int64_t n, int32_t n_linear, const int32_t* dims, int32_t L, const int32_t* K);
+int gr_rq_small_launch(const float* x, int64_t n, const int32_t* dims, const float* const* biases,
+                       const float* packed, float* h1_scratch, float* h2_scratch, int32_t L, const int32_t* K,
+                       const float* const* codebooks, int64_t* idx_out, float* z_out, hipStream_t st);
 int gr_sasrec_fused_launch(const gr_sasrec_params* p, const int64_t* seqs, int64_t B, int32_t n,
                            float* out, int32_t last_only, int32_t* err, hipStream_t st);
 int gr_attn_mfma_launch(const float* qkv, float* out, int64_t B, int n, int H, int hd, float scale,

@@ -567,6 +567,20 @@ extern "C" int gr_rq_encode_packed_f32(const float* x, int64_t n, int32_t n_line
   if (!mlp_chain(n, n_linear, dims) || !quant_chain(n, e, L, K))   // a 1-15-row call: MKL's small orders
     return gr_rq_rows_launch(x, n, n, nullptr, 0, n_linear, dims, weights, biases, nullptr, nullptr, nullptr,
                              nullptr, 0.f, GR_ACT_RELU, L, K, codebooks, z_out, idx_out, best_out, gap_out, st);
+  if (!best_out && !gap_out && option("rq_fused") == 1 && gr_rq_small_ok(n, n_linear, dims, L, K)) {
+    // a short call (16..1024 rows, the reference's batch of 64): the short-call kernels (rq_small.hip)
+    char* ws = reinterpret_cast<char*>(align_up(reinterpret_cast<uintptr_t>(workspace), 256));
+    const size_t ab = act_bytes(n, n_linear, dims);
+    float* pk = packed ? const_cast<float*>(packed) : reinterpret_cast<float*>(ws + 2 * ab);
+    if (!packed) {
+      rc = gr_rq_encoder_pack_launch(n_linear, dims, weights, pk, st);
+      if (rc) return rc;
+    }
+    rc = gr_rq_small_launch(x, n, dims, biases, pk, reinterpret_cast<float*>(ws), reinterpret_cast<float*>(ws + ab),
+                            L, K, codebooks, idx_out, z_out, st);
+    if (rc != GR_ERR_UNSUPPORTED) return rc;
+    clear_error();
+  }
   float* zb = z_out;
   if (!zb) {   // z in the workspace, after the MLP's part
     char* ws = reinterpret_cast<char*>(align_up(reinterpret_cast<uintptr_t>(workspace), 256));

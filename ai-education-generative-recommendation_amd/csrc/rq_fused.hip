@@ -605,23 +605,26 @@ __global__ __launch_bounds__(256) void rq_leftover_kernel(const float* __restric
   rq_l23<1, H1, H2>(cx, t0 + blockIdx.x);
 }
 
-// Packed weight images of the three layers (one launch): W1 and W2 for the 32x32x2 chains (within
-// every 32-deep k group, feature 8j + 2s + h at 16h + 4j + s), W3 for the 16x16x4 chain (within
-// every 16-deep block, feature 4t + g at 4g + t).  The layers' images lie back to back in `out`.
+// Packed weight images (one launch), back to back in `out`: W1 and W2 for the 32x32x2 chains
+// (within every 32-deep k group, feature 8j + 2s + h at 16h + 4j + s), W3 for the 16x16x4 chain
+// (within every 16-deep block, feature 4t + g at 4g + t), then W1 and W2 again in the 16x16x4 order
+// for the short-call kernels (rq_small.hip).
+constexpr int PACK_IMAGES = 5;
 struct PackArgs {
-  const float* w[3];
-  int64_t end[3];   // cumulative element counts
-  int K[3];
+  const float* w[PACK_IMAGES];
+  int64_t end[PACK_IMAGES];   // cumulative element counts
+  int K[PACK_IMAGES];
 };
 __global__ __launch_bounds__(256) void rq_pack_kernel(PackArgs a, float* __restrict__ out) {
   int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= a.end[2]) return;
-  const int l = i < a.end[0] ? 0 : (i < a.end[1] ? 1 : 2);
+  if (i >= a.end[PACK_IMAGES - 1]) return;
+  int l = 0;
+  while (i >= a.end[l]) ++l;
   const int64_t o = i - (l ? a.end[l - 1] : 0);
   const int K = a.K[l];
   const int64_t row = o / K;
   const int p = (int)(o % K);
-  if (l == 2) {   // W3 for the 16x16x4 chain: feature 16b + 4t + g at 16b + 4g + t
+  if (l >= 2) {   // the 16x16x4 order: feature 16b + 4t + g at 16b + 4g + t
     const int b = p & ~15, g = (p >> 2) & 3, t = p & 3;
     out[i] = a.w[l][row * K + b + 4 * t + g];
     return;
@@ -635,7 +638,7 @@ __global__ __launch_bounds__(256) void rq_pack_kernel(PackArgs a, float* __restr
 // Workspace floats the fused path needs for its packed weights (0 when the shape is not fused).
 size_t gr_rq_fused_pack_floats(int32_t n_linear, const int32_t* dims) {
   if (n_linear != 3 || dims[3] != 32 || dims[1] != 256 || dims[2] != 128) return 0;
-  return (size_t)dims[0] * 256 + 256 * 128 + 128 * 32;
+  return 2 * ((size_t)dims[0] * 256 + 256 * 128) + 128 * 32;
 }
 
 // Returns GR_ERR_UNSUPPORTED (without touching the error message) when the encoder shape is not
@@ -647,10 +650,11 @@ int gr_rq_encoder_pack_launch(int32_t n_linear, const int32_t* dims, const float
   if (gr_rq_fused_pack_floats(n_linear, dims) == 0) return GR_ERR_UNSUPPORTED;
   PackArgs pa{};
   int64_t tot = 0;
-  for (int i = 0; i < 3; ++i) {
-    pa.w[i] = weights[i];
-    pa.K[i] = dims[i];
-    tot += (int64_t)dims[i + 1] * dims[i];
+  for (int i = 0; i < PACK_IMAGES; ++i) {
+    const int l = i < 3 ? i : i - 3;   // images 3, 4: W1, W2 in the 16x16x4 order
+    pa.w[i] = weights[l];
+    pa.K[i] = dims[l];
+    tot += (int64_t)dims[l + 1] * dims[l];
     pa.end[i] = tot;
   }
   hipLaunchKernelGGL(rq_pack_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, pa, pack);

@@ -13,5 +13,7 @@ rm -rf /tmp/gr_kt_$TAG
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/gr_kt_$TAG -o run -- \
   python3 "$ROOT/scripts/prof_kernels.py" "$@" > "$OUT/kt.log" 2>&1
 rc=$?
-python3 "$ROOT/scripts/trace_stats.py" $(find /tmp/gr_kt_$TAG -name '*kernel_trace.csv' | head -1) --top 30 > "$OUT/trace_stats.csv" 2>&1
+TR=$(find /tmp/gr_kt_$TAG -name '*kernel_trace.csv' | head -1)
+python3 "$ROOT/scripts/trace_stats.py" "$TR" --top 30 > "$OUT/trace_stats.csv" 2>&1
+if [ "${KT_RAW:-0}" = 1 ]; then cp "$TR" "$OUT/kernel_trace.csv"; fi   # small runs: keep the timeline
 exit $rc

@@ -189,6 +189,32 @@ def test_partition_edges_vs_oracle(n, dev, parity_log):
     assert diff.sum() == 0, f"{diff.sum()} of {n} rows differ"
 
 
+@pytest.mark.parametrize("n,Ks", [
+    (16, [256, 256, 256]), (17, [256, 256, 256]), (31, [256, 256, 256]), (33, [256, 256, 256]),
+    (64, [256, 256, 256]), (100, [256, 256, 256]), (128, [256, 256, 256]), (255, [256, 256, 256]),
+    (256, [256, 256, 256]), (257, [256, 256, 256]), (1000, [256, 256, 256]), (1024, [256, 256, 256]),
+    (1025, [256, 256, 256]), (64, [1, 33, 5, 512]), (48, [16] * 8), (200, [500, 7]),
+])
+def test_short_call_kernels_vs_oracle(n, Ks, dev, parity_log):
+    """Calls of 16-1024 rows (the reference's batch of 64) run on the short-call kernels
+    (rq_small.hip: 16x16x4 chains, layer 1 over 16 feature tiles and layer 2 over 8 per 16 rows,
+    then layer 3 and every quantizer level in one workgroup per 16 rows): IDs and z against the
+    exact-order oracle, codebooks of 1..512 codes (K not a multiple of 16) and 8 levels; 1025 rows
+    take the long-call kernels."""
+    from gr_amd import ops
+    m, x, ref = _random_case(n, 32, Ks, [256, 128], seed=3 * n + len(Ks), dev=dev)
+    idx = m.get_indices(x).cpu().numpy()
+    lin = m.encoder.linears()
+    idx2, z = ops.rq_encode(x, [l.weight for l in lin], [l.bias for l in lin], m.rq.codebooks(), with_z=True)
+    zref = rq_exact.mlp(x.cpu().numpy(), [l.weight.detach().cpu() for l in lin], [l.bias.detach().cpu() for l in lin])
+    diff = (idx != ref).any(1)
+    parity_log(kind="rq_ids_vs_oracle", shape=f"short call n {n} K{Ks}", path="fused", rows=n,
+               rows_differ=int(diff.sum()), z_rows_differ=int((z.cpu().numpy() != zref).any(1).sum()))
+    assert diff.sum() == 0, f"{diff.sum()} of {n} rows differ"
+    assert np.array_equal(idx2.cpu().numpy(), idx)
+    assert np.array_equal(z.cpu().numpy(), zref)
+
+
 def test_full_population_c4_contiguous(dev, parity_log):
     """Config 4 size (10M items, 4x1024 codebooks, 30.7 GB of input in HBM; rows past 2^31 floats
     exercise 64-bit addressing): the 10M-row encode checked against the exact-order oracle on the
