@@ -104,6 +104,8 @@ SIGNATURES = {
     "gr_topk_f32": (ctypes.c_int, [_vp, _i64, _i64, _i64, _i32, _i64, _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
     "gr_score_pairs_f32": (ctypes.c_int, [_vp, _i64, _i32, _vp, _i64, _vp, _i32, _vp, _vp, _vp]),
     "gr_score_count_gt_f32": (ctypes.c_int, [_vp, _i64, _i32, _vp, _i64, _vp, _i32, _vp, _vp]),
+    "gr_score_count_workspace_bytes": (_sz, [_i64]),
+    "gr_score_count_gt_ws_f32": (ctypes.c_int, [_vp, _i64, _i32, _vp, _i64, _vp, _i32, _vp, _vp, _sz, _vp]),
     "gr_merge_topk_f32": (ctypes.c_int, [_vp, _i64, _vp, _i64, _i64, _i32, _i32, _vp, _vp, _vp]),
     "gr_merge_topk_packed": (ctypes.c_int, [_vp, _i32, _i64, _i32, _i32, _vp, _vp, _vp]),
     "gr_score_topk_workspace_bytes": (_sz, [_i64, _i32, _i64, _i32]),

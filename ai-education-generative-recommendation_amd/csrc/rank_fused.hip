@@ -68,7 +68,7 @@ __global__ __launch_bounds__(256, 2) void score_count_kernel(const float* __rest
                                                             const float* __restrict__ thr,
                                                             int mask_col0,
                                                             unsigned long long* __restrict__ cnt_out,
-                                                            int ublocks, int slices) {
+                                                            int ublocks, int slices, int copies) {
   constexpr int NQ = D / 8;
   constexpr int P = D + 4;
   constexpr int LV = RK_CHUNK * D / 4 / 256;
@@ -186,9 +186,27 @@ __global__ __launch_bounds__(256, 2) void score_count_kernel(const float* __rest
 #pragma unroll
       for (int o = 1; o < 32; o <<= 1) x += __shfl_xor(x, o);
       const int64_t u = u0 + ut * 32 + (v & 3) + 8 * (v >> 2) + 4 * hh;
-      if (r == 0 && u < B && x) atomicAdd(&cnt_out[u], (unsigned long long)x);
+      // slice sl adds into copy sl % copies: at most ceil(slices / copies) adds per address (a
+      // short batch split over every CU's slices would otherwise queue hundreds of adds on one word)
+      if (r == 0 && u < B && x) atomicAdd(&cnt_out[(int64_t)(sl % copies) * B + u], (unsigned long long)x);
     }
 }
+
+// counts[u] = sum of the copies' words in copy order (exact integer sums), which are cleared for the
+// next call
+__global__ __launch_bounds__(256) void count_copies_kernel(unsigned long long* __restrict__ ws, int64_t B, int copies,
+                                                           int64_t* __restrict__ counts) {
+  const int64_t u = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (u >= B) return;
+  unsigned long long s = 0;
+  for (int c = 0; c < copies; ++c) {
+    s += ws[(int64_t)c * B + u];
+    ws[(int64_t)c * B + u] = 0;
+  }
+  counts[u] = (int64_t)s;
+}
+
+constexpr int RK_COPIES = 16;   // count copies in the workspace form
 
 static int cu_count() {
   static int cus = 0;
@@ -225,9 +243,9 @@ extern "C" int gr_score_pairs_f32(const float* h, int64_t B, int32_t d, const fl
   return check_launch("gr_score_pairs_f32");
 }
 
-extern "C" int gr_score_count_gt_f32(const float* h, int64_t B, int32_t d, const float* table,
-                                     int64_t rows, const float* thresholds, int32_t mask_col0,
-                                     int64_t* counts_out, void* stream) {
+static int count_launch(const float* h, int64_t B, int32_t d, const float* table, int64_t rows,
+                        const float* thresholds, int32_t mask_col0, int64_t* counts_out, void* workspace,
+                        size_t workspace_bytes, hipStream_t st) {
   using namespace gr;
   clear_error();
   if (B < 0 || rows < 0) return fail(GR_ERR_ARG, "gr_score_count_gt_f32: bad shape");
@@ -236,10 +254,6 @@ extern "C" int gr_score_count_gt_f32(const float* h, int64_t B, int32_t d, const
   if (d != 16 && d != 32 && d != 64 && d != 128)
     return fail(GR_ERR_UNSUPPORTED, "gr_score_count_gt_f32: d must be 16, 32, 64 or 128");
   if (!aligned16(h) || !aligned16(table)) return fail(GR_ERR_ARG, "gr_score_count_gt_f32: h / table not 16-byte aligned");
-  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  if (gr_fill32_launch(counts_out, 0u, B * 2, st) != GR_OK)
-    return fail(GR_ERR_HIP, "gr_score_count_gt_f32: memset failed");
-  if (rows == 0) return GR_OK;
   const int64_t ublocks = (B + 128 * RK_UT - 1) / (128 * RK_UT);
   const int64_t chunks = (rows + RK_CHUNK - 1) / RK_CHUNK;
   const int64_t per_cu = 2;   // resident workgroups per CU (registers, LDS)
@@ -247,13 +261,47 @@ extern "C" int gr_score_count_gt_f32(const float* h, int64_t B, int32_t d, const
   if (slices > chunks) slices = chunks;
   if (slices < 1) slices = 1;
   if (ublocks * slices > 0x7fffffffLL) return fail(GR_ERR_UNSUPPORTED, "gr_score_count_gt_f32: grid too large");
-  const dim3 g((unsigned)(ublocks * slices)), b(256);
-  auto* cnt = reinterpret_cast<unsigned long long*>(counts_out);
-  switch (d) {
-    case 16: hipLaunchKernelGGL(score_count_kernel<16>, g, b, 0, st, h, B, table, rows, thresholds, mask_col0, cnt, (int)ublocks, (int)slices); break;
-    case 32: hipLaunchKernelGGL(score_count_kernel<32>, g, b, 0, st, h, B, table, rows, thresholds, mask_col0, cnt, (int)ublocks, (int)slices); break;
-    case 64: hipLaunchKernelGGL(score_count_kernel<64>, g, b, 0, st, h, B, table, rows, thresholds, mask_col0, cnt, (int)ublocks, (int)slices); break;
-    default: hipLaunchKernelGGL(score_count_kernel<128>, g, b, 0, st, h, B, table, rows, thresholds, mask_col0, cnt, (int)ublocks, (int)slices); break;
+  // the workspace form (a zeroed buffer of RK_COPIES copies) when many slices share each user: the
+  // counts go to slice % RK_COPIES and one more launch sums the copies
+  const bool copies = workspace && workspace_bytes >= gr_score_count_workspace_bytes(B) && slices > 4 * RK_COPIES;
+  unsigned long long* cnt = copies ? reinterpret_cast<unsigned long long*>(align_up(reinterpret_cast<uintptr_t>(workspace), 256))
+                                   : reinterpret_cast<unsigned long long*>(counts_out);
+  if (!copies && gr_fill32_launch(counts_out, 0u, B * 2, st) != GR_OK)
+    return fail(GR_ERR_HIP, "gr_score_count_gt_f32: memset failed");
+  if (rows == 0) {
+    if (copies) return gr_fill32_launch(counts_out, 0u, B * 2, st) == GR_OK ? GR_OK : fail(GR_ERR_HIP, "memset");
+    return GR_OK;
   }
-  return check_launch("gr_score_count_gt_f32");
+  const int nc = copies ? RK_COPIES : 1;
+  const dim3 g((unsigned)(ublocks * slices)), b(256);
+  switch (d) {
+    case 16: hipLaunchKernelGGL(score_count_kernel<16>, g, b, 0, st, h, B, table, rows, thresholds, mask_col0, cnt, (int)ublocks, (int)slices, nc); break;
+    case 32: hipLaunchKernelGGL(score_count_kernel<32>, g, b, 0, st, h, B, table, rows, thresholds, mask_col0, cnt, (int)ublocks, (int)slices, nc); break;
+    case 64: hipLaunchKernelGGL(score_count_kernel<64>, g, b, 0, st, h, B, table, rows, thresholds, mask_col0, cnt, (int)ublocks, (int)slices, nc); break;
+    default: hipLaunchKernelGGL(score_count_kernel<128>, g, b, 0, st, h, B, table, rows, thresholds, mask_col0, cnt, (int)ublocks, (int)slices, nc); break;
+  }
+  int rc = check_launch("gr_score_count_gt_f32");
+  if (rc || !copies) return rc;
+  hipLaunchKernelGGL(count_copies_kernel, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, st, cnt, B, RK_COPIES,
+                     counts_out);
+  return check_launch("gr_score_count_gt_f32 (copies)");
+}
+
+extern "C" size_t gr_score_count_workspace_bytes(int64_t B) {
+  return B <= 0 ? 0 : (size_t)gr::RK_COPIES * (size_t)B * 8 + 256;
+}
+
+extern "C" int gr_score_count_gt_f32(const float* h, int64_t B, int32_t d, const float* table,
+                                     int64_t rows, const float* thresholds, int32_t mask_col0,
+                                     int64_t* counts_out, void* stream) {
+  return count_launch(h, B, d, table, rows, thresholds, mask_col0, counts_out, nullptr, 0,
+                      reinterpret_cast<hipStream_t>(stream));
+}
+
+extern "C" int gr_score_count_gt_ws_f32(const float* h, int64_t B, int32_t d, const float* table,
+                                        int64_t rows, const float* thresholds, int32_t mask_col0,
+                                        int64_t* counts_out, void* workspace, size_t workspace_bytes,
+                                        void* stream) {
+  return count_launch(h, B, d, table, rows, thresholds, mask_col0, counts_out, workspace, workspace_bytes,
+                      reinterpret_cast<hipStream_t>(stream));
 }

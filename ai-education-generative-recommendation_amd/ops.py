@@ -148,6 +148,18 @@ def score_pairs(h, table, ids, mask_col0=True):
     return out
 
 
+_COUNT_WS = {}   # (device, stream) -> zeroed workspace of gr_score_count_gt_ws_f32 (left zero by every call)
+
+
+def _count_workspace(device, nbytes):
+    key = (device, torch.cuda.current_stream(device).cuda_stream)
+    ws = _COUNT_WS.get(key)
+    if ws is None or ws.numel() < nbytes:
+        ws = torch.zeros(nbytes, dtype=torch.uint8, device=device)
+        _COUNT_WS[key] = ws
+    return ws
+
+
 def score_count_gt(h, table, thresholds, mask_col0=True):
     """``#{j : (h . table^T)[b, j] > thresholds[b]}`` without materialising the logits."""
     L.require_gpu(h, table, thresholds)
@@ -156,9 +168,11 @@ def score_count_gt(h, table, thresholds, mask_col0=True):
     B, d = h.shape
     out = torch.empty(B, dtype=torch.int64, device=h.device)
     with torch.cuda.device(h.device):
-        L.check(L.lib().gr_score_count_gt_f32(L.ptr(h), B, d, L.ptr(t), t.shape[0], L.ptr(th),
-                                              1 if mask_col0 else 0, L.ptr(out),
-                                              L.stream_of(h.device)), "gr_score_count_gt_f32")
+        nb = L.lib().gr_score_count_workspace_bytes(B)
+        ws = _count_workspace(h.device, nb)
+        L.check(L.lib().gr_score_count_gt_ws_f32(L.ptr(h), B, d, L.ptr(t), t.shape[0], L.ptr(th),
+                                                 1 if mask_col0 else 0, L.ptr(out), L.ptr(ws), nb,
+                                                 L.stream_of(h.device)), "gr_score_count_gt_ws_f32")
     return out
 
 

@@ -1081,8 +1081,9 @@ def bench_ref_eval(a, dev, cpu):
 
 def _call_pattern(fn, units, reps=200):
     """Per-call cost of a small drop-in call at the reference's own batch size: host time to issue
-    one call (no sync), device time of one call (HIP events), and the pipelined wall time per call
-    (``reps`` calls back to back, one sync at the end)."""
+    one call (no sync), time of one isolated call (HIP events around it: includes the wait for the
+    host's launches), the pipelined wall time per call (``reps`` calls back to back, one sync at the
+    end), and the device time per call of 20 calls replayed as one captured graph."""
     spinup(fn, 0.3)
     torch.cuda.synchronize()
     host = []
@@ -1101,8 +1102,28 @@ def _call_pattern(fn, units, reps=200):
         e_.record()
     torch.cuda.synchronize()
     dev_us = float(np.median([s_.elapsed_time(e_) for s_, e_ in ev])) * 1e3
+    # the GPU's own time per call: 20 calls captured as one graph and replayed (no host issue time;
+    # device_us_per_call above times one isolated call, which waits for the host's launches)
+    graph_us = None
+    try:
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            for _ in range(20):
+                fn()
+        g.replay()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(10):
+            g.replay()
+        e1.record()
+        torch.cuda.synchronize()
+        graph_us = e0.elapsed_time(e1) / 200 * 1e3
+        del g
+    except Exception as ex:   # a call that cannot be captured: reported as such
+        graph_us = f"not capturable: {type(ex).__name__}"
     return {"value": units / wall, "us_per_call": wall * 1e6, "host_us_per_call": float(np.median(host)) * 1e6,
-            "device_us_per_call": dev_us}
+            "device_us_per_call": dev_us, "graph_us_per_call": graph_us}
 
 
 def bench_calls(rq_model, sas_model, sas_n, sas_items, dev, cpu=True):

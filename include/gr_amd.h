@@ -393,6 +393,16 @@ int gr_score_count_gt_f32(const float* h, int64_t B, int32_t d, const float* tab
                           const float* thresholds, int32_t mask_col0, int64_t* counts_out,
                           void* stream);
 
+/* The same counts with a caller workspace of gr_score_count_workspace_bytes(B) bytes that must be
+ * ZERO on entry and is left zero on return (one zeroed buffer serves every call on a stream).  Short
+ * batches split the catalog over every CU, so hundreds of workgroups add into each user's word;
+ * with the workspace the adds are spread over 16 copies and one more launch sums them (in copy
+ * order: exact) -- at B 128 x 100k rows 65 -> ~25 us.  Null / short workspace: the form above. */
+size_t gr_score_count_workspace_bytes(int64_t B);
+int gr_score_count_gt_ws_f32(const float* h, int64_t B, int32_t d, const float* table, int64_t rows,
+                             const float* thresholds, int32_t mask_col0, int64_t* counts_out,
+                             void* workspace, size_t workspace_bytes, void* stream);
+
 /* Fused top-k (+ strict counts) over the full catalog or a catalog shard without materialising
  * logits (SASRec/model.py:107 + evaluate.py:27-32; the per-shard candidate lists of SURVEY §8(e)).
  * Logits are l = h . table^T evaluated with exactly gr_score_f32's instruction sequence, column 0

@@ -68,4 +68,12 @@ if "pred128" in what:   # predict(seqs[128]) at C3 weights (SASRec/evaluate.py:1
     for _ in range(a.calls):
         sm.predict(seqs)
     torch.cuda.synchronize()
+if "rank128" in what:   # evaluate.rank_batch at batch 128 (SASRec/evaluate.py:26-32 without logits)
+    from gr_amd import evaluate as E
+    sm = synth.sasrec_model(100_000, synth.sasrec_params(64, 50, 2, 1, 64, dev), dev)
+    seqs = synth.sequences(128, 50, 100_000, 78, dev)
+    tg = torch.randint(1, 100_001, (128,), generator=torch.Generator(device=dev).manual_seed(9), device=dev)
+    for _ in range(a.calls):
+        E.rank_batch(sm, seqs, tg)
+    torch.cuda.synchronize()
 print("done", what, flush=True)

@@ -484,6 +484,32 @@ def test_fused_two_waves_equal_one_wave(d, heads, mlp, n, blocks, B, dev):
         assert torch.equal(a_, b_)
 
 
+@pytest.mark.parametrize("B,d,rows", [(128, 64, 100001), (5, 16, 707), (300, 32, 20000), (64, 128, 125000)])
+def test_score_count_workspace_form(B, d, rows, dev):
+    """gr_score_count_gt_ws_f32 (counts spread over 16 zeroed copies, then summed) equals the
+    direct-atomic form and a torch count over the materialised logits, and leaves its workspace zero."""
+    import ctypes
+    from gr_amd import _lib as L, ops
+    g = torch.Generator(device=dev).manual_seed(B + d)
+    h = torch.randn(B, d, generator=g, device=dev) * 0.3
+    t = torch.randn(rows, d, generator=g, device=dev)
+    th = ops.score_pairs(h, t, torch.randint(0, rows, (B,), generator=g, device=dev), mask_col0=True)
+    nb = L.lib().gr_score_count_workspace_bytes(B)
+    ws = torch.zeros(nb, dtype=torch.uint8, device=dev)
+    a = torch.empty(B, dtype=torch.int64, device=dev)
+    b = torch.empty(B, dtype=torch.int64, device=dev)
+    st = L.stream_of(dev)
+    for _ in range(2):   # the second call relies on the first leaving the workspace zero
+        L.check(L.lib().gr_score_count_gt_ws_f32(L.ptr(h), B, d, L.ptr(t), rows, L.ptr(th), 1, L.ptr(a), L.ptr(ws),
+                                                 ctypes.c_size_t(nb), st), "ws")
+    L.check(L.lib().gr_score_count_gt_f32(L.ptr(h), B, d, L.ptr(t), rows, L.ptr(th), 1, L.ptr(b), st), "direct")
+    lg = ops.score(h, t)
+    lg[:, 0] = -1e9
+    ref = (lg > th[:, None]).sum(1)
+    assert torch.equal(a, b) and torch.equal(a, ref)
+    assert int(ws.sum().item()) == 0
+
+
 @pytest.mark.parametrize("B,cols,ld", [(7, 100001, 100001), (33, 250000, 250003), (300, 5, 5), (2, 1, 1)])
 def test_segmented_topk_count_vs_torch(B, cols, ld, dev):
     """Segmented top-k / count kernels on long, misaligned (odd stride) rows, single fused pass."""
