@@ -76,4 +76,18 @@ if "rank128" in what:   # evaluate.rank_batch at batch 128 (SASRec/evaluate.py:2
     for _ in range(a.calls):
         E.rank_batch(sm, seqs, tg)
     torch.cuda.synchronize()
+if "c3" in what:   # C3 predict: B 2048, d 64, n 50, 100k items (fused forward + contiguous scoring)
+    sm = synth.sasrec_model(100_000, synth.sasrec_params(64, 50, 2, 1, 64, dev), dev)
+    seqs = synth.sequences(2048, 50, 100_000, 78, dev)
+    for _ in range(a.calls):
+        sm.predict(seqs)
+    torch.cuda.synchronize()
+if "refeval" in what:   # SASRec/evaluate.py at main.py's configuration: d 16, n 20, 706 items, batch 128
+    from gr_amd import evaluate as E
+    sm = synth.sasrec_model(706, synth.sasrec_params(16, 20, 2, 1, 64, dev), dev, seed=16)
+    seqs = synth.sequences(128, 20, 706, 9000, dev)
+    tg = torch.randint(1, 707, (128,), generator=torch.Generator(device=dev).manual_seed(9), device=dev)
+    for _ in range(a.calls):
+        E.rank_batch(sm, seqs, tg)
+    torch.cuda.synchronize()
 print("done", what, flush=True)
