@@ -307,14 +307,22 @@ class RqBinding:
         key = tuple(w._version for w in self.ws) + (_WEIGHT_EPOCH[0],)
         if key != self._pack_key:
             if self._pack_key is not None:
-                # a re-pack writes a fresh image on this stream: an encode still queued on another
-                # stream keeps reading the previous one, which stays allocated until the next re-pack
-                self._prev_packed = self.packed
-                self.packed = torch.empty_like(self._prev_packed)
+                # a re-pack writes a fresh image on this stream; the previous one goes back to the
+                # caching allocator, which does not hand it out again before the work of every
+                # stream recorded on it (below) has finished
+                self.packed = torch.empty_like(self.packed)
+                self._streams = set()
             with torch.cuda.device(self.device):
                 L.check(L.lib().gr_rq_encoder_pack_f32(len(self.ws), self.dims_c, self.w_arr, L.ptr(self.packed),
                                                        L.stream_of(self.device)), "gr_rq_encoder_pack_f32")
             self._pack_key = key
+        st = torch.cuda.current_stream(self.device)
+        streams = getattr(self, "_streams", None)
+        if streams is None:
+            streams = self._streams = set()
+        if st.cuda_stream not in streams:   # an encode on another stream than the allocating one
+            self.packed.record_stream(st)
+            streams.add(st.cuda_stream)
         return L.ptr(self.packed)
 
     def workspace_bytes(self, n):
