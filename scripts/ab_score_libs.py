@@ -1,6 +1,7 @@
 """Device time of SASRec predict's scoring (gr_score_f32 into the contiguous [B, N+1] logits, C3:
 d 64, 100,001 rows) for several builds of the library (scripts/build_variant.sh tags; "base" = the
-default build), interleaved in one process: B 2048 (rotated whole lines), 512 and 128 (direct)."""
+default build), interleaved in one process: B 2048 (rotated whole lines), 512 and 128 (direct); every tag's
+logits are compared bitwise with the first tag's."""
 import os
 import sys
 
@@ -30,6 +31,7 @@ base = os.path.dirname(_lib.LIB_PATH)
 default = _lib.LIB_PATH
 tags = sys.argv[1:] or ["base"]
 res = {t: {} for t in tags}
+same = {t: True for t in tags}
 for rnd in range(3):
     for B in (2048, 512, 128):
         h = torch.randn(B, 64, generator=g, device=dev)
@@ -37,6 +39,12 @@ for rnd in range(3):
         for t in tags:
             _lib._lib = None
             _lib.LIB_PATH = default if t == "base" else os.path.join(base, f"libgr_amd_{t}.so")
+            out.fill_(float("nan"))
             res[t].setdefault(B, []).append(dev_us(lambda: ops.score(h, table, out=out)))
+            if t == tags[0]:
+                ref = out.clone()
+            else:
+                same[t] &= bool(torch.equal(out, ref))
 for t in tags:
-    print(t, "  ".join(f"B {B}: {min(v):7.1f} us" for B, v in res[t].items()), flush=True)
+    print(t, "  ".join(f"B {B}: {min(v):7.1f} us" for B, v in res[t].items()),
+          f"| logits bitwise equal to {tags[0]}: {same[t]}", flush=True)

@@ -109,17 +109,19 @@ def test_predict_contiguous_by_default(dev):
     assert c.view(-1).numel() == a.numel()
 
 
-@pytest.mark.parametrize("B,rows,pad,off", [(2048, 100001, 0, 0), (700, 60001, 0, 0), (300, 100001, 0, 0),
-                                            (1000, 50001, 5, 3), (1500, 40000, 7, 1), (129, 100001, 0, 0)])
-def test_score_unaligned_rows_bitwise(dev, B, rows, pad, off):
+@pytest.mark.parametrize("B,rows,pad,off,d", [(2048, 100001, 0, 0, 64), (700, 60001, 0, 0, 64), (300, 100001, 0, 0, 64),
+                                              (1000, 50001, 5, 3, 64), (1500, 40000, 7, 1, 64), (129, 100001, 0, 0, 64),
+                                              (2048, 100001, 0, 0, 16), (1000, 50001, 5, 3, 16), (1500, 40000, 7, 1, 32),
+                                              (700, 60001, 0, 0, 32)])
+def test_score_unaligned_rows_bitwise(dev, B, rows, pad, off, d):
     """Logits rows off the 128-byte grid: the rotated whole-line kernel (> 160 MB of logits) and the
     direct kernel (smaller) against the aligned layout, bit for bit, including a row stride that is
     not rows (pad), a base that is not line-aligned (off), partial user blocks and a partial last
     chunk; every element written exactly once (NaN-filled canvas, guard columns untouched)."""
     from gr_amd import ops
     g = torch.Generator(device=dev).manual_seed(B + rows)
-    h = torch.randn(B, 64, device=dev, generator=g)
-    table = torch.randn(rows, 64, device=dev, generator=g)
+    h = torch.randn(B, d, device=dev, generator=g)
+    table = torch.randn(rows, d, device=dev, generator=g)
     ref = ops.logits_buffer(B, rows, dev)
     ops.score(h, table, out=ref)
     canvas = torch.full((B, rows + pad + off), float("nan"), device=dev)
