@@ -451,11 +451,52 @@ def rq_mlp(x, weights, biases, bn=None, act="relu", group_sizes=None):
             sizes = [int(g) for g in group_sizes]
             if sum(sizes) != n or any(g < 1 for g in sizes):
                 raise RuntimeError("rq_mlp: group sizes must be positive and sum to the batch")
-            ptr = _group_ptr(sizes, dev)
-            L.check(lib.gr_mlp_exact_groups_f32(L.ptr(x2), n, len(ws), dims_c, L.ptr_array(ws),
-                                                L.ptr_array(bs) if bs is not None else None, *bn_arrs, float(eps),
-                                                _EXACT_ACTS[act], L.ptr(ptr), len(sizes), L.ptr(z),
-                                                L.stream_of(dev)), "gr_mlp_exact_groups_f32")
+            # Groups MKL runs as k-block chains (>= 16 rows) whose per-layer blocks match those of ONE
+            # call over all of them produce the same bits in that call: they go through the MFMA
+            # kernels together; the rest (1-15-row orders) through the per-row kernel, group by group.
+            plans = {}
+
+            def plan(m):
+                if m not in plans:
+                    plans[m] = tuple(mkl_plan(m, dims[i], dims[i + 1])[:2] for i in range(len(ws)))
+                return plans[m]
+
+            big = [i for i, g in enumerate(sizes) if all(k == "chain" for k, _ in plan(g))]
+            if big:
+                pb = plan(sum(sizes[i] for i in big))
+                big = [i for i in big if plan(sizes[i]) == pb]
+            small = [i for i in range(len(sizes)) if i not in set(big)]
+            offs = [0]
+            for g in sizes:
+                offs.append(offs[-1] + g)
+
+            def rows_of(sel):
+                return torch.cat([torch.arange(offs[i], offs[i + 1], device=dev) for i in sel])
+
+            if small:
+                rs = rows_of(small) if big else None
+                xs = x2 if rs is None else x2.index_select(0, rs).contiguous()
+                zs = z if rs is None else torch.empty((xs.shape[0], dims[-1]), dtype=torch.float32, device=dev)
+                ptr = _group_ptr([sizes[i] for i in small], dev)
+                L.check(lib.gr_mlp_exact_groups_f32(L.ptr(xs), xs.shape[0], len(ws), dims_c, L.ptr_array(ws),
+                                                    L.ptr_array(bs) if bs is not None else None, *bn_arrs,
+                                                    float(eps), _EXACT_ACTS[act], L.ptr(ptr), len(small),
+                                                    L.ptr(zs), L.stream_of(dev)), "gr_mlp_exact_groups_f32")
+                if rs is not None:
+                    z.index_copy_(0, rs, zs)
+            if big:
+                rb = rows_of(big) if small else None
+                xb = x2 if rb is None else x2.index_select(0, rb).contiguous()
+                nb2 = xb.shape[0]
+                zb = z if rb is None else torch.empty((nb2, dims[-1]), dtype=torch.float32, device=dev)
+                nbytes2 = lib.gr_rq_mlp_workspace_bytes(nb2, len(ws), dims_c)
+                wsp2 = L.workspace(nbytes2, dev)
+                L.check(lib.gr_mlp_exact_f32(L.ptr(xb), nb2, len(ws), dims_c, L.ptr_array(ws),
+                                             L.ptr_array(bs) if bs is not None else None, *bn_arrs, float(eps),
+                                             _EXACT_ACTS[act], L.ptr(zb), L.ptr(wsp2), nbytes2, L.stream_of(dev)),
+                        "gr_mlp_exact_f32")
+                if rb is not None:
+                    z.index_copy_(0, rb, zb)
             return z
         L.check(lib.gr_mlp_exact_f32(L.ptr(x2), n, len(ws), dims_c, L.ptr_array(ws),
                                      L.ptr_array(bs) if bs is not None else None, *bn_arrs, float(eps),

@@ -106,12 +106,16 @@ def test_small_calls_on_knife_edge_codebooks(dev, fused, parity_log):
 
 def test_collision_groups_use_each_groups_call_order(dev, parity_log):
     """get_indices_groups: every group is one reference call (its own MKL order), as the per-group
-    loop of RQ-VAE/infer.py:116-127; the encoder half against rq_exact per group."""
+    loop of RQ-VAE/infer.py:116-127; the encoder half against rq_exact per group (the chain-order
+    groups batched into one MFMA-kernel call, the small-call groups on the per-row kernel)."""
     x, sd, _, meta = gl.rq_inputs("rq_syn_3x256")
     ws, bs, cbs = _lists(sd, 3)
     m = build_model(meta, sd, dev)
     rng = np.random.default_rng(3)
-    sizes = [int(v) for v in rng.integers(1, 20, 40)]
+    # 1-19-row groups (their own small-call orders, the per-row kernel) mixed with groups of >= 16 rows
+    # that share one k-block-chain order (one MFMA-kernel call over all of them)
+    sizes = [int(v) for v in rng.integers(1, 20, 40)] + [16, 64, 33, 100]
+    sizes = [sizes[i] for i in rng.permutation(len(sizes))]
     rows = rng.permutation(len(x))[:sum(sizes)]
     z = m.encoder(torch.from_numpy(x[rows]).to(dev), group_sizes=sizes).cpu().numpy()
     ref, off = [], 0
