@@ -257,7 +257,7 @@ static int count_launch(const float* h, int64_t B, int32_t d, const float* table
   const int64_t ublocks = (B + 128 * RK_UT - 1) / (128 * RK_UT);
   const int64_t chunks = (rows + RK_CHUNK - 1) / RK_CHUNK;
   const int64_t per_cu = 2;   // resident workgroups per CU (registers, LDS)
-  int64_t slices = (per_cu * cu_count() + ublocks - 1) / ublocks;
+  int64_t slices = per_cu * cu_count() / ublocks;   // rounded down: every workgroup resident at once
   if (slices > chunks) slices = chunks;
   if (slices < 1) slices = 1;
   if (ublocks * slices > 0x7fffffffLL) return fail(GR_ERR_UNSUPPORTED, "gr_score_count_gt_f32: grid too large");

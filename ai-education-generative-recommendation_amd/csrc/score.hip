@@ -552,7 +552,8 @@ int gr_score_launch(const float* h, int64_t B, int32_t d, const float* table, in
   const int64_t chunks = (rows + SC_CHUNK - 1) / SC_CHUNK;
   // direct / rotated kernels: two workgroups per CU; the ring kernel: one
   auto slices_for = [&](int per_cu) {
-    int64_t sl = (per_cu * cus + ublocks - 1) / ublocks;   // all workgroups resident at once
+    // all workgroups resident at once: rounded down (rounding up put the last few in a second round)
+    int64_t sl = per_cu * cus / ublocks;
     if (sl > chunks) sl = chunks;
     return sl < 1 ? (int64_t)1 : sl;
   };

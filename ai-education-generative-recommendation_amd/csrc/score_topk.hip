@@ -357,7 +357,10 @@ static TileWs tile_ws(int64_t B, int64_t rows, int d) {
   TileWs w;
   w.ublocks = (B + 127) / 128;
   w.chunks = (rows + TK_CHUNK - 1) / TK_CHUNK;
-  int64_t sl = (2 * cu_count() + w.ublocks - 1) / w.ublocks;
+  // floor: ublocks x slices stays within the two resident workgroups per CU (rounding up put the
+  // last few workgroups in a second round: 3,000 users = 24 user blocks x 22 slices = 528 > 512,
+  // 1161 vs 831 us on a 125k-row shard, profiles/r05/ab_topk_split.txt)
+  int64_t sl = 2 * cu_count() / w.ublocks;
   if (sl > w.chunks) sl = w.chunks;
   w.slices = sl < 1 ? 1 : sl;
   // tile maxima per user: 32-row tiles, or 16-row half tiles -- half the rows the select kernel

@@ -53,7 +53,10 @@ def _check(h, t, k, id_offset=0, mask_col0=True, seed=0):
                                         (513, 128, 20011, 10), (33, 32, 1, 3), (512, 128, 300007, 10),
                                         (100, 32, 150001, 4), (40, 64, 262145, 16),
                                         (200, 16, 707, 10), (65, 16, 100001, 16),   # d 16: SASRec/main.py:12
-                                        (512, 128, 1000001, 10)])   # C5 full size: 512 users x 1M-item catalog
+                                        (512, 128, 1000001, 10),   # C5 full size: 512 users x 1M-item catalog
+                                        # larger batches: user blocks that do not divide the resident
+                                        # workgroups (2,100 users: 17 blocks), a c5_rank-like shard
+                                        (2100, 128, 125000, 10), (4096, 64, 20011, 16)])
 def test_score_topk_random(B, d, rows, k, dev):
     g = torch.Generator().manual_seed(B * 7 + d + rows)
     h = torch.randn(B, d, generator=g).to(dev)
