@@ -84,6 +84,9 @@ SIGNATURES = {
                                              _vp, _sz, _vp, _vp]),
     "gr_sasrec_predict_ld_f32": (ctypes.c_int, [ctypes.POINTER(SasrecParams), _vp, _i64, _i32, _vp,
                                                 _i64, _vp, _sz, _vp, _vp]),
+    "gr_sasrec_rank_workspace_bytes": (_sz, [ctypes.POINTER(SasrecParams), _i64, _i32]),
+    "gr_sasrec_rank_f32": (ctypes.c_int, [ctypes.POINTER(SasrecParams), _vp, _i64, _i32, _vp, _i32, _vp, _vp,
+                                          _sz, _vp, _sz, _vp, _vp]),
     "gr_sasrec_train_vec_width": (_i32, [ctypes.POINTER(SasrecParams), _i32]),
     "gr_sasrec_train_fwd_f32": (ctypes.c_int, [ctypes.POINTER(SasrecParams), _vp, _i64, _i32, _f32,
                                                ctypes.c_uint64, _vp, ctypes.POINTER(SasrecTrainBufs), _vp,
@@ -147,11 +150,41 @@ def require_gpu(*tensors):
 
 
 def ptr(t):
-    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+    """Device address of ``t`` as a plain int (the argtypes convert it; None: NULL)."""
+    return t.data_ptr() if t is not None else None
+
+
+_raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)
 
 
 def stream_of(device):
-    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+    """Handle of ``device``'s current stream (int) -- the stream every call enqueues on."""
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    if _raw_stream is not None:
+        return _raw_stream(idx)
+    return torch.cuda.current_stream(idx).cuda_stream
+
+
+class _NoGuard:
+    __slots__ = ()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        return False
+
+
+_NO_GUARD = _NoGuard()
+
+
+def on(device):
+    """Device guard for a launch on ``device``: a no-op when it is already the current device (the
+    common case; torch.cuda.device's set / restore costs microseconds per call at the reference's
+    batch sizes), torch.cuda.device otherwise."""
+    if device.index is None or device.index == torch.cuda.current_device():
+        return _NO_GUARD
+    return torch.cuda.device(device)
 
 
 def ptr_array(tensors):

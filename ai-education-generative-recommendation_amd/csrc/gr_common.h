@@ -270,6 +270,15 @@ int gr_rq_rows_launch(const float* x, int64_t n, int64_t call_m, const int64_t* 
                       hipStream_t st);
 // p[0 .. count) = value (32-bit words); a kernel, so it replays inside captured graphs (fill.hip).
 int gr_fill32_launch(void* p, uint32_t value, int64_t count, hipStream_t st);
+// rank_fused.hip: the target logits (gr_score_pairs_f32's kernel) and ranks_out[u] = 1 +
+// #{j : l'[u, j] > thresholds[u]} (gr_score_count_gt_ws_f32's kernels; count_ws zero on entry,
+// left zero, or null)
+int gr_score_pairs_launch(const float* h, int64_t B, int32_t d, const float* table, int64_t rows, const int64_t* ids,
+                          int32_t mask_col0, float* out, int32_t* err_flag, hipStream_t st);
+int gr_score_rank_launch(const float* h, int64_t B, int32_t d, const float* table, int64_t rows, const float* thresholds,
+                         int32_t mask_col0, int64_t* ranks_out, void* count_ws, size_t count_ws_bytes, hipStream_t st);
+// p[0 .. count) = value (64-bit words)
+int gr_fill64_launch(void* p, uint64_t value, int64_t count, hipStream_t st);
 int gr_linear_exact_launch(const float* x, int64_t m, int32_t k, const float* w, int32_t n,
                            const float* bias, const float* bn_mean, const float* bn_var, const float* bn_w,
                            const float* bn_b, float bn_eps, int32_t act, float* y, hipStream_t stream);

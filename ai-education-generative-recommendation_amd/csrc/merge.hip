@@ -3,9 +3,9 @@
 // being padding) — the torch form (dist.merge_topk: two stable argsorts plus the unpacking of the
 // gathered int64 words) took 140 us for 4096 users x 8 ranks x 10 candidates.
 //
-// One wave per user row: lane l holds candidates l, l + 64, ...; k rounds of a 64-bit wave max over
-// the order-preserving key of (value, id) (topk_list.h sel_key: larger = better, padding below every
-// real entry), the winning lane emits and drops its entry.  Exact: no arithmetic on the values.
+// One wave per user row: lane l holds candidates l, l + 64, ...; k rounds of a wave max over the
+// order-preserving value key, then a wave min over the 64-bit ids holding it (padding below every
+// real entry); the winning lane emits and drops its entry.  Exact: no arithmetic on the values.
 #include "gr_common.h"
 #include "topk_list.h"
 
@@ -13,11 +13,22 @@ namespace gr {
 
 constexpr int MG_PER_LANE = 4;   // candidates per lane held in registers (C <= 256)
 
-// src(b, c, &v, &id): candidate c of row b.  Padding (id < 0) becomes (-inf, INT64_MAX).
+// Order-preserving 32-bit key of a value (larger key = larger value, -0 == +0); 0 is reserved for
+// "taken" and lies below every value's key, -inf's included.
+__device__ __forceinline__ uint32_t val_key(float v) {
+  uint32_t u = __float_as_uint(v == 0.f ? 0.f : v);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+
+// src(b, c, &v, &id): candidate c of row b.  Padding (id < 0, or a NaN value) becomes
+// (-inf, INT64_MAX): below every real entry, -inf ones included.  A round selects the best entry
+// by value key (wave max), then by the FULL 64-bit id among the entries holding that value (wave
+// min), so equal values order by id over the whole int64 range (the 64-bit
+// sel_key of topk_list.h keeps only the id's low 32 bits).
 template <typename Src>
 __device__ __forceinline__ void merge_row(Src src, int64_t b, int C, int k, float* vals, int64_t* ids) {
   const int lane = threadIdx.x & 63;
-  uint64_t key[MG_PER_LANE];
+  uint32_t key[MG_PER_LANE];
   float v[MG_PER_LANE];
   int64_t id[MG_PER_LANE];
 #pragma unroll
@@ -34,24 +45,32 @@ __device__ __forceinline__ void merge_row(Src src, int64_t b, int C, int k, floa
         id[u] = ci;
       }
     }
-    key[u] = sel_key(v[u], id[u]);
+    key[u] = val_key(v[u]);
   }
   for (int q = 0; q < k; ++q) {
     int bu = 0;
-    uint64_t best = key[0];
+    uint32_t bk = key[0];
+    int64_t bi = id[0];
 #pragma unroll
     for (int u = 1; u < MG_PER_LANE; ++u)
-      if (key[u] > best) {
-        best = key[u];
+      if (key[u] > bk || (key[u] == bk && id[u] < bi)) {
+        bk = key[u];
+        bi = id[u];
         bu = u;
       }
-    uint64_t m = best;
+    uint32_t m = bk;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
-      const uint64_t om = __shfl_xor(m, o);
+      const uint32_t om = __shfl_xor(m, o);
       m = om > m ? om : m;
     }
-    const uint64_t bal = __ballot(best == m);
+    int64_t mi = bk == m ? bi : INT64_MAX;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const int64_t om = __shfl_xor(mi, o);
+      mi = om < mi ? om : mi;
+    }
+    const uint64_t bal = __ballot(bk == m && bi == mi);
     if (lane == __ffsll((unsigned long long)bal) - 1) {
       float ov = -__builtin_inff();   // m == 0: every candidate taken (k > C), padding
       int64_t oi = -1;
@@ -61,6 +80,7 @@ __device__ __forceinline__ void merge_row(Src src, int64_t b, int C, int k, floa
           ov = v[u];
           oi = id[u] == INT64_MAX ? -1 : id[u];
           key[u] = 0;   // below every entry, padding included: never selected again
+          id[u] = INT64_MAX;
         }
       vals[b * k + q] = ov;
       ids[b * k + q] = oi;

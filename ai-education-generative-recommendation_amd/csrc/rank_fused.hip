@@ -195,10 +195,10 @@ __global__ __launch_bounds__(256, 2) void score_count_kernel(const float* __rest
 // counts[u] = sum of the copies' words in copy order (exact integer sums), which are cleared for the
 // next call
 __global__ __launch_bounds__(256) void count_copies_kernel(unsigned long long* __restrict__ ws, int64_t B, int copies,
-                                                           int64_t* __restrict__ counts) {
+                                                           int64_t* __restrict__ counts, int64_t base) {
   const int64_t u = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (u >= B) return;
-  unsigned long long s = 0;
+  unsigned long long s = (unsigned long long)base;
   for (int c = 0; c < copies; ++c) {
     s += ws[(int64_t)c * B + u];
     ws[(int64_t)c * B + u] = 0;
@@ -226,6 +226,12 @@ extern "C" int gr_score_pairs_f32(const float* h, int64_t B, int32_t d, const fl
                                   int32_t* err_flag, void* stream) {
   using namespace gr;
   clear_error();
+  return gr_score_pairs_launch(h, B, d, table, rows, ids, mask_col0, out, err_flag, reinterpret_cast<hipStream_t>(stream));
+}
+
+int gr_score_pairs_launch(const float* h, int64_t B, int32_t d, const float* table, int64_t rows, const int64_t* ids,
+                          int32_t mask_col0, float* out, int32_t* err_flag, hipStream_t st) {
+  using namespace gr;
   if (B < 0 || rows < 1) return fail(GR_ERR_ARG, "gr_score_pairs_f32: bad shape");
   if (B == 0) return GR_OK;
   if (!h || !table || !ids || !out) return fail(GR_ERR_ARG, "gr_score_pairs_f32: null pointer");
@@ -233,7 +239,6 @@ extern "C" int gr_score_pairs_f32(const float* h, int64_t B, int32_t d, const fl
     return fail(GR_ERR_UNSUPPORTED, "gr_score_pairs_f32: d must be 16, 32, 64 or 128");
   if (!aligned16(h) || !aligned16(table)) return fail(GR_ERR_ARG, "gr_score_pairs_f32: h / table not 16-byte aligned");
   const unsigned grid = (unsigned)((B + 31) / 32);
-  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   switch (d) {
     case 16: hipLaunchKernelGGL(score_pairs_kernel<16>, dim3(grid), dim3(64), 0, st, h, B, table, rows, ids, mask_col0, out, err_flag); break;
     case 32: hipLaunchKernelGGL(score_pairs_kernel<32>, dim3(grid), dim3(64), 0, st, h, B, table, rows, ids, mask_col0, out, err_flag); break;
@@ -243,9 +248,10 @@ extern "C" int gr_score_pairs_f32(const float* h, int64_t B, int32_t d, const fl
   return check_launch("gr_score_pairs_f32");
 }
 
+// counts_out[u] = base + #{j : l'[u, j] > thresholds[u]} (base 1: the 1-based rank of evaluate.py:32)
 static int count_launch(const float* h, int64_t B, int32_t d, const float* table, int64_t rows,
                         const float* thresholds, int32_t mask_col0, int64_t* counts_out, void* workspace,
-                        size_t workspace_bytes, hipStream_t st) {
+                        size_t workspace_bytes, hipStream_t st, int64_t base = 0) {
   using namespace gr;
   clear_error();
   if (B < 0 || rows < 0) return fail(GR_ERR_ARG, "gr_score_count_gt_f32: bad shape");
@@ -266,10 +272,10 @@ static int count_launch(const float* h, int64_t B, int32_t d, const float* table
   const bool copies = workspace && workspace_bytes >= gr_score_count_workspace_bytes(B) && slices > 4 * RK_COPIES;
   unsigned long long* cnt = copies ? reinterpret_cast<unsigned long long*>(align_up(reinterpret_cast<uintptr_t>(workspace), 256))
                                    : reinterpret_cast<unsigned long long*>(counts_out);
-  if (!copies && gr_fill32_launch(counts_out, 0u, B * 2, st) != GR_OK)
+  if (!copies && gr_fill64_launch(counts_out, (uint64_t)base, B, st) != GR_OK)
     return fail(GR_ERR_HIP, "gr_score_count_gt_f32: memset failed");
   if (rows == 0) {
-    if (copies) return gr_fill32_launch(counts_out, 0u, B * 2, st) == GR_OK ? GR_OK : fail(GR_ERR_HIP, "memset");
+    if (copies) return gr_fill64_launch(counts_out, (uint64_t)base, B, st) == GR_OK ? GR_OK : fail(GR_ERR_HIP, "memset");
     return GR_OK;
   }
   const int nc = copies ? RK_COPIES : 1;
@@ -283,7 +289,7 @@ static int count_launch(const float* h, int64_t B, int32_t d, const float* table
   int rc = check_launch("gr_score_count_gt_f32");
   if (rc || !copies) return rc;
   hipLaunchKernelGGL(count_copies_kernel, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, st, cnt, B, RK_COPIES,
-                     counts_out);
+                     counts_out, base);
   return check_launch("gr_score_count_gt_f32 (copies)");
 }
 
@@ -304,4 +310,9 @@ extern "C" int gr_score_count_gt_ws_f32(const float* h, int64_t B, int32_t d, co
                                         void* stream) {
   return count_launch(h, B, d, table, rows, thresholds, mask_col0, counts_out, workspace, workspace_bytes,
                       reinterpret_cast<hipStream_t>(stream));
+}
+
+int gr_score_rank_launch(const float* h, int64_t B, int32_t d, const float* table, int64_t rows, const float* thresholds,
+                         int32_t mask_col0, int64_t* ranks_out, void* count_ws, size_t count_ws_bytes, hipStream_t st) {
+  return count_launch(h, B, d, table, rows, thresholds, mask_col0, ranks_out, count_ws, count_ws_bytes, st, 1);
 }

@@ -563,3 +563,51 @@ extern "C" int gr_rank_f32(const float* logits, int64_t B, int64_t cols, int64_t
                      logits, cols, ld, targets, mask_col0, ranks_out);
   return check_launch("gr_rank_f32");
 }
+
+// evaluate.py:26-32 for one batch in ONE call: the last hidden states of the
+// forward, the target logits with the scoring chain (gr_score_pairs_f32's kernel) and the strict
+// count + 1 (gr_score_count_gt_ws_f32's kernels) -- the [B, item_rows] logits are never written.
+extern "C" size_t gr_sasrec_rank_workspace_bytes(const gr_sasrec_params* p, int64_t B, int32_t n) {
+  if (!p || B < 0 || n < 1) return 0;
+  return gr::ws_layout(p, B, n, nullptr, nullptr) + gr::align_up((size_t)B * 4, 256) + 256;
+}
+
+extern "C" int gr_sasrec_rank_f32(const gr_sasrec_params* p, const int64_t* seqs, int64_t B, int32_t n,
+                                  const int64_t* targets, int32_t mask_col0, int64_t* ranks_out,
+                                  void* workspace, size_t workspace_bytes, void* count_ws,
+                                  size_t count_ws_bytes, int32_t* err_flag, void* stream) {
+  using namespace gr;
+  clear_error();
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (!p) return fail(GR_ERR_ARG, "gr_sasrec_rank_f32: null params");
+  const size_t need = gr_sasrec_rank_workspace_bytes(p, B, n);
+  if (!workspace || workspace_bytes < need)
+    return fail(GR_ERR_WORKSPACE, "gr_sasrec_rank_f32: workspace too small (need " + std::to_string(need) + " bytes)");
+  SasWs w;
+  int rc = sas_prepare(p, B, n, workspace, workspace_bytes, &w);
+  if (rc) return rc;
+  if (B == 0) return GR_OK;
+  if (!seqs || !targets || !ranks_out) return fail(GR_ERR_ARG, "gr_sasrec_rank_f32: null seqs / targets / ranks");
+  if (p->d != 16 && p->d != 32 && p->d != 64 && p->d != 128)
+    return fail(GR_ERR_UNSUPPORTED, "gr_sasrec_rank_f32: d must be 16, 32, 64 or 128 (the fused rank's widths)");
+  float* pairs = reinterpret_cast<float*>(
+      align_up(reinterpret_cast<uintptr_t>(workspace) + ws_layout(p, B, n, nullptr, nullptr), 256));
+  float* h;
+  if (fused_ok(p, n)) {
+    h = w.h;
+    rc = gr_sasrec_fused_launch(p, seqs, B, n, h, 1, err_flag, st);
+    if (rc == GR_ERR_UNSUPPORTED)
+      return fail(GR_ERR_UNSUPPORTED, "sasrec: fused path refused a shape fused_ok accepted");
+  } else {
+    SasOut fin;
+    h = w.o;   // [B, d] final hidden states (the attention-output buffer is free by then)
+    rc = run_forward(p, seqs, B, n, w, err_flag, 1, &fin, h, st);
+    if (!rc && !fin.done)
+      rc = run_layernorm(fin.x, B, p->d, fin.stride, fin.off, p->last_ln_w, p->last_ln_b, p->eps, h, st);
+  }
+  if (rc) return rc;
+  rc = gr_score_pairs_launch(h, B, p->d, p->item_emb, p->item_rows, targets, mask_col0, pairs, err_flag, st);
+  if (rc) return rc;
+  return gr_score_rank_launch(h, B, p->d, p->item_emb, p->item_rows, pairs, mask_col0, ranks_out, count_ws,
+                              count_ws_bytes, st);
+}

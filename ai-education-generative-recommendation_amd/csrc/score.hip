@@ -449,10 +449,14 @@ __global__ __launch_bounds__(256, 2) void score_rot_kernel(const float* __restri
   __syncthreads();
   const int64_t col_lo = c_begin * SC_CHUNK, col_hi = c_end * SC_CHUNK < rows ? c_end * SC_CHUNK : rows;
   const int rows_left = (int)(B - u0 < 64 ? B - u0 : 64);
-  // rotated chunks k - 2 (r2) and k - 1 (r1); line A_{k-1} = lanes p < o from r2, p >= o from r1
-  f32x16 r1[2], r2[2];
+  // rotated chunks k - 2 (r2) and k - 1 (r1); line A_{k-1} = lanes p < o from r2, p >= o from r1.
+  // The two register sets alternate roles (the loop is unrolled by two): chunk k's rotation is
+  // written over r2, which line A_{k-1}'s stores have finished reading -- no copies between
+  // iterations (a copy r2 = r1 cost 32 v_mov per chunk beside the 64 MFMAs).
+  f32x16 ra[2], rb[2];
   // one register t (user tile t >> 4, register t & 15) of line A_L
-  auto store_reg = [&](int64_t L, int t, bool interior) {
+  auto store_reg = [&](const f32x16(&r1)[2], const f32x16(&r2)[2], int64_t L, int t, bool interior)
+      __attribute__((always_inline)) {
     const int ut = t >> 4, v = t & 15;
     const bool lo = rot_addr[v] > (32 * hh + r) * 4;   // p < o
     const float val = lo ? r2[ut][v] : r1[ut][v];
@@ -473,11 +477,11 @@ __global__ __launch_bounds__(256, 2) void score_rot_kernel(const float* __restri
   constexpr int STEPS = KG * QN * 4;                      // (g, q, s) steps of a chunk, 2 MFMAs each
   constexpr int PER = 32 / STEPS > 0 ? 32 / STEPS : 1;    // stores per step
   constexpr int EVERY = STEPS / 32 > 0 ? STEPS / 32 : 1;  // steps per store
-#pragma unroll 1
-  for (int64_t k = c_begin; k < c_end; ++k) {
+  // chunk k with r1 = rotation of chunk k-1, r2 = of chunk k-2 (overwritten with chunk k's);
+  // inter: line A_{k-1} is an interior line, its stores ride between this chunk's MFMAs
+  auto body = [&](int64_t k, f32x16(&r1)[2], f32x16(&r2)[2], auto inter_sel) __attribute__((always_inline)) {
+    const bool inter = inter_sel;   // std::true_type / false_type: a compile-time constant
     const int kb = (int)((k - c_begin) & 1);
-    // line A_{k-1}'s stores ride between this chunk's MFMAs when it is an interior line
-    const bool inter = k > c_begin && line_interior(k - 1);
     f32x16 acc[2];
 #pragma unroll
     for (int ut = 0; ut < 2; ++ut)
@@ -496,34 +500,64 @@ __global__ __launch_bounds__(256, 2) void score_rot_kernel(const float* __restri
           for (int ut = 0; ut < 2; ++ut) acc[ut] = mfma32(hf[ut][g][q][s4], bt[s4], acc[ut]);
           if (inter && step % EVERY == 0) {
 #pragma unroll
-            for (int e = 0; e < PER; ++e) store_reg(k - 1, (step / EVERY) * PER + e, true);
+            for (int e = 0; e < PER; ++e) store_reg(r1, r2, k - 1, (step / EVERY) * PER + e, true);
           }
         }
       }
-    if (k > c_begin && !inter) {
+    if (!inter && k > c_begin) {
 #pragma unroll
-      for (int t = 0; t < 32; ++t) store_reg(k - 1, t, false);
+      for (int t = 0; t < 32; ++t) store_reg(r1, r2, k - 1, t, false);
     }
     if (k + 1 < c_end) {
       swrite(kb ^ 1);
       if (k + 2 < c_end) gload(k + 2);
     }
 #pragma unroll
-    for (int ut = 0; ut < 2; ++ut) {
-      r2[ut] = r1[ut];
+    for (int ut = 0; ut < 2; ++ut)
 #pragma unroll
       for (int v = 0; v < 16; ++v)
-        r1[ut][v] = __int_as_float(__builtin_amdgcn_ds_bpermute(rot_addr[v], __float_as_int(acc[ut][v])));
-    }
+        r2[ut][v] = __int_as_float(__builtin_amdgcn_ds_bpermute(rot_addr[v], __float_as_int(acc[ut][v])));
     __syncthreads();
+  };
+  // Two chunks per trip, the register sets alternating roles (chunk k writes its rotation over the
+  // older set): no copies between chunks.  Steady state (interior lines: the line's stores ride
+  // between the MFMAs, a compile-time choice) after the slice's first two chunks (compile-time
+  // edges); the rest -- the slice's end, a partial user block's chunks -- tests each line at run
+  // time.  In the one-body form of round 5, 32 v_mov (set copies) and 32 scalar branches (the
+  // per-step line test) sat beside every chunk's 64 MFMAs.
+  const std::true_type interior{};
+  const std::false_type edge{};
+  auto runtime_line = [&](int64_t k) { return k > c_begin && line_interior(k - 1); };
+  int64_t k = c_begin;
+  const int64_t k_hi = !full_rows ? k : (c_end < rows / SC_CHUNK + 1 ? c_end : rows / SC_CHUNK + 1);
+  if (full_rows && c_begin + 2 <= k_hi) {
+    body(k, ra, rb, edge);           // no line yet
+    body(k + 1, rb, ra, edge);       // the slice's first line (masked)
+#pragma unroll 1
+    for (k += 2; k + 2 <= k_hi; k += 2) {
+      body(k, ra, rb, interior);     // chunk k's rotation -> rb
+      body(k + 1, rb, ra, interior); // chunk k+1's -> ra
+    }
   }
-  // line A_{c_end - 1}, then the line after the last chunk (its lanes p < o)
+#pragma unroll 1
+  for (; k + 2 <= c_end; k += 2) {
+    body(k, ra, rb, runtime_line(k));
+    body(k + 1, rb, ra, runtime_line(k + 1));
+  }
+  // newest rotation in ra (rb: the one before) unless one chunk is left
+  auto finish = [&](const f32x16(&r1)[2], const f32x16(&r2)[2]) __attribute__((always_inline)) {
+    // line A_{c_end - 1}, then the line after the last chunk (its lanes p < o, from chunk c_end - 1)
 #pragma unroll
-  for (int t = 0; t < 32; ++t) store_reg(c_end - 1, t, false);
+    for (int t = 0; t < 32; ++t) store_reg(r1, r2, c_end - 1, t, false);
 #pragma unroll
-  for (int ut = 0; ut < 2; ++ut) r2[ut] = r1[ut];
-#pragma unroll
-  for (int t = 0; t < 32; ++t) store_reg(c_end, t, false);
+    for (int t = 0; t < 32; ++t) store_reg(r1, r1, c_end, t, false);
+  };
+  if (k < c_end) {
+    body(k, ra, rb, runtime_line(k));
+    finish(rb, ra);
+  } else {
+    finish(ra, rb);
+  }
 }
 
 }  // namespace gr

@@ -26,33 +26,62 @@ def shard_range(n, rank, world):
     return n * rank // world, n * (rank + 1) // world
 
 
-def all_gather_rows(t, group=None, sizes=None):
+def all_gather_rows(t, group=None, sizes=None, async_op=False):
     """Concatenate a [n_r, ...] tensor over ranks (n_r may differ by rank).  ``sizes`` (every
-    rank's n_r, e.g. from ``shard_range``) skips the size exchange and its host synchronisation."""
+    rank's n_r, e.g. from ``shard_range``) skips the size exchange and its host synchronisation.
+
+    Over RCCL the rows land in ONE [world * max(n_r), ...] tensor (``all_gather_into_tensor``: one
+    collective, no per-rank list, no concatenation when every rank holds the same count -- the C5
+    bench's case); other backends (gloo) gather a list.  ``async_op``: returns ``(result, work)``
+    with ``result`` valid after ``work.wait()`` (RCCL only; elsewhere the gather has completed)."""
     world = dist.get_world_size(group)
     if sizes is None:
         n = torch.tensor([t.shape[0]], dtype=torch.int64, device=t.device)
         sz = [torch.zeros_like(n) for _ in range(world)]
         dist.all_gather(sz, n, group=group)
         sizes = [int(s.item()) for s in sz]
+    if sizes[dist.get_rank(group)] != t.shape[0]:
+        raise ValueError(f"all_gather_rows: this rank holds {t.shape[0]} rows, sizes say "
+                         f"{sizes[dist.get_rank(group)]}")
     m = max(sizes)
-    pad = torch.zeros((m - t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
-    buf = torch.cat([t, pad])
-    out = [torch.empty_like(buf) for _ in range(world)]
-    dist.all_gather(out, buf, group=group)
-    return torch.cat([o[:s] for o, s in zip(out, sizes)])
+    buf = t.contiguous()
+    if t.shape[0] < m:
+        buf = torch.cat([buf, torch.zeros((m - t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)])
+    if t.is_cuda and dist.get_backend(group) == "nccl":
+        out = torch.empty((world * m,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+        work = dist.all_gather_into_tensor(out, buf, group=group, async_op=async_op)
+        if any(s != m for s in sizes):
+            if async_op:
+                work.wait()
+                work = None
+            out = torch.cat([out[r * m:r * m + s] for r, s in enumerate(sizes)])
+        return (out, work) if async_op else out
+    parts = [torch.empty_like(buf) for _ in range(world)]
+    dist.all_gather(parts, buf, group=group)
+    out = torch.cat([o[:s] for o, s in zip(parts, sizes)])
+    return (out, None) if async_op else out
 
 
 def merge_topk(vals, ids, k):
-    """Top-k of candidate lists [B, C] (values, global ids): value descending, ties to the lower id;
-    ids < 0 are padding.  On the GPU one wave per row (ops.merge_topk, gr_merge_topk_f32); the
-    torch form below (two stable sorts) serves CPU tensors (the gloo tests) with the same result."""
-    if vals.is_cuda and vals.shape[1] <= 256:
+    """Top-k of candidate lists [B, C] (values, global ids): value descending, ties to the lower id.
+    Padding: an entry whose id is < 0 or whose value is NaN (a NaN never ranks).  The result has
+    exactly ``k`` columns; when fewer than ``k`` real candidates exist the rest are (-inf, -1).
+    ``k`` < 1 raises ValueError.  fp32 CUDA rows of <= 256 candidates: one wave per row
+    (ops.merge_topk, gr_merge_topk_f32); everything else (CPU tensors -- the gloo tests -- other
+    dtypes, wider rows): the torch form below (two stable sorts), with the same result."""
+    if k < 1:
+        raise ValueError(f"merge_topk: k must be >= 1, got {k}")
+    if vals.is_cuda and vals.dtype == torch.float32 and vals.shape[1] <= 256:
         from . import ops
         return ops.merge_topk(vals, ids, k)
-    v = torch.where(ids < 0, torch.full_like(vals, float("-inf")), vals)
+    pad = (ids < 0) | torch.isnan(vals)
+    v = torch.where(pad, torch.full_like(vals, float("-inf")), vals)
     big = torch.iinfo(torch.int64).max
-    i = torch.where(ids < 0, torch.full_like(ids, big), ids)
+    i = torch.where(pad, torch.full_like(ids, big), ids.to(torch.int64))
+    if v.shape[1] < k:                                             # fewer candidates than k: pad
+        extra = k - v.shape[1]
+        v = torch.cat([v, torch.full((v.shape[0], extra), float("-inf"), dtype=v.dtype, device=v.device)], 1)
+        i = torch.cat([i, torch.full((i.shape[0], extra), big, dtype=i.dtype, device=i.device)], 1)
     o1 = torch.argsort(i, dim=1, descending=False, stable=True)                    # secondary key: id ascending
     v1, i1 = v.gather(1, o1), i.gather(1, o1)
     o2 = torch.argsort(v1, dim=1, descending=True, stable=True)  # primary key: value descending

@@ -3,9 +3,9 @@ evaluation of SASRec/train.py:33-56.
 
 The reference computes ``logits = model.predict(x)`` ([B, N+1] fp32), masks column 0 with -1e9,
 gathers the target's logit and counts strictly greater logits (evaluate.py:26-32).  Here the rank
-comes from ``ops.score_rank``: the last hidden state from the fused SASRec forward, then the target
-logit and the strict-'>' count straight from the scoring kernel's MFMA tiles — the [B, N+1] logits
-are never written (``materialize=True`` runs the reference's predict + rank sequence instead; both
+of a batch is ONE C-ABI call, ``ops.sasrec_rank`` (``gr_sasrec_rank_f32``): the last hidden state
+from the fused SASRec forward, then the target logit and the strict-'>' count straight from the
+scoring kernel's MFMA tiles — the [B, N+1] logits are never written (``materialize=True`` runs the reference's predict + rank sequence instead; both
 give the same ranks, tests/test_evaluate_gpu.py).  HR@k / NDCG@k are then formed on the host in
 float64 exactly as the reference does (per-user Python list, ``np.mean``, evaluate.py:35-47).
 """
@@ -29,8 +29,8 @@ def rank_batch(model, input_ids, targets, materialize=False):
         return (logits > t).sum(dim=1) + 1
     if model.d not in (16, 32, 64, 128):   # the fused kernels' widths; others: predict + rank kernel
         return ops.rank(model.predict(input_ids), targets, mask_col0=True)
-    h = model.last_hidden(input_ids)
-    return ops.score_rank(h, model.item_emb.weight.detach(), targets, mask_col0=True)
+    # forward + target logit + strict count in one C-ABI call (gr_sasrec_rank_f32)
+    return ops.sasrec_rank(model._binding(input_ids), input_ids, targets, mask_col0=True)
 
 
 def hr_ndcg(ranks, top_k):
@@ -63,11 +63,14 @@ def multi_k(ranks, topk_list, targets=None):
 
 
 @torch.no_grad()
-def evaluate(params, dataset=None, model=None, materialize=False, save_csv=True):
+def evaluate(params, dataset=None, model=None, materialize=False, save_csv=True, with_multi_k=False):
     """SASRec/evaluate.py:evaluate(params).  ``dataset`` / ``model`` may be passed in directly (the
     reference builds them from ``params['data_path']`` / ``params['ckpt']``); checkpoints are read
-    with ``torch.load(weights_only=True)``.  Returns {"Hit@k": ..., "NDCG@k": ...} (plus every k of
-    ``params['topk_list']`` when present) and the rank vector."""
+    with ``torch.load(weights_only=True)``.  Returns ``(results, ranks)``: ``results`` is exactly the
+    reference's dict {"Hit@top_k", "NDCG@top_k"} (evaluate.py:51), which is also all the CSV row
+    carries (evaluate.py:52, 57-89).  ``with_multi_k``: a third value, {"Hit@k", "NDCG@k"} for every
+    k of ``params['topk_list']`` with train.py:33-56's semantics (target-0 users dropped) -- kept
+    out of ``results`` and out of the CSV so both keep the reference's schema."""
     from .sasrec import SASRec
     device = torch.device(params["device"])
     if dataset is None:
@@ -87,14 +90,17 @@ def evaluate(params, dataset=None, model=None, materialize=False, save_csv=True)
     top_k = params.get("top_k", 10)
     hit, ndcg = hr_ndcg(ranks, top_k)
     results = {f"Hit@{top_k}": hit, f"NDCG@{top_k}": ndcg}
+    if save_csv and params.get("params_path"):
+        save_results_to_csv(params, results)
+    if not with_multi_k:
+        return results, ranks
+    multi = {}
     if params.get("topk_list"):        # train.py:33-56 semantics: target-0 users dropped
         hk, nk = multi_k(ranks, params["topk_list"], tgts)
         for k in params["topk_list"]:
-            results.setdefault(f"Hit@{k}", hk[k])
-            results.setdefault(f"NDCG@{k}", nk[k])
-    if save_csv and params.get("params_path"):
-        save_results_to_csv(params, results)
-    return results, ranks
+            multi[f"Hit@{k}"] = hk[k]
+            multi[f"NDCG@{k}"] = nk[k]
+    return results, ranks, multi
 
 
 @torch.no_grad()

@@ -60,7 +60,7 @@ def linear(x, weight, bias=None, act="none", residual=None, out=None):
     y = out if out is not None else torch.empty((m, n), dtype=torch.float32, device=x.device)
     a = {"none": L.GR_ACT_NONE, "relu": L.GR_ACT_RELU, "sigmoid": L.GR_ACT_SIGMOID, "tanh": L.GR_ACT_TANH,
          "leakyrelu": L.GR_ACT_LEAKYRELU}[act]
-    with torch.cuda.device(x.device):
+    with L.on(x.device):
         L.check(L.lib().gr_linear_f32(L.ptr(x2), m, k, L.ptr(w), n, L.ptr(b), L.ptr(r),
                                       n if r is not None else 0, a, L.ptr(y), n,
                                       L.stream_of(x.device)), "gr_linear_f32")
@@ -75,7 +75,7 @@ def score(h, table, out=None):
     B, d = h.shape
     rows = t.shape[0]
     y = out if out is not None else logits_buffer(B, rows, h.device)
-    with torch.cuda.device(h.device):
+    with L.on(h.device):
         L.check(L.lib().gr_score_f32(L.ptr(h), B, d, L.ptr(t), rows, L.ptr(y), y.stride(0),
                                      L.stream_of(h.device)), "gr_score_f32")
     return y
@@ -89,7 +89,7 @@ def rank(logits, targets, mask_col0=True):
     t = targets.reshape(-1).to(torch.int64).contiguous()
     B, cols = logits.shape
     out = torch.empty(B, dtype=torch.int64, device=logits.device)
-    with torch.cuda.device(logits.device):
+    with L.on(logits.device):
         L.check(L.lib().gr_rank_f32(L.ptr(logits), B, cols, logits.stride(0), L.ptr(t),
                                     1 if mask_col0 else 0, L.ptr(out),
                                     L.stream_of(logits.device)), "gr_rank_f32")
@@ -104,7 +104,7 @@ def count_gt(logits, thresholds):
     th = L.as_f32(thresholds.reshape(-1))
     B, cols = logits.shape
     out = torch.empty(B, dtype=torch.int64, device=logits.device)
-    with torch.cuda.device(logits.device):
+    with L.on(logits.device):
         L.check(L.lib().gr_count_gt_f32(L.ptr(logits), B, cols, logits.stride(0), L.ptr(th),
                                         L.ptr(out), L.stream_of(logits.device)), "gr_count_gt_f32")
     return out
@@ -124,7 +124,7 @@ def topk(logits, k, id_offset=0, thresholds=None):
     cnt = torch.empty(B, dtype=torch.int64, device=dev) if th is not None else None
     nbytes = L.lib().gr_topk_workspace_bytes(B, cols, k)
     wsp = L.workspace(nbytes, dev)
-    with torch.cuda.device(dev):
+    with L.on(dev):
         L.check(L.lib().gr_topk_f32(L.ptr(logits), B, cols, logits.stride(0), k, id_offset,
                                     L.ptr(vals), L.ptr(ids), L.ptr(th), L.ptr(cnt), L.ptr(wsp), nbytes,
                                     L.stream_of(dev)), "gr_topk_f32")
@@ -140,7 +140,7 @@ def score_pairs(h, table, ids, mask_col0=True):
     B, d = h.shape
     out = torch.empty(B, dtype=torch.float32, device=h.device)
     err = err_flag(h.device)
-    with torch.cuda.device(h.device):
+    with L.on(h.device):
         L.check(L.lib().gr_score_pairs_f32(L.ptr(h), B, d, L.ptr(t), t.shape[0], L.ptr(ids),
                                            1 if mask_col0 else 0, L.ptr(out), L.ptr(err),
                                            L.stream_of(h.device)), "gr_score_pairs_f32")
@@ -152,12 +152,20 @@ _COUNT_WS = {}   # (device, stream) -> zeroed workspace of gr_score_count_gt_ws_
 
 
 def _count_workspace(device, nbytes):
+    """The count kernel's workspace, which it expects zero on entry and leaves zero on exit.
+    Eager calls reuse one cached, once-zeroed buffer per (device, stream).  Under graph capture a
+    fresh buffer is allocated and zeroed by a node of the graph itself, and never cached: a cached
+    buffer first zeroed inside a capture holds zeros only after a replay, and the capture stream's
+    key is reused by later captures."""
+    if torch.cuda.is_current_stream_capturing():
+        # zeroed by a fill KERNEL node of the graph (torch.zeros), so every replay starts from zeros
+        return torch.zeros(nbytes, dtype=torch.uint8, device=device), None
     key = (device, torch.cuda.current_stream(device).cuda_stream)
     ws = _COUNT_WS.get(key)
     if ws is None or ws.numel() < nbytes:
         ws = torch.zeros(nbytes, dtype=torch.uint8, device=device)
         _COUNT_WS[key] = ws
-    return ws
+    return ws, key
 
 
 def score_count_gt(h, table, thresholds, mask_col0=True):
@@ -167,12 +175,17 @@ def score_count_gt(h, table, thresholds, mask_col0=True):
     th = L.as_f32(thresholds.reshape(-1))
     B, d = h.shape
     out = torch.empty(B, dtype=torch.int64, device=h.device)
-    with torch.cuda.device(h.device):
+    with L.on(h.device):
         nb = L.lib().gr_score_count_workspace_bytes(B)
-        ws = _count_workspace(h.device, nb)
-        L.check(L.lib().gr_score_count_gt_ws_f32(L.ptr(h), B, d, L.ptr(t), t.shape[0], L.ptr(th),
-                                                 1 if mask_col0 else 0, L.ptr(out), L.ptr(ws), nb,
-                                                 L.stream_of(h.device)), "gr_score_count_gt_ws_f32")
+        ws, key = _count_workspace(h.device, nb)
+        try:
+            L.check(L.lib().gr_score_count_gt_ws_f32(L.ptr(h), B, d, L.ptr(t), t.shape[0], L.ptr(th),
+                                                     1 if mask_col0 else 0, L.ptr(out), L.ptr(ws), nb,
+                                                     L.stream_of(h.device)), "gr_score_count_gt_ws_f32")
+        except Exception:
+            if key is not None:   # a failed call may leave non-zero words: never reuse the buffer
+                _COUNT_WS.pop(key, None)
+            raise
     return out
 
 
@@ -198,7 +211,7 @@ def score_topk(h, table, k, id_offset=0, thresholds=None, mask_col0=True):
     cnt = torch.empty(B, dtype=torch.int64, device=dev) if th is not None else None
     nbytes = L.lib().gr_score_topk_workspace_bytes(B, d, rows, k)
     wsp = L.workspace(nbytes, dev)
-    with torch.cuda.device(dev):
+    with L.on(dev):
         L.check(L.lib().gr_score_topk_f32(L.ptr(h), B, d, L.ptr(t), rows, id_offset,
                                           1 if mask_col0 else 0, k, L.ptr(th), L.ptr(cnt),
                                           L.ptr(vals), L.ptr(ids), L.ptr(wsp), nbytes,
@@ -215,7 +228,7 @@ def merge_topk(vals, ids, k):
     i = ids.to(torch.int64).contiguous()
     out_v = torch.empty((B, k), dtype=torch.float32, device=vals.device)
     out_i = torch.empty((B, k), dtype=torch.int64, device=vals.device)
-    with torch.cuda.device(vals.device):
+    with L.on(vals.device):
         L.check(L.lib().gr_merge_topk_f32(L.ptr(v), v.stride(0), L.ptr(i), i.stride(0), B, C, k,
                                           L.ptr(out_v), L.ptr(out_i), L.stream_of(vals.device)),
                 "gr_merge_topk_f32")
@@ -230,7 +243,7 @@ def merge_topk_packed(packed, world, kk, k):
     B = packed.numel() // (world * 2 * kk)
     out_v = torch.empty((B, k), dtype=torch.float32, device=packed.device)
     out_i = torch.empty((B, k), dtype=torch.int64, device=packed.device)
-    with torch.cuda.device(packed.device):
+    with L.on(packed.device):
         L.check(L.lib().gr_merge_topk_packed(L.ptr(packed), world, B, kk, k, L.ptr(out_v), L.ptr(out_i),
                                              L.stream_of(packed.device)), "gr_merge_topk_packed")
     return out_v, out_i
@@ -254,7 +267,7 @@ def rq_quantize(z, codebooks, with_gap=False):
     best = torch.empty((n, len(cbs)), dtype=torch.float32, device=dev) if with_gap else None
     lib = L.lib()
     st = L.stream_of(dev)
-    with torch.cuda.device(dev):
+    with L.on(dev):
         # code_norms = NULL: the kernel recomputes the norms from its LDS image of each codebook
         L.check(lib.gr_rq_quantize_f32(L.ptr(z), n, e, len(cbs), L.i32_array(Ks), L.ptr_array(cbs),
                                        None, L.ptr(idx), L.ptr(best), L.ptr(gap), st),
@@ -305,6 +318,18 @@ class RqBinding:
         if self.packed is None or not self.frozen:
             return None
         key = tuple(w._version for w in self.ws) + (_WEIGHT_EPOCH[0],)
+        capturing = torch.cuda.is_current_stream_capturing()
+        if key != self._pack_key and capturing:
+            # a pack recorded into a graph would run only at replay, leaving the eager image stale
+            raise RuntimeError("rq_encode: the packed encoder image is out of date inside a graph capture; "
+                               "run one eager get_indices after the last weight change, then capture "
+                               "(graphs that encode must be re-captured after weight changes)")
+        if capturing:
+            # a captured graph bakes in this image's pointer: keep the image alive for the binding's
+            # lifetime, so replays after a later re-pack read the old weights, never freed memory
+            refs = self.__dict__.setdefault("_graph_images", [])
+            if not any(r is self.packed for r in refs):
+                refs.append(self.packed)
         if key != self._pack_key:
             if self._pack_key is not None:
                 # a re-pack writes a fresh image on this stream; the previous one goes back to the
@@ -312,7 +337,7 @@ class RqBinding:
                 # stream recorded on it (below) has finished
                 self.packed = torch.empty_like(self.packed)
                 self._streams = set()
-            with torch.cuda.device(self.device):
+            with L.on(self.device):
                 L.check(L.lib().gr_rq_encoder_pack_f32(len(self.ws), self.dims_c, self.w_arr, L.ptr(self.packed),
                                                        L.stream_of(self.device)), "gr_rq_encoder_pack_f32")
             self._pack_key = key
@@ -394,7 +419,7 @@ def rq_encode(x, weights=None, biases=None, codebooks=None, with_gap=False, with
     gap = torch.empty((n, nl), dtype=torch.float32, device=dev) if with_gap else None
     best = torch.empty((n, nl), dtype=torch.float32, device=dev) if with_gap else None
     z = torch.empty((n, b.dims[-1]), dtype=torch.float32, device=dev) if with_z else None
-    with torch.cuda.device(dev):
+    with L.on(dev):
         L.check(L.lib().gr_rq_encode_packed_f32(L.ptr(x2), n, len(b.ws), b.dims_c, b.w_arr, b.b_arr,
                                                 b.packed_ptr(), nl, b.ks_c, b.c_arr, L.ptr(idx), L.ptr(best),
                                                 L.ptr(gap), L.ptr(z), L.ptr(wsp), nbytes, L.stream_of(dev)),
@@ -446,7 +471,7 @@ def rq_mlp(x, weights, biases, bn=None, act="relu", group_sizes=None):
             ts = [L.as_f32(t) for t in group]
             keep.append(ts)
             bn_arrs[j] = L.ptr_array(ts)
-    with torch.cuda.device(dev):
+    with L.on(dev):
         if group_sizes is not None:
             sizes = [int(g) for g in group_sizes]
             if sum(sizes) != n or any(g < 1 for g in sizes):
@@ -462,9 +487,12 @@ def rq_mlp(x, weights, biases, bn=None, act="relu", group_sizes=None):
                 return plans[m]
 
             big = [i for i, g in enumerate(sizes) if all(k == "chain" for k, _ in plan(g))]
-            if big:
+            while big:   # the kept groups' one call must have every kept group's own order
                 pb = plan(sum(sizes[i] for i in big))
-                big = [i for i in big if plan(sizes[i]) == pb]
+                keep = [i for i in big if plan(sizes[i]) == pb]
+                if keep == big:
+                    break
+                big = keep
             small = [i for i in range(len(sizes)) if i not in set(big)]
             offs = [0]
             for g in sizes:
@@ -556,7 +584,7 @@ def rq_quantize_sk(z, codebooks, sk_eps, sk_iters, group_sizes=None):
     nbytes = lib.gr_rq_encode_sk_workspace_bytes(n, e, len(cbs), ks_c)
     wsp = L.workspace(nbytes, dev)
     idx = torch.empty((n, len(cbs)), dtype=torch.int64, device=dev)
-    with torch.cuda.device(dev):
+    with L.on(dev):
         L.check(lib.gr_rq_encode_sk_f32(L.ptr(z), n, e, len(cbs), ks_c, L.ptr_array(cbs), eps_c,
                                         int(sk_iters), L.ptr(ptr), len(sizes), L.ptr(idx), L.ptr(wsp),
                                         nbytes, L.stream_of(dev)), "gr_rq_encode_sk_f32")
@@ -598,7 +626,9 @@ class SasrecBinding:
         p.last_ln_w = f(model.last_layernorm.weight)
         p.last_ln_b = f(model.last_layernorm.bias)
         self.p = p
+        self.p_ref = ctypes.byref(p)
         self.device = model.item_emb.weight.device
+        self._ws = {}
 
     def _f(self, t):
         L.require_gpu(t)
@@ -613,7 +643,23 @@ class SasrecBinding:
         return ctypes.cast(a, ctypes.c_void_p)
 
     def workspace_bytes(self, B, n):
-        return L.lib().gr_sasrec_workspace_bytes(ctypes.byref(self.p), B, n)
+        key = (0, B, n)
+        nb = self._ws.get(key)
+        if nb is None:
+            nb = L.lib().gr_sasrec_workspace_bytes(self.p_ref, B, n)
+            if len(self._ws) < 256:
+                self._ws[key] = nb
+        return nb
+
+    def rank_workspace_bytes(self, B, n):
+        key = (1, B, n)
+        nb = self._ws.get(key)
+        if nb is None:
+            nb = (L.lib().gr_sasrec_rank_workspace_bytes(self.p_ref, B, n),
+                  L.lib().gr_score_count_workspace_bytes(B))
+            if len(self._ws) < 256:
+                self._ws[key] = nb
+        return nb
 
 
 def sasrec_binding(model):
@@ -656,10 +702,44 @@ def sasrec_forward(binding, log_seqs, last_only=False):
     nbytes = binding.workspace_bytes(B, n)
     wsp = L.workspace(nbytes, dev)
     err = err_flag(dev)
-    with torch.cuda.device(dev):
-        L.check(L.lib().gr_sasrec_forward_f32(ctypes.byref(binding.p), L.ptr(ids), B, n, L.ptr(out),
+    with L.on(dev):
+        L.check(L.lib().gr_sasrec_forward_f32(binding.p_ref, L.ptr(ids), B, n, L.ptr(out),
                                               1 if last_only else 0, L.ptr(wsp), nbytes, L.ptr(err),
                                               L.stream_of(dev)), "gr_sasrec_forward_f32")
+    _check_err(err)
+    return out
+
+
+def sasrec_rank(binding, log_seqs, targets, mask_col0=True):
+    """One batch of SASRec/evaluate.py:26-32 in ONE C-ABI call (``gr_sasrec_rank_f32``): the 1-based
+    strict rank of each target over the full catalog, column 0 taken as -1e9 when ``mask_col0``,
+    from the forward's last hidden states -- the logits are never written.  Bitwise the ranks of
+    ``ops.rank(predict(seqs), targets)`` (the same fp32 scoring chain)."""
+    ids = _sas_ids(log_seqs, binding)
+    B, n = ids.shape
+    t = targets.reshape(-1)
+    if t.dtype != torch.int64:
+        t = t.to(torch.int64)
+    if not t.is_contiguous():
+        t = t.contiguous()
+    if t.shape[0] != B:
+        raise RuntimeError(f"sasrec_rank: {t.shape[0]} targets for {B} sequences")
+    dev = ids.device
+    nbytes, cnb = binding.rank_workspace_bytes(B, n)
+    wsp = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    out = torch.empty(B, dtype=torch.int64, device=dev)
+    err = err_flag(dev)
+    cws, key = _count_workspace(dev, cnb)
+    with L.on(dev):
+        try:
+            L.check(L.lib().gr_sasrec_rank_f32(binding.p_ref, ids.data_ptr(), B, n, t.data_ptr(),
+                                               1 if mask_col0 else 0, out.data_ptr(), wsp.data_ptr(), nbytes,
+                                               L.ptr(cws), cnb, err.data_ptr(),
+                                               L.stream_of(dev)), "gr_sasrec_rank_f32")
+        except Exception:
+            if key is not None:
+                _COUNT_WS.pop(key, None)
+            raise
     _check_err(err)
     return out
 
@@ -693,8 +773,8 @@ def sasrec_predict(binding, log_seqs, out=None):
     nbytes = binding.workspace_bytes(B, n)
     wsp = L.workspace(nbytes, dev)
     err = err_flag(dev)
-    with torch.cuda.device(dev):
-        L.check(L.lib().gr_sasrec_predict_ld_f32(ctypes.byref(binding.p), L.ptr(ids), B, n,
+    with L.on(dev):
+        L.check(L.lib().gr_sasrec_predict_ld_f32(binding.p_ref, L.ptr(ids), B, n,
                                                  L.ptr(logits), ld, L.ptr(wsp), nbytes, L.ptr(err),
                                                  L.stream_of(dev)), "gr_sasrec_predict_ld_f32")
     _check_err(err)
@@ -718,7 +798,7 @@ class _SampledBCE(torch.autograd.Function):
         coef = torch.empty(B * n * (J + 1), dtype=torch.float32, device=dev)
         sums = torch.empty(2, dtype=torch.float32, device=dev)
         err = err_flag(dev)
-        with torch.cuda.device(dev):
+        with L.on(dev):
             L.check(L.lib().gr_sampled_bce_fwd_f32(L.ptr(feats), B, n, d, L.ptr(table), rows,
                                                    L.ptr(targets), L.ptr(negs), J, float(eps),
                                                    L.ptr(row_loss), L.ptr(coef), L.ptr(sums),
@@ -739,7 +819,7 @@ class _SampledBCE(torch.autograd.Function):
         g = g_loss.to(device=dev, dtype=torch.float32).reshape(1).contiguous()
         dfeats = torch.empty_like(feats)
         dtable = torch.empty_like(table)
-        with torch.cuda.device(dev):
+        with L.on(dev):
             L.check(L.lib().gr_sampled_bce_bwd_f32(L.ptr(feats), B, n, d, L.ptr(table), rows,
                                                    L.ptr(targets), L.ptr(negs), negs.shape[1],
                                                    L.ptr(coef), L.ptr(g), L.ptr(dfeats),
@@ -792,7 +872,7 @@ def neg_samples(seq, item_num, num_neg=1, seed=None, seed_tensor=None):
         seed = 0 if seed_tensor is not None else int(torch.randint(0, 2 ** 62, (1,)).item()) ^ next(_NEG_CALLS)
     out = torch.empty((B, num_neg), dtype=torch.int64, device=s.device)
     err = err_flag(s.device)
-    with torch.cuda.device(s.device):
+    with L.on(s.device):
         if seed_tensor is not None:
             if seed_tensor.dtype != torch.int64 or seed_tensor.numel() != 1 or seed_tensor.device != s.device:
                 raise RuntimeError("neg_samples: seed_tensor must be one int64 element on the sequences' device")
@@ -864,7 +944,7 @@ class _SasTrain(torch.autograd.Function):
         out = e(B, n, d)
         err = err_flag(dev)
         cb = L.SasrecTrainBufs(**{k: v.data_ptr() for k, v in bufs.items()})
-        with torch.cuda.device(dev):
+        with L.on(dev):
             L.check(L.lib().gr_sasrec_train_fwd_f32(ctypes.byref(p), L.ptr(seqs), B, n, float(p_drop), 0,
                                                     L.ptr(seed_snap), ctypes.byref(cb), L.ptr(out), L.ptr(err),
                                                     L.stream_of(dev)), "gr_sasrec_train_fwd_f32")
@@ -884,7 +964,7 @@ class _SasTrain(torch.autograd.Function):
         g_item = torch.zeros((p.item_rows, d), dtype=torch.float32, device=dev)
         cb = L.SasrecTrainBufs(g_vec=g_vec.data_ptr(), **{k: v.data_ptr() for k, v in bufs.items()})
         dout = dout.contiguous().float()
-        with torch.cuda.device(dev):
+        with L.on(dev):
             L.check(L.lib().gr_sasrec_train_bwd_f32(ctypes.byref(p), L.ptr(seqs), B, n, float(ctx.p_drop), 0,
                                                     L.ptr(ctx.seed), ctypes.byref(cb), L.ptr(dout), L.ptr(g_item),
                                                     L.stream_of(dev)), "gr_sasrec_train_bwd_f32")
@@ -1173,7 +1253,7 @@ class _RqQuantTrain(torch.autograd.Function):
         idx = torch.empty((n, len(codebooks)), dtype=torch.int64, device=dev)
         xq = torch.empty((n, e), dtype=torch.float32, device=dev)
         sq = torch.empty((n, len(codebooks)), dtype=torch.float32, device=dev)
-        with torch.cuda.device(dev):
+        with L.on(dev):
             L.check(lib.gr_rq_quantize_sk_train_f32(L.ptr(z), n, e, len(codebooks), ks_c, L.ptr_array(codebooks),
                                                     eps_c, int(sk_iters), L.ptr(_group_ptr([n], dev)), 1,
                                                     L.ptr(idx), L.ptr(xq), L.ptr(sq), L.ptr(wsp), nbytes,
@@ -1194,7 +1274,7 @@ class _RqQuantTrain(torch.autograd.Function):
         g_xq = g_xq.contiguous() if g_xq is not None else None
         dz = torch.empty_like(z)
         dcs = [torch.empty_like(c) for c in codebooks]
-        with torch.cuda.device(dev):
+        with L.on(dev):
             L.check(L.lib().gr_rq_quantize_sk_train_bwd_f32(
                 L.ptr(z), n, e, len(codebooks), L.i32_array([c.shape[0] for c in codebooks]),
                 L.ptr_array(codebooks), L.ptr(idx), L.ptr(g_xq) if g_xq is not None else None, L.ptr(g_rq),
@@ -1231,7 +1311,7 @@ class _MlpTrain(torch.autograd.Function):
         dims = [x.shape[1]] + [w.shape[0] for w in ws]
         outs = [torch.empty((M, dd), dtype=torch.float32, device=dev) for dd in dims[1:]]
         xd0 = torch.empty_like(x) if p > 0 else x
-        with torch.cuda.device(dev):
+        with L.on(dev):
             L.check(L.lib().gr_mlp_train_fwd_f32(L.ptr(x), M, n, L.i32_array(dims), L.ptr_array(ws),
                                                  L.ptr_array(bs), float(p), L.ptr(snap),
                                                  L.ptr(xd0) if p > 0 else None, L.ptr_array(outs),
@@ -1249,7 +1329,7 @@ class _MlpTrain(torch.autograd.Function):
         dev = xd0.device
         dz = dout.contiguous().float()
         gw, gb = [None] * n, [None] * n
-        with torch.cuda.device(dev):
+        with L.on(dev):
             for i in reversed(range(n)):
                 K, N = acts[i].shape[1], ws[i].shape[0]
                 dW = torch.empty_like(ws[i])

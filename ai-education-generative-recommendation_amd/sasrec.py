@@ -57,10 +57,12 @@ class SASRec(nn.Module):
         """model.py:49-96: ``[B, n]`` item ids -> ``[B, n, d]`` final hidden states.
 
         Eval mode (or grad disabled): one C-ABI call, ``gr_sasrec_forward_f32``, no autograd graph.
-        Train mode with grad enabled (the SASRec/train.py:131 call): the same blocks as torch modules
-        under autograd, dropout active — the transformer's backward is not a kernel here; the
-        step's scoring, loss and negative sampling are (``ops.sampled_bce_loss``,
-        ``ops.neg_samples``)."""
+        Train mode with grad enabled (the SASRec/train.py:131 call), dropout active: the fused
+        training kernels of sasrec_train.hip when the shape fits them (``ops.sasrec_train_forward``:
+        one launch forward, one launch backward -- ``gr_sasrec_train_fwd_f32`` /
+        ``gr_sasrec_train_bwd_f32``), otherwise the same blocks as torch modules under autograd
+        (``fused_train = False`` forces the latter).  The step's scoring, loss and negative sampling
+        are kernels too (``ops.sampled_bce_loss``, ``ops.neg_samples``)."""
         if self.training and torch.is_grad_enabled():
             return self._forward_autograd(log_seqs)
         with torch.no_grad():

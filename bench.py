@@ -118,6 +118,10 @@ def sas_exec_flop_per_user(d, n, items, mlp=64, blocks=2, causal=True, tail_h=Fa
 # rehearsal mode); "cpu" for the launcher self-test (GR_BENCH_DEVICE=cpu, no GPU needed)
 COLL_DEV = "cuda"
 
+# C5 at N > 1: the pipelined exchange's user sub-batches per step (dist.sharded_rank_topk_batches),
+# from the c5_rank leg's overlapped_ms_p2 / _p4 figures (P = 4 scores in launches too small)
+C5_PIPELINE_DEFAULT = 2
+
 
 def per_rank(x, world):
     """``x`` (this rank's float) from every rank, in rank order (a collective at world > 1)."""
@@ -165,8 +169,10 @@ def parse():
     ap.add_argument("--c5-rank-world", type=int, default=8,
                     help="c5_rank leg: the world size whose per-rank step it times on one GPU")
     ap.add_argument("--c5-items", type=int, default=1_000_000)
-    ap.add_argument("--c5-pipeline", type=int, default=1,
-                    help="C5 at N>1: user sub-batches per step whose exchange overlaps the next one's scoring")
+    ap.add_argument("--c5-pipeline", type=int, default=0,
+                    help="C5 user sub-batches per step whose exchange overlaps the next one's scoring "
+                         f"(0 = auto: 1 at N = 1, where there is no exchange; at N > 1 the faster of 1 and "
+                         f"{C5_PIPELINE_DEFAULT}, timed on a few steps)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--train-batch", type=int, default=128, help="sas_train leg: users per rank per step")
     ap.add_argument("--legs", default="", help="comma list of legs to run (default: " + ",".join(LEGS) + "; also " + ",".join(OPT_LEGS) + ")")
@@ -328,14 +334,46 @@ def cpu_median(fn, units, unit, sample, warm=3, reps=10, agree=None):
     return res
 
 
-def rq_agreement(cpu_idx, gpu_idx):
-    """Rows whose semantic IDs differ between the host restatement and the GPU."""
+def rq_agreement(cpu_idx, gpu_idx, detail=None):
+    """Rows whose semantic IDs differ between the host restatement and the GPU, each characterised
+    against the near-tie certificate: ``detail`` = (GPU best [n, L], GPU gap
+    [n, L], GPU z [n, e], host z [n, e]).  A differing row is "flagged" when some level's GPU
+    best/second-best gap is within ``near_tie_bound`` (gr_amd.rqvae: the fp32 disagreement two
+    implementations whose encoder outputs differ by |dz| <= Z_TAU |z| can show); an unflagged
+    differing row would be a real parity break.  Also reported: this host's encoder deviation
+    max |z_host - z_gpu| / |z_gpu| against Z_TAU, the assumption the certificate rests on."""
+    from gr_amd.rqvae import Z_TAU, near_tie_bound
     cpu_idx, gpu_idx = cpu_idx.cpu(), gpu_idx.cpu()
     diff = (cpu_idx != gpu_idx).any(1)
-    return {"rows": int(cpu_idx.shape[0]), "rows_ids_differ": int(diff.sum()),
-            "note": "oracle/rq_oracle (torch CPU ops, this host's MKL) vs the GPU get_indices on the same "
-                    "items; the bit-exact claim is pinned on the fixture host's reference outputs "
-                    "(tests/golden), this count is this host's CPU path"}
+    res = {"rows": int(cpu_idx.shape[0]), "rows_ids_differ": int(diff.sum()),
+           "note": "oracle/rq_oracle (torch CPU ops, this host's MKL) vs the GPU get_indices on the same "
+                   "items; the bit-exact claim is pinned on the fixture host's reference outputs "
+                   "(tests/golden), this count is this host's CPU path"}
+    if detail is None:
+        return res
+    best, gap, zg, zc = (t.detach().cpu().double() for t in detail)
+    zn2 = (zg * zg).sum(1)
+    bound = near_tie_bound(best, gap, zn2)
+    flagged = (gap <= bound).any(1)
+    dzr = (zc - zg).norm(dim=1) / zn2.sqrt().clamp_min(1e-30)
+    rows = []
+    for r in torch.nonzero(diff).flatten().tolist()[:32]:
+        lv = int(torch.nonzero(cpu_idx[r] != gpu_idx[r]).flatten()[0])
+        rows.append({"row": r, "first_level_differing": lv, "gpu_gap": float(gap[r, lv]),
+                     "near_tie_bound": float(bound[r, lv]), "gap_over_bound": float(gap[r, lv] / bound[r, lv]),
+                     "flagged": bool(flagged[r]), "host_dz_over_z": float(dzr[r]),
+                     "host_z_bitwise_equal": bool(torch.equal(zc[r], zg[r]))})
+    res.update({"rows_ids_differ_flagged": int((diff & flagged).sum()),
+                "rows_ids_differ_unflagged": int((diff & ~flagged).sum()),
+                "rows_flagged_total": int(flagged.sum()),
+                "host_z_rows_bitwise_equal": int((zc == zg).all(1).sum()),
+                "host_dz_over_z_max": float(dzr.max()), "z_tau": Z_TAU,
+                "host_dz_within_z_tau": bool(float(dzr.max()) <= Z_TAU),
+                "differing_rows": rows,
+                "certificate": "flagged = some level's GPU best/second-best distance gap <= near_tie_bound "
+                               "(gr_amd/rqvae.py): an fp32 tie window two implementations with |dz| <= "
+                               "Z_TAU |z| may resolve either way"})
+    return res
 
 
 def sas_agreement(cpu_logits, gpu_logits, seed=0):
@@ -372,10 +410,13 @@ def cpu_rq_baseline(model, n_items, tag):
     cbs = [c.cpu() for c in model.rq.codebooks()]
     xg = synth.items(n_items, 12345, "cuda")
     gpu_idx = model.get_indices(xg).cpu()
+    _, best, gap, zg = ops.rq_encode(xg, binding=model.encode_binding(), with_gap=True, with_z=True)
     x = xg.cpu()
+    torch.set_num_threads(cpu_threads())
+    zc = rq_oracle.mlp_encode(x, ws, bs)   # this host's encoder output for the same call (one batch)
     return cpu_median(lambda: rq_oracle.get_indices(x, ws, bs, cbs), n_items, "items/s",
                       f"oracle/rq_oracle.get_indices, {tag}: batch of {n_items} synthetic items (fp32 torch CPU)",
-                      agree=lambda out: rq_agreement(out, gpu_idx))
+                      agree=lambda out: rq_agreement(out, gpu_idx, (best, gap, zg, zc)))
 
 
 def cpu_sas_baseline(model, B, n, items, tag, table=None, params=None):
@@ -526,24 +567,41 @@ def bench_sas_c5(a, world, rank, dev, time_it=True):
     torch.cuda.synchronize()
     setup_s = time.perf_counter() - t0
 
-    P = max(1, a.c5_pipeline)
-    cuts = [B * j // P for j in range(P + 1)]
-
     def gather_h():
         hl = model.last_hidden(lseqs)
         return D.all_gather_rows(hl, sizes=usizes) if dist.is_initialized() else hl
 
-    def step():
-        h = gather_h()
-        if P == 1:
-            return D.sharded_rank_topk(h, shard, lo, targets, k=10)
-        # the exchange of sub-batch j overlapped with the scoring of sub-batch j+1
-        return D.sharded_rank_topk_batches([h[x:y] for x, y in zip(cuts[:-1], cuts[1:])], shard, lo,
-                                           [targets[x:y] for x, y in zip(cuts[:-1], cuts[1:])], k=10)
+    def make_step(P):
+        cuts = [B * j // P for j in range(P + 1)]
+
+        def step():
+            h = gather_h()
+            if P == 1:
+                return D.sharded_rank_topk(h, shard, lo, targets, k=10)
+            # the exchange of sub-batch j overlapped with the scoring of sub-batch j+1
+            return D.sharded_rank_topk_batches([h[x:y] for x, y in zip(cuts[:-1], cuts[1:])], shard, lo,
+                                               [targets[x:y] for x, y in zip(cuts[:-1], cuts[1:])], k=10)
+        return step
 
     if not time_it:   # setup only (the shard leg alone): no C5 launches in its profile
         return None, model, gather_h(), targets, shard
     steps, warm = max(2, min(a.steps, 10)), 2
+    # the user sub-batches per step: --c5-pipeline, or (0, the default) chosen automatically at
+    # N > 1 -- the serial exchange (P = 1) and the pipelined one (P = C5_PIPELINE_DEFAULT) are each
+    # timed on a few steps, max over ranks (so every rank picks the same), and the faster runs: the
+    # pipelined form hides the collectives' latency but scores in smaller launches (c5_rank leg)
+    probe = None
+    if a.c5_pipeline > 0:
+        P = a.c5_pipeline
+    elif not dist.is_initialized():
+        P = 1
+    else:
+        probe = {}
+        for Pc in (1, C5_PIPELINE_DEFAULT):
+            pw, _ = timed(make_step(Pc), 3, 1, world)
+            probe[f"p{Pc}_ms_per_step"] = pw / 3 * 1e3
+        P = min((1, C5_PIPELINE_DEFAULT), key=lambda x: probe[f"p{x}_ms_per_step"])
+    step = make_step(P)
     wall, dev_ms = timed(step, steps, warm, world)
     r = step()
     check = result_checksum(r if P == 1 else tuple(torch.cat(t) for t in zip(*r)), world)
@@ -562,6 +620,7 @@ def bench_sas_c5(a, world, rank, dev, time_it=True):
                        "rows_per_rank": hi - lo,
                        "users_forwarded_per_rank": uhi - ulo, "table_rows_built_per_rank": (hi - lo) + model.item_num,
                        "setup_s": setup_s,
+                       "pipeline_sub_batches": P, "pipeline_probe": probe,
                        "parallelism": f"catalog-sharded x{world}: RCCL all-gather h + top-k, all-reduce counts"
                        + (f", {P} pipelined sub-batches" if P > 1 else "") if world > 1 else "single shard"},
             "result_checksum": check,
@@ -930,6 +989,125 @@ def bench_c5_shard(a, table, h, targets, dev, shards=8):
                      "frac_of_fp32_peak_step": flop / (dev_ms * 1e-3) / 1e12 / FP32_PEAK_TFLOPS}}
 
 
+def _one_rank_rccl(dev):
+    """A one-rank RCCL process group on ``dev`` for a leg that needs collectives at N = 1 (None if
+    one is already up -- then it is the caller's -- or RCCL fails to initialise; the error string
+    is returned instead)."""
+    if dist.is_initialized():
+        return None
+    try:
+        with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
+            sk.bind(("127.0.0.1", 0))
+            port = sk.getsockname()[1]
+        dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                                device_id=dev)
+        return True
+    except Exception as ex:   # reported in the leg, the rest of the bench continues
+        return f"{type(ex).__name__}: {ex}"
+
+
+def c5_rank_with_collectives(a, dev, W, B, d, k, lo, h, shard, t, own, loc, m0, forward, gathered):
+    """rank 0's C5 step at N = ``W`` WITH its collectives, timed on one GPU
+    through a one-rank RCCL group, every message at its N = W size (the all-gather of the [B, d]
+    hidden states, the all-reduces of B target logits and B counts, the all-gather of the
+    [W, B, 2k] packed candidates -- a one-rank all-gather moves its whole output):
+      * serial_ms: the exchange as dist.sharded_rank_topk runs it (bench.py's pre-r6 N > 1 step);
+      * overlapped_ms: as dist.sharded_rank_topk_batches runs it with P user sub-batches (the N > 1
+        default): the target all-reduce of sub-batch b+1 and the count all-reduce + candidate
+        all-gather of sub-batch b run on RCCL's stream under sub-batch b+1's scoring.
+    The messages' xGMI latency between ranks is not on one GPU: these are the collectives' issue,
+    launch and local-copy costs at the real sizes, not the 8-GPU wall time."""
+    from gr_amd import dist as D
+    pg = _one_rank_rccl(dev)
+    if isinstance(pg, str):
+        return {"collectives_error": pg}
+    if pg is None and (dist.get_backend() != "nccl" or dist.get_world_size() != 1):
+        return {"collectives_error": f"an existing {dist.get_backend()} group of {dist.get_world_size()} ranks "
+                                     "(the leg needs a one-rank RCCL group)"}
+    try:
+        hin = h.clone()
+        hout = torch.empty_like(h)
+        packed_in = gathered.clone().view(W * B, -1)
+
+        def serial():
+            forward()
+            dist.all_gather_into_tensor(hout, hin)
+            tl = torch.where(own, ops.score_pairs(hout, shard, loc, mask_col0=m0), torch.zeros_like(hout[:, 0]))
+            dist.all_reduce(tl)
+            v, i, c = ops.score_topk(hout, shard, k, lo, thresholds=tl, mask_col0=m0)
+            dist.all_reduce(c)
+            packed_in[:B].copy_(D._pack(v, i))
+            gout = torch.empty((W, B, 2 * k), dtype=torch.int64, device=dev)
+            dist.all_gather_into_tensor(gout.view(W * B, -1), packed_in)
+            ops.merge_topk_packed(gout, W, k, k)
+            return c + 1
+
+        def overlapped_fn(P):
+            cuts = [B * j // P for j in range(P + 1)]
+            subs = list(zip(cuts[:-1], cuts[1:]))
+            pins = [torch.stack([gathered[r, x:y] for r in range(W)]).contiguous() for x, y in subs]
+
+            def step():
+                forward()
+                dist.all_gather_into_tensor(hout, hin)
+
+                def tstart(j):
+                    x, y = subs[j]
+                    tl = torch.where(own[x:y], ops.score_pairs(hout[x:y], shard, loc[x:y], mask_col0=m0),
+                                     torch.zeros_like(hout[x:y, 0]))
+                    return tl, dist.all_reduce(tl, async_op=True)
+
+                def sstart(j, st):
+                    x, y = subs[j]
+                    tl, w = st
+                    w.wait()
+                    v, i, c = ops.score_topk(hout[x:y], shard, k, lo, thresholds=tl, mask_col0=m0)
+                    w1 = dist.all_reduce(c, async_op=True)
+                    pins[j][0].copy_(D._pack(v, i))
+                    gout = torch.empty_like(pins[j])
+                    w2 = dist.all_gather_into_tensor(gout.view(-1, 2 * k), pins[j].view(-1, 2 * k), async_op=True)
+                    return c, gout, w1, w2
+
+                def finish(sc):
+                    c, gout, w1, w2 = sc
+                    w1.wait()
+                    w2.wait()
+                    ops.merge_topk_packed(gout, W, k, k)
+                    return c + 1
+
+                out, prev = [], None
+                pend = tstart(0)
+                for j in range(len(subs)):
+                    cur = pend
+                    if j + 1 < len(subs):
+                        pend = tstart(j + 1)
+                    sc = sstart(j, cur)
+                    if prev is not None:
+                        out.append(finish(prev))
+                    prev = sc
+                out.append(finish(prev))
+                return out
+            return step
+
+        steps_ = max(2, min(a.steps, 10))
+        _, ser_ms = timed(serial, steps_, 2, 1)
+        res = {"serial_ms": ser_ms, "serial_value": B / (ser_ms * 1e-3)}
+        best = None
+        for P in (2, 4):
+            _, o_ms = timed(overlapped_fn(P), steps_, 2, 1)
+            res[f"overlapped_ms_p{P}"] = o_ms
+            if best is None or o_ms < best[1]:
+                best = (P, o_ms)
+        P_def = C5_PIPELINE_DEFAULT
+        res.update({"overlapped_ms": res.get(f"overlapped_ms_p{P_def}", best[1]), "overlapped_pipeline": P_def,
+                    "overlapped_value": B / (res.get(f"overlapped_ms_p{P_def}", best[1]) * 1e-3),
+                    "collectives_backend": "nccl (RCCL), one-rank group, N = %d message sizes" % W})
+        return res
+    finally:
+        if pg is True:
+            dist.destroy_process_group()
+
+
 def bench_c5_rank(a, dev):
     """the per-rank unit of the N-GPU C5 point (N = ``--c5-rank-world``, 8),
     timed on one GPU.  Rank 0's step of ``bench_sas_c5`` at world N: the transformer forward of its
@@ -989,21 +1167,30 @@ def bench_c5_rank(a, dev):
         merge()
         return c + 1
 
-    wall, dev_ms = timed(step, max(2, min(a.steps, 10)), 2, 1)
+    steps_ = max(2, min(a.steps, 10))
+    wall, dev_ms = timed(step, steps_, 2, 1)
     split = {"forward_ms": kernel_ms(forward), "score_pairs_ms": kernel_ms(pairs),
              "score_topk_ms": kernel_ms(topk), "merge_topk_ms": kernel_ms(merge)}
     fl_topk = 2 * d * (hi - lo) * B
     coll = B * d * 4 + B * 4 + B * 8 + B * k * 16
-    return {"metric": "seqs_scored/s", "value": B / (dev_ms * 1e-3), "unit": "seqs/s",
+    colls = c5_rank_with_collectives(a, dev, W, B, d, k, lo, h, shard, t, own, loc, m0, forward, gathered)
+    # the step bench.py's N > 1 run picks automatically: the faster of the serial and pipelined
+    # exchange (bench_sas_c5's probe)
+    val_ms = min(colls.get("serial_ms") or dev_ms, colls.get("overlapped_ms") or dev_ms)
+    return {"metric": "seqs_scored/s", "value": B / (val_ms * 1e-3), "unit": "seqs/s",
             "scaling": f"one rank of the N = {W} C5 point, projected to the whole job",
-            "ms_per_step": dev_ms, "wall_ms_per_step": wall / max(2, min(a.steps, 10)) * 1e3,
+            "ms_per_step": val_ms, "wall_ms_per_step": wall / steps_ * 1e3,
             "config": {"workload": f"c5_rank: rank 0 of N = {W}: forward of {B // W} users (d {d}, n {n}), "
                                    f"target logits + rank + top-{k} of all {B} users on rows [{lo}, {hi}) "
                                    f"of the {items + 1}-row catalog, merge of {W} x {k} candidates",
                        "users_per_step": B, "users_forwarded": B // W, "rows": hi - lo},
-            "projected_value_note": f"value = the {B} users of one N = {W} step / this rank's device time per "
-                                    f"step: the N-GPU throughput when the ~{coll / 1e6:.1f} MB of collectives "
-                                    f"per rank overlap (dist.sharded_rank_topk_batches) or cost nothing",
+            "projected_value_note": f"value = the {B} users of one N = {W} step / this rank's step time WITH "
+                                    f"its collectives: min(serial_ms, overlapped_ms), the exchange bench.py's "
+                                    f"N > 1 run selects by timing both (every collective at its N = {W} message "
+                                    f"size through a one-rank RCCL group; xGMI latency between ranks is not on "
+                                    f"one GPU). no_collectives_ms: the kernels alone",
+            "no_collectives_ms": dev_ms, "no_collectives_value": B / (dev_ms * 1e-3),
+            **colls,
             "collective_bytes_per_rank": coll,
             "split": split,
             "roofline": roofline("score_topk_kernel<128,10,", fl_topk, split["score_topk_ms"], "c5_rank",
@@ -1283,6 +1470,18 @@ def main():
                       ("rq_train_step", "rq_train_step_items_per_s"), ("sasrec_train", "sasrec_train_seqs_per_s")):
         if isinstance(line.get(leg), dict) and line[leg].get("value") is not None:
             summ[name] = line[leg]["value"]
+    # the bench host's CPU-path disagreement, characterised, where the tail shows it
+    for tag, obj in (("c2", line), ("c4", line.get("rq_c4") or {})):
+        ag = (obj.get("cpu_baseline") or {}).get("agreement") or {}
+        if "rows_ids_differ" in ag:
+            summ[f"{tag}_host_rows"] = ag["rows"]
+            summ[f"{tag}_host_rows_differ"] = ag["rows_ids_differ"]
+            if "rows_ids_differ_unflagged" in ag:
+                summ[f"{tag}_host_rows_differ_unflagged"] = ag["rows_ids_differ_unflagged"]
+                summ[f"{tag}_host_dz_over_z_max"] = ag["host_dz_over_z_max"]
+    for key in ("serial_ms", "overlapped_ms"):
+        if isinstance(line.get("c5_rank"), dict) and key in line["c5_rank"]:
+            summ[f"c5_rank_{key}"] = line["c5_rank"][key]
     line["summary"] = summ
     if rank == 0:
         print(json.dumps(line), flush=True)

@@ -305,6 +305,20 @@ int gr_sasrec_predict_ld_f32(const gr_sasrec_params* p, const int64_t* seqs, int
                              float* logits, int64_t ld, void* workspace, size_t workspace_bytes,
                              int32_t* err_flag, void* stream);
 
+/* One batch of SASRec/evaluate.py:26-32 in one call, the logits never written: ranks_out[b] =
+ * #{j : l[b, j] > l[b, targets[b]]} + 1 with l = predict(seqs) and column 0 taken as -1e9 when
+ * mask_col0 (evaluate.py:27) -- the forward's last hidden states, then the target logit and the
+ * strict count on the scoring kernel's exact fp32 chain (gr_score_pairs_f32 /
+ * gr_score_count_gt_ws_f32 below; bitwise the ranks of the materialised sequence).  d in {16, 32,
+ * 64, 128}.  workspace: gr_sasrec_rank_workspace_bytes; count_ws (optional, may be NULL): zero on
+ * entry and left zero, gr_score_count_workspace_bytes(B).  err_flag as gr_sasrec_forward_f32 (also
+ * set for a target outside [0, item_rows)). */
+size_t gr_sasrec_rank_workspace_bytes(const gr_sasrec_params* p, int64_t B, int32_t n);
+int gr_sasrec_rank_f32(const gr_sasrec_params* p, const int64_t* seqs, int64_t B, int32_t n,
+                       const int64_t* targets, int32_t mask_col0, int64_t* ranks_out, void* workspace,
+                       size_t workspace_bytes, void* count_ws, size_t count_ws_bytes, int32_t* err_flag,
+                       void* stream);
+
 /* SASRec training, the transformer part of one step (SASRec/train.py:131 `model.forward` in train
  * mode and the backward that `loss.backward()`, train.py:161-172, runs through model.py:49-96).
  * One workgroup per sequence; n <= 64, d <= 64 (d % num_heads == 0), mlp_layer <= 128, <= 8 blocks.
@@ -420,8 +434,10 @@ int gr_score_topk_f32(const float* h, int64_t B, int32_t d, const float* table, 
 /* ------------------------------------------------------------------------------------------ */
 /* Merge of catalog shards' top-k lists (the catalog-sharded counterpart of
  * SASRec/evaluate.py's per-user ranking): per row b, the k best of C candidates (cand_vals[b, c],
- * cand_ids[b, c]) by (value desc, id asc); ids < 0 are padding, emitted as (-inf, -1) when fewer
- * than k real candidates remain.  C <= 256.  ldv / ldi: row strides (elements). */
+ * cand_ids[b, c]) by (value desc, id asc) -- the id order compares all 64 bits, so any id in
+ * [0, INT64_MAX) orders exactly; ids < 0 and NaN values are padding, emitted as (-inf, -1) when
+ * fewer than k real candidates remain (the output always has k columns).  k >= 1, C <= 256.
+ * ldv / ldi: row strides (elements). */
 int gr_merge_topk_f32(const float* cand_vals, int64_t ldv, const int64_t* cand_ids, int64_t ldi,
                       int64_t B, int32_t C, int32_t k, float* vals_out, int64_t* ids_out, void* stream);
 /* The same merge straight from the all-gathered exchange buffer: packed [world][B][2 kk] int64, per

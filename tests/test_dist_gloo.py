@@ -112,6 +112,16 @@ def test_merge_topk_tie_and_padding_rules():
     assert i.tolist() == [[4, 9, 1, 5]] and v.tolist() == [[3.0, 3.0, 2.0, 1.0]]
     v, i = merge_topk(vals, ids, 5)
     assert i[0, 4].item() == -1
+    # fewer candidates than k: k columns, padded (-inf, -1) -- as the GPU kernel emits
+    v, i = merge_topk(vals, ids, 8)
+    assert v.shape == (1, 8) and i[0, 4:].tolist() == [-1] * 4 and (v[0, 4:] == float("-inf")).all()
+    # NaN is padding, never ranked first; wide ids order by all 64 bits
+    vals2 = torch.tensor([[float("nan"), 2.0, 2.0, 2.0]])
+    ids2 = torch.tensor([[0, 2 ** 33 + 1, 2 ** 33, 2 ** 32 - 1]])
+    v, i = merge_topk(vals2, ids2, 4)
+    assert i.tolist() == [[2 ** 32 - 1, 2 ** 33, 2 ** 33 + 1, -1]]
+    with pytest.raises(ValueError):
+        merge_topk(vals, ids, 0)
 
 
 def test_shard_range_partitions():

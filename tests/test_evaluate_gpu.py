@@ -34,6 +34,61 @@ def test_pairs_and_count_equal_materialised_logits(B, d, rows, dev):
     assert torch.equal(ops.score_count_gt(h, t, thr, mask_col0=False), (logits > thr[:, None]).sum(1))
 
 
+@pytest.mark.parametrize("d,n,items,B,heads", [(16, 20, 706, 128, 1), (16, 20, 706, 1, 1), (64, 50, 100_000, 128, 1),
+                                                (32, 30, 5000, 300, 2), (128, 200, 20000, 64, 1), (64, 50, 3000, 2049, 1)])
+def test_sasrec_rank_one_call_equals_materialised(d, n, items, B, heads, dev):
+    """gr_sasrec_rank_f32 (forward + target logit + strict count + 1 in one call)
+    against evaluate.py:27-32 run on the GPU's own predict() logits: equal ranks, every user; also
+    with column 0 unmasked, and the one-call path through evaluate.rank_batch."""
+    from gr_amd import ops, synth
+    from gr_amd.evaluate import rank_batch
+    p = synth.sasrec_params(d, n, 2, heads, 64, dev)
+    m = synth.sasrec_model(items, p, dev, seed=d + n)
+    seqs = synth.sequences(B, n, items, 31 + B, dev)
+    g = torch.Generator(device=dev).manual_seed(B)
+    tg = torch.randint(0, items + 1, (B,), generator=g, device=dev)
+    tg[0] = 0
+    logits = m.predict(seqs)
+    lg = logits.clone()
+    lg[:, 0] = -1e9
+    ref = (lg > lg.gather(1, tg[:, None])).sum(1) + 1
+    r1 = ops.sasrec_rank(m._binding(seqs), seqs, tg)
+    assert torch.equal(r1, ref)
+    assert torch.equal(rank_batch(m, seqs, tg), ref)
+    ref0 = (logits > logits.gather(1, tg[:, None])).sum(1) + 1
+    assert torch.equal(ops.sasrec_rank(m._binding(seqs), seqs, tg, mask_col0=False), ref0)
+
+
+def test_count_workspace_under_graph_capture(dev):
+    """score_count_gt's zero-on-entry workspace stays correct across a captured call,
+    its replays, eager calls on the same stream and a second capture."""
+    from gr_amd import ops
+    g = torch.Generator().manual_seed(77)
+    h = torch.randn(200, 64, generator=g).to(dev)
+    t = torch.randn(5000, 64, generator=g).to(dev)
+    thr = torch.randn(200, generator=g).to(dev)
+    ref = (ops.score(h, t) > thr[:, None]).sum(1)
+    s = torch.cuda.Stream(dev)
+    s.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(s):
+        graphs, outs = [], []
+        for _ in range(2):
+            gr = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(gr, stream=s):
+                outs.append(ops.score_count_gt(h, t, thr, mask_col0=False))
+            graphs.append(gr)
+            for _ in range(3):
+                gr.replay()
+                s.synchronize()
+                assert torch.equal(outs[-1], ref)
+                assert torch.equal(ops.score_count_gt(h, t, thr, mask_col0=False), ref)   # eager, same stream
+        graphs[0].replay()
+        s.synchronize()
+        assert torch.equal(outs[0], ref)
+    torch.cuda.current_stream(dev).wait_stream(s)
+    assert torch.equal(ops.score_count_gt(h, t, thr, mask_col0=False), ref)
+
+
 @pytest.mark.parametrize("name", ["sas_csv_c1", "sas_syn_c3", "sas_syn_c5"])
 def test_fused_rank_matches_fixture(name, dev):
     from gr_amd import SASRec, ops
@@ -71,9 +126,20 @@ def test_evaluate_harness_config1(dev, tmp_path):
     res, ranks = evaluate(params, dataset=ds)
     assert np.array_equal(ranks, out["ranks"][c1_fixture_perm(ds.user_ids)])
     assert res["Hit@10"] == meta["hr10"]
-    res2, ranks2 = evaluate(params, dataset=ds, materialize=True, save_csv=False)
+    assert list(res) == ["Hit@10", "NDCG@10"]            # evaluate.py:51: exactly these two keys
+    res2, ranks2, multi = evaluate(params, dataset=ds, materialize=True, save_csv=False, with_multi_k=True)
     assert np.array_equal(ranks2, ranks) and res2 == res
-    assert os.path.exists(params["params_path"])
+    assert sorted(multi) == sorted(f"{m}@{k}" for k in (2, 5, 10, 20) for m in ("Hit", "NDCG"))
+    # the CSV row of evaluate.py:57-89: task_id, the hyper-parameters present in params, then
+    # Hit@top_k / NDCG@top_k at 6 decimals -- no multi-k columns
+    import csv
+    with open(params["params_path"], newline="", encoding="utf-8") as f:
+        rows = list(csv.reader(f))
+    hp = [k for k in ["d", "num_blocks", "num_heads", "dropout", "lr", "batch_size", "epochs",
+                      "mlp_layer", "max_len", "top_k"] if k in params]
+    assert rows[0] == ["task_id"] + hp + ["Hit@10", "NDCG@10"]
+    assert len(rows) == 2
+    assert rows[1][0] == "c1" and rows[1][-2:] == [f"{res['Hit@10']:.6f}", f"{res['NDCG@10']:.6f}"]
 
 
 def test_train_evaluate_valid_mask(dev):

@@ -142,6 +142,33 @@ def test_merge_topk_kernels_equal_torch_merge(B, C, k, dev):
     assert torch.equal(v2.cpu(), ref_v) and torch.equal(i2.cpu(), ref_i)
 
 
+@pytest.mark.parametrize("B,C,k", [(64, 40, 10), (7, 5, 10), (3, 256, 16)])
+def test_merge_topk_wide_ids_nan_and_short_rows(B, C, k, dev):
+    """ids at and above 2^32 (equal values must still order by the full 64-bit id), NaN
+    entries (padding on both paths), fewer real candidates than k (k columns on both paths, padded
+    with (-inf, -1)), and the dispatch rules of dist.merge_topk (non-fp32 -> torch form, k < 1 ->
+    ValueError)."""
+    from gr_amd import dist as D, ops
+    g = torch.Generator().manual_seed(B * C + k)
+    vals = torch.randn(B, C, generator=g).round(decimals=1)          # many exact value ties
+    base = torch.tensor([2 ** 32 - 3, 2 ** 32 - 2, 2 ** 32 - 1, 2 ** 32, 2 ** 32 + 1, 2 ** 40, 5, 0])
+    ids = torch.cat([base, torch.randint(0, 2 ** 62, (C,), generator=g)])[:C].repeat(B, 1)
+    ids = torch.stack([r[torch.randperm(C, generator=g)] for r in ids])
+    vals[:, ::3] = 0.5                                                 # one value under many wide ids
+    vals[torch.rand(B, C, generator=g) < 0.1] = float("nan")
+    ids[torch.rand(B, C, generator=g) < 0.1] = -1
+    ref_v, ref_i = D.merge_topk(vals, ids, k)
+    assert ref_v.shape == (B, k)
+    v, i = ops.merge_topk(vals.to(dev), ids.to(dev), k)
+    assert torch.equal(v.cpu(), ref_v) and torch.equal(i.cpu(), ref_i)
+    v3, i3 = D.merge_topk(vals.to(dev), ids.to(dev), k)               # dispatch: the kernel
+    assert torch.equal(v3.cpu(), ref_v) and torch.equal(i3.cpu(), ref_i)
+    v4, i4 = D.merge_topk(vals.double().to(dev), ids.to(dev), k)      # fp64: the torch form
+    assert torch.equal(v4.float().cpu(), ref_v) and torch.equal(i4.cpu(), ref_i)
+    with pytest.raises(ValueError):
+        D.merge_topk(vals.to(dev), ids.to(dev), 0)
+
+
 def test_score_topk_rejects_bad_args(dev):
     from gr_amd import ops
     h = torch.randn(4, 64, device=dev)
@@ -192,16 +219,28 @@ def _gloo_gpu_worker(rank, world, port, data, out, backend="gloo"):
     cuts = [0, 40, 41, h.shape[0]]
     res = D.sharded_rank_topk_batches([h[a:b] for a, b in zip(cuts[:-1], cuts[1:])], table[lo:hi].contiguous(),
                                       lo, [targets[a:b] for a, b in zip(cuts[:-1], cuts[1:])], k)
+    # the hidden-state gather of the C5 step: every rank's user slice back into the whole batch,
+    # balanced (all_gather_into_tensor over RCCL, no padding) and uneven (padded, then sliced)
+    sizes = [D.shard_range(h.shape[0], r_, world)[1] - D.shard_range(h.shape[0], r_, world)[0] for r_ in range(world)]
+    ulo, uhi = D.shard_range(h.shape[0], rank, world)
+    hg = D.all_gather_rows(h[ulo:uhi], sizes=sizes)
+    usz = [3 + r_ for r_ in range(world)]
+    hu, wk = D.all_gather_rows(h[sum(usz[:rank]):sum(usz[:rank + 1])], sizes=usz, async_op=True)
+    if wk is not None:
+        wk.wait()
+    gathered_ok = torch.equal(hg, h) and torch.equal(hu, h[:sum(usz)])
     out[rank] = (rk.cpu(), v.cpu(), i.cpu(), torch.cat([r_[0] for r_ in res]).cpu(),
-                 torch.cat([r_[1] for r_ in res]).cpu(), torch.cat([r_[2] for r_ in res]).cpu())
+                 torch.cat([r_[1] for r_ in res]).cpu(), torch.cat([r_[2] for r_ in res]).cpu(), gathered_ok)
     dist.barrier()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,backend", [(2, "gloo"), (3, "gloo"), (1, "nccl")])
+@pytest.mark.parametrize("world,backend", [(2, "gloo"), (3, "gloo"), (8, "gloo"), (1, "nccl")])
 def test_catalog_sharded_fused_multi_rank(world, backend, dev):
     """The catalog-sharded exchange over real ranks (gloo, every rank on this GPU) with the fused
-    HIP kernels: every rank returns the full-catalog rank / top-k bit for bit.  The one-rank RCCL
+    HIP kernels: every rank returns the full-catalog rank / top-k bit for bit, both through the
+    serial exchange and the pipelined one (sharded_rank_topk_batches, bench.py's N > 1 default);
+    world 8 is the C5 node's shard count.  The one-rank RCCL
     case runs every collective of the exchange (a one-rank group still issues them) through the
     "nccl" backend and bench.py's ``device_id`` initialisation: RCCL needs one GPU per rank, so
     this box cannot hold more than one."""
@@ -229,7 +268,8 @@ def test_catalog_sharded_fused_multi_rank(world, backend, dev):
     out = mgr.dict()
     mp.spawn(_gloo_gpu_worker, args=(world, port, (h, table, tg, k), out, backend), nprocs=world, join=True)
     for r in range(world):
-        rk, v, i, pr, pv, pi = out[r]
+        rk, v, i, pr, pv, pi, gathered_ok = out[r]
+        assert gathered_ok
         assert torch.equal(rk, ref_rank)
         assert torch.equal(i, ref_i) and torch.equal(v, ref_v)
         assert torch.equal(pr, ref_rank) and torch.equal(pi, ref_i) and torch.equal(pv, ref_v)
