@@ -247,7 +247,7 @@ int gr_rq_small_launch(const float* x, int64_t n, const int32_t* dims, const flo
                        const float* packed, float* h1_scratch, float* h2_scratch, int32_t L, const int32_t* K,
                        const float* const* codebooks, int64_t* idx_out, float* z_out, hipStream_t st);
 int gr_sasrec_fused_launch(const gr_sasrec_params* p, const int64_t* seqs, int64_t B, int32_t n,
-                           float* out, int32_t last_only, int32_t* err, hipStream_t st);
+                           float* out, int32_t last_only, int32_t* err, hipStream_t st, int64_t* init_out = nullptr, int64_t init_val = 0);
 int gr_attn_mfma_launch(const float* qkv, float* out, int64_t B, int n, int H, int hd, float scale,
                         int last_tile_only, hipStream_t st);
 int gr_score_launch(const float* h, int64_t B, int32_t d, const float* table, int64_t rows,
@@ -270,13 +270,15 @@ int gr_rq_rows_launch(const float* x, int64_t n, int64_t call_m, const int64_t* 
                       hipStream_t st);
 // p[0 .. count) = value (32-bit words); a kernel, so it replays inside captured graphs (fill.hip).
 int gr_fill32_launch(void* p, uint32_t value, int64_t count, hipStream_t st);
-// rank_fused.hip: the target logits (gr_score_pairs_f32's kernel) and ranks_out[u] = 1 +
-// #{j : l'[u, j] > thresholds[u]} (gr_score_count_gt_ws_f32's kernels; count_ws zero on entry,
-// left zero, or null)
+// rank_fused.hip: the target logits (gr_score_pairs_f32's kernel), and ranks_out[u] = 1 +
+// #{j : l'[u, j] > l'[u, ids[u]]} in one count launch that computes the target logits itself
+// (gr_score_count_gt_ws_f32's kernels; count_ws zero on entry, left zero, or null; ranks_preinit:
+// ranks_out already holds 1, written by the forward kernel)
 int gr_score_pairs_launch(const float* h, int64_t B, int32_t d, const float* table, int64_t rows, const int64_t* ids,
                           int32_t mask_col0, float* out, int32_t* err_flag, hipStream_t st);
-int gr_score_rank_launch(const float* h, int64_t B, int32_t d, const float* table, int64_t rows, const float* thresholds,
-                         int32_t mask_col0, int64_t* ranks_out, void* count_ws, size_t count_ws_bytes, hipStream_t st);
+int gr_score_rank_launch(const float* h, int64_t B, int32_t d, const float* table, int64_t rows, const int64_t* ids,
+                         int32_t mask_col0, int64_t* ranks_out, void* count_ws, size_t count_ws_bytes,
+                         int32_t* err_flag, bool ranks_preinit, hipStream_t st);
 // p[0 .. count) = value (64-bit words)
 int gr_fill64_launch(void* p, uint64_t value, int64_t count, hipStream_t st);
 int gr_linear_exact_launch(const float* x, int64_t m, int32_t k, const float* w, int32_t n,

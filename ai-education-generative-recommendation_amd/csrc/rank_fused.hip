@@ -61,14 +61,20 @@ __global__ __launch_bounds__(64) void score_pairs_kernel(const float* __restrict
 // compare-and-count epilogue overlaps another's MFMAs (as in score_topk.hip).
 constexpr int RK_UT = 1;
 
-template <int D>
+// PAIRS: the thresholds are the users' target logits, computed here from the target ids with
+// score_pairs_kernel's MFMA tile (the same operands in the same order: bitwise its values) instead of
+// read from thr -- one launch less per rank call (gr_sasrec_rank_f32).  Every slice of a user block
+// recomputes its users' pairs (one short MFMA chain per 32 users).
+template <int D, bool PAIRS = false>
 __global__ __launch_bounds__(256, 2) void score_count_kernel(const float* __restrict__ h, int64_t B,
                                                             const float* __restrict__ table,
                                                             int64_t rows,
                                                             const float* __restrict__ thr,
                                                             int mask_col0,
                                                             unsigned long long* __restrict__ cnt_out,
-                                                            int ublocks, int slices, int copies) {
+                                                            int ublocks, int slices, int copies,
+                                                            const int64_t* __restrict__ ids = nullptr,
+                                                            int32_t* err = nullptr) {
   constexpr int NQ = D / 8;
   constexpr int P = D + 4;
   constexpr int LV = RK_CHUNK * D / 4 / 256;
@@ -95,10 +101,38 @@ __global__ __launch_bounds__(256, 2) void score_count_kernel(const float* __rest
       const f32x4 v = *reinterpret_cast<const f32x4*>(h + uc * D + sc_feat(gq, hh));
       hf[ut][gq] = u < B ? v : f32x4{0.f, 0.f, 0.f, 0.f};
     }
+    if (PAIRS) {   // score_pairs_kernel's tile: A = the users, B = their target rows; the diagonal
+      int64_t t = ids[uc];
+      if (t < 0 || t >= rows) {
+        if (u < B) set_err(err, 1);
+        t = 0;
+      }
+      f32x16 pacc;
 #pragma unroll
-    for (int v = 0; v < 16; ++v) {
-      const int64_t uu = u0 + ut * 32 + (v & 3) + 8 * (v >> 2) + 4 * hh;
-      th[ut][v] = thr[uu < B ? uu : B - 1];
+      for (int v = 0; v < 16; ++v) pacc[v] = 0.f;
+#pragma unroll
+      for (int gq = 0; gq < NQ; ++gq) {
+        const f32x4 a = *reinterpret_cast<const f32x4*>(h + uc * D + sc_feat(gq, hh));
+        const f32x4 bt = *reinterpret_cast<const f32x4*>(table + t * D + sc_feat(gq, hh));
+#pragma unroll
+        for (int s = 0; s < 4; ++s) pacc = mfma32(a[s], bt[s], pacc);
+      }
+      float dg = 0.f;   // user r's target logit, on the lane half with ((r >> 2) & 1) == hh
+#pragma unroll
+      for (int v = 0; v < 16; ++v)
+        if ((v & 3) + 8 * (v >> 2) + 4 * hh == r) dg = pacc[v];
+      if (mask_col0 && t == 0) dg = RK_MASK;
+#pragma unroll
+      for (int v = 0; v < 16; ++v) {   // register v's user (v&3) + 8(v>>2) + 4hh: from its diagonal lane
+        const int uu = (v & 3) + 8 * (v >> 2) + 4 * hh;
+        th[ut][v] = __shfl(dg, uu + 32 * ((uu >> 2) & 1));
+      }
+    } else {
+#pragma unroll
+      for (int v = 0; v < 16; ++v) {
+        const int64_t uu = u0 + ut * 32 + (v & 3) + 8 * (v >> 2) + 4 * hh;
+        th[ut][v] = thr[uu < B ? uu : B - 1];
+      }
     }
   }
   f32x4 st[LV];
@@ -249,14 +283,17 @@ int gr_score_pairs_launch(const float* h, int64_t B, int32_t d, const float* tab
 }
 
 // counts_out[u] = base + #{j : l'[u, j] > thresholds[u]} (base 1: the 1-based rank of evaluate.py:32)
+// pair_ids (rank mode): thresholds = the target logits of pair_ids, computed in the count kernel;
+// preinit: counts_out already holds base (written by the forward), so the direct form skips its fill.
 static int count_launch(const float* h, int64_t B, int32_t d, const float* table, int64_t rows,
                         const float* thresholds, int32_t mask_col0, int64_t* counts_out, void* workspace,
-                        size_t workspace_bytes, hipStream_t st, int64_t base = 0) {
+                        size_t workspace_bytes, hipStream_t st, int64_t base = 0,
+                        const int64_t* pair_ids = nullptr, int32_t* err = nullptr, bool preinit = false) {
   using namespace gr;
   clear_error();
   if (B < 0 || rows < 0) return fail(GR_ERR_ARG, "gr_score_count_gt_f32: bad shape");
   if (B == 0) return GR_OK;
-  if (!h || !table || !thresholds || !counts_out) return fail(GR_ERR_ARG, "gr_score_count_gt_f32: null pointer");
+  if (!h || !table || !(thresholds || pair_ids) || !counts_out) return fail(GR_ERR_ARG, "gr_score_count_gt_f32: null pointer");
   if (d != 16 && d != 32 && d != 64 && d != 128)
     return fail(GR_ERR_UNSUPPORTED, "gr_score_count_gt_f32: d must be 16, 32, 64 or 128");
   if (!aligned16(h) || !aligned16(table)) return fail(GR_ERR_ARG, "gr_score_count_gt_f32: h / table not 16-byte aligned");
@@ -272,7 +309,7 @@ static int count_launch(const float* h, int64_t B, int32_t d, const float* table
   const bool copies = workspace && workspace_bytes >= gr_score_count_workspace_bytes(B) && slices > 4 * RK_COPIES;
   unsigned long long* cnt = copies ? reinterpret_cast<unsigned long long*>(align_up(reinterpret_cast<uintptr_t>(workspace), 256))
                                    : reinterpret_cast<unsigned long long*>(counts_out);
-  if (!copies && gr_fill64_launch(counts_out, (uint64_t)base, B, st) != GR_OK)
+  if (!copies && !preinit && gr_fill64_launch(counts_out, (uint64_t)base, B, st) != GR_OK)
     return fail(GR_ERR_HIP, "gr_score_count_gt_f32: memset failed");
   if (rows == 0) {
     if (copies) return gr_fill64_launch(counts_out, (uint64_t)base, B, st) == GR_OK ? GR_OK : fail(GR_ERR_HIP, "memset");
@@ -280,12 +317,20 @@ static int count_launch(const float* h, int64_t B, int32_t d, const float* table
   }
   const int nc = copies ? RK_COPIES : 1;
   const dim3 g((unsigned)(ublocks * slices)), b(256);
+#define GR_CNT(DD)                                                                                           \
+  if (pair_ids)                                                                                              \
+    hipLaunchKernelGGL((score_count_kernel<DD, true>), g, b, 0, st, h, B, table, rows, thresholds, mask_col0, \
+                       cnt, (int)ublocks, (int)slices, nc, pair_ids, err);                                   \
+  else                                                                                                       \
+    hipLaunchKernelGGL((score_count_kernel<DD, false>), g, b, 0, st, h, B, table, rows, thresholds, mask_col0, \
+                       cnt, (int)ublocks, (int)slices, nc, nullptr, nullptr)
   switch (d) {
-    case 16: hipLaunchKernelGGL(score_count_kernel<16>, g, b, 0, st, h, B, table, rows, thresholds, mask_col0, cnt, (int)ublocks, (int)slices, nc); break;
-    case 32: hipLaunchKernelGGL(score_count_kernel<32>, g, b, 0, st, h, B, table, rows, thresholds, mask_col0, cnt, (int)ublocks, (int)slices, nc); break;
-    case 64: hipLaunchKernelGGL(score_count_kernel<64>, g, b, 0, st, h, B, table, rows, thresholds, mask_col0, cnt, (int)ublocks, (int)slices, nc); break;
-    default: hipLaunchKernelGGL(score_count_kernel<128>, g, b, 0, st, h, B, table, rows, thresholds, mask_col0, cnt, (int)ublocks, (int)slices, nc); break;
+    case 16: GR_CNT(16); break;
+    case 32: GR_CNT(32); break;
+    case 64: GR_CNT(64); break;
+    default: GR_CNT(128); break;
   }
+#undef GR_CNT
   int rc = check_launch("gr_score_count_gt_f32");
   if (rc || !copies) return rc;
   hipLaunchKernelGGL(count_copies_kernel, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, st, cnt, B, RK_COPIES,
@@ -312,7 +357,11 @@ extern "C" int gr_score_count_gt_ws_f32(const float* h, int64_t B, int32_t d, co
                       reinterpret_cast<hipStream_t>(stream));
 }
 
-int gr_score_rank_launch(const float* h, int64_t B, int32_t d, const float* table, int64_t rows, const float* thresholds,
-                         int32_t mask_col0, int64_t* ranks_out, void* count_ws, size_t count_ws_bytes, hipStream_t st) {
-  return count_launch(h, B, d, table, rows, thresholds, mask_col0, ranks_out, count_ws, count_ws_bytes, st, 1);
+int gr_score_rank_launch(const float* h, int64_t B, int32_t d, const float* table, int64_t rows, const int64_t* ids,
+                         int32_t mask_col0, int64_t* ranks_out, void* count_ws, size_t count_ws_bytes,
+                         int32_t* err_flag, bool ranks_preinit, hipStream_t st) {
+  if (rows < 1) return gr::fail(GR_ERR_ARG, "gr_sasrec_rank_f32: empty item table");
+  if (!ids) return gr::fail(GR_ERR_ARG, "gr_sasrec_rank_f32: null targets");
+  return count_launch(h, B, d, table, rows, nullptr, mask_col0, ranks_out, count_ws, count_ws_bytes, st, 1, ids,
+                      err_flag, ranks_preinit);
 }

@@ -565,8 +565,10 @@ extern "C" int gr_rank_f32(const float* logits, int64_t B, int64_t cols, int64_t
 }
 
 // evaluate.py:26-32 for one batch in ONE call: the last hidden states of the
-// forward, the target logits with the scoring chain (gr_score_pairs_f32's kernel) and the strict
-// count + 1 (gr_score_count_gt_ws_f32's kernels) -- the [B, item_rows] logits are never written.
+// forward (which also writes every rank's starting 1), then one count launch that forms each
+// target logit with the scoring chain (gr_score_pairs_f32's tile) and counts the strictly greater
+// logits (gr_score_count_gt_ws_f32's kernel) -- two launches (three when the count spreads over the
+// workspace copies), the [B, item_rows] logits never written.
 extern "C" size_t gr_sasrec_rank_workspace_bytes(const gr_sasrec_params* p, int64_t B, int32_t n) {
   if (!p || B < 0 || n < 1) return 0;
   return gr::ws_layout(p, B, n, nullptr, nullptr) + gr::align_up((size_t)B * 4, 256) + 256;
@@ -590,14 +592,15 @@ extern "C" int gr_sasrec_rank_f32(const gr_sasrec_params* p, const int64_t* seqs
   if (!seqs || !targets || !ranks_out) return fail(GR_ERR_ARG, "gr_sasrec_rank_f32: null seqs / targets / ranks");
   if (p->d != 16 && p->d != 32 && p->d != 64 && p->d != 128)
     return fail(GR_ERR_UNSUPPORTED, "gr_sasrec_rank_f32: d must be 16, 32, 64 or 128 (the fused rank's widths)");
-  float* pairs = reinterpret_cast<float*>(
-      align_up(reinterpret_cast<uintptr_t>(workspace) + ws_layout(p, B, n, nullptr, nullptr), 256));
   float* h;
+  bool preinit = false;
   if (fused_ok(p, n)) {
+    // the forward also writes ranks_out[b] = 1 (the count's start), so the count needs no fill
     h = w.h;
-    rc = gr_sasrec_fused_launch(p, seqs, B, n, h, 1, err_flag, st);
+    rc = gr_sasrec_fused_launch(p, seqs, B, n, h, 1, err_flag, st, ranks_out, 1);
     if (rc == GR_ERR_UNSUPPORTED)
       return fail(GR_ERR_UNSUPPORTED, "sasrec: fused path refused a shape fused_ok accepted");
+    preinit = true;
   } else {
     SasOut fin;
     h = w.o;   // [B, d] final hidden states (the attention-output buffer is free by then)
@@ -606,8 +609,7 @@ extern "C" int gr_sasrec_rank_f32(const gr_sasrec_params* p, const int64_t* seqs
       rc = run_layernorm(fin.x, B, p->d, fin.stride, fin.off, p->last_ln_w, p->last_ln_b, p->eps, h, st);
   }
   if (rc) return rc;
-  rc = gr_score_pairs_launch(h, B, p->d, p->item_emb, p->item_rows, targets, mask_col0, pairs, err_flag, st);
-  if (rc) return rc;
-  return gr_score_rank_launch(h, B, p->d, p->item_emb, p->item_rows, pairs, mask_col0, ranks_out, count_ws,
-                              count_ws_bytes, st);
+  // the target logits and the strict count in one launch (score_count_kernel<D, true>)
+  return gr_score_rank_launch(h, B, p->d, p->item_emb, p->item_rows, targets, mask_col0, ranks_out, count_ws,
+                              count_ws_bytes, err_flag, preinit, st);
 }

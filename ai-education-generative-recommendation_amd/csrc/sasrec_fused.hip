@@ -240,6 +240,8 @@ struct SasFusedArgs {
   int64_t item_rows;
   int nb, d, heads, mlp, n;
   float eps, scale;
+  int64_t* init_out;   // optional: init_out[b] = init_val for every sequence b (the rank call's
+  int64_t init_val;    // count starts from it: gr_sasrec_rank_f32 needs no separate fill launch)
 };
 
 namespace sf {
@@ -297,6 +299,7 @@ __global__ __launch_bounds__(256) void sasrec_fused_kernel(const SasFusedArgs a,
   const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
   const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (b >= B) return;   // whole wave; the kernel has no barrier
+  if (a.init_out && lane == 0) a.init_out[b] = a.init_val;
   const int d = a.d, n = a.n, mlp = a.mlp;
   const int hd = d / a.heads;
   // per wave: the parked X (DT*TT*16*64 floats) + 1024 floats of scratch for the last-position tail
@@ -792,6 +795,7 @@ __global__ __launch_bounds__(256, 2) void sasrec_fused2_kernel(const SasFusedArg
   const int64_t bs = (int64_t)blockIdx.x * 2 + sq;
   const bool live = bs < B;
   const int64_t b = live ? bs : B - 1;
+  if (a.init_out && live && w == 0 && lane == 0) a.init_out[b] = a.init_val;
   const int d = a.d, n = a.n, mlp = a.mlp;
   const int hd = d / a.heads;
   constexpr int KV = DT * 16 * 64;   // one 32-token tile of K^T (or V), lane-major
@@ -1049,7 +1053,8 @@ __global__ __launch_bounds__(256, 2) void sasrec_fused2_kernel(const SasFusedArg
 // Returns GR_ERR_UNSUPPORTED (error message untouched) for any other shape: the caller then runs
 // the layer-wise pipeline.
 int gr_sasrec_fused_launch(const gr_sasrec_params* p, const int64_t* seqs, int64_t B, int32_t n,
-                           float* out, int32_t last_only, int32_t* err, hipStream_t st) {
+                           float* out, int32_t last_only, int32_t* err, hipStream_t st, int64_t* init_out,
+                           int64_t init_val) {
   using namespace gr;
   const int d = p->d, H = p->n_heads;
   if (n > 64 || d > 64 || d % 8 || (d / H) % 8 || p->mlp > 128 || p->mlp % 4 ||
@@ -1074,6 +1079,8 @@ int gr_sasrec_fused_launch(const gr_sasrec_params* p, const int64_t* seqs, int64
   a.item_rows = p->item_rows; a.nb = p->n_blocks; a.d = d; a.heads = H; a.mlp = p->mlp; a.n = n;
   a.eps = p->eps;
   a.scale = (float)std::sqrt(1.0 / (double)(d / H));
+  a.init_out = init_out;
+  a.init_val = init_val;
   const int TT = n > 32 ? 2 : 1, DT = d > 32 ? 2 : 1, MT = (p->mlp + 31) / 32;
   const dim3 g((unsigned)((B + 3) / 4)), blk(256);
   const bool exact = d == 32 * DT && p->mlp == 32 * MT;

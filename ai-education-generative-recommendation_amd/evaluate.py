@@ -5,9 +5,11 @@ The reference computes ``logits = model.predict(x)`` ([B, N+1] fp32), masks colu
 gathers the target's logit and counts strictly greater logits (evaluate.py:26-32).  Here the rank
 of a batch is ONE C-ABI call, ``ops.sasrec_rank`` (``gr_sasrec_rank_f32``): the last hidden state
 from the fused SASRec forward, then the target logit and the strict-'>' count straight from the
-scoring kernel's MFMA tiles — the [B, N+1] logits are never written (``materialize=True`` runs the reference's predict + rank sequence instead; both
-give the same ranks, tests/test_evaluate_gpu.py).  HR@k / NDCG@k are then formed on the host in
-float64 exactly as the reference does (per-user Python list, ``np.mean``, evaluate.py:35-47).
+scoring kernel's MFMA tiles — the [B, N+1] logits are never written (``materialize=True`` runs
+the reference's predict + rank sequence instead; both give the same ranks,
+tests/test_evaluate_gpu.py).  HR@k / NDCG@k are then formed on the host in float64 with the
+reference's values (its per-user lists built as arrays, the same ``np.mean``, evaluate.py:35-47;
+bitwise the loop, tests/test_data.py).
 """
 import csv
 import os
@@ -33,33 +35,41 @@ def rank_batch(model, input_ids, targets, materialize=False):
     return ops.sasrec_rank(model._binding(input_ids), input_ids, targets, mask_col0=True)
 
 
+def _ndcg_terms(ranks, top_k):
+    """The per-user lists of evaluate.py:36-42 as float64 arrays, element for element: a hit is 1,
+    its NDCG term ``1 / np.log2(r + 1)`` evaluated exactly as the reference's loop evaluates it (numpy
+    int64 scalar r, scalar log2, true divide) -- once per distinct rank <= top_k, then gathered --
+    and every miss 0.  np.mean of these arrays is np.mean of the reference's lists (the lists are
+    converted to the same float64 arrays), without the per-user Python loop (~10 ms at 95,423 users)."""
+    r = np.asarray(ranks).astype(np.int64, copy=False).reshape(-1)
+    hit = r <= top_k
+    lut = np.zeros(max(int(top_k), 0) + 2, dtype=np.float64)
+    for v in np.unique(r[hit]):
+        lut[int(v)] = 1 / np.log2(np.int64(v) + 1)
+    ndcg = np.where(hit, lut[np.clip(r, 0, len(lut) - 1)], 0.0)
+    return hit.astype(np.float64), ndcg
+
+
 def hr_ndcg(ranks, top_k):
     """evaluate.py:35-47: per-user hit / 1/log2(r+1), averaged with np.mean (float64)."""
-    ht, ndcg = [], []
-    for r in np.asarray(ranks):
-        if r <= top_k:
-            ht.append(1)
-            ndcg.append(1 / np.log2(r + 1))
-        else:
-            ht.append(0)
-            ndcg.append(0)
+    ht, ndcg = _ndcg_terms(ranks, top_k)
+    if ht.size == 0:
+        return float(np.mean([])), float(np.mean([]))
     return float(np.mean(ht)), float(np.mean(ndcg))
 
 
 def multi_k(ranks, topk_list, targets=None):
     """SASRec/train.py:33-56: {k: HR@k}, {k: NDCG@k} for every k of ``topk_list``.  With ``targets``
     the users whose target is 0 are dropped first (train.py:42-45 ``valid_mask``)."""
-    hits = {k: [] for k in topk_list}
-    ndcgs = {k: [] for k in topk_list}
     ranks = np.asarray(ranks)
     if targets is not None:
         ranks = ranks[np.asarray(targets) != 0]
-    for r in ranks:
-        for k in topk_list:
-            hits[k].append(1 if r <= k else 0)
-            ndcgs[k].append(1 / np.log2(r + 1) if r <= k else 0)
-    return ({k: float(np.mean(v)) if v else 0.0 for k, v in hits.items()},
-            {k: float(np.mean(v)) if v else 0.0 for k, v in ndcgs.items()})
+    hk, nk = {}, {}
+    for k in topk_list:   # the per-user lists of train.py:46-50 as arrays (_ndcg_terms), same np.mean
+        ht, nd = _ndcg_terms(ranks, k)
+        hk[k] = float(np.mean(ht)) if ht.size else 0.0
+        nk[k] = float(np.mean(nd)) if nd.size else 0.0
+    return hk, nk
 
 
 @torch.no_grad()

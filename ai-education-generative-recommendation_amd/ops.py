@@ -149,6 +149,24 @@ def score_pairs(h, table, ids, mask_col0=True):
 
 
 _COUNT_WS = {}   # (device, stream) -> zeroed workspace of gr_score_count_gt_ws_f32 (left zero by every call)
+_SCRATCH = {}    # (device index, stream) -> scratch workspace of the short calls (no contents carried)
+SCRATCH_CACHE_BYTES = 16 << 20
+
+
+def scratch(nbytes, device):
+    """Caller-owned scratch for one call (``L.workspace``), reused across the calls of one stream when
+    small: a call's kernels finish with it before any later call on the same stream starts (stream
+    order), and the library never keeps pointers.  Saves an allocation per call at the reference's
+    batch sizes (get_indices(x[64]), rank of 128 users).  Under graph capture: a fresh allocation
+    (the graph's pool owns it)."""
+    if nbytes > SCRATCH_CACHE_BYTES or torch.cuda.is_current_stream_capturing():
+        return L.workspace(nbytes, device)
+    key = (device.index, L.stream_of(device))
+    ws = _SCRATCH.get(key)
+    if ws is None or ws.numel() < nbytes:
+        ws = L.workspace(max(nbytes, 1 << 16), device)
+        _SCRATCH[key] = ws
+    return ws
 
 
 def _count_workspace(device, nbytes):
@@ -295,6 +313,7 @@ class RqBinding:
             if w.shape[1] != self.dims[i]:
                 raise RuntimeError(f"rq_encode: Linear {i} expects {w.shape[1]} inputs, got {self.dims[i]}")
         self.Ks = [c.shape[0] for c in self.cbs]
+        self.n_linear = len(self.ws)
         self.dims_c, self.ks_c = L.i32_array(self.dims), L.i32_array(self.Ks)
         self.w_arr, self.b_arr, self.c_arr = L.ptr_array(self.ws), L.ptr_array(self.bs), L.ptr_array(self.cbs)
         self.device = self.ws[0].device
@@ -341,14 +360,14 @@ class RqBinding:
                 L.check(L.lib().gr_rq_encoder_pack_f32(len(self.ws), self.dims_c, self.w_arr, L.ptr(self.packed),
                                                        L.stream_of(self.device)), "gr_rq_encoder_pack_f32")
             self._pack_key = key
-        st = torch.cuda.current_stream(self.device)
+        st = L.stream_of(self.device)
         streams = getattr(self, "_streams", None)
         if streams is None:
             streams = self._streams = set()
-        if st.cuda_stream not in streams:   # an encode on another stream than the allocating one
-            self.packed.record_stream(st)
-            streams.add(st.cuda_stream)
-        return L.ptr(self.packed)
+        if st not in streams:   # an encode on another stream than the allocating one
+            self.packed.record_stream(torch.cuda.current_stream(self.device))
+            streams.add(st)
+        return self.packed.data_ptr()
 
     def workspace_bytes(self, n):
         nb = self._ws_bytes.get(n)
@@ -408,21 +427,21 @@ def rq_encode(x, weights=None, biases=None, codebooks=None, with_gap=False, with
     x2 = L.as_f32(x)
     if x2.dim() != 2 or x2.shape[1] != b.in_dim:
         raise RuntimeError(f"rq_encode: expected [n, {b.in_dim}] inputs, got {tuple(x2.shape)}")
-    if x2.device != b.device:
-        raise RuntimeError(f"rq_encode: inputs on {x2.device}, parameters on {b.device}")
-    n = x2.shape[0]
     dev = x2.device
+    if dev != b.device:
+        raise RuntimeError(f"rq_encode: inputs on {dev}, parameters on {b.device}")
+    n = x2.shape[0]
     nbytes = b.workspace_bytes(n)
-    wsp = L.workspace(nbytes, dev)
+    wsp = scratch(nbytes, dev)
     nl = len(b.cbs)
     idx = torch.empty((n, nl), dtype=torch.int64, device=dev)
     gap = torch.empty((n, nl), dtype=torch.float32, device=dev) if with_gap else None
     best = torch.empty((n, nl), dtype=torch.float32, device=dev) if with_gap else None
     z = torch.empty((n, b.dims[-1]), dtype=torch.float32, device=dev) if with_z else None
     with L.on(dev):
-        L.check(L.lib().gr_rq_encode_packed_f32(L.ptr(x2), n, len(b.ws), b.dims_c, b.w_arr, b.b_arr,
-                                                b.packed_ptr(), nl, b.ks_c, b.c_arr, L.ptr(idx), L.ptr(best),
-                                                L.ptr(gap), L.ptr(z), L.ptr(wsp), nbytes, L.stream_of(dev)),
+        L.check(L.lib().gr_rq_encode_packed_f32(x2.data_ptr(), n, b.n_linear, b.dims_c, b.w_arr, b.b_arr,
+                                                b.packed_ptr(), nl, b.ks_c, b.c_arr, idx.data_ptr(), L.ptr(best),
+                                                L.ptr(gap), L.ptr(z), wsp.data_ptr(), nbytes, L.stream_of(dev)),
                 "gr_rq_encode_packed_f32")
     out = [idx]
     if with_gap:
@@ -700,7 +719,7 @@ def sasrec_forward(binding, log_seqs, last_only=False):
     d = binding.p.d
     out = torch.empty((B, d) if last_only else (B, n, d), dtype=torch.float32, device=dev)
     nbytes = binding.workspace_bytes(B, n)
-    wsp = L.workspace(nbytes, dev)
+    wsp = scratch(nbytes, dev)
     err = err_flag(dev)
     with L.on(dev):
         L.check(L.lib().gr_sasrec_forward_f32(binding.p_ref, L.ptr(ids), B, n, L.ptr(out),
@@ -726,7 +745,7 @@ def sasrec_rank(binding, log_seqs, targets, mask_col0=True):
         raise RuntimeError(f"sasrec_rank: {t.shape[0]} targets for {B} sequences")
     dev = ids.device
     nbytes, cnb = binding.rank_workspace_bytes(B, n)
-    wsp = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    wsp = scratch(nbytes, dev)
     out = torch.empty(B, dtype=torch.int64, device=dev)
     err = err_flag(dev)
     cws, key = _count_workspace(dev, cnb)
@@ -771,7 +790,7 @@ def sasrec_predict(binding, log_seqs, out=None):
         raise ValueError("sasrec_predict: out must be fp32 [B, item_rows] on the ids' device with unit column stride")
     ld = logits.stride(0) if B > 1 else rows
     nbytes = binding.workspace_bytes(B, n)
-    wsp = L.workspace(nbytes, dev)
+    wsp = scratch(nbytes, dev)
     err = err_flag(dev)
     with L.on(dev):
         L.check(L.lib().gr_sasrec_predict_ld_f32(binding.p_ref, L.ptr(ids), B, n,

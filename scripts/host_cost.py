@@ -46,6 +46,14 @@ def main():
     out["rq_encode_binding"] = med_us(lambda: ops.rq_encode(x, binding=b), a.reps)
     out["encode_binding_lookup"] = med_us(lambda: rq.encode_binding(), a.reps)
     out["packed_ptr"] = med_us(lambda: b.packed_ptr(), a.reps)
+    # the C call alone, every argument prebuilt (its host cost = validation + the HIP launches)
+    nb = b.workspace_bytes(64)
+    wsp = torch.empty(nb, dtype=torch.uint8, device=dev)
+    idx = torch.empty((64, 3), dtype=torch.int64, device=dev)
+    args = (x.data_ptr(), 64, len(b.ws), b.dims_c, b.w_arr, b.b_arr, b.packed_ptr(), 3, b.ks_c, b.c_arr,
+            idx.data_ptr(), None, None, None, wsp.data_ptr(), nb, L.stream_of(dev))
+    fn = L.lib().gr_rq_encode_packed_f32
+    out["c_call_rq_encode_packed"] = med_us(lambda: fn(*args), a.reps)
     items, n, d = 706, 20, 16
     p = synth.sasrec_params(d, n, 2, 1, 64, dev)
     sm = synth.sasrec_model(items, p, dev, seed=16)

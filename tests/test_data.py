@@ -111,6 +111,28 @@ def test_metrics_match_reference_tail(tmp_path):
     assert rows[1][3] == f"{hit:.6f}"
 
 
+def test_metric_arrays_equal_reference_loops():
+    """hr_ndcg / multi_k build the reference's per-user lists as arrays (one scalar log2 per distinct
+    rank): bitwise the loops of evaluate.py:36-47 and train.py:46-53 on many rank vectors."""
+    rng = np.random.default_rng(5)
+    for n, hi in [(1, 3), (7, 12), (1000, 30), (95_423, 800), (4096, 11), (50_000, 100_000)]:
+        ranks = rng.integers(1, hi, n)
+        for top_k in (1, 2, 5, 10, 20):
+            ht, nd = [], []
+            for r in ranks:
+                if r <= top_k:
+                    ht.append(1)
+                    nd.append(1 / np.log2(r + 1))
+                else:
+                    ht.append(0)
+                    nd.append(0)
+            assert hr_ndcg(ranks, top_k) == (float(np.mean(ht)), float(np.mean(nd)))
+        hk, nk = multi_k(ranks, [2, 5, 10, 20])
+        for k in (2, 5, 10, 20):
+            assert nk[k] == float(np.mean([1 / np.log2(r + 1) if r <= k else 0 for r in ranks]))
+            assert hk[k] == float(np.mean([1 if r <= k else 0 for r in ranks]))
+
+
 def test_multi_k_drops_target_zero_users():
     """train.py:42-45: users with target 0 are removed before ranking (valid_mask)."""
     ranks = np.array([1, 3, 10, 11, 2], np.int64)

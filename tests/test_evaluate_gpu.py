@@ -57,6 +57,13 @@ def test_sasrec_rank_one_call_equals_materialised(d, n, items, B, heads, dev):
     assert torch.equal(rank_batch(m, seqs, tg), ref)
     ref0 = (logits > logits.gather(1, tg[:, None])).sum(1) + 1
     assert torch.equal(ops.sasrec_rank(m._binding(seqs), seqs, tg, mask_col0=False), ref0)
+    # a target outside the table raises IndexError at the next check (evaluate.py:30's gather would)
+    ops.check_errors(dev)
+    bad = tg.clone()
+    bad[-1] = items + 5
+    ops.sasrec_rank(m._binding(seqs), seqs, bad)
+    with pytest.raises(IndexError):
+        ops.check_errors(dev)
 
 
 def test_count_workspace_under_graph_capture(dev):
