@@ -203,6 +203,73 @@ def _sharded_rank_topk_fused(h, table_shard, row_offset, targets, k, group, mask
     return _exchange(cnt, v, i, k, group, world)
 
 
+class _RankStages:
+    """The three stages of one batch's catalog-sharded rank + top-k with every collective issued
+    ``async_op=True`` (RCCL runs it on its own stream after the work it depends on; the host never
+    blocks): ``targets_start`` (the owner's target logits -> all-reduce), ``score_start`` (local
+    strict counts + top-k -> count all-reduce + candidate all-gather), ``finish`` (wait, merge).
+    Shared by ``sharded_rank_topk_batches`` and ``ShardedRankPipeline``."""
+
+    def __init__(self, table_shard, row_offset, k, group, mask_row0, scorer, counter, topk_fn, h0):
+        self.table, self.lo, self.k, self.group = table_shard, row_offset, k, group
+        self.world = _world(group)
+        self.rows = rows = table_shard.shape[0]
+        self.fused = (scorer is None and counter is None and topk_fn is None and h0.is_cuda and rows > 0
+                      and 1 <= k <= 16 and h0.shape[1] in (16, 32, 64, 128))
+        if not self.fused:
+            s_fn, c_fn, t_fn = _default_ops()
+            scorer, counter, topk_fn = scorer or s_fn, counter or c_fn, topk_fn or t_fn
+        self.scorer, self.counter, self.topk_fn = scorer, counter, topk_fn
+        self.m0 = bool(mask_row0 and row_offset == 0)
+        self.kk = min(k, rows)
+
+    def targets_start(self, h, t):
+        t = t.reshape(-1).to(torch.int64)
+        rows, lo = self.rows, self.lo
+        own = (t >= lo) & (t < lo + rows)
+        local = torch.where(own, t - lo, torch.zeros_like(t))
+        logits = None
+        if self.fused:
+            from . import ops
+            tl = ops.score_pairs(h, self.table, local, mask_col0=self.m0)
+        else:
+            logits = self.scorer(h, self.table)
+            if self.m0 and rows > 0:
+                logits[:, 0] = -1e9                                  # evaluate.py:27
+            tl = (logits.gather(1, local.unsqueeze(1)).squeeze(1) if rows > 0   # an empty shard owns
+                  else torch.zeros(t.shape, dtype=logits.dtype, device=logits.device))   # no target
+        ts = torch.where(own, tl, torch.zeros(t.shape, dtype=tl.dtype, device=tl.device))
+        return ts, logits, dist.all_reduce(ts, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+
+    def score_start(self, h, st):
+        ts, logits, work = st
+        work.wait()
+        k, kk = self.k, self.kk
+        if self.fused:
+            from . import ops
+            v, i, cnt = ops.score_topk(h, self.table, kk, self.lo, thresholds=ts, mask_col0=self.m0)
+        elif kk > 0:
+            cnt = self.counter(logits, ts)
+            v, i = self.topk_fn(logits, kk, self.lo)
+        else:   # empty shard (a catalog smaller than the world): no count, no candidate
+            cnt = torch.zeros(logits.shape[0], dtype=torch.int64, device=logits.device)
+            v = torch.empty((logits.shape[0], 0), dtype=logits.dtype, device=logits.device)
+            i = torch.empty((logits.shape[0], 0), dtype=torch.int64, device=logits.device)
+        if kk < k:
+            v = torch.cat([v, torch.full((v.shape[0], k - kk), float("-inf"), dtype=v.dtype, device=v.device)], 1)
+            i = torch.cat([i, torch.full((i.shape[0], k - kk), -1, dtype=i.dtype, device=i.device)], 1)
+        w1 = dist.all_reduce(cnt, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+        gathered, w2 = _gather_packed(_pack(v, i), self.world, self.group, async_op=True)
+        return cnt, gathered, w1, w2
+
+    def finish(self, sc):
+        cnt, gathered, w1, w2 = sc
+        w1.wait()
+        w2.wait()
+        v, i = _merge_gathered(gathered, self.world, self.k, self.k)
+        return cnt + 1, v, i
+
+
 @torch.no_grad()
 def sharded_rank_topk_batches(hs, table_shard, row_offset, targets, k=10, group=None, mask_row0=True,
                               scorer=None, counter=None, topk_fn=None):
@@ -217,71 +284,61 @@ def sharded_rank_topk_batches(hs, table_shard, row_offset, targets, k=10, group=
     if not world or len(hs) <= 1:
         return [sharded_rank_topk(h, table_shard, row_offset, t, k, group, mask_row0, scorer, counter, topk_fn)
                 for h, t in zip(hs, targets)]
-    rows = table_shard.shape[0]
-    fused = (scorer is None and counter is None and topk_fn is None and hs[0].is_cuda and rows > 0
-             and 1 <= k <= 16 and hs[0].shape[1] in (16, 32, 64, 128))
-    if not fused:
-        s_fn, c_fn, t_fn = _default_ops()
-        scorer, counter, topk_fn = scorer or s_fn, counter or c_fn, topk_fn or t_fn
-    m0 = bool(mask_row0 and row_offset == 0)
-    kk = min(k, rows)
-
-    def targets_start(b):   # the owner's target logits -> all-reduce (async)
-        h, t = hs[b], targets[b].reshape(-1).to(torch.int64)
-        own = (t >= row_offset) & (t < row_offset + rows)
-        local = torch.where(own, t - row_offset, torch.zeros_like(t))
-        logits = None
-        if fused:
-            from . import ops
-            tl = ops.score_pairs(h, table_shard, local, mask_col0=m0)
-        else:
-            logits = scorer(h, table_shard)
-            if m0 and rows > 0:
-                logits[:, 0] = -1e9                                  # evaluate.py:27
-            tl = (logits.gather(1, local.unsqueeze(1)).squeeze(1) if rows > 0   # an empty shard owns
-                  else torch.zeros(t.shape, dtype=logits.dtype, device=logits.device))   # no target
-        ts = torch.where(own, tl, torch.zeros(t.shape, dtype=tl.dtype, device=tl.device))
-        return ts, logits, dist.all_reduce(ts, op=dist.ReduceOp.SUM, group=group, async_op=True)
-
-    def score_start(b, st):   # local counts + top-k, then their exchange (async)
-        ts, logits, work = st
-        work.wait()
-        if fused:
-            from . import ops
-            v, i, cnt = ops.score_topk(hs[b], table_shard, kk, row_offset, thresholds=ts, mask_col0=m0)
-        elif kk > 0:
-            cnt = counter(logits, ts)
-            v, i = topk_fn(logits, kk, row_offset)
-        else:   # empty shard (a catalog smaller than the world): no count, no candidate
-            cnt = torch.zeros(logits.shape[0], dtype=torch.int64, device=logits.device)
-            v = torch.empty((logits.shape[0], 0), dtype=logits.dtype, device=logits.device)
-            i = torch.empty((logits.shape[0], 0), dtype=torch.int64, device=logits.device)
-        if kk < k:
-            v = torch.cat([v, torch.full((v.shape[0], k - kk), float("-inf"), dtype=v.dtype, device=v.device)], 1)
-            i = torch.cat([i, torch.full((i.shape[0], k - kk), -1, dtype=i.dtype, device=i.device)], 1)
-        w1 = dist.all_reduce(cnt, op=dist.ReduceOp.SUM, group=group, async_op=True)
-        gathered, w2 = _gather_packed(_pack(v, i), world, group, async_op=True)
-        return cnt, gathered, w1, w2
-
-    def finish(sc):
-        cnt, gathered, w1, w2 = sc
-        w1.wait()
-        w2.wait()
-        v, i = _merge_gathered(gathered, world, k, k)
-        return cnt + 1, v, i
-
+    S = _RankStages(table_shard, row_offset, k, group, mask_row0, scorer, counter, topk_fn, hs[0])
     out, prev = [], None
-    pend = targets_start(0)
+    pend = S.targets_start(hs[0], targets[0])
     for b in range(len(hs)):
         cur = pend
         if b + 1 < len(hs):
-            pend = targets_start(b + 1)
-        sc = score_start(b, cur)
+            pend = S.targets_start(hs[b + 1], targets[b + 1])
+        sc = S.score_start(hs[b], cur)
         if prev is not None:
-            out.append(finish(prev))
+            out.append(S.finish(prev))
         prev = sc
-    out.append(finish(prev))
+    out.append(S.finish(prev))
     return out
+
+
+class ShardedRankPipeline:
+    """Cross-step form of ``sharded_rank_topk`` for a stream of batches (the
+    exchange overlapped with the NEXT batch's work, without cutting a batch into smaller scoring
+    launches).  ``submit(h, targets)`` runs the batch's target-logit all-reduce and its local
+    scoring, issues its count all-reduce + candidate all-gather asynchronously and returns the
+    PREVIOUS batch's result (None for the first), whose merge it enqueues after this batch's
+    scoring; ``flush()`` returns the last batch's result.  Whatever the caller runs between two
+    submits -- the next batch's transformer forward and hidden-state all-gather in bench.py's C5
+    step -- runs under the collectives (RCCL's stream is FIFO: the next all-gather of h queues
+    behind them, the compute stream does not).  Results are ``sharded_rank_topk``'s, bitwise.
+    Without a process group there is nothing to overlap: ``submit`` returns the batch's own result
+    once it is flushed, like any other rank."""
+
+    def __init__(self, table_shard, row_offset, k=10, group=None, mask_row0=True,
+                 scorer=None, counter=None, topk_fn=None):
+        self.args = (table_shard, row_offset, k, group, mask_row0, scorer, counter, topk_fn)
+        self.stages, self.prev = None, None
+
+    @torch.no_grad()
+    def submit(self, h, targets):
+        table_shard, row_offset, k, group, mask_row0, scorer, counter, topk_fn = self.args
+        if not _world(group):   # no exchange: the result is final at once, held for one submit
+            cur = sharded_rank_topk(h, table_shard, row_offset, targets, k, group, mask_row0,
+                                    scorer, counter, topk_fn)
+            out, self.prev = self.prev, ("done", cur)
+            return None if out is None else out[1]
+        if self.stages is None:
+            self.stages = _RankStages(table_shard, row_offset, k, group, mask_row0, scorer, counter, topk_fn, h)
+        S = self.stages
+        sc = S.score_start(h, S.targets_start(h, targets))
+        out = self.flush()
+        self.prev = ("pending", sc)
+        return out
+
+    @torch.no_grad()
+    def flush(self):
+        prev, self.prev = self.prev, None
+        if prev is None:
+            return None
+        return prev[1] if prev[0] == "done" else self.stages.finish(prev[1])
 
 
 def hr_ndcg(ranks, top_k=10):

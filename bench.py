@@ -118,9 +118,11 @@ def sas_exec_flop_per_user(d, n, items, mlp=64, blocks=2, causal=True, tail_h=Fa
 # rehearsal mode); "cpu" for the launcher self-test (GR_BENCH_DEVICE=cpu, no GPU needed)
 COLL_DEV = "cuda"
 
-# C5 at N > 1: the pipelined exchange's user sub-batches per step (dist.sharded_rank_topk_batches),
+# C5 at N > 1: the split exchange's user sub-batches per step (dist.sharded_rank_topk_batches),
 # from the c5_rank leg's overlapped_ms_p2 / _p4 figures (P = 4 scores in launches too small)
 C5_PIPELINE_DEFAULT = 2
+# the exchange forms bench_sas_c5's auto mode times at N > 1 (make_step)
+C5_EXCHANGES = ("serial", "split", "xstep")
 
 
 def per_rank(x, world):
@@ -169,10 +171,12 @@ def parse():
     ap.add_argument("--c5-rank-world", type=int, default=8,
                     help="c5_rank leg: the world size whose per-rank step it times on one GPU")
     ap.add_argument("--c5-items", type=int, default=1_000_000)
-    ap.add_argument("--c5-pipeline", type=int, default=0,
-                    help="C5 user sub-batches per step whose exchange overlaps the next one's scoring "
-                         f"(0 = auto: 1 at N = 1, where there is no exchange; at N > 1 the faster of 1 and "
-                         f"{C5_PIPELINE_DEFAULT}, timed on a few steps)")
+    ap.add_argument("--c5-exchange", default="auto", choices=("auto",) + C5_EXCHANGES,
+                    help="C5 exchange form at N > 1: serial; split (--c5-pipeline user sub-batches, each "
+                         "one's exchange under the next one's scoring); xstep (the exchange under the next "
+                         "step's forward); auto: the fastest, timed on a few steps (serial at N = 1)")
+    ap.add_argument("--c5-pipeline", type=int, default=C5_PIPELINE_DEFAULT,
+                    help="user sub-batches per step of the split exchange")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--train-batch", type=int, default=128, help="sas_train leg: users per rank per step")
     ap.add_argument("--legs", default="", help="comma list of legs to run (default: " + ",".join(LEGS) + "; also " + ",".join(OPT_LEGS) + ")")
@@ -217,19 +221,26 @@ def spinup(fn, seconds=None, world=1):
             torch.cuda.synchronize()
 
 
-def timed(fn, steps, warmup, world):
+def timed(fn, steps, warmup, world, tail=None):
     """Spin-up, W untimed warmup steps, then exactly K steps between barrier+synchronize; returns
     (max-over-ranks wall seconds, mean device ms per step from two HIP events on the launch stream
-    around the K steps -- no markers between steps, which would themselves open dispatch gaps)."""
+    around the K steps -- no markers between steps, which would themselves open dispatch gaps).
+    ``tail``: a step that leaves work for the next one (the cross-step C5 exchange) is completed by
+    it -- once before the timed region (the warmup's leftover) and once inside it, after the K
+    steps, so the region holds exactly K steps' work."""
     spinup(fn, world=world)
     for _ in range(warmup):
         fn()
+    if tail is not None:
+        tail()
     sync_all(world)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
     e0.record()
     for _ in range(steps):
         fn()
+    if tail is not None:
+        tail()
     e1.record()
     sync_all(world)
     wall = time.perf_counter() - t0
@@ -571,40 +582,53 @@ def bench_sas_c5(a, world, rank, dev, time_it=True):
         hl = model.last_hidden(lseqs)
         return D.all_gather_rows(hl, sizes=usizes) if dist.is_initialized() else hl
 
-    def make_step(P):
+    pipe = D.ShardedRankPipeline(shard, lo, k=10)
+
+    def make_step(mode):
+        """(step, tail) of one exchange form: "serial" (dist.sharded_rank_topk), "split" (the step's
+        users cut into --c5-pipeline sub-batches, each one's exchange under the next one's scoring:
+        dist.sharded_rank_topk_batches), "xstep" (the whole batch scored at once, its exchange under
+        the NEXT step's forward + all-gather: dist.ShardedRankPipeline)."""
+        P = max(2, a.c5_pipeline)
         cuts = [B * j // P for j in range(P + 1)]
 
-        def step():
+        def serial():
+            return D.sharded_rank_topk(gather_h(), shard, lo, targets, k=10)
+
+        def split():
             h = gather_h()
-            if P == 1:
-                return D.sharded_rank_topk(h, shard, lo, targets, k=10)
-            # the exchange of sub-batch j overlapped with the scoring of sub-batch j+1
-            return D.sharded_rank_topk_batches([h[x:y] for x, y in zip(cuts[:-1], cuts[1:])], shard, lo,
-                                               [targets[x:y] for x, y in zip(cuts[:-1], cuts[1:])], k=10)
-        return step
+            r = D.sharded_rank_topk_batches([h[x:y] for x, y in zip(cuts[:-1], cuts[1:])], shard, lo,
+                                            [targets[x:y] for x, y in zip(cuts[:-1], cuts[1:])], k=10)
+            return tuple(torch.cat(t) for t in zip(*r))
+
+        def xstep():
+            return pipe.submit(gather_h(), targets)
+        return {"serial": (serial, None), "split": (split, None), "xstep": (xstep, pipe.flush)}[mode]
 
     if not time_it:   # setup only (the shard leg alone): no C5 launches in its profile
         return None, model, gather_h(), targets, shard
     steps, warm = max(2, min(a.steps, 10)), 2
-    # the user sub-batches per step: --c5-pipeline, or (0, the default) chosen automatically at
-    # N > 1 -- the serial exchange (P = 1) and the pipelined one (P = C5_PIPELINE_DEFAULT) are each
-    # timed on a few steps, max over ranks (so every rank picks the same), and the faster runs: the
-    # pipelined form hides the collectives' latency but scores in smaller launches (c5_rank leg)
+    # the exchange form: --c5-exchange, or ("auto", the default) at N > 1 each form is timed on a
+    # few steps, max over ranks (so every rank picks the same), and the fastest runs; at N = 1
+    # there is no exchange to hide ("serial": a single shard, no collectives at all)
     probe = None
-    if a.c5_pipeline > 0:
-        P = a.c5_pipeline
+    if a.c5_exchange != "auto":
+        mode = a.c5_exchange
     elif not dist.is_initialized():
-        P = 1
+        mode = "serial"
     else:
         probe = {}
-        for Pc in (1, C5_PIPELINE_DEFAULT):
-            pw, _ = timed(make_step(Pc), 3, 1, world)
-            probe[f"p{Pc}_ms_per_step"] = pw / 3 * 1e3
-        P = min((1, C5_PIPELINE_DEFAULT), key=lambda x: probe[f"p{x}_ms_per_step"])
-    step = make_step(P)
-    wall, dev_ms = timed(step, steps, warm, world)
+        for mc in C5_EXCHANGES:
+            st_, tl_ = make_step(mc)
+            pw, _ = timed(st_, 3, 1, world, tail=tl_)
+            probe[f"{mc}_ms_per_step"] = pw / 3 * 1e3
+        mode = min(C5_EXCHANGES, key=lambda x: probe[f"{x}_ms_per_step"])
+    step, tail = make_step(mode)
+    wall, dev_ms = timed(step, steps, warm, world, tail=tail)
     r = step()
-    check = result_checksum(r if P == 1 else tuple(torch.cat(t) for t in zip(*r)), world)
+    if tail is not None:
+        r = tail()
+    check = result_checksum(r, world)
     h = gather_h()
     ts = torch.zeros(B, device=dev)
     topk_ms = kernel_ms(lambda: ops.score_topk(h, shard, 10, lo, thresholds=ts, mask_col0=(lo == 0)))
@@ -620,9 +644,10 @@ def bench_sas_c5(a, world, rank, dev, time_it=True):
                        "rows_per_rank": hi - lo,
                        "users_forwarded_per_rank": uhi - ulo, "table_rows_built_per_rank": (hi - lo) + model.item_num,
                        "setup_s": setup_s,
-                       "pipeline_sub_batches": P, "pipeline_probe": probe,
-                       "parallelism": f"catalog-sharded x{world}: RCCL all-gather h + top-k, all-reduce counts"
-                       + (f", {P} pipelined sub-batches" if P > 1 else "") if world > 1 else "single shard"},
+                       "exchange": mode, "exchange_probe": probe,
+                       "pipeline_sub_batches": max(2, a.c5_pipeline) if mode == "split" else 1,
+                       "parallelism": f"catalog-sharded x{world}: RCCL all-gather h + top-k, all-reduce counts, "
+                       f"{mode} exchange" if world > 1 else "single shard"},
             "result_checksum": check,
             "roofline": roofline(TOPK_PASS, 2 * d * (hi - lo) * B, topk_ms, "c5",
                                  call_kernels=TOPK_CALL_KERNELS,
@@ -1012,9 +1037,11 @@ def c5_rank_with_collectives(a, dev, W, B, d, k, lo, h, shard, t, own, loc, m0, 
     hidden states, the all-reduces of B target logits and B counts, the all-gather of the
     [W, B, 2k] packed candidates -- a one-rank all-gather moves its whole output):
       * serial_ms: the exchange as dist.sharded_rank_topk runs it (bench.py's pre-r6 N > 1 step);
-      * overlapped_ms: as dist.sharded_rank_topk_batches runs it with P user sub-batches (the N > 1
-        default): the target all-reduce of sub-batch b+1 and the count all-reduce + candidate
-        all-gather of sub-batch b run on RCCL's stream under sub-batch b+1's scoring.
+      * overlapped_ms: as dist.sharded_rank_topk_batches runs it with P user sub-batches (the
+        "split" form): the target all-reduce of sub-batch b+1 and the count all-reduce + candidate
+        all-gather of sub-batch b run on RCCL's stream under sub-batch b+1's scoring;
+      * xstep_ms: as dist.ShardedRankPipeline runs it (the "xstep" form): the whole batch scored in
+        one launch, its count all-reduce + candidate all-gather under the NEXT step's forward.
     The messages' xGMI latency between ranks is not on one GPU: these are the collectives' issue,
     launch and local-copy costs at the real sizes, not the 8-GPU wall time."""
     from gr_amd import dist as D
@@ -1089,6 +1116,35 @@ def c5_rank_with_collectives(a, dev, W, B, d, k, lo, h, shard, t, own, loc, m0, 
                 return out
             return step
 
+        xs = {"prev": None, "j": 0}
+        xpins = [packed_in, packed_in.clone()]
+
+        def xflush():
+            prev, xs["prev"] = xs["prev"], None
+            if prev is None:
+                return None
+            c, gout, w1, w2 = prev
+            w1.wait()
+            w2.wait()
+            ops.merge_topk_packed(gout, W, k, k)
+            return c + 1
+
+        def xstep():   # as dist.ShardedRankPipeline runs it: the exchange under the next step's forward
+            forward()
+            dist.all_gather_into_tensor(hout, hin)
+            tl = torch.where(own, ops.score_pairs(hout, shard, loc, mask_col0=m0), torch.zeros_like(hout[:, 0]))
+            dist.all_reduce(tl)
+            v, i, c = ops.score_topk(hout, shard, k, lo, thresholds=tl, mask_col0=m0)
+            w1 = dist.all_reduce(c, async_op=True)
+            pin = xpins[xs["j"] & 1]
+            xs["j"] += 1
+            pin[:B].copy_(D._pack(v, i))
+            gout = torch.empty((W, B, 2 * k), dtype=torch.int64, device=dev)
+            w2 = dist.all_gather_into_tensor(gout.view(W * B, -1), pin, async_op=True)
+            out = xflush()
+            xs["prev"] = (c, gout, w1, w2)
+            return out
+
         steps_ = max(2, min(a.steps, 10))
         _, ser_ms = timed(serial, steps_, 2, 1)
         res = {"serial_ms": ser_ms, "serial_value": B / (ser_ms * 1e-3)}
@@ -1099,8 +1155,12 @@ def c5_rank_with_collectives(a, dev, W, B, d, k, lo, h, shard, t, own, loc, m0, 
             if best is None or o_ms < best[1]:
                 best = (P, o_ms)
         P_def = C5_PIPELINE_DEFAULT
-        res.update({"overlapped_ms": res.get(f"overlapped_ms_p{P_def}", best[1]), "overlapped_pipeline": P_def,
-                    "overlapped_value": B / (res.get(f"overlapped_ms_p{P_def}", best[1]) * 1e-3),
+        _, x_ms = timed(xstep, steps_, 2, 1, tail=xflush)
+        forms = {"serial": ser_ms, "split": res.get(f"overlapped_ms_p{P_def}", best[1]), "xstep": x_ms}
+        res.update({"overlapped_ms": forms["split"], "overlapped_pipeline": P_def,
+                    "overlapped_value": B / (forms["split"] * 1e-3),
+                    "xstep_ms": x_ms, "xstep_value": B / (x_ms * 1e-3),
+                    "exchange_best": min(forms, key=forms.get),
                     "collectives_backend": "nccl (RCCL), one-rank group, N = %d message sizes" % W})
         return res
     finally:
@@ -1176,7 +1236,8 @@ def bench_c5_rank(a, dev):
     colls = c5_rank_with_collectives(a, dev, W, B, d, k, lo, h, shard, t, own, loc, m0, forward, gathered)
     # the step bench.py's N > 1 run picks automatically: the faster of the serial and pipelined
     # exchange (bench_sas_c5's probe)
-    val_ms = min(colls.get("serial_ms") or dev_ms, colls.get("overlapped_ms") or dev_ms)
+    val_ms = min(colls.get("serial_ms") or dev_ms, colls.get("overlapped_ms") or dev_ms,
+                 colls.get("xstep_ms") or dev_ms)
     return {"metric": "seqs_scored/s", "value": B / (val_ms * 1e-3), "unit": "seqs/s",
             "scaling": f"one rank of the N = {W} C5 point, projected to the whole job",
             "ms_per_step": val_ms, "wall_ms_per_step": wall / steps_ * 1e3,
@@ -1185,7 +1246,7 @@ def bench_c5_rank(a, dev):
                                    f"of the {items + 1}-row catalog, merge of {W} x {k} candidates",
                        "users_per_step": B, "users_forwarded": B // W, "rows": hi - lo},
             "projected_value_note": f"value = the {B} users of one N = {W} step / this rank's step time WITH "
-                                    f"its collectives: min(serial_ms, overlapped_ms), the exchange bench.py's "
+                                    f"its collectives: min(serial_ms, overlapped_ms, xstep_ms), the exchange bench.py's "
                                     f"N > 1 run selects by timing both (every collective at its N = {W} message "
                                     f"size through a one-rank RCCL group; xGMI latency between ranks is not on "
                                     f"one GPU). no_collectives_ms: the kernels alone",
@@ -1479,7 +1540,7 @@ def main():
             if "rows_ids_differ_unflagged" in ag:
                 summ[f"{tag}_host_rows_differ_unflagged"] = ag["rows_ids_differ_unflagged"]
                 summ[f"{tag}_host_dz_over_z_max"] = ag["host_dz_over_z_max"]
-    for key in ("serial_ms", "overlapped_ms"):
+    for key in ("serial_ms", "overlapped_ms", "xstep_ms"):
         if isinstance(line.get("c5_rank"), dict) and key in line["c5_rank"]:
             summ[f"c5_rank_{key}"] = line["c5_rank"][key]
     line["summary"] = summ

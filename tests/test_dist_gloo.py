@@ -65,6 +65,12 @@ def _worker(rank, world, port, data, out):
         assert torch.equal(r0, r1) and torch.equal(v0, v1) and torch.equal(i0, i1)
     pr = torch.cat([r_[0] for r_ in res])
     pi = torch.cat([r_[2] for r_ in res])
+    # the cross-step form: submit returns the previous batch's result, flush the last one's
+    pipe = D.ShardedRankPipeline(table[lo:hi], lo, k, scorer=cpu_score, counter=cpu_count, topk_fn=cpu_topk)
+    got = [pipe.submit(hb, tb) for hb, tb in zip(hs, ts)] + [pipe.flush()]
+    assert got[0] is None and pipe.flush() is None
+    for r_a, r_b in zip(res, got[1:]):
+        assert all(torch.equal(x, y) for x, y in zip(r_a, r_b))
     out[rank] = (rk, v, i, hg, (pr, pi))
     dist.barrier()
     dist.destroy_process_group()

@@ -229,6 +229,14 @@ def _gloo_gpu_worker(rank, world, port, data, out, backend="gloo"):
     if wk is not None:
         wk.wait()
     gathered_ok = torch.equal(hg, h) and torch.equal(hu, h[:sum(usz)])
+    # the cross-step form (bench.py's "xstep" exchange): two submits of the whole batch, each
+    # result bitwise the serial exchange's
+    pipe = D.ShardedRankPipeline(table[lo:hi].contiguous(), lo, k)
+    x0 = pipe.submit(h, targets)
+    x1 = pipe.submit(h, targets)
+    x2 = pipe.flush()
+    gathered_ok = gathered_ok and x0 is None and pipe.flush() is None and all(
+        torch.equal(a_, b_) for xr in (x1, x2) for a_, b_ in zip(xr, (rk, v, i)))
     out[rank] = (rk.cpu(), v.cpu(), i.cpu(), torch.cat([r_[0] for r_ in res]).cpu(),
                  torch.cat([r_[1] for r_ in res]).cpu(), torch.cat([r_[2] for r_ in res]).cpu(), gathered_ok)
     dist.barrier()
@@ -239,7 +247,8 @@ def _gloo_gpu_worker(rank, world, port, data, out, backend="gloo"):
 def test_catalog_sharded_fused_multi_rank(world, backend, dev):
     """The catalog-sharded exchange over real ranks (gloo, every rank on this GPU) with the fused
     HIP kernels: every rank returns the full-catalog rank / top-k bit for bit, both through the
-    serial exchange and the pipelined one (sharded_rank_topk_batches, bench.py's N > 1 default);
+    serial exchange, the split one (sharded_rank_topk_batches) and the cross-step one
+    (ShardedRankPipeline) -- the three forms bench.py's N > 1 run chooses between;
     world 8 is the C5 node's shard count.  The one-rank RCCL
     case runs every collective of the exchange (a one-rank group still issues them) through the
     "nccl" backend and bench.py's ``device_id`` initialisation: RCCL needs one GPU per rank, so
