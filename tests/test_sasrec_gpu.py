@@ -289,10 +289,11 @@ def test_tail_h_form_vs_full_block_and_oracle(d, heads, n, blocks, B, dev):
 
 @pytest.mark.parametrize("d,heads,n,blocks,B", [(128, 1, 200, 2, 37), (128, 2, 130, 2, 9), (64, 1, 100, 2, 17),
                                                 (64, 2, 77, 1, 5), (128, 1, 33, 1, 3), (128, 1, 200, 2, 1500),
-                                                (128, 2, 97, 3, 40)])
+                                                (128, 2, 97, 3, 40), (128, 1, 256, 1, 70), (64, 1, 20, 1, 2000)])
 def test_attn_persist_vs_oracle(d, heads, n, blocks, B, dev):
     """Layer-wise causal attention at head width 64 / 128 (attn_persist_kernel: a persistent grid of
-    one wave per SIMD over static longest-first item lists; B 1500: ~14 items per wave) through the
+    one wave per SIMD over static longest-first item lists; B 1500: ~14 items per wave; n 20 at
+    B 2000: one query tile, more items than waves) through the
     full forward, against the CPU oracle; the row-tile (d 128) and per-op paths agree within the
     oracle tolerance, and every row is batch-invariant (a sub-batch gives the same bits)."""
     from gr_amd import _lib, synth
