@@ -295,14 +295,47 @@ def call_traffic(leg, kernels, anchor):
     return tot / calls, f"{t.get('source', '')}, leg {leg}"
 
 
+# the rocprofv3 --kernel-trace summary of the default bench command on this tree
+# (scripts/trace_stats.py over the same run as profiles/r06/rocprof_kernel_stats.csv)
+ROCPROF_TRACE = os.path.join("profiles", "r06", "rocprof_trace_stats.csv")
+
+
+def rocprof_median_us(kernel, near_ms):
+    """Median launch duration (us) of ``kernel`` (prefix of the demangled name, spaces ignored) in the
+    committed rocprofv3 trace summary, so the bench line carries the profiler's figure beside its own
+    event timing.  A kernel profiled at several launch shapes (C2 / C4 encoders,
+    the C5 / shard top-k passes) is matched to the shape whose median is nearest ``near_ms``; the
+    chosen shape's grid is reported.  None when the summary is absent."""
+    import csv
+    p = os.path.join(ROOT, ROCPROF_TRACE)
+    if not os.path.exists(p):
+        return None
+    rows = []
+    for r in csv.DictReader(open(p)):
+        name = r.get("kernel", "").replace("void ", "").replace("gr::", "").replace(" ", "")
+        if name.startswith(kernel.replace(" ", "")):
+            rows.append((float(r["median_us"]), int(r["grid_threads"]), int(r["calls"])))
+    if not rows:
+        return None
+    med, grid, calls = min(rows, key=lambda x: abs(x[0] - near_ms * 1e3))
+    return {"median_us": med, "grid_threads": grid, "launches": calls, "shapes_profiled": len(rows)}
+
+
 def roofline(kernel, flop, ms, leg, bound="mfma", call_kernels=None, note=None):
     """``kernel`` names the dominant kernel (prefix of its profiled name); ``call_kernels`` lists
     the kernel-name prefixes one timed call launches (default: ``kernel`` alone), so ``traffic``
-    is per call, like ``achieved``."""
+    is per call, like ``achieved``.  ``frac`` is from this run's HIP-event timing; ``frac_rocprof``
+    from the committed rocprofv3 median of the same kernel (``rocprof_source``)."""
     ach = flop / (ms * 1e-3) / 1e12
     tr, src = call_traffic(leg, call_kernels or [kernel], kernel)
+    rp = rocprof_median_us(kernel, ms) if not call_kernels or call_kernels == [kernel] else None
+    extra = {}
+    if rp is not None:
+        extra = {"kernel_us_rocprof_median": rp["median_us"],
+                 "frac_rocprof": flop / (rp["median_us"] * 1e-6) / 1e12 / FP32_PEAK_TFLOPS,
+                 "rocprof_source": f"{ROCPROF_TRACE} (grid {rp['grid_threads']}, {rp['launches']} launches)"}
     return {"bound": bound, "achieved": ach, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
-            "frac": ach / FP32_PEAK_TFLOPS, "traffic": tr, "traffic_source": src, "kernel": kernel,
+            "frac": ach / FP32_PEAK_TFLOPS, **extra, "traffic": tr, "traffic_source": src, "kernel": kernel,
             "flop_per_launch": flop, "kernel_ms": ms, **({"note": note} if note else {})}
 
 
@@ -1543,6 +1576,11 @@ def main():
     for key in ("serial_ms", "overlapped_ms", "xstep_ms"):
         if isinstance(line.get("c5_rank"), dict) and key in line["c5_rank"]:
             summ[f"c5_rank_{key}"] = line["c5_rank"][key]
+    rf = line.get("sasrec", {}).get("roofline") if isinstance(line.get("sasrec"), dict) else None
+    if isinstance(rf, dict):   # both figures of the C3 scoring kernel
+        summ["c3_score_frac_event"] = rf.get("frac")
+        if "frac_rocprof" in rf:
+            summ["c3_score_frac_rocprof"] = rf["frac_rocprof"]
     line["summary"] = summ
     if rank == 0:
         print(json.dumps(line), flush=True)
