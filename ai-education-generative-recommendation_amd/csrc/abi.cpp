@@ -11,7 +11,8 @@ void set_error(const std::string& msg) { g_last_error = msg; }
 void clear_error() { g_last_error.clear(); }
 
 // Path switches (gr_set_option), read by the launchers at each call.  Each selects between two
-// kernel paths that give BITWISE the same results (the tests run both); none changes numerics.
+// kernel paths that give BITWISE the same results (the tests run both), except attn_k16: two fp32
+// chains of the hd 128 attention, both tested against the oracle within the logits tolerance.
 // Kernel variants measured slower and the options that selected them were removed in round 5
 // (DESIGN.md §7 keeps their measurements).
 struct Opt {
@@ -36,10 +37,14 @@ static std::atomic<int64_t> g_emb_proj{1};
 // topk_half (gr_score_topk_f32's tile maxima: 2 = 16-row half tiles where the re-scored bytes saved
 // exceed the extra maxima traffic (short catalogs), 32-row tiles otherwise; 1 / 0 = forced)
 static std::atomic<int64_t> g_topk_half{2};
+// attn_k16 (hd 64 / 128 attention: 1 = 32-query tiles over 16-key steps at two waves per SIMD,
+// 0 = the persistent 32 x 32-step kernel; a different fp32 chain, both within the logits tolerance)
+static std::atomic<int64_t> g_attn_k16{1};
 
 static const Opt kOpts[] = {
     {"rq_fused", &g_rq_fused, 0, 1},   {"sas_fused", &g_sas_fused, 0, 3}, {"sas_rowtile", &g_sas_rowtile, 0, 1},
     {"lin_wres", &g_lin_wres, 0, 1},   {"emb_proj", &g_emb_proj, 0, 1},   {"topk_half", &g_topk_half, 0, 2},
+    {"attn_k16", &g_attn_k16, 0, 1},
 };
 
 static const Opt* find_opt(const char* name) {

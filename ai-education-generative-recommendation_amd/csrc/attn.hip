@@ -405,6 +405,187 @@ __global__ __launch_bounds__(64) void attn_persist_kernel(const float* __restric
   }
 }
 
+// hd 64 / 128, round 6: 32-query tiles over 16-KEY steps on v_mfma_f32_16x16x4_f32, two waves per
+// SIMD.  The 32-query form above holds Q, K, V and O of a 32 x 32 step (272 registers at hd 128)
+// and the compiler moves operands through the accumulator file every key tile; here a step takes
+// 16 keys, so K and V halve (HD/4 each) while Q and O (HD/2 each, two 16-query halves) keep the
+// 32-query reuse of every K / V fetch: ~214 registers, no AGPRs, two waves per SIMD.
+// Per lane (r = lane & 15, kk = lane >> 4), query half qs:
+//   S^T[key][query] = K . q^T: A = K[16kt + r][kk HD/4 + j], B = q[q0 + 16qs + r][kk HD/4 + j],
+//   steps j = 0 .. HD/4 - 1; D register c = S[query q0 + 16qs + r][key 16kt + 4kk + c].
+//   O^T += V^T P^T over chunks c: key 16kt + 4kk + c in lane group kk, B = P = that register, A =
+//   V[key][f(ft, r)], f(ft, r) = 64 (ft >> 2) + 4r + (ft & 3) (V as float4s); D register c of
+//   O^T tile (ft, qs) = O[query q0 + 16qs + r][feature f(ft, 4kk + c)].
+// Online softmax per query (lazy rescale, AT_LAZY), row max / sum over the four lane groups by two
+// exchanges; each lane carries the state of its two queries.  K / V of key step kt + 1 are loaded
+// under step kt, the next item's first K / V under the item's last step, and its Q after the item's
+// stores (loading Q under the last step too keeps both items' operands live: 64 spilled registers
+// at hd 128).  Buffer loads on the (sequence, head)
+// base with lane-constant offsets; rows past n read 0 and are masked.  A different fp32 chain than
+// the form above (16x16x4 steps): within the logits tolerance, not bitwise equal to it; every row
+// sees the same instruction sequence whichever tiles are launched.
+template <int HD>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2)))
+void attn_k16_kernel(const float* __restrict__ qkv, float* __restrict__ out, int n, int H, float scale, int nbh,
+                     int qt_lo, int wx) {
+  constexpr int QJ = HD / 4;        // q / k values per lane and row (steps of the S chain)
+  constexpr int QV = HD / 16;       // ... as float4
+  constexpr int FTN = HD / 16;      // O^T feature tiles per query half
+  constexpr int VG = HD / 64;       // float4 of V per (lane, key)
+  const int lane = threadIdx.x, r = lane & 15, kk = lane >> 4;
+  const int T = (n + 31) / 32, nt = T - qt_lo;
+  const int x = blockIdx.x & 7, k = blockIdx.x >> 3;
+  const int mx = (nbh - x + 7) / 8, items = mx * nt;
+  const int d = H * HD;
+  const int rs4 = 3 * d * 4;        // row stride, bytes
+  auto item_of = [&](int rnd) {
+    const int j = rnd * wx + ((rnd & 1) ? wx - 1 - k : k);
+    return j < items ? j : -1;
+  };
+  int rnd = 0;
+  int j = item_of(0);
+  if (j < 0) return;
+  const int vQ = r * rs4 + kk * QJ * 4;
+  const int vK = r * rs4 + (d + kk * QJ) * 4;
+  const int vV = 4 * kk * rs4 + (2 * d + 4 * r) * 4;
+  auto rsrc_of = [&](int jj, int& qt_, int& bh_) {
+    qt_ = T - 1 - jj / mx;
+    bh_ = x + 8 * (jj % mx);
+    const float* bs = qkv + (int64_t)(bh_ / H) * n * 3 * d + (bh_ % H) * HD;
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(bs), 0, n * rs4, 0x00020000);
+  };
+  f32x4 qf[2][QV], kf[QV], vf[4][VG];
+  auto load_q = [&](auto rsrc, int qt_) {
+#pragma unroll
+    for (int qs = 0; qs < 2; ++qs)
+#pragma unroll
+      for (int i = 0; i < QV; ++i)
+        qf[qs][i] = __builtin_bit_cast(
+            f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, vQ, (32 * qt_ + 16 * qs) * rs4 + 16 * i, 0));
+  };
+  auto load_k = [&](auto rsrc, int kt) {
+#pragma unroll
+    for (int i = 0; i < QV; ++i)
+      kf[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, vK, 16 * kt * rs4 + 16 * i, 0));
+  };
+  auto load_v = [&](auto rsrc, int kt) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int g = 0; g < VG; ++g)
+        vf[c][g] = __builtin_bit_cast(
+            f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, vV, (16 * kt + c) * rs4 + 256 * g, 0));
+  };
+  int qt, bh;
+  auto rsrc = rsrc_of(j, qt, bh);
+  load_q(rsrc, qt);
+  load_k(rsrc, 0);
+  load_v(rsrc, 0);
+  while (true) {
+#pragma unroll
+    for (int qs = 0; qs < 2; ++qs)
+#pragma unroll
+      for (int i = 0; i < QV; ++i) qf[qs][i] = qf[qs][i] * scale;   // q * sqrt(1/hd) (functional.py:6578)
+    const int q0 = qt * 32;
+    f32x4 O[2][FTN];
+#pragma unroll
+    for (int qs = 0; qs < 2; ++qs)
+#pragma unroll
+      for (int ft = 0; ft < FTN; ++ft) O[qs][ft] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float m[2] = {-INFINITY, -INFINITY}, l[2] = {0.f, 0.f};
+    const int nj = item_of(rnd + 1);
+    int nqt = 0, nbh_ = 0;
+    const auto nrsrc = nj >= 0 ? rsrc_of(nj, nqt, nbh_) : rsrc;
+    const int kt_last = (q0 + 31 < n - 1 ? q0 + 31 : n - 1) / 16;
+    for (int kt = 0; kt <= kt_last; ++kt) {
+      f32x4 S[2];
+      S[0] = f32x4{0.f, 0.f, 0.f, 0.f};
+      S[1] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int i = 0; i < QV; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          S[0] = mfma16(kf[i][e], qf[0][i][e], S[0]);
+          S[1] = mfma16(kf[i][e], qf[1][i][e], S[1]);
+        }
+      if (kt < kt_last) load_k(rsrc, kt + 1);
+      else if (nj >= 0) load_k(nrsrc, 0);
+      const bool edge = 16 * kt + 15 > q0 || 16 * kt + 16 > n;
+      float ts[2];
+#pragma unroll
+      for (int qs = 0; qs < 2; ++qs) {
+        const int qi = q0 + 16 * qs + r;
+        float tmax = -INFINITY;
+        if (edge) {
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            const int key = 16 * kt + 4 * kk + c;
+            if (key > qi || key >= n) S[qs][c] = -INFINITY;
+            tmax = fmaxf(tmax, S[qs][c]);
+          }
+        } else {
+#pragma unroll
+          for (int c = 0; c < 4; ++c) tmax = fmaxf(tmax, S[qs][c]);
+        }
+        tmax = fmaxf(tmax, __shfl_xor(tmax, 16));
+        tmax = fmaxf(tmax, __shfl_xor(tmax, 32));
+        const bool up = tmax > m[qs] + AT_LAZY;
+        if (__any(up)) {
+          const float mn = up ? tmax : m[qs];
+          const float alpha = __expf(m[qs] - mn);
+          l[qs] *= alpha;
+          m[qs] = mn;
+#pragma unroll
+          for (int ft = 0; ft < FTN; ++ft) O[qs][ft] *= alpha;
+        }
+        float t = 0.f;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const float e = __expf(S[qs][c] - m[qs]);
+          S[qs][c] = e;
+          t += e;
+        }
+        ts[qs] = t;
+      }
+#pragma unroll
+      for (int qs = 0; qs < 2; ++qs) {
+        float t = ts[qs];
+        t += __shfl_xor(t, 16);
+        t += __shfl_xor(t, 32);
+        l[qs] += t;
+      }
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+#pragma unroll
+        for (int ft = 0; ft < FTN; ++ft)
+#pragma unroll
+          for (int qs = 0; qs < 2; ++qs) O[qs][ft] = mfma16(vf[c][ft >> 2][ft & 3], S[qs][c], O[qs][ft]);
+      if (kt < kt_last) load_v(rsrc, kt + 1);
+      else if (nj >= 0) load_v(nrsrc, 0);
+    }
+#pragma unroll
+    for (int qs = 0; qs < 2; ++qs) {
+      const int qi = q0 + 16 * qs + r;
+      if (qi < n) {
+        const float inv = 1.0f / l[qs];
+        float* orow = out + ((int64_t)(bh / H) * n + qi) * d + (bh % H) * HD;
+#pragma unroll
+        for (int g = 0; g < VG; ++g)
+#pragma unroll
+          for (int c = 0; c < 4; ++c)
+            *reinterpret_cast<f32x4*>(orow + 64 * g + 16 * kk + 4 * c) =
+                f32x4{O[qs][4 * g][c], O[qs][4 * g + 1][c], O[qs][4 * g + 2][c], O[qs][4 * g + 3][c]} * inv;
+      }
+    }
+    if (nj < 0) break;
+    load_q(nrsrc, nqt);
+    ++rnd;
+    rsrc = nrsrc;
+    qt = nqt;
+    bh = nbh_;
+  }
+}
+
 }  // namespace gr
 
 // Returns GR_ERR_UNSUPPORTED (message untouched) for head widths the kernel is not built for.
@@ -425,6 +606,13 @@ int gr_attn_mfma_launch(const float* qkv, float* out, int64_t B, int n, int H, i
       (void)hipGetDevice(&dev);
       (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
       simds = 4 * (cus > 0 ? cus : 256);
+    }
+    // hd 128: 16-key steps at two waves per SIMD (C5: 0.322 -> 0.313 ms per last_hidden,
+    // profiles/r06/ab_attn_k16.txt); hd 64 measured no faster there and keeps the 32 x 32 steps
+    if (hd == 128 && option("attn_k16") == 1 && (int64_t)n * 3 * hd * H * 4 < (1LL << 31)) {
+      const int wx2 = (2 * simds + 7) / 8;
+      hipLaunchKernelGGL(attn_k16_kernel<128>, dim3(8 * wx2), dim3(64), 0, st, qkv, out, n, H, scale, (int)nbh, qt_lo, wx2);
+      return check_launch("sasrec attention (16-key steps)");
     }
     const int wx = (simds + 7) / 8;
     if (hd == 128)

@@ -72,6 +72,9 @@ const char* gr_last_error(void);
  *                   half tile when the catalog is below ~3,700 64-row chunks per 128 features (the
  *                   select kernel then re-scores half as many rows), else of every 32-row tile;
  *                   1: always half tiles; 0: never.
+ *   "attn_k16"      1 (default): head width 128 attention on 32-query tiles over 16-key steps at
+ *                   two waves per SIMD; 0: 32 x 32 steps at one wave per SIMD.  Different fp32
+ *                   chains of the same attention (both within the logits tolerance).
  * A last-position forward (predict, last_hidden) runs its final block as the one-query tail on
  * LN_a(X): q . K_j = (W_k^T q) . H_j (+ a term constant over j that cancels in the softmax) and
  * p . V = W_v (p . H) + b_v, so K|V of the B n rows are never projected (sas_tail_h2_kernel; the

@@ -291,9 +291,10 @@ def test_tail_h_form_vs_full_block_and_oracle(d, heads, n, blocks, B, dev):
                                                 (64, 2, 77, 1, 5), (128, 1, 33, 1, 3), (128, 1, 200, 2, 1500),
                                                 (128, 2, 97, 3, 40), (128, 1, 256, 1, 70), (64, 1, 20, 1, 2000)])
 def test_attn_persist_vs_oracle(d, heads, n, blocks, B, dev):
-    """Layer-wise causal attention at head width 64 / 128 (attn_persist_kernel: a persistent grid of
-    one wave per SIMD over static longest-first item lists; B 1500: ~14 items per wave; n 20 at
-    B 2000: one query tile, more items than waves) through the
+    """Layer-wise causal attention at head width 64 / 128 (hd 128: attn_k16_kernel, 32-query tiles over
+    16-key steps at two waves per SIMD, and with option attn_k16 0 attn_persist_kernel, 32 x 32 steps
+    at one wave per SIMD; both persistent grids over static longest-first item lists; B 1500: ~14
+    items per wave; n 20 at B 2000: one query tile, more items than waves) through the
     full forward, against the CPU oracle; the row-tile (d 128) and per-op paths agree within the
     oracle tolerance, and every row is batch-invariant (a sub-batch gives the same bits)."""
     from gr_amd import _lib, synth
@@ -302,17 +303,24 @@ def test_attn_persist_vs_oracle(d, heads, n, blocks, B, dev):
     p = synth.sasrec_params(d, n, blocks, heads, 64, dev)
     m = synth.sasrec_model(items, p, dev, seed=d + n)
     seqs = synth.sequences(B, n, items, 3 + n, dev)
-    try:
-        _lib.set_option("sas_fused", 0)
-        f = m.forward(seqs)
-        sub = m.forward(seqs[:3])
-    finally:
-        _lib.set_option("sas_fused", 2)
-    assert torch.equal(sub, f[:3])
     pick = torch.arange(0, B, max(1, B // 64), device=dev)
     sd = {k: v.detach().cpu() for k, v in m.state_dict().items()}
     ref_f = sasrec_oracle.forward(seqs[pick].cpu(), sd, blocks, heads, 1e-8)
-    assert (f[pick].cpu() - ref_f).abs().max().item() < 5e-5
+    outs = {}
+    try:
+        _lib.set_option("sas_fused", 0)
+        for k16 in (1, 0):   # hd 128: attn_k16_kernel (16-key steps) by default, then the 32 x 32 steps
+            _lib.set_option("attn_k16", k16)
+            f = m.forward(seqs)
+            sub = m.forward(seqs[:3])
+            assert torch.equal(sub, f[:3])
+            assert (f[pick].cpu() - ref_f).abs().max().item() < 5e-5
+            outs[k16] = f
+    finally:
+        _lib.set_option("sas_fused", 2)
+        _lib.set_option("attn_k16", 1)
+    # the two forms are different fp32 chains of the same attention
+    assert (outs[1] - outs[0]).abs().max().item() < 2e-5
 
 
 @pytest.mark.parametrize("d,heads,n,blocks,B", [(64, 1, 50, 2, 300), (64, 2, 64, 2, 33), (32, 4, 20, 1, 17),
