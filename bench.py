@@ -138,7 +138,8 @@ def per_rank(x, world):
 def result_checksum(res, world):
     """a digest of the merged C5 result (1-based ranks, top-k values and ids, all
     [B]-sized and identical on every rank after the exchange), gathered from every rank so the line
-    shows the ranks agreed; the digest is independent of the world size (the same bits at N = 1)."""
+    shows the ranks agreed.  For the same users it is independent of the world size: B = c5_batch x N,
+    so N = 1 with --c5-batch 4096 reproduces the N = 8 digest (profiles/r06/c5_digest_world_independence.txt)."""
     import hashlib
     rk, v, i = res
     hsh = hashlib.sha256()
