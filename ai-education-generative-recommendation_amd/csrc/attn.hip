@@ -43,27 +43,6 @@ struct AttnTile {                  // one 32-query tile owned by a wave
 
 constexpr float AT_LAZY = 8.f;   // lazy-rescale threshold (natural-log units)
 
-// Pairwise exchanges of the row reductions on the VALU (gfx950 v_permlane16/32_swap) instead of
-// ds_bpermute through the LDS unit: swapping a register with itself leaves each lane its own value
-// in one result and its partner's (lane ^ 16, or lane ^ 32) in the other, so max / + of the two is
-// bitwise the "x op __shfl_xor(x, m)" of before (both ops commute).
-__device__ __forceinline__ float xor16_max(float x) {
-  const auto p = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
-  return fmaxf(__uint_as_float(p[0]), __uint_as_float(p[1]));
-}
-__device__ __forceinline__ float xor32_max(float x) {
-  const auto p = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
-  return fmaxf(__uint_as_float(p[0]), __uint_as_float(p[1]));
-}
-__device__ __forceinline__ float xor16_add(float x) {
-  const auto p = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
-  return __uint_as_float(p[0]) + __uint_as_float(p[1]);
-}
-__device__ __forceinline__ float xor32_add(float x) {
-  const auto p = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
-  return __uint_as_float(p[0]) + __uint_as_float(p[1]);
-}
-
 // Two workgroups per CU: at hd = 128 that caps the kernel at 256 VGPRs (a few spill), and still
 // measured 85 vs 114 us per C5 call against one (steady state) — the second workgroup's MFMAs
 // fill the gaps of the first's barriers and softmax.  Used for hd = 32 (and for the persistent
@@ -375,7 +354,7 @@ __global__ __launch_bounds__(64) void attn_persist_kernel(const float* __restric
 #pragma unroll
         for (int v = 0; v < 16; ++v) tmax = fmaxf(tmax, S[v]);
       }
-      tmax = xor32_max(tmax);
+      tmax = xmax<32>(tmax);
       const bool up = tmax > m + AT_LAZY;
       if (__any(up)) {
         const float mn = up ? tmax : m;
@@ -392,7 +371,7 @@ __global__ __launch_bounds__(64) void attn_persist_kernel(const float* __restric
         S[v] = e;
         ts += e;
       }
-      ts = xor32_add(ts);
+      ts = xsum<32>(ts);
       l += ts;
       }
 #pragma unroll
@@ -548,7 +527,7 @@ void attn_k16_kernel(const float* __restrict__ qkv, float* __restrict__ out, int
 #pragma unroll
           for (int c = 0; c < 4; ++c) tmax = fmaxf(tmax, S[qs][c]);
         }
-        tmax = xor32_max(xor16_max(tmax));
+        tmax = xmax<32>(xmax<16>(tmax));
         const bool up = tmax > m[qs] + AT_LAZY;
         if (__any(up)) {
           const float mn = up ? tmax : m[qs];
@@ -570,7 +549,7 @@ void attn_k16_kernel(const float* __restrict__ qkv, float* __restrict__ out, int
 #pragma unroll
       for (int qs = 0; qs < 2; ++qs) {
         float t = ts[qs];
-        t = xor32_add(xor16_add(t));
+        t = xsum<32>(xsum<16>(t));
         l[qs] += t;
       }
 #pragma unroll

@@ -226,6 +226,50 @@ __host__ __device__ inline int mkl_kblock(int K) { return mkl_plan(1 << 20, K, 2
 // (gq = 4 g + q); d = 16 is the same chain over two groups.
 __device__ __forceinline__ int sc_feat(int gq, int hh) { return 8 * gq + 4 * hh; }
 
+// Butterfly steps on the VALU: xsum<O>(v) = v + (v of lane ^ O), xmax<O>(v) = fmaxf(v, that), each
+// bitwise the "v op __shfl_xor(v, O)" it replaces (both ops commute) without the ds_bpermute round
+// trip through the LDS unit (~100+ cycles on a reduction's dependency chain).  O = 32 / 16:
+// v_permlane32_swap / v_permlane16_swap of the register with itself leave each lane its own value
+// in one result and its partner's in the other; O = 8: DPP row_ror:8; 4: DPP row_shl:4 / row_shr:4
+// by the lane's bit 2; 2 / 1: DPP quad_perm.
+template <int O>
+__device__ __forceinline__ float xpartner(float v) {
+  static_assert(O == 1 || O == 2 || O == 4 || O == 8, "DPP partners within a row of 16");
+  const int x = __float_as_int(v);
+  if constexpr (O == 1) return __int_as_float(__builtin_amdgcn_update_dpp(x, x, 0xB1, 0xF, 0xF, false));
+  else if constexpr (O == 2) return __int_as_float(__builtin_amdgcn_update_dpp(x, x, 0x4E, 0xF, 0xF, false));
+  else if constexpr (O == 8) return __int_as_float(__builtin_amdgcn_update_dpp(x, x, 0x128, 0xF, 0xF, false));
+  else {
+    const int up = __builtin_amdgcn_update_dpp(x, x, 0x104, 0xF, 0xF, false);   // lane i + 4
+    const int dn = __builtin_amdgcn_update_dpp(x, x, 0x114, 0xF, 0xF, false);   // lane i - 4
+    return __int_as_float((__lane_id() & 4) ? dn : up);
+  }
+}
+template <int O>
+__device__ __forceinline__ float xsum(float v) {
+  if constexpr (O == 32) {
+    const auto p = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return __uint_as_float(p[0]) + __uint_as_float(p[1]);
+  } else if constexpr (O == 16) {
+    const auto p = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return __uint_as_float(p[0]) + __uint_as_float(p[1]);
+  } else {
+    return v + xpartner<O>(v);
+  }
+}
+template <int O>
+__device__ __forceinline__ float xmax(float v) {
+  if constexpr (O == 32) {
+    const auto p = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return fmaxf(__uint_as_float(p[0]), __uint_as_float(p[1]));
+  } else if constexpr (O == 16) {
+    const auto p = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return fmaxf(__uint_as_float(p[0]), __uint_as_float(p[1]));
+  } else {
+    return fmaxf(v, xpartner<O>(v));
+  }
+}
+
 // f32-input MFMA 16x16x4: an fma chain over its four k slots in ascending order (lane group
 // l >> 4 = k; profiles/r03_mfma_order.txt).  Lane l supplies A[i = l&15][k = l>>4] and
 // B[k = l>>4][j = l&15]; D register v of lane l holds row 4 (l>>4) + v, column l&15.

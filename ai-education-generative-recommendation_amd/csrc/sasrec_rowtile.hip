@@ -77,8 +77,7 @@ __device__ __forceinline__ void rt_layernorm(float* img, const float* __restrict
   float s = 0.f;
 #pragma unroll
   for (int i = 0; i < 8; ++i) s += (v[i][0] + v[i][1]) + (v[i][2] + v[i][3]);
-  s += __shfl_xor(s, 1);
-  s += __shfl_xor(s, 2);
+  s = xsum<2>(xsum<1>(s));
   const float mean = s * (1.0f / RT_D);
   float q = 0.f;
 #pragma unroll
@@ -88,8 +87,7 @@ __device__ __forceinline__ void rt_layernorm(float* img, const float* __restrict
       const float d = v[i][e] - mean;
       q = fmaf(d, d, q);
     }
-  q += __shfl_xor(q, 1);
-  q += __shfl_xor(q, 2);
+  q = xsum<2>(xsum<1>(q));
   const float rstd = 1.0f / sqrtf(q * (1.0f / RT_D) + eps);
   if (!dst_global) {
 #pragma unroll
@@ -137,8 +135,7 @@ __device__ __forceinline__ void rt_layernorm_lds(float* img, const float* ws, co
   float s = 0.f;
 #pragma unroll
   for (int i = 0; i < 8; ++i) s += (v[i][0] + v[i][1]) + (v[i][2] + v[i][3]);
-  s += __shfl_xor(s, 1);
-  s += __shfl_xor(s, 2);
+  s = xsum<2>(xsum<1>(s));
   const float mean = s * (1.0f / RT_D);
   float q = 0.f;
 #pragma unroll
@@ -148,8 +145,7 @@ __device__ __forceinline__ void rt_layernorm_lds(float* img, const float* ws, co
       const float d = v[i][e] - mean;
       q = fmaf(d, d, q);
     }
-  q += __shfl_xor(q, 1);
-  q += __shfl_xor(q, 2);
+  q = xsum<2>(xsum<1>(q));
   const float rstd = 1.0f / sqrtf(q * (1.0f / RT_D) + eps);
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
@@ -221,9 +217,7 @@ __device__ __forceinline__ void rt_layernorm8(float* img, const float* __restric
   float s = 0.f;
 #pragma unroll
   for (int i = 0; i < 4; ++i) s += (v[i][0] + v[i][1]) + (v[i][2] + v[i][3]);
-  s += __shfl_xor(s, 1);
-  s += __shfl_xor(s, 2);
-  s += __shfl_xor(s, 4);
+  s = xsum<4>(xsum<2>(xsum<1>(s)));
   const float mean = s * (1.0f / RT_D);
   float q = 0.f;
 #pragma unroll
@@ -233,9 +227,7 @@ __device__ __forceinline__ void rt_layernorm8(float* img, const float* __restric
       const float d = v[i][e] - mean;
       q = fmaf(d, d, q);
     }
-  q += __shfl_xor(q, 1);
-  q += __shfl_xor(q, 2);
-  q += __shfl_xor(q, 4);
+  q = xsum<4>(xsum<2>(xsum<1>(q)));
   const float rstd = 1.0f / sqrtf(q * (1.0f / RT_D) + eps);
   if (!dst_global) {
 #pragma unroll

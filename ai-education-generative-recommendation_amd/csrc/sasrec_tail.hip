@@ -37,14 +37,38 @@ constexpr int ST_U = 8;                      // rows / keys in flight per lane g
 
 // Segmented lane groups: a group of L = k/4 consecutive lanes (L a power of two <= 64) covers a
 // k-vector with one float4 per lane; 64/L groups per wave, 4 waves per workgroup.
-__device__ __forceinline__ float seg_sum(float v, int L) {
-  for (int o = L >> 1; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+// VX: the butterfly steps on the VALU (gr_common.h xsum: v_permlane*_swap / DPP), bitwise the
+// __shfl_xor (ds_bpermute) form -- shorter dependency chains, more VALU instructions: the kernel
+// takes it when a CU holds one sequence (latency-bound), the ds_bpermute form at two per CU (B 512:
+// 38.7 vs 45.4 us; B 128: 24.5 vs 18.5 us; profiles/r06/ab_tail_vx.txt).
+template <bool VX>
+__device__ __forceinline__ float seg_sum(float v, int L) {   // o = L/2 .. 1
+  if (!VX) {
+    for (int o = L >> 1; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+  }
+  if (L > 32) v = xsum<32>(v);
+  if (L > 16) v = xsum<16>(v);
+  if (L > 8) v = xsum<8>(v);
+  if (L > 4) v = xsum<4>(v);
+  if (L > 2) v = xsum<2>(v);
+  if (L > 1) v = xsum<1>(v);
   return v;
+}
+
+template <bool VX>
+__device__ __forceinline__ float wave_sum64(float v) {   // o = 32 .. 1
+  if (!VX) {
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+  }
+  return xsum<1>(xsum<2>(xsum<4>(xsum<8>(xsum<16>(xsum<32>(v))))));
 }
 
 // out[o] = bias[o] + W[o, 0..k) . v (v in LDS), o < rows: one lane group per output row, 16-B
 // coalesced row reads, ST_U rows in flight per group (the kernel is latency-bound: one sequence
 // per workgroup, every phase a dependent step).
+template <bool VX>
 __device__ __forceinline__ void st_gemv(const float* __restrict__ W, const float* __restrict__ bias,
                                         const float* v, int rows, int k, float* out) {
   if (GR_TDIAG == 2) return;
@@ -66,27 +90,28 @@ __device__ __forceinline__ void st_gemv(const float* __restrict__ W, const float
       acc = fmaf(a[u][1], x[1], acc);
       acc = fmaf(a[u][2], x[2], acc);
       acc = fmaf(a[u][3], x[3], acc);
-      acc = seg_sum(acc, L);
+      acc = seg_sum<VX>(acc, L);
       if (l == 0 && o < rows) out[o] = acc + bias[o];
     }
   }
 }
 
 // F.layer_norm of one d-vector in LDS (biased variance, eps inside the sqrt); wave 0 reduces.
+template <bool VX>
 __device__ __forceinline__ void st_layernorm(const float* in, const float* __restrict__ w,
                                              const float* __restrict__ b, int d, float eps, float* out,
                                              float* stat) {
   if (threadIdx.x < 64) {
     float s = 0.f;
     for (int c = threadIdx.x; c < d; c += 64) s += in[c];
-    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+    s = wave_sum64<VX>(s);
     const float mean = s / (float)d;
     float v = 0.f;
     for (int c = threadIdx.x; c < d; c += 64) {
       const float t = in[c] - mean;
       v = fmaf(t, t, v);
     }
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    v = wave_sum64<VX>(v);
     if (threadIdx.x == 0) {
       stat[0] = mean;
       stat[1] = 1.0f / sqrtf(v / (float)d + eps);
@@ -133,7 +158,7 @@ __device__ __forceinline__ void st_gemv_issue(const float* __restrict__ W, const
 // st_gemv with the first chunk from st_gemv_issue (same fma order: bitwise st_gemv's result).
 // Epilogue: out[o] = acc + bias, then RELU: max(., 0) (NaN kept), or with `res`: res[o] + (acc +
 // bias) -- the separate passes' exact values (res may alias out: each o is one lane's).
-template <bool RELU = false>
+template <bool VX, bool RELU = false>
 __device__ __forceinline__ void st_gemv_finish(const float* __restrict__ W, const float* __restrict__ bias,
                                                const float* v, int rows, int k, float* out, const GemvRows& g,
                                                const float* res = nullptr) {
@@ -149,7 +174,7 @@ __device__ __forceinline__ void st_gemv_finish(const float* __restrict__ W, cons
     acc = fmaf(g.a[u][1], x[1], acc);
     acc = fmaf(g.a[u][2], x[2], acc);
     acc = fmaf(g.a[u][3], x[3], acc);
-    acc = seg_sum(acc, L);
+    acc = seg_sum<VX>(acc, L);
     if (l == 0 && o < rows) {
       float y = acc + g.bias[u];
       if (RELU) y = y < 0.f ? 0.f : y;
@@ -170,7 +195,7 @@ __device__ __forceinline__ void st_gemv_finish(const float* __restrict__ W, cons
       acc = fmaf(a[u][1], x[1], acc);
       acc = fmaf(a[u][2], x[2], acc);
       acc = fmaf(a[u][3], x[3], acc);
-      acc = seg_sum(acc, L);
+      acc = seg_sum<VX>(acc, L);
       if (l == 0 && o < rows) {
         float y = acc + bias[o];
         if (RELU) y = y < 0.f ? 0.f : y;
@@ -190,7 +215,7 @@ __device__ __forceinline__ void st_gemv_finish(const float* __restrict__ W, cons
 // reassociated sums round differently from the reference formulation, within the logits
 // tolerance (tests/test_sasrec_gpu.py::test_tail_h_form_vs_full_block_and_oracle).
 // HM = the number of heads (a power of two <= 8).
-template <int HM>
+template <int HM, bool VX>
 __global__ __launch_bounds__(ST_NT, 2) void sas_tail_h2_kernel(const SasTailArgs a, const float* __restrict__ X,
                                                           const float* __restrict__ Hs, const float* __restrict__ wk,
                                                           const float* __restrict__ wv, const float* __restrict__ bv,
@@ -227,7 +252,7 @@ __global__ __launch_bounds__(ST_NT, 2) void sas_tail_h2_kernel(const SasTailArgs
     lnw[3 * d + c] = a.ln_b[c];
   }
   __syncthreads();
-  st_gemv_finish(a.wq, a.bq, hl, d, d, q, g0);
+  st_gemv_finish<VX>(a.wq, a.bq, hl, d, d, q, g0);
   st_gemv_issue(wv, bv, hd, d, g0);                 // head 0's W_v rows, used after the H pass
   __syncthreads();
   if (GR_TDIAG != 3) {   // q'_h = W_k,h^T q_h
@@ -281,7 +306,7 @@ __global__ __launch_bounds__(ST_NT, 2) void sas_tail_h2_kernel(const SasTailArgs
         t = fmaf(h4[uu][1], q4[1], t);
         t = fmaf(h4[uu][2], q4[2], t);
         t = fmaf(h4[uu][3], q4[3], t);
-        sc[uu] = seg_sum(t, L);
+        sc[uu] = seg_sum<VX>(t, L);
       }
 #pragma unroll
       for (int uu = 0; uu < ST_U; ++uu) {
@@ -316,21 +341,21 @@ __global__ __launch_bounds__(ST_NT, 2) void sas_tail_h2_kernel(const SasTailArgs
     }
     __syncthreads();
   }
-  st_gemv_finish(wv, bv, u, hd, d, o, g0);                      // o_0 = Wv_0 u_0 + bv_0
+  st_gemv_finish<VX>(wv, bv, u, hd, d, o, g0);                      // o_0 = Wv_0 u_0 + bv_0
   for (int hh = 1; hh < HM; ++hh)
-    st_gemv(wv + (int64_t)hh * hd * d, bv + hh * hd, u + hh * d, hd, d, o + hh * hd);
+    st_gemv<VX>(wv + (int64_t)hh * hd * d, bv + hh * hd, u + hh * d, hd, d, o + hh * hd);
   st_gemv_issue(a.wo, a.bo, d, d, g0);
   st_gemv_issue(a.w1, a.b1, a.mlp, d, g1);                      // FFN1 rows, used after the LayerNorm
   __syncthreads();
-  st_gemv_finish(a.wo, a.bo, o, d, d, x1, g0, xl);              // x + out_proj (model.py:84)
+  st_gemv_finish<VX>(a.wo, a.bo, o, d, d, x1, g0, xl);              // x + out_proj (model.py:84)
   st_gemv_issue(a.w2, a.b2, d, a.mlp, g0);
   __syncthreads();
-  st_layernorm(x1, lnw, lnw + d, d, a.eps, l1, stat);
-  st_gemv_finish<true>(a.w1, a.b1, l1, a.mlp, d, fh, g1);       // relu(W1 . + b1)
+  st_layernorm<VX>(x1, lnw, lnw + d, d, a.eps, l1, stat);
+  st_gemv_finish<VX, true>(a.w1, a.b1, l1, a.mlp, d, fh, g1);       // relu(W1 . + b1)
   __syncthreads();
-  st_gemv_finish(a.w2, a.b2, fh, d, a.mlp, x1, g0, x1);         // x1 + W2 f + b2 (model.py:94)
+  st_gemv_finish<VX>(a.w2, a.b2, fh, d, a.mlp, x1, g0, x1);         // x1 + W2 f + b2 (model.py:94)
   __syncthreads();
-  st_layernorm(x1, lnw + 2 * d, lnw + 3 * d, d, a.eps, l1, stat);  // last_layernorm (model.py:96)
+  st_layernorm<VX>(x1, lnw + 2 * d, lnw + 3 * d, d, a.eps, l1, stat);  // last_layernorm (model.py:96)
   for (int c = tid; c < d; c += ST_NT) out[b * d + c] = l1[c];
 }
 
@@ -371,11 +396,24 @@ int gr_sasrec_tail_h_launch(const gr_sasrec_params* p, int blk, const float* X, 
     if (!aligned16(q)) return GR_ERR_UNSUPPORTED;
   a.d = d; a.n = n; a.heads = H; a.mlp = p->mlp; a.eps = p->eps;
   a.scale = (float)std::sqrt(1.0 / (double)(d / H));
-  switch (H) {
-    case 1: hipLaunchKernelGGL(sas_tail_h2_kernel<1>, dim3((unsigned)B), dim3(ST_NT), 0, st, a, X, Hs, wk, wv, bv, out); break;
-    case 2: hipLaunchKernelGGL(sas_tail_h2_kernel<2>, dim3((unsigned)B), dim3(ST_NT), 0, st, a, X, Hs, wk, wv, bv, out); break;
-    case 4: hipLaunchKernelGGL(sas_tail_h2_kernel<4>, dim3((unsigned)B), dim3(ST_NT), 0, st, a, X, Hs, wk, wv, bv, out); break;
-    default: hipLaunchKernelGGL(sas_tail_h2_kernel<8>, dim3((unsigned)B), dim3(ST_NT), 0, st, a, X, Hs, wk, wv, bv, out); break;
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1) cus = 256;
   }
+  const bool vx = B <= cus;   // one sequence per CU: latency-bound, the VALU butterflies pay
+#define GR_TAIL(HM)                                                                                           \
+  if (vx)                                                                                                     \
+    hipLaunchKernelGGL((sas_tail_h2_kernel<HM, true>), dim3((unsigned)B), dim3(ST_NT), 0, st, a, X, Hs, wk, wv, bv, out); \
+  else                                                                                                        \
+    hipLaunchKernelGGL((sas_tail_h2_kernel<HM, false>), dim3((unsigned)B), dim3(ST_NT), 0, st, a, X, Hs, wk, wv, bv, out)
+  switch (H) {
+    case 1: GR_TAIL(1); break;
+    case 2: GR_TAIL(2); break;
+    case 4: GR_TAIL(4); break;
+    default: GR_TAIL(8); break;
+  }
+#undef GR_TAIL
   return check_launch("sasrec tail (H form, one pass)");
 }

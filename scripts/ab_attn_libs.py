@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""A/B of the row-tile SASRec forward (C5 shapes: the attention kernel sits inside it) between builds
+"""A/B of the SASRec forward (C5 shapes: the row-tile chain and its attention; C3 / d 16: the fused kernel) between builds
 of the library: each build runs in its own process (GR_AMD_LIB), times last_hidden / forward with HIP
 events (steady state) and saves the outputs; the parent checks them bitwise against the first build.
 
@@ -12,8 +12,9 @@ import sys
 
 import torch
 
-SHAPES = [  # d, heads, n, B
+SHAPES = [  # d, heads, n, B (the last two: the fused d <= 64 forward -- C3, and main.py's d 16)
     (128, 1, 200, 512), (128, 2, 200, 256), (128, 1, 100, 300), (64, 1, 200, 128), (128, 1, 65, 7),
+    (64, 1, 50, 2048), (16, 1, 20, 128),
 ]
 
 
