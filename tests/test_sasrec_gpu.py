@@ -287,6 +287,21 @@ def test_tail_h_form_vs_full_block_and_oracle(d, heads, n, blocks, B, dev):
     assert ((got - ref).abs() / ref.abs().amax(1, keepdim=True)).max().item() <= TOL
 
 
+@pytest.mark.parametrize("heads", [1, 2])
+def test_tail_reduction_forms_bitwise(heads, dev):
+    """sas_tail_h2_kernel's two reduction forms (gr_common.h xsum on the VALU when B <= CUs, ds_bpermute
+    above) are the same sums: rows of a 600-sequence call (ds_bpermute form) equal the same rows
+    computed in a 100-sequence call (VALU form) bit for bit."""
+    from gr_amd import synth
+    d, n, items = 128, 200, 3000
+    p = synth.sasrec_params(d, n, 2, heads, 64, dev)
+    m = synth.sasrec_model(items, p, dev, seed=91 + heads)
+    seqs = synth.sequences(600, n, items, 97, dev)
+    big = m.last_hidden(seqs)
+    small = m.last_hidden(seqs[200:300].contiguous())
+    assert torch.equal(big[200:300], small)
+
+
 @pytest.mark.parametrize("d,heads,n,blocks,B", [(128, 1, 200, 2, 37), (128, 2, 130, 2, 9), (64, 1, 100, 2, 17),
                                                 (64, 2, 77, 1, 5), (128, 1, 33, 1, 3), (128, 1, 200, 2, 1500),
                                                 (128, 2, 97, 3, 40), (128, 1, 256, 1, 70), (64, 1, 20, 1, 2000)])
