@@ -317,6 +317,7 @@ class RqBinding:
         self.dims_c, self.ks_c = L.i32_array(self.dims), L.i32_array(self.Ks)
         self.w_arr, self.b_arr, self.c_arr = L.ptr_array(self.ws), L.ptr_array(self.bs), L.ptr_array(self.cbs)
         self.device = self.ws[0].device
+        self.dev_index = self.device.index if self.device.index is not None else torch.cuda.current_device()
         self._ws_bytes = {}
         # the fused encoder's packed weight image (frozen weights only, see packed_ptr)
         nf = L.lib().gr_rq_encoder_pack_floats(len(self.ws), self.dims_c)
@@ -368,6 +369,30 @@ class RqBinding:
             self.packed.record_stream(torch.cuda.current_stream(self.device))
             streams.add(st)
         return self.packed.data_ptr()
+
+    def encode_fast(self, x):
+        """rq_encode's common call -- fp32 contiguous [n, in_dim] rows on the binding's (current)
+        device, eager, semantic IDs only -- with the per-call host work cut to the checks and the
+        launch (the reference's get_indices(x[64]) is host-bound).  None: not that case; the
+        general path (which also raises the errors) runs instead.  Same C call, same results."""
+        if (x.dtype is not torch.float32 or x.dim() != 2 or x.shape[1] != self.in_dim or not x.is_cuda
+                or not x.is_contiguous() or x.get_device() != self.dev_index
+                or self.dev_index != torch.cuda.current_device() or torch.cuda.is_current_stream_capturing()):
+            return None
+        pk = self.packed_ptr()
+        n = x.shape[0]
+        st = L.stream_of(self.device)
+        nbytes = self._ws_bytes.get(n) or self.workspace_bytes(n)
+        ws = _SCRATCH.get((self.dev_index, st))
+        if ws is None or ws.numel() < nbytes:
+            ws = scratch(nbytes, self.device)
+        idx = torch.empty((n, len(self.cbs)), dtype=torch.int64, device=self.device)
+        rc = L.lib().gr_rq_encode_packed_f32(x.data_ptr(), n, self.n_linear, self.dims_c, self.w_arr, self.b_arr,
+                                             pk, len(self.cbs), self.ks_c, self.c_arr, idx.data_ptr(), None, None,
+                                             None, ws.data_ptr(), nbytes, st)
+        if rc:
+            L.check(rc, "gr_rq_encode_packed_f32")
+        return idx
 
     def workspace_bytes(self, n):
         nb = self._ws_bytes.get(n)
@@ -422,6 +447,10 @@ def rq_encode(x, weights=None, biases=None, codebooks=None, with_gap=False, with
     minus best) and the encoder output ``z`` when requested.  ``binding`` (an :class:`RqBinding`)
     replaces ``weights`` / ``biases`` / ``codebooks``.
     """
+    if binding is not None and not with_gap and not with_z:
+        idx = binding.encode_fast(x)
+        if idx is not None:
+            return idx
     b = binding if binding is not None else RqBinding(weights, biases, codebooks)
     L.require_gpu(x)
     x2 = L.as_f32(x)

@@ -340,12 +340,25 @@ class RQVAE(nn.Module):
         if xs.dim() != 2 or xs.shape[1] != self.in_dim:
             raise RuntimeError(f"get_indices expects [B, {self.in_dim}] inputs, got {tuple(xs.shape)}")
 
-    @torch.no_grad()
     def get_indices(self, xs, use_sk=False):
         """rqvae.py:67-71: ``[B, in_dim]`` fp32 -> ``[B, L]`` int64 semantic IDs (one C-ABI call).
 
         ``use_sk=True`` with a level whose ``sk_epsilon > 0`` assigns that level by Sinkhorn over the
-        whole batch (vq.py:76-84), as the reference does; the batch is one group."""
+        whole batch (vq.py:76-84), as the reference does; the batch is one group.  The reference's
+        eval call (no Sinkhorn, no BatchNorm, eval mode) goes straight to the cached binding's
+        ``encode_fast`` -- its outputs never carry autograd history, so it needs no no_grad scope."""
+        if not use_sk and not self.bn and not self.training:
+            c = self.__dict__.get("_gr_rq_binding")
+            if c is not None and c[2].direct and tuple(t.data_ptr() for t in c[0]) == c[1]:
+                b = c[2]
+                b.frozen = self.__dict__.get("_gr_frozen", True)
+                idx = b.encode_fast(xs)
+                if idx is not None:
+                    return idx
+        with torch.no_grad():
+            return self._get_indices(xs, use_sk)
+
+    def _get_indices(self, xs, use_sk):
         self._check_encode(xs, use_sk)
         if use_sk and any(q.sk_epsilon > 0 for q in self.rq.vq_layers):
             return ops.rq_quantize_sk(self.encoder(xs), self.rq.codebooks(), self.sk_eps(), self.rq.sk_iters)
