@@ -27,6 +27,10 @@
 
 namespace gr {
 
+#ifndef GR_SC_NT
+#define GR_SC_NT 2     // cache-policy bits of score_rot_kernel's interior whole-line stores: 2 = nt
+#endif                 // (streaming; 0 = default policy, A/B builds)
+
 constexpr int SC_CHUNK = 32;   // items per chunk (one 32-item MFMA tile)
 constexpr int SC_RING = 3;     // chunks of logits staged in LDS (ring kernel)
 
@@ -464,7 +468,7 @@ __global__ __launch_bounds__(256, 2) void score_rot_kernel(const float* __restri
     const int vo = PREOFF ? voff[v] : lane_c + rot_addr[v] - (lo ? 128 : 0);
     const int so = (int)(L * SC_CHUNK * 4) + ut * ut_off + (PREOFF ? 0 : (int)(bv * ld * 4));
     if (interior) {
-      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(val), rs, vo, so, 0);
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(val), rs, vo, so, GR_SC_NT);
     } else {
       // column of this lane's element relative to 32 L: r - o = q - 32 [p < o]; all 32-bit
       const int colrel = ((rot_addr[v] >> 2) - 32 * hh) - (lo ? 32 : 0);

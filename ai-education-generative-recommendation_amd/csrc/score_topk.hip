@@ -66,14 +66,16 @@ __global__ __launch_bounds__(256, 2) void score_topk_kernel(
   int cgt = 0;
 
   f32x4 st[LV];
+  // chunk c through a buffer resource over its own rows (base and size scalar): float4 f at byte
+  // 16 f, rows past the catalog read as zero (masked below) -- no 64-bit address or clamp per load
   auto gload = [&](int64_t c) {
+    const int64_t left = (rows - c * TK_CHUNK) * D * 4;
+    const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(table + c * TK_CHUNK * D), 0,
+                                                      (int)(left < TK_CHUNK * D * 4 ? left : TK_CHUNK * D * 4),
+                                                      0x00020000);
 #pragma unroll
-    for (int i = 0; i < LV; ++i) {
-      const int f = tid + 256 * i, row = f / (D / 4), col = (f % (D / 4)) * 4;
-      int64_t item = c * TK_CHUNK + row;
-      item = item < rows ? item : rows - 1;
-      st[i] = *reinterpret_cast<const f32x4*>(table + item * D + col);
-    }
+    for (int i = 0; i < LV; ++i)
+      st[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, 16 * (tid + 256 * i), 0, 0));
   };
   auto swrite = [&](int b) {
 #pragma unroll
