@@ -125,6 +125,7 @@ __global__ __launch_bounds__(256, 2) void score_topk_kernel(
     // writing 32- or 64-byte runs per user measured slower (1097-1101 vs 1078-1080 us at C5,
     // 175.6-176.4 vs 172 us on a shard, same results; profiles/r03_ab_topk_staged.txt): the call is
     // MFMA-bound and the extra LDS traffic / barriers cost more than the write traffic saved
+    float mt[2];   // MODE 2: the chunk's two tile maxima, one 8-byte store
 #pragma unroll
     for (int it = 0; it < 2; ++it) {
       float m = -INFINITY, m1 = -INFINITY;   // fmaxf skips the NaN of rows past the catalog
@@ -139,10 +140,11 @@ __global__ __launch_bounds__(256, 2) void score_topk_kernel(
       if (MODE == 3) {
         m1 = fmaxf(m1, __shfl_xor(m1, 32));
         if (hh == 0 && u < B) *reinterpret_cast<f32x2*>(cv + u * seg_stride + 4 * vc + 2 * it) = f32x2{m, m1};
-      } else if (hh == 0 && u < B) {
-        cv[u * seg_stride + 2 * vc + it] = m;
+      } else {
+        mt[it] = m;
       }
     }
+    if (MODE == 2 && hh == 0 && u < B) *reinterpret_cast<f32x2*>(cv + u * seg_stride + 2 * vc) = f32x2{mt[0], mt[1]};
     if (vc + 1 < v_end) swrite(buf ^ 1);
     __syncthreads();
     buf ^= 1;
